@@ -1,0 +1,346 @@
+"""bh_amd — Python host binding of the MI355X Barnes–Hut engine (libbh_engine.so).
+
+Everything here is plumbing over the C-ABI in include/bh_engine.h; the physics runs in the
+HIP kernels of barnes-hut-n-body_amd/csrc.  There is no CPU fallback: if the shared
+library is missing or no GPU is visible, the calls fail loudly.
+
+Two layers:
+  * `Engine` — 1:1 with the C-ABI, numpy SoA arrays in/out (used by bench.py and tests).
+  * `PhysicsEngine`, `Body`, `Quad`, `Config` — a mirror of the reference's Kotlin surface
+    (/root/reference/src/main/kotlin/BarnesHutAlg.kt = BHA, Config.kt = CFG) with the same
+    names and call pattern NBodyPanel uses, so parity tests read like the reference's use.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import scenes  # noqa: F401  (re-export)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libbh_engine.so"))
+
+BH_OK = 0
+BH_E_INVALID = -1
+BH_E_DEVICE = -2
+BH_E_COMM = -3
+BH_E_CAPACITY = -4
+BH_E_STATE = -5
+
+EXPORTED_SYMBOLS = (
+    "bh_default_params", "bh_create", "bh_create_dist", "bh_comm_unique_id", "bh_destroy",
+    "bh_last_error", "bh_set_params", "bh_get_params", "bh_reset_bodies", "bh_step",
+    "bh_num_bodies", "bh_get_bodies", "bh_compute_accelerations", "bh_get_quads",
+    "bh_last_timings", "bh_last_tree_nodes", "bh_traverse_kernel_ms", "bh_set_profiling",
+    "bh_synchronize", "bh_scene_galaxy_disk", "bh_scene_kepler_disk", "bh_scene_uniform",
+)
+
+
+class BhParams(ctypes.Structure):
+    """struct bh_params (include/bh_engine.h) — Config fields read by step()."""
+    _fields_ = [
+        ("G", ctypes.c_double),
+        ("dt", ctypes.c_double),
+        ("theta", ctypes.c_double),
+        ("soft2", ctypes.c_double),
+        ("width_px", ctypes.c_int32),
+        ("height_px", ctypes.c_int32),
+        ("merge_max_mass", ctypes.c_double),
+        ("merge_min_dist", ctypes.c_double),
+    ]
+
+
+class BhError(RuntimeError):
+    def __init__(self, rc, msg):
+        super().__init__(f"bh_engine error {rc}: {msg}")
+        self.rc = rc
+
+
+_lib = None
+_D = ctypes.POINTER(ctypes.c_double)
+_I64P = ctypes.POINTER(ctypes.c_int64)
+_VP = ctypes.c_void_p
+
+
+def load_library(path: str | None = None):
+    """Load libbh_engine.so (raises if it was not built: there is no fallback)."""
+    global _lib
+    if _lib is not None and path is None:
+        return _lib
+    p = path or LIB_PATH
+    if not os.path.exists(p):
+        raise FileNotFoundError(
+            f"{p} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`")
+    lib = ctypes.CDLL(p, mode=ctypes.RTLD_GLOBAL)
+    lib.bh_default_params.argtypes = [ctypes.POINTER(BhParams)]
+    lib.bh_default_params.restype = None
+    lib.bh_create.argtypes = [ctypes.POINTER(BhParams), ctypes.c_int, ctypes.POINTER(_VP)]
+    lib.bh_create_dist.argtypes = [ctypes.POINTER(BhParams), ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(_VP)]
+    lib.bh_comm_unique_id.argtypes = [ctypes.c_char_p]
+    lib.bh_destroy.argtypes = [_VP]
+    lib.bh_destroy.restype = None
+    lib.bh_last_error.argtypes = [_VP]
+    lib.bh_last_error.restype = ctypes.c_char_p
+    lib.bh_set_params.argtypes = [_VP, ctypes.POINTER(BhParams)]
+    lib.bh_get_params.argtypes = [_VP, ctypes.POINTER(BhParams)]
+    lib.bh_reset_bodies.argtypes = [_VP, ctypes.c_int64, _D, _D, _D, _D, _D]
+    lib.bh_step.argtypes = [_VP, ctypes.c_int32]
+    lib.bh_num_bodies.argtypes = [_VP]
+    lib.bh_num_bodies.restype = ctypes.c_int64
+    lib.bh_get_bodies.argtypes = [_VP, _D, _D, _D, _D, _D, ctypes.c_int64, _I64P]
+    lib.bh_compute_accelerations.argtypes = [_VP, _D, _D, _I64P]
+    lib.bh_get_quads.argtypes = [_VP, _D, _D, _D, ctypes.c_int64, _I64P]
+    lib.bh_last_timings.argtypes = [_VP, _D]
+    lib.bh_last_tree_nodes.argtypes = [_VP]
+    lib.bh_last_tree_nodes.restype = ctypes.c_int64
+    lib.bh_traverse_kernel_ms.argtypes = [_VP, _D, _I64P]
+    lib.bh_set_profiling.argtypes = [_VP, ctypes.c_int]
+    lib.bh_synchronize.argtypes = [_VP]
+    lib.bh_scene_galaxy_disk.argtypes = (
+        [ctypes.c_int32] + [ctypes.c_double] * 6 + [ctypes.c_int32, ctypes.c_int64]
+        + [ctypes.c_double] * 9 + [_D] * 5)
+    lib.bh_scene_kepler_disk.argtypes = (
+        [ctypes.c_int32, ctypes.c_int32, ctypes.c_double, ctypes.c_double, ctypes.c_int64]
+        + [ctypes.c_double] * 6 + [_D] * 5)
+    lib.bh_scene_uniform.argtypes = [ctypes.c_int32, ctypes.c_double, ctypes.c_int64,
+                                     ctypes.c_int32, ctypes.c_int32] + [_D] * 5
+    if path is None:
+        _lib = lib
+    return lib
+
+
+def _dp(a):
+    return a.ctypes.data_as(_D) if a is not None else None
+
+
+def default_params(**over) -> BhParams:
+    p = BhParams()
+    load_library().bh_default_params(ctypes.byref(p))
+    for k, v in over.items():
+        setattr(p, k, v)
+    return p
+
+
+def comm_unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    rc = load_library().bh_comm_unique_id(buf)
+    if rc != BH_OK:
+        raise BhError(rc, "bh_comm_unique_id failed")
+    return buf.raw
+
+
+class Engine:
+    """The C-ABI, one call per method.  State lives in HBM; arrays are copied in/out."""
+
+    def __init__(self, params: BhParams | None = None, device: int = 0, rank: int = 0,
+                 world: int = 1, unique_id: bytes | None = None):
+        self._lib = load_library()
+        self._h = _VP()
+        self.params = params if params is not None else default_params()
+        if world > 1:
+            rc = self._lib.bh_create_dist(ctypes.byref(self.params), device, rank, world,
+                                          unique_id, ctypes.byref(self._h))
+        else:
+            rc = self._lib.bh_create(ctypes.byref(self.params), device, ctypes.byref(self._h))
+        if rc != BH_OK:
+            raise BhError(rc, "engine creation failed (is a GPU visible?)")
+        self.rank, self.world = rank, world
+
+    def _check(self, rc):
+        if rc != BH_OK:
+            raise BhError(rc, self._lib.bh_last_error(self._h).decode())
+
+    def close(self):
+        if self._h:
+            self._lib.bh_destroy(self._h)
+            self._h = _VP()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_params(self, params: BhParams):
+        self.params = params
+        self._check(self._lib.bh_set_params(self._h, ctypes.byref(params)))
+
+    def reset_bodies(self, x, y, vx, vy, m):
+        arrs = [np.ascontiguousarray(a, dtype=np.float64) for a in (x, y, vx, vy, m)]
+        n = len(arrs[0])
+        if any(len(a) != n for a in arrs):
+            raise ValueError("x, y, vx, vy, m must have equal lengths")
+        self._check(self._lib.bh_reset_bodies(self._h, n, *[_dp(a) for a in arrs]))
+
+    def step(self, k: int = 1):
+        self._check(self._lib.bh_step(self._h, int(k)))
+
+    def num_bodies(self) -> int:
+        return int(self._lib.bh_num_bodies(self._h))
+
+    def get_bodies(self):
+        n = self.num_bodies()
+        out = [np.empty(n, dtype=np.float64) for _ in range(5)]
+        got = ctypes.c_int64(0)
+        self._check(self._lib.bh_get_bodies(self._h, *[_dp(a) for a in out], n, ctypes.byref(got)))
+        return tuple(a[: got.value] for a in out)
+
+    def compute_accelerations(self, visits: bool = False):
+        n = self.num_bodies()
+        ax = np.empty(n, dtype=np.float64)
+        ay = np.empty(n, dtype=np.float64)
+        vis = np.empty(n, dtype=np.int64) if visits else None
+        self._check(self._lib.bh_compute_accelerations(
+            self._h, _dp(ax), _dp(ay), vis.ctypes.data_as(_I64P) if visits else None))
+        return (ax, ay, vis) if visits else (ax, ay)
+
+    def get_quads(self):
+        need = ctypes.c_int64(0)
+        rc = self._lib.bh_get_quads(self._h, None, None, None, 0, ctypes.byref(need))
+        if rc not in (BH_OK, BH_E_CAPACITY):
+            self._check(rc)
+        n = need.value
+        cx, cy, h = (np.empty(n, dtype=np.float64) for _ in range(3))
+        self._check(self._lib.bh_get_quads(self._h, _dp(cx), _dp(cy), _dp(h), n, ctypes.byref(need)))
+        return cx, cy, h
+
+    def set_profiling(self, on: bool):
+        self._check(self._lib.bh_set_profiling(self._h, 1 if on else 0))
+
+    def last_timings(self):
+        out = np.zeros(5, dtype=np.float64)
+        self._check(self._lib.bh_last_timings(self._h, _dp(out)))
+        return dict(zip(("build", "traverse", "integrate", "merge", "allgather"), out.tolist()))
+
+    def traverse_kernel_ms(self):
+        avg = ctypes.c_double(0.0)
+        cnt = ctypes.c_int64(0)
+        self._check(self._lib.bh_traverse_kernel_ms(self._h, ctypes.byref(avg), ctypes.byref(cnt)))
+        return avg.value, cnt.value
+
+    def last_tree_nodes(self) -> int:
+        return int(self._lib.bh_last_tree_nodes(self._h))
+
+    def synchronize(self):
+        self._check(self._lib.bh_synchronize(self._h))
+
+
+# ---- mirror of the reference's Kotlin surface ----------------------------------------------
+
+@dataclass
+class Body:  # BHA:21-25
+    x: float
+    y: float
+    vx: float
+    vy: float
+    m: float
+
+
+@dataclass(frozen=True)
+class Quad:  # BHA:53-82
+    cx: float
+    cy: float
+    h: float
+
+    def contains(self, b: Body) -> bool:  # BHA:61-62
+        return (b.x >= self.cx - self.h and b.x < self.cx + self.h
+                and b.y >= self.cy - self.h and b.y < self.cy + self.h)
+
+    def child(self, which: int) -> "Quad":  # BHA:73-81
+        hh = self.h / 2.0
+        return Quad(self.cx + (hh if which & 1 else -hh), self.cy + (hh if which & 2 else -hh), hh)
+
+
+class Config:  # CFG:2-39 — mutable globals read live by step()
+    WIDTH_PX = 2400
+    HEIGHT_PX = 800
+    G = 80.0
+    DT = 0.005
+    SOFTENING = 1.0
+    SOFT2 = 1.0 * 1.0
+    theta = 0.30
+    R = 100.0
+    N = 5000
+    CENTRAL_MASS = 50_000.0
+    MIN_R = 8.0
+    TOTAL_SATELLITE_MASS = 5_000.0
+
+
+class BHTree:
+    """getTreeForDebug() result: visitQuads (BHA:265-274) over a pre-order quad list."""
+
+    def __init__(self, cx, cy, h):
+        self._q = (cx, cy, h)
+
+    def visit_quads(self, visit):
+        cx, cy, h = self._q
+        for i in range(len(cx)):
+            visit(Quad(float(cx[i]), float(cy[i]), float(h[i])))
+
+    visitQuads = visit_quads
+
+
+class PhysicsEngine:
+    """PhysicsEngine(initialBodies) (BHA:287) — writes results back into the same Body
+    objects (BHA:414-432) and shrinks the caller's list on a merge (BHA:519)."""
+
+    def __init__(self, initial_bodies: list, device: int = 0):
+        self._bodies = initial_bodies
+        self.merge_max_mass = 4_000.0          # BHA:315
+        self.merge_min_dist = Config.MIN_R     # BHA:321
+        self._eng = Engine(self._params(), device=device)
+        self._push()
+
+    def _params(self) -> BhParams:
+        return default_params(G=Config.G, dt=Config.DT, theta=Config.theta, soft2=Config.SOFT2,
+                              width_px=int(Config.WIDTH_PX), height_px=int(Config.HEIGHT_PX),
+                              merge_max_mass=self.merge_max_mass,
+                              merge_min_dist=self.merge_min_dist)
+
+    def _push(self):
+        bs = self._bodies
+        self._eng.reset_bodies(*(np.array([getattr(b, f) for b in bs], dtype=np.float64)
+                                 for f in ("x", "y", "vx", "vy", "m")))
+
+    def _pull(self):
+        x, y, vx, vy, m = self._eng.get_bodies()
+        n = len(x)
+        bs = self._bodies
+        if n != len(bs):
+            # merge: the reference removes victims from the same list, keeping order;
+            # the survivors' identities are the kept indices in order.
+            del bs[n:]
+        for i in range(n):
+            b = bs[i]
+            b.x, b.y, b.vx, b.vy, b.m = float(x[i]), float(y[i]), float(vx[i]), float(vy[i]), float(m[i])
+
+    def step(self):  # BHA:405-439
+        self._eng.set_params(self._params())
+        self._push()
+        self._eng.step(1)
+        self._pull()
+
+    def get_bodies(self):  # BHA:335
+        return self._bodies
+
+    def reset_bodies(self, new_bodies: list):  # BHA:342-349
+        self._bodies = new_bodies
+        self._push()
+
+    def get_tree_for_debug(self) -> BHTree:  # BHA:329-332
+        self._eng.set_params(self._params())
+        cx, cy, h = self._eng.get_quads()
+        self._pull()
+        return BHTree(cx, cy, h)
+
+    getBodies = get_bodies
+    resetBodies = reset_bodies
+    getTreeForDebug = get_tree_for_debug
+
+    @property
+    def engine(self) -> Engine:
+        return self._eng

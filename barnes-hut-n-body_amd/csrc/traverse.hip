@@ -1,0 +1,130 @@
+// Force evaluation — replaces BHTree.accumulateForce/pointForceAcc and the coroutine driver
+// PhysicsEngine.computeAccelerations (BHA:215-259, BHA:374-395).
+//
+// One lane = one body, bodies in Morton order so a wavefront's 64 bodies are spatial
+// neighbours.  The wave walks ONE shared pre-order cursor over the flattened tree:
+//   * the node record is wave-uniform (scalar loads, one fetch serves 64 bodies);
+//   * every lane evaluates the reference's own criterion s2 < theta2*dist2 (BHA:228) for
+//     itself; a lane that accepts a node adds its point force and ignores that node's
+//     subtree (resume = node.next); the cursor descends (cur + 1) iff at least one lane
+//     opened the node (__ballot), otherwise it skips the subtree (cur = next).
+// Because the cursor order is the reference's DFS order and each lane only sums the nodes
+// its own recursive DFS would have summed, every body's force is the reference's sum in the
+// reference's order: bit-identical, not merely close (no Burtscher "open for all").
+#include "bh_device.hpp"
+
+namespace bh {
+namespace {
+
+constexpr int TB = 256;
+
+template <bool SORTED_OUT, bool COUNT>
+__global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
+                                                 const uint32_t *__restrict__ d_T,
+                                                 const double *__restrict__ sx,
+                                                 const double *__restrict__ sy,
+                                                 const double *__restrict__ sm,
+                                                 const uint32_t *__restrict__ perm, int64_t lo,
+                                                 int64_t hi, ForceParams fp, Geometry g,
+                                                 double *__restrict__ ax, double *__restrict__ ay,
+                                                 double *__restrict__ a_sorted,
+                                                 uint32_t *__restrict__ visits) {
+    const int64_t p = lo + (int64_t)blockIdx.x * TB + threadIdx.x;
+    const bool valid = p < hi;
+    const double bx = valid ? sx[p] : 0.0;
+    const double by = valid ? sy[p] : 0.0;
+    const double bm = valid ? sm[p] : 1.0;
+    const double Gm = fp.G * bm;  // (Config.G * b.m) is evaluated first (BHA:256)
+    const double soft2 = fp.soft2, theta2 = fp.theta2;
+    const uint32_t self = (uint32_t)p;
+    double fx = 0.0, fy = 0.0;
+    uint32_t nvis = 0;
+    // lane is active for node `cur` iff cur >= resume; invalid lanes never are.
+    uint32_t resume = valid ? 0u : 0xFFFFFFFFu;
+    const uint32_t T = __builtin_amdgcn_readfirstlane(*d_T);
+    uint32_t cur = 0;
+    while (cur < T) {
+        const Node nd = nodes[cur];
+        const uint32_t meta = __builtin_amdgcn_readfirstlane(nd.meta);
+        uint32_t next = __builtin_amdgcn_readfirstlane(nd.next);
+        next = next > cur ? next : cur + 1;  // structural guard: the cursor always advances
+        if (meta & NODE_SKIP) {              // mass == 0.0 (BHA:216), uniform
+            cur = next;
+            continue;
+        }
+        const bool active = cur >= resume;
+        if (COUNT) nvis += active ? 1u : 0u;
+        const double dx = nd.comX - bx;  // BHA:223-225 == BHA:251-253
+        const double dy = nd.comY - by;
+        const double d2 = dx * dx + dy * dy + soft2;
+        bool contrib, open;
+        if (meta & NODE_LEAF) {  // BHA:217-221: skip self by identity
+            contrib = active && ((meta & NODE_BODY_MASK) != self);
+            open = false;
+        } else {
+            const bool acc = g.s2[meta & NODE_DEPTH_MASK] < theta2 * d2;  // BHA:226-228
+            contrib = active && acc;
+            open = active && !acc;
+        }
+        if (contrib) {  // BHA:250-259, expression order as written
+            const double invR = 1.0 / sqrt(d2);
+            const double invR2 = 1.0 / d2;
+            const double f = Gm * nd.mass * invR2;
+            fx += f * dx * invR;
+            fy += f * dy * invR;
+            resume = next;
+        }
+        const bool any_open = __ballot(open) != 0ull;  // wave-uniform
+        cur = any_open ? cur + 1 : next;
+    }
+    if (!valid) return;
+    const double rax = fx / bm;  // BHA:390-391
+    const double ray = fy / bm;
+    if (SORTED_OUT) {
+        a_sorted[2 * p] = rax;
+        a_sorted[2 * p + 1] = ray;
+    } else {
+        const uint32_t o = perm[p];
+        ax[o] = rax;
+        ay[o] = ray;
+    }
+    if (COUNT) visits[perm[p]] = nvis;
+}
+
+__global__ __launch_bounds__(TB) void k_scatter(const double *__restrict__ a_sorted,
+                                                const uint32_t *__restrict__ perm, int64_t n,
+                                                double *__restrict__ ax, double *__restrict__ ay) {
+    int64_t p = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (p >= n) return;
+    uint32_t o = perm[p];
+    ax[o] = a_sorted[2 * p];
+    ay[o] = a_sorted[2 * p + 1];
+}
+
+}  // namespace
+
+void traverse(const Node *nodes, const uint32_t *d_T, const double *sx, const double *sy,
+              const double *sm, const uint32_t *perm, int64_t lo, int64_t hi, const Geometry &g,
+              const ForceParams &fp, double *ax, double *ay, double *a_sorted, uint32_t *visits,
+              hipStream_t s) {
+    if (hi <= lo) return;
+    unsigned grid = (unsigned)((hi - lo + TB - 1) / TB);
+    if (visits) {
+        k_traverse<false, true><<<grid, TB, 0, s>>>(nodes, d_T, sx, sy, sm, perm, lo, hi, fp, g, ax,
+                                                    ay, a_sorted, visits);
+    } else if (a_sorted) {
+        k_traverse<true, false><<<grid, TB, 0, s>>>(nodes, d_T, sx, sy, sm, perm, lo, hi, fp, g, ax,
+                                                    ay, a_sorted, visits);
+    } else {
+        k_traverse<false, false><<<grid, TB, 0, s>>>(nodes, d_T, sx, sy, sm, perm, lo, hi, fp, g, ax,
+                                                     ay, a_sorted, visits);
+    }
+}
+
+void scatter_sorted_acc(const double *a_sorted, const uint32_t *perm, int64_t n, double *ax,
+                        double *ay, hipStream_t s) {
+    if (n <= 0) return;
+    k_scatter<<<(unsigned)((n + TB - 1) / TB), TB, 0, s>>>(a_sorted, perm, n, ax, ay);
+}
+
+}  // namespace bh

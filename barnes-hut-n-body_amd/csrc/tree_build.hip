@@ -1,0 +1,364 @@
+// Quadtree build on the GPU — replaces BHTree.insert/insertIntoChild/subdivide/computeMass
+// and PhysicsEngine.buildTree (BHA:125-202, BHA:359-366).
+//
+// Why a sort reproduces the reference's serial insertion: a PR-quadtree with <= 1 body per
+// leaf is a pure function of the point set — a cell is subdivided iff >= 2 bodies reach it,
+// and the child a body goes to is chosen by `x < cx`, `y < cy` against exact cell centres
+// (BHA:153-154).  So every body's root-to-leaf path is its Morton key, computed here by the
+// same exact comparisons (never by a rounding division).  The one order-dependent part of
+// the reference — the deterministic jitter applied when a cell with h < 1e-3 is subdivided
+// (BHA:146-151), which mutates positions and can drop bodies — is confined to the cells at
+// the first depth J with h < 1e-3 that hold >= 2 bodies.  Those "jitter cells" are replayed
+// exactly, in body-index order, by one thread each (k_jitter) after a STABLE sort.
+//
+// Pipeline (all on one stream, no host synchronisation):
+//   k_morton  keys (2 bits per level, J levels) + identity payload
+//   radix sort (stable)            -> keys_s, perm
+//   k_prep    gather sorted x,y,m; c(a) = common digit count of neighbours; slot counts
+//   exclusive scan                 -> base (pre-order slot of each sorted body's nodes)
+//   k_emit    internal node skeletons (depth, next) + leaf records
+//   k_jitter  replay of BHA:125-156 inside each jitter cell
+//   k_com[L]  L = J..0: centre of mass bottom-up, children 0..3 in order (BHA:184-200)
+#include <hipcub/hipcub.hpp>
+
+#include "bh_device.hpp"
+
+namespace bh {
+namespace {
+
+constexpr int TB = 256;
+
+__device__ __forceinline__ int common_digits(uint64_t k1, uint64_t k2, int J) {
+    uint64_t d = k1 ^ k2;
+    if (d == 0) return J;
+    return (__clzll((long long)d) - (64 - 2 * J)) >> 1;
+}
+
+// BHA:61-62 evaluated exactly as written.
+__device__ __forceinline__ bool quad_contains(double cx, double cy, double h, double x, double y) {
+    return x >= cx - h && x < cx + h && y >= cy - h && y < cy + h;
+}
+
+// Cell centre at depth L along the digits of `key` (BHA:73-81 applied L times).
+__device__ void cell_centre(const Geometry &g, uint64_t key, int L, double &cx, double &cy) {
+    cx = g.root_cx;
+    cy = g.root_cy;
+    for (int d = 0; d < L; ++d) {
+        int digit = (int)((key >> (2 * (g.J - 1 - d))) & 3u);
+        double hh = g.h[d + 1];
+        cx = (digit & 1) ? cx + hh : cx - hh;
+        cy = (digit & 2) ? cy + hh : cy - hh;
+    }
+}
+
+__global__ __launch_bounds__(TB) void k_morton(int64_t n, const double *__restrict__ x,
+                                               const double *__restrict__ y, Geometry g,
+                                               uint64_t *__restrict__ keys,
+                                               uint32_t *__restrict__ idx) {
+    int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= n) return;
+    double px = x[i], py = y[i];
+    double cx = g.root_cx, cy = g.root_cy;
+    uint64_t key;
+    if (!quad_contains(cx, cy, g.root_h, px, py)) {
+        key = sentinel_key(g.J);  // BHA:126 — not inserted
+    } else {
+        key = 0;
+        for (int d = 0; d < g.J; ++d) {
+            int ix = (px < cx) ? 0 : 1;  // BHA:153
+            int iy = (py < cy) ? 0 : 1;  // BHA:154
+            double hh = g.h[d + 1];
+            cx = ix ? cx + hh : cx - hh;
+            cy = iy ? cy + hh : cy - hh;
+            key = (key << 2) | (uint64_t)(ix | (iy << 1));
+        }
+    }
+    keys[i] = key;
+    idx[i] = (uint32_t)i;
+}
+
+__global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *__restrict__ keys_s,
+                                             const uint32_t *__restrict__ perm,
+                                             const double *__restrict__ x,
+                                             const double *__restrict__ y,
+                                             const double *__restrict__ m, double *__restrict__ sx,
+                                             double *__restrict__ sy, double *__restrict__ sm,
+                                             int8_t *__restrict__ cpl, uint32_t *__restrict__ cnt) {
+    int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (a > n) return;
+    if (a == n) {
+        cnt[n] = 0;
+        return;
+    }
+    const uint64_t SENT = sentinel_key(J);
+    uint64_t k = keys_s[a];
+    uint32_t i = perm[a];
+    sx[a] = x[i];
+    sy[a] = y[i];
+    sm[a] = m[i];
+    int c_cur = -1, c_prev = -1;
+    if (k != SENT) {
+        if (a + 1 < n) {
+            uint64_t k2 = keys_s[a + 1];
+            if (k2 != SENT) c_cur = common_digits(k, k2, J);
+        }
+        if (a > 0) c_prev = common_digits(keys_s[a - 1], k, J);
+    }
+    cpl[a] = (int8_t)c_cur;
+    // internal nodes starting at a: depths c_prev+1 .. c_cur; plus a's leaf.
+    cnt[a] = (k == SENT) ? 0u : 1u + (uint32_t)max(0, c_cur - c_prev);
+}
+
+// Largest index e >= from with (keys_s[e] >> shift) == pref (keys_s[from] matches).
+__device__ __forceinline__ int64_t run_end(const uint64_t *__restrict__ keys_s, int64_t n,
+                                           int64_t from, int shift, uint64_t pref) {
+    int64_t lo = from, step = 1;
+    while (lo + step < n && (keys_s[lo + step] >> shift) == pref) {
+        lo += step;
+        step <<= 1;
+    }
+    int64_t hi = min(lo + step, n);  // keys_s[hi] does not match (or hi == n)
+    while (hi - lo > 1) {
+        int64_t mid = lo + ((hi - lo) >> 1);
+        if ((keys_s[mid] >> shift) == pref) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, const uint64_t *__restrict__ keys_s,
+                                             const int8_t *__restrict__ cpl,
+                                             const uint32_t *__restrict__ base,
+                                             const double *__restrict__ sx,
+                                             const double *__restrict__ sy,
+                                             const double *__restrict__ sm,
+                                             Node *__restrict__ nodes) {
+    int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (a >= n) return;
+    uint64_t k = keys_s[a];
+    if (k == sentinel_key(J)) return;
+    int cp = a > 0 ? (int)cpl[a - 1] : -1;
+    int cc = (int)cpl[a];
+    uint32_t b0 = base[a];
+    int64_t end = a;
+    for (int L = cc; L > cp; --L) {  // deepest first: ends are nested
+        int shift = 2 * (J - L);
+        end = run_end(keys_s, n, end, shift, k >> shift);
+        Node nd;
+        nd.comX = 0.0;
+        nd.comY = 0.0;
+        nd.mass = 0.0;
+        nd.next = base[end + 1];
+        nd.meta = (uint32_t)L;
+        nodes[b0 + (uint32_t)(L - cp - 1)] = nd;
+    }
+    uint32_t li = b0 + (uint32_t)max(0, cc - cp);
+    double mm = sm[a];
+    Node leaf;
+    leaf.comX = sx[a];  // BHA:176-178
+    leaf.comY = sy[a];
+    leaf.mass = mm;
+    leaf.next = li + 1;
+    leaf.meta = NODE_LEAF | (uint32_t)a | (mm == 0.0 ? NODE_SKIP : 0u);
+    nodes[li] = leaf;
+}
+
+// ---- exact replay of BHA:125-156 inside one jitter cell (depth J, h_J < 1e-3) ---------
+struct JitterCtx {
+    double *sx, *sy, *x, *y;
+    const uint32_t *perm;
+    uint32_t *err;
+};
+
+// BHA:146-151: x += (lsb(x)==0 ? +eps : -eps); y += (lsb(y)==0 ? -eps : +eps)
+__device__ __forceinline__ void jitter(const JitterCtx &c, int64_t j) {
+    const double eps = 1e-3;
+    double px = c.sx[j], py = c.sy[j];
+    px += ((__double_as_longlong(px) & 1ll) == 0) ? +eps : -eps;
+    py += ((__double_as_longlong(py) & 1ll) == 0) ? -eps : +eps;
+    c.sx[j] = px;
+    c.sy[j] = py;
+    uint32_t o = c.perm[j];
+    c.x[o] = px;  // the mutation is permanent in the reference (Body is shared)
+    c.y[o] = py;
+}
+
+// insertIntoChild on a depth-(J+1) cell: the body is jittered and must then land in a
+// grandchild of width h_J < 1e-3 — impossible after a 1e-3 move, so it is dropped
+// (BHA:126).  If geometry ever allowed it we flag instead of guessing.
+__device__ void into_child_deep(const JitterCtx &c, int64_t j, double qcx, double qcy, double qh) {
+    jitter(c, j);
+    double px = c.sx[j], py = c.sy[j];
+    double hh = qh / 2.0;
+    double gcx = (px < qcx) ? qcx - hh : qcx + hh;
+    double gcy = (py < qcy) ? qcy - hh : qcy + hh;
+    if (quad_contains(gcx, gcy, hh, px, py)) atomicOr(c.err, 1u);
+}
+
+__global__ __launch_bounds__(TB) void k_jitter(int64_t n, Geometry g,
+                                               const uint64_t *__restrict__ keys_s,
+                                               const int8_t *__restrict__ cpl,
+                                               const uint32_t *__restrict__ base, double *sx,
+                                               double *sy, const double *__restrict__ sm,
+                                               double *x, double *y,
+                                               const uint32_t *__restrict__ perm, Node *nodes,
+                                               uint32_t *err) {
+    int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (a >= n) return;
+    const int J = g.J;
+    if ((int)cpl[a] != J) return;
+    int cp = a > 0 ? (int)cpl[a - 1] : -1;
+    if (cp == J) return;  // not the first body of its jitter cell
+    int64_t b = a;
+    while (b < n && (int)cpl[b] == J) ++b;  // run = sorted bodies a..b (index order: stable sort)
+
+    JitterCtx c{sx, sy, x, y, perm, err};
+    double ccx, ccy;
+    cell_centre(g, keys_s[a], J, ccx, ccy);
+    const double hJ = g.h[J];
+    const double hc = g.h[J + 1];
+
+    // state of the 4 children: -1 empty, >= 0 leaf body (sorted pos), -2 subdivided
+    int64_t ch[4] = {-1, -1, -1, -1};
+    int64_t occ = -1;
+    bool sub = false;
+
+    auto into_child = [&](int64_t j) {  // BHA:145-156 on the jitter cell
+        jitter(c, j);
+        double px = c.sx[j], py = c.sy[j];
+        int ix = (px < ccx) ? 0 : 1;
+        int iy = (py < ccy) ? 0 : 2;
+        int q = ix + iy;
+        double qcx = (q & 1) ? ccx + hc : ccx - hc;
+        double qcy = (q & 2) ? ccy + hc : ccy - hc;
+        if (!quad_contains(qcx, qcy, hc, px, py)) return;  // BHA:126 dropped
+        if (ch[q] == -1) {                                // BHA:127-129
+            ch[q] = j;
+            return;
+        }
+        if (ch[q] >= 0) {  // BHA:131-135 subdivide, push existing down
+            int64_t e = ch[q];
+            ch[q] = -2;
+            into_child_deep(c, e, qcx, qcy, hc);
+        }
+        into_child_deep(c, j, qcx, qcy, hc);  // BHA:136
+    };
+
+    for (int64_t j = a; j <= b; ++j) {  // BHA:363 insertion in list order
+        if (!sub && occ < 0) {
+            occ = j;
+            continue;
+        }
+        if (!sub) {
+            sub = true;
+            int64_t e = occ;
+            occ = -1;
+            into_child(e);
+        }
+        into_child(j);
+    }
+    (void)hJ;
+
+    // Write the cell's children into its k = b - a + 1 contiguous slots, child order 0..3.
+    uint32_t s0 = base[a] + (uint32_t)(J - cp);
+    uint32_t k = (uint32_t)(b - a + 1);
+    uint32_t w = 0;
+    uint32_t jmask = 0;
+    for (int q = 0; q < 4; ++q) {
+        if (ch[q] == -2) jmask |= 1u << q;
+        if (ch[q] < 0) continue;
+        int64_t j = ch[q];
+        double mm = sm[j];
+        Node leaf;
+        leaf.comX = sx[j];
+        leaf.comY = sy[j];
+        leaf.mass = mm;
+        leaf.next = s0 + w + 1;
+        leaf.meta = NODE_LEAF | (uint32_t)j | (mm == 0.0 ? NODE_SKIP : 0u);
+        nodes[s0 + w] = leaf;
+        ++w;
+    }
+    for (; w < k; ++w) {
+        Node dead;
+        dead.comX = 0.0;
+        dead.comY = 0.0;
+        dead.mass = 0.0;
+        dead.next = s0 + w + 1;
+        dead.meta = NODE_SKIP;
+        nodes[s0 + w] = dead;
+    }
+    // remember which children were subdivided (for getTreeForDebug/visitQuads)
+    uint32_t ni = base[a] + (uint32_t)(J - cp - 1);
+    nodes[ni].meta = (uint32_t)J | (jmask << NODE_JMASK_SHIFT);
+}
+
+// BHA:173-202 for the internal nodes at depth L.
+__global__ __launch_bounds__(TB) void k_com(int64_t n, int L, Geometry g,
+                                            const uint64_t *__restrict__ keys_s,
+                                            const int8_t *__restrict__ cpl,
+                                            const uint32_t *__restrict__ base, Node *nodes) {
+    int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (a >= n) return;
+    int cc = (int)cpl[a];
+    if (cc < L) return;
+    int cp = a > 0 ? (int)cpl[a - 1] : -1;
+    if (cp >= L) return;
+    uint32_t ni = base[a] + (uint32_t)(L - cp - 1);
+    Node nd = nodes[ni];
+    double mSum = 0.0, cx = 0.0, cy = 0.0;
+    uint32_t c = ni + 1;
+    while (c < nd.next) {  // children in pre-order == child order 0..3
+        Node ch = nodes[c];
+        if (ch.mass > 0.0) {
+            mSum += ch.mass;
+            cx += ch.comX * ch.mass;
+            cy += ch.comY * ch.mass;
+        }
+        c = max(ch.next, c + 1);
+    }
+    nd.mass = mSum;
+    if (mSum > 0.0) {
+        nd.comX = cx / mSum;
+        nd.comY = cy / mSum;
+    } else {  // BHA:197-199 (never visited: mass == 0)
+        cell_centre(g, keys_s[a], L, nd.comX, nd.comY);
+        nd.meta |= NODE_SKIP;
+    }
+    nodes[ni] = nd;
+}
+
+inline unsigned grid_for(int64_t n) { return (unsigned)((n + TB - 1) / TB); }
+
+}  // namespace
+
+size_t tree_cub_bytes(int64_t n, int J) {
+    size_t sort_bytes = 0, scan_bytes = 0;
+    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (uint64_t *)nullptr, (uint64_t *)nullptr,
+                                       (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, 0,
+                                       2 * J + 1);
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                     (int)(n + 1));
+    return sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
+}
+
+hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStream_t s) {
+    if (n <= 0) return hipMemsetAsync(b.base, 0, sizeof(uint32_t), s);
+    hipError_t st;
+    k_morton<<<grid_for(n), TB, 0, s>>>(n, b.x, b.y, g, b.keys, b.idx);
+    size_t bytes = b.cub_bytes;
+    st = hipcub::DeviceRadixSort::SortPairs(b.cub_tmp, bytes, b.keys, b.keys_s, b.idx, b.perm,
+                                            (int)n, 0, 2 * g.J + 1, s);
+    if (st != hipSuccess) return st;
+    k_prep<<<grid_for(n + 1), TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.x, b.y, b.m, b.sx, b.sy, b.sm,
+                                          b.cpl, b.cnt);
+    bytes = b.cub_bytes;
+    st = hipcub::DeviceScan::ExclusiveSum(b.cub_tmp, bytes, b.cnt, b.base, (int)(n + 1), s);
+    if (st != hipSuccess) return st;
+    k_emit<<<grid_for(n), TB, 0, s>>>(n, g.J, b.keys_s, b.cpl, b.base, b.sx, b.sy, b.sm, b.nodes);
+    k_jitter<<<grid_for(n), TB, 0, s>>>(n, g, b.keys_s, b.cpl, b.base, b.sx, b.sy, b.sm, b.x, b.y,
+                                        b.perm, b.nodes, b.scalars + 1);
+    for (int L = g.J; L >= 0; --L)
+        k_com<<<grid_for(n), TB, 0, s>>>(n, L, g, b.keys_s, b.cpl, b.base, b.nodes);
+    return hipGetLastError();
+}
+
+}  // namespace bh

@@ -1,0 +1,206 @@
+#!/usr/bin/env python3
+"""Benchmark: body-steps/s of the reference's PhysicsEngine.step() (BHA:405-439) on MI355X.
+
+Workload (BASELINE.json metric "body-steps/sec at N=1e6, theta=0.5"): configuration C3, two
+colliding galaxy disks (NBodyPanel.kt:83-100 scaled: 8e5 + 2e5 bodies, seeds 1/2), theta 0.5,
+dt 0.005, G 80, eps^2 1, merge rule on.  One step = the full reference step: two tree builds,
+two force evaluations, kick-drift-kick, merge.  Inputs are resident in HBM before timing.
+
+Multi-GPU (torchrun, one rank per GPU): weak scaling — each rank adds 1e6 bodies to the same
+two-disk geometry (c3x<N>), state is replicated, force evaluation is sharded over ranks by
+Morton range and accelerations are all-gathered by RCCL over xGMI inside the engine.
+
+Prints ONE JSON line on rank 0 (see the driver contract in the task statement).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "barnes-hut-n-body_amd"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+NODE_BYTES = 32        # one fp64 node record (comX, comY, mass, s2/next) — SURVEY §8d
+BODY_EVAL_BYTES = 40   # body read (x, y, m) + acceleration write (ax, ay) per evaluation
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", default="c3", help="c3 (default), c2, c4, c1_code, c1_baseline")
+    ap.add_argument("--theta", type=float, default=0.5)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-steps", type=int, default=1)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    return ap.parse_args()
+
+
+def scene_for(config, world):
+    from bh_amd import scenes
+    if config == "c3" and world > 1:
+        return scenes.config_scene(f"c3x{world}"), f"c3x{world}"
+    return scenes.config_scene(config), config
+
+
+WORKLOAD_DESC = {
+    "c3": "two colliding galaxy disks (8e5 r=300 + 2e5 r=100 y=160 vx=-50), N=1e6",
+    "c2": "Kepler disk N=1e5 (BodyFactory.makeKeplerDisk, seed 3)",
+    "c4": "uniform cloud N=1e7 over 2400x800, m=0.5",
+    "c1_code": "defaultBodies(): two galaxy disks 10000 + 2500",
+    "c1_baseline": "BASELINE 'R' scene: two galaxy disks 2 x 1000",
+}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world and world > 1:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    import bh_amd
+
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+    torch.cuda.set_device(local_rank)
+
+    params = bh_amd.default_params(theta=args.theta)
+    if world > 1:
+        uid = [bh_amd.comm_unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(uid, src=0)
+        eng = bh_amd.Engine(params, device=local_rank, rank=rank, world=world, unique_id=uid[0])
+    else:
+        eng = bh_amd.Engine(params, device=local_rank)
+
+    arrs, scene_name = scene_for(args.config, world)
+    n0 = len(arrs[0])
+
+    # V-bar: mean non-empty nodes visited per body per evaluation on this scene,
+    # counted by the engine on a separate instance so the timed state is untouched.
+    probe = bh_amd.Engine(params, device=local_rank)
+    probe.reset_bodies(*arrs)
+    _, _, vis = probe.compute_accelerations(visits=True)
+    vbar = float(np.mean(vis)) if len(vis) else 0.0
+    probe.close()
+    del probe
+
+    eng.reset_bodies(*arrs)
+    if args.warmup > 0:
+        eng.step(args.warmup)
+    n_start = eng.num_bodies()
+
+    eng.set_profiling(True)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    eng.synchronize()
+    t0 = time.perf_counter()
+    eng.step(args.steps)  # blocks until the device work is complete
+    eng.synchronize()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    t1 = time.perf_counter()
+    elapsed = t1 - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    n_end = eng.num_bodies()
+    trav_ms, trav_launches = eng.traverse_kernel_ms()
+    phases = eng.last_timings()
+    eng.set_profiling(False)
+
+    bodies = 0.5 * (n_start + n_end)  # the merge rule can remove a handful of bodies
+    value = bodies * args.steps / elapsed
+    ms_per_step = 1e3 * elapsed / max(args.steps, 1)
+
+    # Roofline of the dominant kernel (traversal): algorithmic bytes per launch / duration.
+    bodies_per_launch = bodies / world
+    bytes_per_launch = (NODE_BYTES * vbar + BODY_EVAL_BYTES) * bodies_per_launch
+    achieved = bytes_per_launch / (trav_ms * 1e-3) / 1e9 if trav_ms > 0 else 0.0
+    roofline = {
+        "bound": "hbm",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBS, 4),
+        "traffic": None,
+        "kernel": "k_traverse",
+        "kernel_avg_ms": round(trav_ms, 4),
+        "launches": trav_launches,
+        "vbar_nodes_per_body_eval": round(vbar, 2),
+        "bytes_per_launch": round(bytes_per_launch),
+    }
+
+    cpu_baseline = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        import oracle
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        ref = oracle.Oracle(*arrs, theta=args.theta, threads=threads)
+        ref.step(1)  # same first step the GPU warmup took; bounded sample follows
+        c0 = time.perf_counter()
+        ref.step(args.cpu_steps)
+        c1 = time.perf_counter()
+        cpu_baseline = {
+            "value": round(ref.num_bodies() * args.cpu_steps / (c1 - c0), 1),
+            "unit": "body-steps/s",
+            "cores": threads,
+            "kind": "port",
+            "sample": f"{args.cpu_steps} full step(s) of {scene_name} ({ref.num_bodies()} bodies) "
+                      f"with the C restatement of the reference CPU path (oracle/bh_oracle.c: "
+                      f"serial pointer-tree build, {threads} workers on an atomic body queue)",
+            "seconds": round(c1 - c0, 3),
+        }
+        ref.close()
+
+    if rank == 0:
+        line = {
+            "metric": "body-steps/sec at N=1e6, theta=0.5; achieved HBM GB/s vs roofline",
+            "value": round(value, 1),
+            "unit": "body-steps/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms_per_step, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (seeded BodyFactory scenes generated in-process)",
+            "config": {
+                "workload": f"{scene_name}: {WORKLOAD_DESC.get(args.config, args.config)}",
+                "n_bodies": int(n_start),
+                "theta": args.theta,
+                "dt": params.dt,
+                "G": params.G,
+                "soft2": params.soft2,
+                "root": "2400x800",
+                "evals_per_step": 2,
+                "parallelism": f"replicated state, force sharded x{world} (RCCL all-gather)"
+                if world > 1 else "single GPU",
+            },
+            "phase_ms": {k: round(v, 3) for k, v in phases.items()},
+            "roofline": roofline,
+            "cpu_baseline": cpu_baseline,
+        }
+        print(json.dumps(line), flush=True)
+    eng.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

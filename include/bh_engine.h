@@ -1,0 +1,139 @@
+/*
+ * bh_engine.h — C-ABI drop-in boundary of the MI355X Barnes–Hut engine.
+ *
+ * Replaces the reference's PhysicsEngine / Body / BHTree Kotlin surface
+ * (/root/reference/src/main/kotlin/BarnesHutAlg.kt = BHA, Config.kt = CFG) as consumed by
+ * NBodyPanel (NBodyPanel.kt = PNL).  Plain pointers and sizes only: a JNI / Panama / ctypes
+ * shim binds these symbols directly (INTEGRATION.md shows the Kotlin-side binding).
+ *
+ * Semantics are the reference's, bit for bit in IEEE binary64:
+ *   - bodies are SoA fp64 arrays (x, y, vx, vy, m) in the caller's list order (BHA:21-25);
+ *   - one bh_step() == one PhysicsEngine.step() (BHA:405-439): build, a(t), kick, drift,
+ *     build, a(t+dt), kick, merge (BHA:463-532), so N may shrink;
+ *   - the quadtree jitter (BHA:146-151) mutates positions exactly as the reference does;
+ *   - bodies outside the root cell are not inserted but still integrate (BHA:126).
+ *
+ * Errors: every int-returning call returns 0 on success and a negative BH_E* code on
+ * failure; bh_last_error() returns a human-readable message.  Nothing aborts the process.
+ * Threading: one host thread per engine handle; calls are synchronous (results are
+ * visible to bh_get_bodies on return), like step() under runBlocking (BHA:408,426).
+ */
+#ifndef BH_ENGINE_H
+#define BH_ENGINE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define BH_OK 0
+#define BH_E_INVALID (-1)  /* bad argument */
+#define BH_E_DEVICE (-2)   /* HIP runtime error */
+#define BH_E_COMM (-3)     /* RCCL error */
+#define BH_E_CAPACITY (-4) /* caller buffer too small; *n_out holds the required size */
+#define BH_E_STATE (-5)    /* call not valid in this state */
+
+/* The Config.kt fields the hot path reads live, plus the merge knobs.
+ * Replaces: Config.G (CFG:11), Config.DT (CFG:14), Config.theta (CFG:23),
+ * Config.SOFT2 (CFG:20), Config.WIDTH_PX/HEIGHT_PX (CFG:5,8; root cell BHA:360-361),
+ * PhysicsEngine.mergeMaxMass (BHA:315), PhysicsEngine.mergeMinDist (BHA:321). */
+typedef struct bh_params {
+    double G;
+    double dt;
+    double theta;
+    double soft2;
+    int32_t width_px;
+    int32_t height_px;
+    double merge_max_mass;
+    double merge_min_dist;
+} bh_params;
+
+/* Reference defaults (CFG:5-23, BHA:315,321). */
+void bh_default_params(bh_params *p);
+
+typedef struct bh_engine bh_engine;
+
+/* new PhysicsEngine(...) (BHA:287) on HIP device `device`, single GPU. */
+int bh_create(const bh_params *p, int device, bh_engine **out);
+
+/* Multi-GPU member: one process per GPU; `unique_id` is the 128-byte RCCL id produced by
+ * bh_comm_unique_id() on rank 0 and broadcast by the caller (e.g. torch.distributed).
+ * Every rank holds the full replicated state; force evaluation is sharded over ranks by
+ * Morton-ordered body ranges and the accelerations are all-gathered over xGMI. */
+int bh_create_dist(const bh_params *p, int device, int rank, int world, const void *unique_id,
+                   bh_engine **out);
+int bh_comm_unique_id(void *out128);
+
+void bh_destroy(bh_engine *e);
+const char *bh_last_error(const bh_engine *e);
+
+/* Live Config mutation (PNL:247-260 change theta/DT/G between steps). */
+int bh_set_params(bh_engine *e, const bh_params *p);
+int bh_get_params(const bh_engine *e, bh_params *p);
+
+/* PhysicsEngine.resetBodies(newBodies) (BHA:342-349): copy-in of n bodies. */
+int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, const double *vx,
+                    const double *vy, const double *m);
+
+/* k x PhysicsEngine.step() (BHA:405-439). */
+int bh_step(bh_engine *e, int32_t k);
+
+/* getBodies().size */
+int64_t bh_num_bodies(const bh_engine *e);
+
+/* PhysicsEngine.getBodies() (BHA:335) copy-out; any pointer may be NULL to skip it.
+ * Returns BH_E_CAPACITY with *n_out = N if cap < N. */
+int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, double *m,
+                  int64_t cap, int64_t *n_out);
+
+/* buildTree() + computeAccelerations() (BHA:359-395) on the current state, exactly as
+ * the first half of step() does it (including the jitter's position mutation).  ax/ay
+ * (length N, caller order) receive F/m.  visits (nullable, length N) receives the number
+ * of non-empty nodes each body's traversal visited (accumulateForce calls passing the
+ * mass == 0 test, BHA:216) — the V of the roofline byte model. */
+int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visits);
+
+/* getTreeForDebug().visitQuads{} (BHA:265-274,329-332): pre-order list of every cell
+ * (cx, cy, h) of the last tree, or of a freshly built one if the cache was dropped
+ * (after resetBodies or a merge, BHA:348,526).  BH_E_CAPACITY + *n_out if cap too small. */
+int bh_get_quads(bh_engine *e, double *cx, double *cy, double *h, int64_t cap, int64_t *n_out);
+
+/* Per-phase device timings (ms) of the last bh_step call, summed over its steps:
+ * [0] tree build, [1] traversal, [2] integration, [3] merge, [4] all-gather. */
+int bh_last_timings(const bh_engine *e, double *out5);
+
+/* Number of tree nodes (non-empty + skip slots) of the last build; for byte models. */
+int64_t bh_last_tree_nodes(const bh_engine *e);
+
+/* Traversal kernel timing for roofline: average duration (ms) of the force-evaluation
+ * kernel over the launches of the last bh_step, measured with HIP events on the
+ * engine's own stream; *launches receives the count. */
+int bh_traverse_kernel_ms(const bh_engine *e, double *avg_ms, int64_t *launches);
+
+/* Enable/disable per-phase event timing (default off: no events in the hot loop). */
+int bh_set_profiling(bh_engine *e, int enabled);
+
+/* Block until all device work of this engine is complete. */
+int bh_synchronize(bh_engine *e);
+
+/* ---- scene generation (BodyFactory.kt = BF), host-side, deterministic -------------
+ * Kotlin's kotlin.random.Random(seed) XorWow stream (kotlin-stdlib 2.2.20) restated so
+ * that seeded scenes are reproducible; caller provides arrays of length n_total. */
+int bh_scene_galaxy_disk(int32_t n_total, double eps_m2, double phi0, double bar_taper_r,
+                         double radial_scale, double speed_jitter, double radial_jitter,
+                         int32_t clockwise, int64_t seed, double vx, double vy, double x,
+                         double y, double r, double min_r, double central_mass,
+                         double total_satellite_mass, double G, double *ox, double *oy,
+                         double *ovx, double *ovy, double *om);
+int bh_scene_kepler_disk(int32_t n_total, int32_t clockwise, double radial_jitter,
+                         double speed_jitter, int64_t seed, double vx, double vy, double x,
+                         double y, double r, double G, double *ox, double *oy, double *ovx,
+                         double *ovy, double *om);
+int bh_scene_uniform(int32_t n, double m, int64_t seed, int32_t width_px, int32_t height_px,
+                     double *ox, double *oy, double *ovx, double *ovy, double *om);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* BH_ENGINE_H */

@@ -1,0 +1,482 @@
+/*
+ * ORACLE — TEST INFRASTRUCTURE ONLY.
+ *
+ * A CPU restatement, line by line, of the reference Barnes–Hut hot path
+ * (/root/reference/src/main/kotlin/BarnesHutAlg.kt, "BHA" below; Config.kt "CFG").
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it,
+ * and only as the checker / the timed "reference-algorithm CPU path".  The product
+ * (barnes-hut-n-body_amd/, libbh_engine.so) never links or calls anything here.
+ *
+ * PARITY UNPINNED: the reference is Kotlin/JVM with no tests, no fixtures and no
+ * golden vectors, and no JVM exists in this image, so this
+ * restatement cannot be checked against the reference's own outputs.  It is pinned
+ * instead by (1) an independent pure-Python restatement (oracle/py_oracle.py) that
+ * must agree bit for bit, (2) hand-computed known-answer tests, (3) physics
+ * invariants (theta = 0 == direct sum), all under tests/.
+ *
+ * Numerics: JVM >= 17 floating point is strict IEEE-754 binary64 (JEP 306) with no
+ * fused multiply-add, so this file is compiled with -ffp-contract=off and without
+ * fast-math; every expression keeps the reference's left-to-right association.
+ *
+ * Structure mirrors the reference: a pointer quadtree (here: indices into a node
+ * pool) with <= 1 body per leaf, built serially in body-index order; recursive
+ * centre-of-mass; recursive per-body traversal; worker threads pulling body indices
+ * from one atomic counter (BHA:374-395); kick-drift-kick (BHA:405-439); the merge
+ * rule (BHA:463-532).
+ */
+#define _GNU_SOURCE
+#include <math.h>
+#include <pthread.h>
+#include <stdatomic.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "bh_oracle.h"
+
+/* ---- Body (BHA:21-25) and Quad (BHA:53-82) ---------------------------------- */
+typedef struct { double x, y, vx, vy, m; } Body;
+typedef struct { double cx, cy, h; } Quad;
+
+/* BHA:61-62 — half-open [cx-h, cx+h) x [cy-h, cy+h), bounds evaluated as written. */
+static int quad_contains(const Quad *q, const Body *b) {
+    return b->x >= q->cx - q->h && b->x < q->cx + q->h &&
+           b->y >= q->cy - q->h && b->y < q->cy + q->h;
+}
+
+/* BHA:73-81 — child 0=(-,-), 1=(+,-), 2=(-,+), 3=(+,+); hh = h / 2.0. */
+static Quad quad_child(const Quad *q, int which) {
+    double hh = q->h / 2.0;
+    Quad c;
+    switch (which) {
+    case 0: c.cx = q->cx - hh; c.cy = q->cy - hh; break;
+    case 1: c.cx = q->cx + hh; c.cy = q->cy - hh; break;
+    case 2: c.cx = q->cx - hh; c.cy = q->cy + hh; break;
+    default: c.cx = q->cx + hh; c.cy = q->cy + hh; break;
+    }
+    c.h = hh;
+    return c;
+}
+
+/* ---- BHTree (BHA:95-275) ------------------------------------------------------
+ * Node pool: a node's 4 children are allocated consecutively by subdivide().
+ * `body` is the body index (identity, BHA:219 `single === b`) or -1;
+ * `child` is the index of child 0, or -1 for a leaf (BHA:100,112).               */
+typedef struct {
+    Quad q;
+    int64_t body;
+    int64_t child;
+    double mass, comX, comY; /* BHA:103-109 */
+} Node;
+
+typedef struct {
+    Node *nodes;
+    int64_t n, cap;
+    Body *bodies;
+} Tree;
+
+static int64_t tree_alloc4(Tree *t, const Quad *parent) {
+    if (t->n + 4 > t->cap) {
+        int64_t nc = t->cap ? t->cap * 2 : 1024;
+        while (nc < t->n + 4) nc *= 2;
+        t->nodes = (Node *)realloc(t->nodes, (size_t)nc * sizeof(Node));
+        t->cap = nc;
+    }
+    int64_t first = t->n;
+    for (int i = 0; i < 4; ++i) { /* BHA:160-165 */
+        Node *c = &t->nodes[first + i];
+        c->q = quad_child(parent, i);
+        c->body = -1;
+        c->child = -1;
+        c->mass = 0.0; c->comX = 0.0; c->comY = 0.0;
+    }
+    t->n += 4;
+    return first;
+}
+
+static void tree_insert(Tree *t, int64_t node, int64_t bi);
+
+/* BHA:145-156 — deterministic jitter below h < 1e-3, then child by ix + iy. */
+static void insert_into_child(Tree *t, int64_t node, int64_t bi) {
+    Body *b = &t->bodies[bi];
+    Quad q = t->nodes[node].q;
+    if (q.h < 1e-3) {
+        const double eps = 1e-3;
+        uint64_t bx, by;
+        memcpy(&bx, &b->x, 8);
+        b->x += ((bx & 1ULL) == 0ULL) ? +eps : -eps;
+        memcpy(&by, &b->y, 8);
+        b->y += ((by & 1ULL) == 0ULL) ? -eps : +eps;
+    }
+    int ix = (b->x < q.cx) ? 0 : 1;
+    int iy = (b->y < q.cy) ? 0 : 2;
+    tree_insert(t, t->nodes[node].child + ix + iy, bi);
+}
+
+/* BHA:125-137 */
+static void tree_insert(Tree *t, int64_t node, int64_t bi) {
+    if (!quad_contains(&t->nodes[node].q, &t->bodies[bi])) return; /* BHA:126 dropped */
+    if (t->nodes[node].body < 0 && t->nodes[node].child < 0) {      /* BHA:127-129 */
+        t->nodes[node].body = bi;
+        return;
+    }
+    if (t->nodes[node].child < 0) { /* BHA:131 subdivide (BHA:159-166) */
+        Quad q = t->nodes[node].q;
+        int64_t first = tree_alloc4(t, &q);
+        t->nodes[node].child = first;
+    }
+    int64_t existing = t->nodes[node].body; /* BHA:132-135 */
+    if (existing >= 0) {
+        t->nodes[node].body = -1;
+        insert_into_child(t, node, existing);
+    }
+    insert_into_child(t, node, bi); /* BHA:136 */
+}
+
+/* BHA:173-202 — post-order, children 0..3 in order, skipping mass <= 0. */
+static void compute_mass(Tree *t, int64_t node) {
+    Node *nd = &t->nodes[node];
+    if (nd->child < 0) {
+        if (nd->body >= 0) {
+            const Body *b = &t->bodies[nd->body];
+            nd->mass = b->m; nd->comX = b->x; nd->comY = b->y;
+        } else {
+            nd->mass = 0.0; nd->comX = nd->q.cx; nd->comY = nd->q.cy;
+        }
+        return;
+    }
+    double mSum = 0.0, cx = 0.0, cy = 0.0;
+    int64_t ch = nd->child;
+    for (int i = 0; i < 4; ++i) {
+        compute_mass(t, ch + i);
+        const Node *c = &t->nodes[ch + i];
+        if (c->mass > 0.0) {
+            mSum += c->mass;
+            cx += c->comX * c->mass;
+            cy += c->comY * c->mass;
+        }
+    }
+    nd = &t->nodes[node];
+    nd->mass = mSum;
+    if (mSum > 0.0) {
+        nd->comX = cx / mSum;
+        nd->comY = cy / mSum;
+    } else {
+        nd->comX = nd->q.cx;
+        nd->comY = nd->q.cy;
+    }
+}
+
+typedef struct {
+    double G, soft2, theta2;
+} ForceCtx;
+
+/* BHA:250-259 — ((G*b.m)*m)*invR2 ; fx += (f*dx)*invR. */
+static inline void point_force_acc(const ForceCtx *c, const Body *b, double px, double py, double m,
+                                   double *fx, double *fy) {
+    double dx = px - b->x;
+    double dy = py - b->y;
+    double r2 = dx * dx + dy * dy + c->soft2;
+    double invR = 1.0 / sqrt(r2);
+    double invR2 = 1.0 / r2;
+    double f = c->G * b->m * m * invR2;
+    *fx += f * dx * invR;
+    *fy += f * dy * invR;
+}
+
+/* BHA:215-239 — recursive DFS; `visits` counts calls that pass the mass == 0 test. */
+static void accumulate_force(const Tree *t, const ForceCtx *c, int64_t node, int64_t bi,
+                             double *fx, double *fy, int64_t *visits) {
+    const Node *nd = &t->nodes[node];
+    if (nd->mass == 0.0) return; /* BHA:216 */
+    ++*visits;
+    const Body *b = &t->bodies[bi];
+    if (nd->child < 0) { /* BHA:217-222 */
+        if (nd->body < 0 || nd->body == bi) return;
+        point_force_acc(c, b, nd->comX, nd->comY, nd->mass, fx, fy);
+        return;
+    }
+    double dx = nd->comX - b->x; /* BHA:223-226 */
+    double dy = nd->comY - b->y;
+    double dist2 = dx * dx + dy * dy + c->soft2;
+    double hh = nd->q.h * 2.0;
+    double s2 = hh * hh;
+    if (s2 < c->theta2 * dist2) { /* BHA:228-230 */
+        point_force_acc(c, b, nd->comX, nd->comY, nd->mass, fx, fy);
+    } else { /* BHA:233-237 */
+        int64_t ch = nd->child;
+        accumulate_force(t, c, ch + 0, bi, fx, fy, visits);
+        accumulate_force(t, c, ch + 1, bi, fx, fy, visits);
+        accumulate_force(t, c, ch + 2, bi, fx, fy, visits);
+        accumulate_force(t, c, ch + 3, bi, fx, fy, visits);
+    }
+}
+
+/* ---- PhysicsEngine (BHA:287-532) ------------------------------------------- */
+struct oracle_engine {
+    oracle_params p;
+    Body *bodies;
+    int64_t n, cap;
+    double *ax, *ay; /* BHA:298-301 */
+    int64_t acc_cap;
+    int64_t *visits; /* per-body visit counts of the last evaluation */
+    Tree tree;       /* last built tree (BHA:304 lastTree) */
+    int tree_valid;
+    int threads;
+};
+
+/* BHA:359-366 — root Quad(W/2, H/2, max(W,H)/2 + 2); insert in list order. */
+static void build_tree(oracle_engine *e) {
+    Tree *t = &e->tree;
+    t->n = 0;
+    t->bodies = e->bodies;
+    if (t->cap < 1) {
+        t->cap = 1024;
+        t->nodes = (Node *)realloc(t->nodes, (size_t)t->cap * sizeof(Node));
+    }
+    int W = e->p.width_px, H = e->p.height_px;
+    double half = (double)(W > H ? W : H) / 2.0 + 2.0;
+    Node *root = &t->nodes[0];
+    root->q.cx = (double)W / 2.0;
+    root->q.cy = (double)H / 2.0;
+    root->q.h = half;
+    root->body = -1; root->child = -1;
+    root->mass = 0.0; root->comX = 0.0; root->comY = 0.0;
+    t->n = 1;
+    for (int64_t i = 0; i < e->n; ++i) tree_insert(t, 0, i);
+    compute_mass(t, 0);
+    e->tree_valid = 1;
+}
+
+typedef struct {
+    oracle_engine *e;
+    const int64_t *subset; /* NULL: all bodies */
+    int64_t count;
+    atomic_long next;
+    ForceCtx ctx;
+} AccJob;
+
+static void *acc_worker(void *arg) {
+    AccJob *j = (AccJob *)arg;
+    oracle_engine *e = j->e;
+    for (;;) { /* BHA:384-392 — one body per grab */
+        long k = atomic_fetch_add(&j->next, 1);
+        if (k >= j->count) break;
+        int64_t i = j->subset ? j->subset[k] : k;
+        double fx = 0.0, fy = 0.0;
+        int64_t v = 0;
+        accumulate_force(&e->tree, &j->ctx, 0, i, &fx, &fy, &v);
+        const Body *b = &e->bodies[i];
+        e->ax[i] = fx / b->m;
+        e->ay[i] = fy / b->m;
+        e->visits[i] = v;
+    }
+    return NULL;
+}
+
+/* BHA:374-395 — workers = min(cores, max(n,1)); theta2 from the live theta. */
+static void compute_accelerations(oracle_engine *e, const int64_t *subset, int64_t count) {
+    AccJob j;
+    j.e = e;
+    j.subset = subset;
+    j.count = count;
+    atomic_init(&j.next, 0);
+    j.ctx.G = e->p.G;
+    j.ctx.soft2 = e->p.soft2;
+    j.ctx.theta2 = e->p.theta * e->p.theta;
+    int64_t nw = e->threads;
+    if (nw > (count > 1 ? count : 1)) nw = count > 1 ? count : 1;
+    if (nw <= 1) {
+        acc_worker(&j);
+        return;
+    }
+    pthread_t *th = (pthread_t *)malloc(sizeof(pthread_t) * (size_t)nw);
+    for (int64_t w = 0; w < nw; ++w) pthread_create(&th[w], NULL, acc_worker, &j);
+    for (int64_t w = 0; w < nw; ++w) pthread_join(th[w], NULL);
+    free(th);
+}
+
+static void ensure_acc(oracle_engine *e) {
+    if (e->acc_cap < e->n) {
+        e->acc_cap = e->n;
+        e->ax = (double *)realloc(e->ax, sizeof(double) * (size_t)(e->n ? e->n : 1));
+        e->ay = (double *)realloc(e->ay, sizeof(double) * (size_t)(e->n ? e->n : 1));
+        e->visits = (int64_t *)realloc(e->visits, sizeof(int64_t) * (size_t)(e->n ? e->n : 1));
+    }
+}
+
+/* BHA:463-532 — merge rule.  The reference scans [0,n) in parallel chunks and
+ * concatenates victims in chunk order, then sorts them descending: the victim list is
+ * therefore exactly {j != i : d2 < minD2} in descending order, which a serial scan
+ * reproduces.  Mass is added in descending j, then i = indexOf(bi), then i++.        */
+static void merge_close_bodies(oracle_engine *e) {
+    double minDist = e->p.merge_min_dist;
+    if (minDist <= 0.0 || e->n <= 1) return;
+    double minD2 = minDist * minDist;
+    int64_t *victims = NULL;
+    int64_t vcap = 0;
+    int64_t i = 0;
+    while (i < e->n) {
+        if (e->bodies[i].m > e->p.merge_max_mass) {
+            int64_t n = e->n;
+            if (n > 1) {
+                int64_t nv = 0;
+                double bix = e->bodies[i].x, biy = e->bodies[i].y;
+                for (int64_t j = 0; j < n; ++j) {
+                    if (j == i) continue;
+                    double dx = e->bodies[j].x - bix;
+                    double dy = e->bodies[j].y - biy;
+                    if (dx * dx + dy * dy < minD2) {
+                        if (nv == vcap) {
+                            vcap = vcap ? vcap * 2 : 64;
+                            victims = (int64_t *)realloc(victims, sizeof(int64_t) * (size_t)vcap);
+                        }
+                        victims[nv++] = j;
+                    }
+                }
+                if (nv > 0) {
+                    /* victims ascending by construction; remove in descending order */
+                    int64_t bi_idx = i;
+                    for (int64_t v = nv - 1; v >= 0; --v) {
+                        int64_t j = victims[v];
+                        /* BHA:518 bi.m += bj.m; BHA:519 removeAt(j) */
+                        e->bodies[bi_idx].m += e->bodies[j].m;
+                        memmove(&e->bodies[j], &e->bodies[j + 1], sizeof(Body) * (size_t)(e->n - j - 1));
+                        e->n -= 1;
+                        if (j < bi_idx) bi_idx -= 1; /* indexOf(bi) */
+                    }
+                    i = bi_idx; /* BHA:522-523 */
+                    e->tree_valid = 0; /* BHA:526 lastTree = null */
+                }
+            }
+        }
+        ++i;
+    }
+    free(victims);
+}
+
+/* ---- exported API --------------------------------------------------------- */
+
+oracle_engine *oracle_create(const oracle_params *p, int64_t n, const double *x, const double *y,
+                             const double *vx, const double *vy, const double *m) {
+    oracle_engine *e = (oracle_engine *)calloc(1, sizeof(oracle_engine));
+    e->p = *p;
+    e->threads = p->threads > 0 ? p->threads : (int)sysconf(_SC_NPROCESSORS_ONLN);
+    if (e->threads < 1) e->threads = 1;
+    oracle_reset_bodies(e, n, x, y, vx, vy, m);
+    return e;
+}
+
+void oracle_set_params(oracle_engine *e, const oracle_params *p) {
+    e->p = *p;
+    e->threads = p->threads > 0 ? p->threads : (int)sysconf(_SC_NPROCESSORS_ONLN);
+    if (e->threads < 1) e->threads = 1;
+}
+
+/* BHA:342-349 */
+void oracle_reset_bodies(oracle_engine *e, int64_t n, const double *x, const double *y,
+                         const double *vx, const double *vy, const double *m) {
+    if (n > e->cap) {
+        e->bodies = (Body *)realloc(e->bodies, sizeof(Body) * (size_t)n);
+        e->cap = n;
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        e->bodies[i].x = x[i]; e->bodies[i].y = y[i];
+        e->bodies[i].vx = vx[i]; e->bodies[i].vy = vy[i];
+        e->bodies[i].m = m[i];
+    }
+    e->n = n;
+    ensure_acc(e);
+    e->tree_valid = 0;
+}
+
+int64_t oracle_num_bodies(const oracle_engine *e) { return e->n; }
+
+void oracle_get_bodies(const oracle_engine *e, double *x, double *y, double *vx, double *vy, double *m) {
+    for (int64_t i = 0; i < e->n; ++i) {
+        x[i] = e->bodies[i].x; y[i] = e->bodies[i].y;
+        vx[i] = e->bodies[i].vx; vy[i] = e->bodies[i].vy;
+        m[i] = e->bodies[i].m;
+    }
+}
+
+/* BHA:405-439 — one step = build, a(t), kick, drift, build, a(t+dt), kick, merge. */
+int oracle_step(oracle_engine *e, int k) {
+    for (int s = 0; s < k; ++s) {
+        int64_t n = e->n;
+        ensure_acc(e);
+        build_tree(e);
+        compute_accelerations(e, NULL, n);
+        double dtHalf = e->p.dt * 0.5; /* BHA:412 */
+        for (int64_t i = 0; i < n; ++i) {
+            e->bodies[i].vx += e->ax[i] * dtHalf;
+            e->bodies[i].vy += e->ay[i] * dtHalf;
+        }
+        for (int64_t i = 0; i < n; ++i) { /* BHA:419-422 */
+            e->bodies[i].x += e->bodies[i].vx * e->p.dt;
+            e->bodies[i].y += e->bodies[i].vy * e->p.dt;
+        }
+        build_tree(e);
+        compute_accelerations(e, NULL, n);
+        for (int64_t i = 0; i < n; ++i) {
+            e->bodies[i].vx += e->ax[i] * dtHalf;
+            e->bodies[i].vy += e->ay[i] * dtHalf;
+        }
+        merge_close_bodies(e); /* BHA:438 */
+    }
+    return 0;
+}
+
+/* buildTree + computeAccelerations on the current state (mutates positions through
+ * the jitter exactly like the reference's build).  subset == NULL: every body.   */
+int oracle_accel(oracle_engine *e, int64_t count, const int64_t *subset, double *ax, double *ay,
+                 int64_t *visits) {
+    ensure_acc(e);
+    build_tree(e);
+    if (!subset) count = e->n;
+    compute_accelerations(e, subset, count);
+    for (int64_t k = 0; k < count; ++k) {
+        int64_t i = subset ? subset[k] : k;
+        if (ax) ax[k] = e->ax[i];
+        if (ay) ay[k] = e->ay[i];
+        if (visits) visits[k] = e->visits[i];
+    }
+    return 0;
+}
+
+/* BHA:265-274 visitQuads on getTreeForDebug() (BHA:329-332). */
+static void visit_quads(const Tree *t, int64_t node, double *cx, double *cy, double *h, int64_t cap,
+                        int64_t *k) {
+    const Node *nd = &t->nodes[node];
+    if (*k < cap) {
+        cx[*k] = nd->q.cx; cy[*k] = nd->q.cy; h[*k] = nd->q.h;
+    }
+    ++*k;
+    if (nd->child >= 0)
+        for (int i = 0; i < 4; ++i) visit_quads(t, nd->child + i, cx, cy, h, cap, k);
+}
+
+int64_t oracle_quads(oracle_engine *e, double *cx, double *cy, double *h, int64_t cap) {
+    if (!e->tree_valid) build_tree(e);
+    int64_t k = 0;
+    visit_quads(&e->tree, 0, cx, cy, h, cap, &k);
+    return k;
+}
+
+/* Tree statistics for the roofline byte model. */
+void oracle_tree_stats(oracle_engine *e, int64_t *n_nodes, int64_t *n_nonempty) {
+    if (!e->tree_valid) build_tree(e);
+    int64_t ne = 0;
+    for (int64_t i = 0; i < e->tree.n; ++i) ne += e->tree.nodes[i].mass != 0.0;
+    *n_nodes = e->tree.n;
+    *n_nonempty = ne;
+}
+
+void oracle_destroy(oracle_engine *e) {
+    if (!e) return;
+    free(e->bodies);
+    free(e->ax); free(e->ay); free(e->visits);
+    free(e->tree.nodes);
+    free(e);
+}

@@ -1,0 +1,236 @@
+"""GPU parity: the HIP engine (through the C-ABI) vs the CPU oracle on identical inputs.
+
+The bar is bit-identity of every fp64 word (positions, velocities, masses, accelerations,
+per-body node-visit counts): the reference is strict IEEE binary64 (JVM >= 17) and the engine
+reproduces its tree, criterion, summation order and expression order exactly.  The
+north-star tolerance (<= 1e-6 relative position drift after 100 steps) is therefore met with
+margin 0; where NaN can arise (zero-mass bodies), NaN payloads are compared as "both NaN".
+"""
+import numpy as np
+import pytest
+
+import bh_amd
+import oracle
+from bh_amd import scenes
+from conftest import bits_equal
+
+pytestmark = pytest.mark.gpu
+
+FIELDS = ("x", "y", "vx", "vy", "m")
+
+
+def _pair(arrs, **kw):
+    theta = kw.pop("theta", 0.5)
+    p = bh_amd.default_params(theta=theta, **kw)
+    eng = bh_amd.Engine(p, device=0)
+    eng.reset_bodies(*arrs)
+    ref = oracle.Oracle(*arrs, theta=theta, **kw)
+    return eng, ref
+
+
+def _assert_state_equal(eng, ref, nan_ok=False):
+    got, want = eng.get_bodies(), ref.get_bodies()
+    assert len(got[0]) == len(want[0]), f"N: engine {len(got[0])} vs oracle {len(want[0])}"
+    for k, name in enumerate(FIELDS):
+        if nan_ok:
+            assert np.array_equal(got[k], want[k], equal_nan=True), name
+        else:
+            bad = np.flatnonzero(got[k].view(np.int64) != want[k].view(np.int64))
+            assert bad.size == 0, f"{name}: {bad.size} words differ, first at {bad[:5]}"
+
+
+def _assert_acc_equal(eng, ref, nan_ok=False):
+    ax, ay, vis = eng.compute_accelerations(visits=True)
+    rax, ray, rvis = ref.accelerations(visits=True)
+    if nan_ok:
+        assert np.array_equal(ax, rax, equal_nan=True)
+        assert np.array_equal(ay, ray, equal_nan=True)
+    else:
+        assert bits_equal(ax, rax), f"ax differs at {np.flatnonzero(ax.view(np.int64) != rax.view(np.int64))[:5]}"
+        assert bits_equal(ay, ray)
+    assert np.array_equal(vis, rvis), "node-visit counts differ"
+    _assert_state_equal(eng, ref, nan_ok=nan_ok)  # the jitter's mutation must match too
+    return vis
+
+
+def test_two_body_known_answer():
+    # a1 = G m2 d / (|d|^2 + eps^2)^{3/2}: d = (3, 4), |d|^2 + 1 = 26
+    arrs = (np.array([100.0, 103.0]), np.array([100.0, 104.0]), np.zeros(2), np.zeros(2),
+            np.array([1.0, 2.0]))
+    eng, ref = _pair(arrs, merge_min_dist=0.0)
+    ax, ay = eng.compute_accelerations()
+    rax, ray = ref.accelerations()
+    assert bits_equal(ax, rax) and bits_equal(ay, ray)
+    k = 80.0 / 26.0 ** 1.5
+    np.testing.assert_allclose(ax, [k * 2 * 3, -k * 1 * 3], rtol=1e-14)
+    np.testing.assert_allclose(ay, [k * 2 * 4, -k * 1 * 4], rtol=1e-14)
+
+
+@pytest.mark.parametrize("theta", [0.0, 0.2, 0.3, 0.5, 1.0, 1.6])
+def test_theta_sweep_accelerations(theta):
+    arrs = scenes.two_disks(2500, 700)
+    eng, ref = _pair(arrs, theta=theta)
+    _assert_acc_equal(eng, ref)
+
+
+def test_c1_baseline_100_steps():
+    """BASELINE 'R' scene, 2 x 1000 bodies, theta 0.5: 100 full steps, bit-identical."""
+    arrs = scenes.config_scene("c1_baseline")
+    eng, ref = _pair(arrs, theta=0.5)
+    eng.step(100)
+    ref.step(100)
+    _assert_state_equal(eng, ref)
+
+
+def test_c1_code_default_scene():
+    """The code's defaultBodies() (12 500 bodies) at the code's theta 0.30, 10 steps."""
+    arrs = scenes.config_scene("c1_code")
+    eng, ref = _pair(arrs, theta=0.30)
+    eng.step(10)
+    ref.step(10)
+    _assert_state_equal(eng, ref)
+
+
+def test_jitter_coincident_and_near_bodies():
+    """Exact duplicates and pairs closer than 1e-3 force the h < 1e-3 jitter (BHA:146-151),
+    which mutates positions and drops bodies from the tree; replayed in index order."""
+    rng = np.random.default_rng(7)
+    base = scenes.uniform(3000, 1.0, seed=11)
+    x, y, vx, vy, m = (a.copy() for a in base)
+    # 40 exact duplicates of existing bodies, 40 near pairs (2e-4 apart), a 6-fold stack
+    dup = rng.choice(3000, 40, replace=False)
+    near = rng.choice(3000, 40, replace=False)
+    ex = np.concatenate([x[dup], x[near] + 2e-4, np.full(6, 1234.5678)])
+    ey = np.concatenate([y[dup], y[near] - 1.5e-4, np.full(6, 321.0123)])
+    n_extra = len(ex)
+    x = np.concatenate([x, ex])
+    y = np.concatenate([y, ey])
+    vx = np.concatenate([vx, np.zeros(n_extra)])
+    vy = np.concatenate([vy, np.zeros(n_extra)])
+    m = np.concatenate([m, np.full(n_extra, 1.0)])
+    perm = rng.permutation(len(x))  # interleave so insertion order matters
+    arrs = tuple(a[perm] for a in (x, y, vx, vy, m))
+    eng, ref = _pair(arrs, theta=0.5, merge_min_dist=0.0)
+    _assert_acc_equal(eng, ref)
+    eng.step(3)
+    ref.step(3)
+    _assert_state_equal(eng, ref)
+
+
+def test_bodies_outside_root_cell():
+    """Bodies outside [cx-h, cx+h) are never inserted (BHA:126) but still feel and integrate."""
+    arrs = scenes.uniform(500, 1.0, seed=5)
+    x = np.concatenate([arrs[0], [-3.0, 2402.0, 1200.0 + 1202.0, 1200.0 - 1202.0, 600.0]])
+    y = np.concatenate([arrs[1], [400.0, 400.0, 100.0, 100.0, -802.0 - 1e-9]])
+    k = 5
+    arrs = (x, y, np.concatenate([arrs[2], np.zeros(k)]), np.concatenate([arrs[3], np.zeros(k)]),
+            np.concatenate([arrs[4], np.full(k, 3.0)]))
+    eng, ref = _pair(arrs, theta=0.5)
+    _assert_acc_equal(eng, ref)
+    eng.step(5)
+    ref.step(5)
+    _assert_state_equal(eng, ref)
+
+
+def test_merge_rule():
+    """Heavy bodies (m > 4000) absorb bodies with d^2 < 64 (BHA:463-532): 7.9 eaten, 8.1 not;
+    a heavy absorbed by a later heavy carries its grown mass; N shrinks."""
+    bx = [1000.0, 1007.9, 1008.1, 1000.0, 1003.0, 1500.0, 1504.0, 1200.0, 1200.5]
+    by = [400.0, 400.0, 400.0, 406.0, 403.0, 300.0, 300.0, 200.0, 200.0]
+    bm = [5000.0, 1.0, 1.0, 2.0, 4500.0, 10.0, 9000.0, 3.0, 4001.0]
+    field = scenes.uniform(300, 0.5, seed=9)
+    arrs = (np.concatenate([bx, field[0]]), np.concatenate([by, field[1]]),
+            np.concatenate([np.zeros(9), field[2]]), np.concatenate([np.zeros(9), field[3]]),
+            np.concatenate([bm, field[4]]))
+    eng, ref = _pair(arrs, theta=0.5, dt=0.0)  # dt = 0: positions fixed, pure merge
+    eng.step(1)
+    ref.step(1)
+    _assert_state_equal(eng, ref)
+    assert eng.num_bodies() < len(arrs[0])
+    eng2, ref2 = _pair(arrs, theta=0.5)
+    eng2.step(20)
+    ref2.step(20)
+    _assert_state_equal(eng2, ref2)
+
+
+@pytest.mark.parametrize("n", [0, 1, 2])
+def test_tiny_and_empty(n):
+    arrs = tuple(a[:n] for a in scenes.uniform(4, 2.0, seed=1))
+    eng, ref = _pair(arrs)
+    eng.step(3)
+    ref.step(3)
+    _assert_state_equal(eng, ref)
+
+
+def test_zero_and_negative_mass():
+    arrs = [a.copy() for a in scenes.uniform(400, 1.0, seed=3)]
+    arrs[4][[5, 17]] = 0.0     # a = 0/0 for these (NaN), skipped as nodes
+    arrs[4][[9]] = -2.0        # visited as a leaf, excluded from parents' COM (BHA:189-192)
+    eng, ref = _pair(tuple(arrs), merge_min_dist=0.0)
+    _assert_acc_equal(eng, ref, nan_ok=True)
+
+
+def test_other_screen_geometry():
+    """Config.WIDTH_PX/HEIGHT_PX = a 1920x1080 screen (Main.kt:11-12): root h = 962, so the
+    jitter depth is 20 instead of 21."""
+    arrs = scenes.two_disks(1500, 400)
+    eng, ref = _pair(arrs, theta=0.5, width_px=1920, height_px=1080)
+    _assert_acc_equal(eng, ref)
+    eng.step(5)
+    ref.step(5)
+    _assert_state_equal(eng, ref)
+
+
+def test_live_config_changes_between_steps():
+    """theta / DT / G are read live at every step (PNL:247-260)."""
+    arrs = scenes.two_disks(1500, 400)
+    eng, ref = _pair(arrs, theta=0.5)
+    for theta, dt, G in ((0.5, 0.005, 80.0), (0.9, 0.01, 60.0), (0.3, -0.005, 80.0)):
+        eng.set_params(bh_amd.default_params(theta=theta, dt=dt, G=G))
+        ref.set_params(oracle.params(theta=theta, dt=dt, G=G))
+        eng.step(2)
+        ref.step(2)
+    _assert_state_equal(eng, ref)
+
+
+def test_quads_match_visit_quads():
+    arrs = scenes.two_disks(800, 200)
+    eng, ref = _pair(arrs, theta=0.5, merge_min_dist=0.0)
+    eng.step(1)
+    ref.step(1)
+    got = eng.get_quads()
+    want = ref.quads()
+    for g, w in zip(got, want):
+        assert bits_equal(g, w)
+
+
+def test_deterministic_rerun():
+    arrs = scenes.config_scene("c1_code")
+    a = bh_amd.Engine(bh_amd.default_params(theta=0.5))
+    a.reset_bodies(*arrs)
+    a.step(3)
+    b = bh_amd.Engine(bh_amd.default_params(theta=0.5))
+    b.reset_bodies(*arrs)
+    b.step(3)
+    for u, v in zip(a.get_bodies(), b.get_bodies()):
+        assert bits_equal(u, v)
+
+
+def test_c2_kepler_1e5_steps():
+    arrs = scenes.config_scene("c2")
+    eng, ref = _pair(arrs, theta=0.5)
+    eng.step(3)
+    ref.step(3)
+    _assert_state_equal(eng, ref)
+
+
+def test_c3_1e6_full_size_sampled():
+    """The bench workload (two colliding disks, N = 1e6, theta 0.5): one evaluation, every
+    body's acceleration and visit count against the oracle; then one full step."""
+    arrs = scenes.config_scene("c3")
+    eng, ref = _pair(arrs, theta=0.5)
+    vis = _assert_acc_equal(eng, ref)
+    assert vis.mean() > 10
+    eng.step(1)
+    ref.step(1)
+    _assert_state_equal(eng, ref)
