@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = (
     "bh_last_error", "bh_set_params", "bh_get_params", "bh_reset_bodies", "bh_step",
     "bh_num_bodies", "bh_get_bodies", "bh_compute_accelerations", "bh_get_quads",
     "bh_last_timings", "bh_last_tree_nodes", "bh_traverse_kernel_ms", "bh_set_profiling",
-    "bh_synchronize", "bh_scene_galaxy_disk", "bh_scene_kepler_disk", "bh_scene_uniform",
+    "bh_synchronize", "bh_shard_range", "bh_scene_galaxy_disk", "bh_scene_kepler_disk", "bh_scene_uniform",
 )
 
 
@@ -100,6 +100,7 @@ def load_library(path: str | None = None):
     lib.bh_traverse_kernel_ms.argtypes = [_VP, _D, _I64P]
     lib.bh_set_profiling.argtypes = [_VP, ctypes.c_int]
     lib.bh_synchronize.argtypes = [_VP]
+    lib.bh_shard_range.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, _I64P, _I64P]
     lib.bh_scene_galaxy_disk.argtypes = (
         [ctypes.c_int32] + [ctypes.c_double] * 6 + [ctypes.c_int32, ctypes.c_int64]
         + [ctypes.c_double] * 9 + [_D] * 5)
@@ -123,6 +124,17 @@ def default_params(**over) -> BhParams:
     for k, v in over.items():
         setattr(p, k, v)
     return p
+
+
+def shard_range(n: int, rank: int, world: int):
+    """Morton-order range [lo, hi) of bodies whose forces `rank` evaluates (bh_shard_range)."""
+    lo = ctypes.c_int64(0)
+    hi = ctypes.c_int64(0)
+    rc = load_library().bh_shard_range(int(n), int(rank), int(world), ctypes.byref(lo),
+                                       ctypes.byref(hi))
+    if rc != BH_OK:
+        raise BhError(rc, "bh_shard_range: invalid arguments")
+    return lo.value, hi.value
 
 
 def comm_unique_id() -> bytes:

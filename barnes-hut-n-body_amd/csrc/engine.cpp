@@ -304,8 +304,8 @@ int evaluate(bh_engine *e, uint32_t *visits) {
         TRY(mark(e, 1));
     } else {
         int64_t chunk = (n + e->world - 1) / e->world;
-        int64_t lo = std::min<int64_t>(n, e->rank * chunk);
-        int64_t hi = std::min<int64_t>(n, lo + chunk);
+        int64_t lo = 0, hi = 0;
+        bh_shard_range(n, e->rank, e->world, &lo, &hi);
         traverse(e->nodes, d_T, e->sx, e->sy, e->sm, e->perm, lo, hi, e->geo, fp, e->ax, e->ay,
                  e->a_sorted, nullptr, e->stream);
         HIPCHK(e, hipGetLastError());
@@ -807,6 +807,14 @@ int bh_traverse_kernel_ms(const bh_engine *e, double *avg_ms, int64_t *launches)
 int bh_set_profiling(bh_engine *e, int enabled) {
     if (!e) return BH_E_INVALID;
     e->profiling = enabled != 0;
+    return BH_OK;
+}
+
+int bh_shard_range(int64_t n, int rank, int world, int64_t *lo, int64_t *hi) {
+    if (n < 0 || world < 1 || rank < 0 || rank >= world || !lo || !hi) return BH_E_INVALID;
+    const int64_t chunk = (n + world - 1) / world;
+    *lo = std::min<int64_t>(n, (int64_t)rank * chunk);
+    *hi = std::min<int64_t>(n, *lo + chunk);
     return BH_OK;
 }
 

@@ -114,6 +114,11 @@ int bh_traverse_kernel_ms(const bh_engine *e, double *avg_ms, int64_t *launches)
 /* Enable/disable per-phase event timing (default off: no events in the hot loop). */
 int bh_set_profiling(bh_engine *e, int enabled);
 
+/* Morton-order body range [lo, hi) whose forces rank `rank` of `world` evaluates for n
+ * bodies (equal-count contiguous chunks of ceil(n / world); the all-gather exchanges
+ * 2 * ceil(n / world) doubles per rank).  Host-only; used by the engine itself. */
+int bh_shard_range(int64_t n, int rank, int world, int64_t *lo, int64_t *hi);
+
 /* Block until all device work of this engine is complete. */
 int bh_synchronize(bh_engine *e);
 
