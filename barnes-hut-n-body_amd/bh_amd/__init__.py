@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = (
     "bh_last_error", "bh_set_params", "bh_get_params", "bh_reset_bodies", "bh_step",
     "bh_num_bodies", "bh_get_bodies", "bh_compute_accelerations", "bh_get_quads",
     "bh_last_timings", "bh_last_tree_nodes", "bh_traverse_kernel_ms", "bh_set_profiling",
-    "bh_synchronize", "bh_shard_range", "bh_scene_galaxy_disk", "bh_scene_kepler_disk", "bh_scene_uniform",
+    "bh_synchronize", "bh_shard_range", "bh_traversal_stats", "bh_scene_galaxy_disk", "bh_scene_kepler_disk", "bh_scene_uniform",
 )
 
 
@@ -100,6 +100,7 @@ def load_library(path: str | None = None):
     lib.bh_traverse_kernel_ms.argtypes = [_VP, _D, _I64P]
     lib.bh_set_profiling.argtypes = [_VP, ctypes.c_int]
     lib.bh_synchronize.argtypes = [_VP]
+    lib.bh_traversal_stats.argtypes = [_VP, _I64P, _I64P, _I64P]
     lib.bh_shard_range.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, _I64P, _I64P]
     lib.bh_scene_galaxy_disk.argtypes = (
         [ctypes.c_int32] + [ctypes.c_double] * 6 + [ctypes.c_int32, ctypes.c_int64]
@@ -233,6 +234,14 @@ class Engine:
         cnt = ctypes.c_int64(0)
         self._check(self._lib.bh_traverse_kernel_ms(self._h, ctypes.byref(avg), ctypes.byref(cnt)))
         return avg.value, cnt.value
+
+    def traversal_stats(self):
+        """(lane visits, wave iterations, waves) of the last compute_accelerations(visits=True);
+        lane efficiency = lane_visits / (64 * wave_iters)."""
+        a, b, c = ctypes.c_int64(0), ctypes.c_int64(0), ctypes.c_int64(0)
+        self._check(self._lib.bh_traversal_stats(self._h, ctypes.byref(a), ctypes.byref(b),
+                                                 ctypes.byref(c)))
+        return a.value, b.value, c.value
 
     def last_tree_nodes(self) -> int:
         return int(self._lib.bh_last_tree_nodes(self._h))

@@ -77,7 +77,7 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
 void traverse(const Node *nodes, const uint32_t *d_T, const double *sx, const double *sy,
               const double *sm, const uint32_t *perm, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *ax, double *ay, double *a_sorted, uint32_t *visits,
-              hipStream_t s);
+              uint32_t *wave_iters, hipStream_t s);
 void scatter_sorted_acc(const double *a_sorted, const uint32_t *perm, int64_t n, double *ax,
                         double *ay, hipStream_t s);
 

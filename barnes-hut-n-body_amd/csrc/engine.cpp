@@ -65,6 +65,8 @@ struct bh_engine {
     size_t node_cap = 0;
     uint32_t *scalars = nullptr;  // [0] unused, [1] error flags, [2] heavy count, [3] pair count
     uint32_t *visits32 = nullptr;
+    uint32_t *wave_iters = nullptr;  // per-wave union of visited nodes (diagnostics)
+    int64_t stat_lane_visits = 0, stat_wave_iters = 0, stat_waves = 0;
 
     // merge
     uint32_t *heavy = nullptr;
@@ -203,6 +205,7 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(dev_alloc(e, e->cnt, cap + 1));
         TRY(dev_alloc(e, e->base, cap + 1));
         TRY(dev_alloc(e, e->visits32, cap));
+        TRY(dev_alloc(e, e->wave_iters, cap / 64 + 2));
         TRY(dev_alloc(e, e->heavy, cap));
         TRY(dev_alloc(e, e->keep, cap));
         TRY(dev_alloc(e, e->pos, cap));
@@ -299,7 +302,7 @@ int evaluate(bh_engine *e, uint32_t *visits) {
     const uint32_t *d_T = e->base + n;
     if (e->world == 1 || visits) {
         traverse(e->nodes, d_T, e->sx, e->sy, e->sm, e->perm, 0, n, e->geo, fp, e->ax, e->ay,
-                 nullptr, visits, e->stream);
+                 nullptr, visits, e->wave_iters, e->stream);
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
     } else {
@@ -307,7 +310,7 @@ int evaluate(bh_engine *e, uint32_t *visits) {
         int64_t lo = 0, hi = 0;
         bh_shard_range(n, e->rank, e->world, &lo, &hi);
         traverse(e->nodes, d_T, e->sx, e->sy, e->sm, e->perm, lo, hi, e->geo, fp, e->ax, e->ay,
-                 e->a_sorted, nullptr, e->stream);
+                 e->a_sorted, nullptr, nullptr, e->stream);
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
         NCCLCHK(e, ncclAllGather(e->a_sorted + 2 * e->rank * chunk, e->a_sorted, (size_t)(2 * chunk),
@@ -640,7 +643,7 @@ void bh_destroy(bh_engine *e) {
     void *ptrs[] = {e->x, e->y, e->vx, e->vy, e->m, e->alt[0], e->alt[1], e->alt[2], e->alt[3],
                     e->alt[4], e->ax, e->ay, e->a_sorted, e->keys, e->keys_s, e->idx, e->perm,
                     e->sx, e->sy, e->sm, e->cpl, e->cnt, e->base, e->nodes, e->scalars,
-                    e->visits32, e->heavy, e->keep, e->pos, e->pairs, e->mdead, e->mupd,
+                    e->visits32, e->wave_iters, e->heavy, e->keep, e->pos, e->pairs, e->mdead, e->mupd,
                     e->mupd_mass, e->hmass, e->cub_tmp};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
@@ -746,7 +749,20 @@ int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visi
         if (visits) {
             std::vector<uint32_t> v((size_t)n);
             HIPCHK(e, hipMemcpy(v.data(), e->visits32, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
-            for (int64_t i = 0; i < n; ++i) visits[i] = v[(size_t)i];
+            int64_t lane_sum = 0;
+            for (int64_t i = 0; i < n; ++i) {
+                visits[i] = v[(size_t)i];
+                lane_sum += v[(size_t)i];
+            }
+            const int64_t waves = (n + 63) / 64;
+            std::vector<uint32_t> wi((size_t)waves);
+            HIPCHK(e, hipMemcpy(wi.data(), e->wave_iters, sizeof(uint32_t) * waves,
+                                hipMemcpyDeviceToHost));
+            int64_t wsum = 0;
+            for (uint32_t c : wi) wsum += c;
+            e->stat_lane_visits = lane_sum;
+            e->stat_wave_iters = wsum;
+            e->stat_waves = waves;
         }
     }
     if (e->profiling) TRY(collect_timings(e));
@@ -801,6 +817,15 @@ int bh_traverse_kernel_ms(const bh_engine *e, double *avg_ms, int64_t *launches)
     if (!e || !avg_ms) return BH_E_INVALID;
     *avg_ms = e->trav_launches ? e->trav_ms_sum / (double)e->trav_launches : 0.0;
     if (launches) *launches = e->trav_launches;
+    return BH_OK;
+}
+
+int bh_traversal_stats(const bh_engine *e, int64_t *lane_visits, int64_t *wave_iters,
+                       int64_t *waves) {
+    if (!e || !lane_visits || !wave_iters || !waves) return BH_E_INVALID;
+    *lane_visits = e->stat_lane_visits;
+    *wave_iters = e->stat_wave_iters;
+    *waves = e->stat_waves;
     return BH_OK;
 }
 

@@ -3,7 +3,7 @@
 //
 // One lane = one body, bodies in Morton order so a wavefront's 64 bodies are spatial
 // neighbours.  The wave walks ONE shared pre-order cursor over the flattened tree:
-//   * the node record is wave-uniform (scalar loads, one fetch serves 64 bodies);
+//   * the node record is wave-uniform (one 32-byte scalar load serves 64 bodies);
 //   * every lane evaluates the reference's own criterion s2 < theta2*dist2 (BHA:228) for
 //     itself; a lane that accepts a node adds its point force and ignores that node's
 //     subtree (resume = node.next); the cursor descends (cur + 1) iff at least one lane
@@ -11,12 +11,53 @@
 // Because the cursor order is the reference's DFS order and each lane only sums the nodes
 // its own recursive DFS would have summed, every body's force is the reference's sum in the
 // reference's order: bit-identical, not merely close (no Burtscher "open for all").
+//
+// The kernel is bound by fp64 VALU issue (the IEEE sqrt and two IEEE divisions per
+// interaction), not by HBM: the node stream is shared by 64 lanes and served from the
+// scalar cache / L2.  See DESIGN.md for the roofline accounting.
 #include "bh_device.hpp"
 
 namespace bh {
 namespace {
 
 constexpr int TB = 256;
+
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+// ---- exact fast paths for RN(sqrt(x)) and RN(1/x) ------------------------------------
+// These are the instruction sequences the compiler emits for IEEE sqrt(double) and
+// 1.0 / double on gfx950, with the operand-range scaling (v_cmp + v_ldexp / v_div_scale /
+// v_div_fmas scaling) and the special-value fix-ups (v_cmp_class / v_div_fixup) removed.
+// For a finite normal operand in [2^-600, 2^600] those removed steps are identities (no
+// scaling is triggered, no special value occurs), so the results are bit-identical to the
+// full sequences; callers take this path only when every lane's operand is in that range.
+__device__ __forceinline__ double sqrt_rn_inrange(double x) {
+    double y = __builtin_amdgcn_rsq(x);
+    double g = x * y;
+    double h = y * 0.5;
+    double r = __builtin_fma(-h, g, 0.5);
+    g = __builtin_fma(g, r, g);
+    h = __builtin_fma(h, r, h);
+    double d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    d = __builtin_fma(-g, g, x);
+    g = __builtin_fma(d, h, g);
+    return g;
+}
+
+__device__ __forceinline__ double rcp_rn_inrange(double b) {
+    double y = __builtin_amdgcn_rcp(b);
+    double e = __builtin_fma(-b, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    e = __builtin_fma(-b, y, 1.0);
+    y = __builtin_fma(y, e, y);
+    double r = __builtin_fma(-b, y, 1.0);  // q = 1.0 * y = y exactly
+    return __builtin_fma(r, y, y);
+}
+
+__device__ __forceinline__ bool in_fast_range(double x) {
+    return x >= 0x1p-600 && x <= 0x1p600;
+}
 
 template <bool SORTED_OUT, bool COUNT>
 __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
@@ -28,7 +69,8 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
                                                  int64_t hi, ForceParams fp, Geometry g,
                                                  double *__restrict__ ax, double *__restrict__ ay,
                                                  double *__restrict__ a_sorted,
-                                                 uint32_t *__restrict__ visits) {
+                                                 uint32_t *__restrict__ visits,
+                                                 uint32_t *__restrict__ wave_iters) {
     const int64_t p = lo + (int64_t)blockIdx.x * TB + threadIdx.x;
     const bool valid = p < hi;
     const double bx = valid ? sx[p] : 0.0;
@@ -38,24 +80,28 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     const double soft2 = fp.soft2, theta2 = fp.theta2;
     const uint32_t self = (uint32_t)p;
     double fx = 0.0, fy = 0.0;
-    uint32_t nvis = 0;
+    uint32_t nvis = 0, niters = 0;
     // lane is active for node `cur` iff cur >= resume; invalid lanes never are.
     uint32_t resume = valid ? 0u : 0xFFFFFFFFu;
     const uint32_t T = __builtin_amdgcn_readfirstlane(*d_T);
     uint32_t cur = 0;
     while (cur < T) {
-        const Node nd = nodes[cur];
-        const uint32_t meta = __builtin_amdgcn_readfirstlane(nd.meta);
-        uint32_t next = __builtin_amdgcn_readfirstlane(nd.next);
+        const double4_t raw = *reinterpret_cast<const double4_t *>(nodes + cur);
+        const uint64_t w = (uint64_t)__double_as_longlong(raw.w);
+        const uint32_t meta = __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
+        uint32_t next = __builtin_amdgcn_readfirstlane((uint32_t)w);
         next = next > cur ? next : cur + 1;  // structural guard: the cursor always advances
         if (meta & NODE_SKIP) {              // mass == 0.0 (BHA:216), uniform
             cur = next;
             continue;
         }
         const bool active = cur >= resume;
-        if (COUNT) nvis += active ? 1u : 0u;
-        const double dx = nd.comX - bx;  // BHA:223-225 == BHA:251-253
-        const double dy = nd.comY - by;
+        if (COUNT) {
+            nvis += active ? 1u : 0u;
+            niters += 1;
+        }
+        const double dx = raw.x - bx;  // BHA:223-225 == BHA:251-253
+        const double dy = raw.y - by;
         const double d2 = dx * dx + dy * dy + soft2;
         bool contrib, open;
         if (meta & NODE_LEAF) {  // BHA:217-221: skip self by identity
@@ -66,10 +112,17 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
             contrib = active && acc;
             open = active && !acc;
         }
+        const bool all_fast = __ballot(contrib && !in_fast_range(d2)) == 0ull;
         if (contrib) {  // BHA:250-259, expression order as written
-            const double invR = 1.0 / sqrt(d2);
-            const double invR2 = 1.0 / d2;
-            const double f = Gm * nd.mass * invR2;
+            double invR, invR2;
+            if (all_fast) {
+                invR = rcp_rn_inrange(sqrt_rn_inrange(d2));
+                invR2 = rcp_rn_inrange(d2);
+            } else {
+                invR = 1.0 / sqrt(d2);
+                invR2 = 1.0 / d2;
+            }
+            const double f = Gm * raw.z * invR2;
             fx += f * dx * invR;
             fy += f * dy * invR;
             resume = next;
@@ -77,6 +130,7 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
         const bool any_open = __ballot(open) != 0ull;  // wave-uniform
         cur = any_open ? cur + 1 : next;
     }
+    if (COUNT && (threadIdx.x & 63) == 0) wave_iters[(p - lo) >> 6] = niters;
     if (!valid) return;
     const double rax = fx / bm;  // BHA:390-391
     const double ray = fy / bm;
@@ -106,18 +160,18 @@ __global__ __launch_bounds__(TB) void k_scatter(const double *__restrict__ a_sor
 void traverse(const Node *nodes, const uint32_t *d_T, const double *sx, const double *sy,
               const double *sm, const uint32_t *perm, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *ax, double *ay, double *a_sorted, uint32_t *visits,
-              hipStream_t s) {
+              uint32_t *wave_iters, hipStream_t s) {
     if (hi <= lo) return;
     unsigned grid = (unsigned)((hi - lo + TB - 1) / TB);
     if (visits) {
         k_traverse<false, true><<<grid, TB, 0, s>>>(nodes, d_T, sx, sy, sm, perm, lo, hi, fp, g, ax,
-                                                    ay, a_sorted, visits);
+                                                    ay, a_sorted, visits, wave_iters);
     } else if (a_sorted) {
         k_traverse<true, false><<<grid, TB, 0, s>>>(nodes, d_T, sx, sy, sm, perm, lo, hi, fp, g, ax,
-                                                    ay, a_sorted, visits);
+                                                    ay, a_sorted, visits, wave_iters);
     } else {
         k_traverse<false, false><<<grid, TB, 0, s>>>(nodes, d_T, sx, sy, sm, perm, lo, hi, fp, g, ax,
-                                                     ay, a_sorted, visits);
+                                                     ay, a_sorted, visits, wave_iters);
     }
 }
 

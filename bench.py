@@ -93,6 +93,8 @@ def main():
     probe.reset_bodies(*arrs)
     _, _, vis = probe.compute_accelerations(visits=True)
     vbar = float(np.mean(vis)) if len(vis) else 0.0
+    lane_visits, wave_iters, waves = probe.traversal_stats()
+    lane_eff = lane_visits / (64.0 * wave_iters) if wave_iters else 0.0
     probe.close()
     del probe
 
@@ -142,6 +144,7 @@ def main():
         "kernel_avg_ms": round(trav_ms, 4),
         "launches": trav_launches,
         "vbar_nodes_per_body_eval": round(vbar, 2),
+        "wave_lane_efficiency": round(lane_eff, 4),
         "bytes_per_launch": round(bytes_per_launch),
     }
 

@@ -111,6 +111,12 @@ int64_t bh_last_tree_nodes(const bh_engine *e);
  * engine's own stream; *launches receives the count. */
 int bh_traverse_kernel_ms(const bh_engine *e, double *avg_ms, int64_t *launches);
 
+/* Lane efficiency of the last bh_compute_accelerations(..., visits != NULL): the sum over
+ * bodies of visited nodes, the sum over wavefronts of nodes the wave's shared cursor stopped
+ * at (union of its 64 bodies' traversals), and the number of wavefronts. */
+int bh_traversal_stats(const bh_engine *e, int64_t *lane_visits, int64_t *wave_iters,
+                       int64_t *waves);
+
 /* Enable/disable per-phase event timing (default off: no events in the hot loop). */
 int bh_set_profiling(bh_engine *e, int enabled);
 
