@@ -78,6 +78,7 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     const double bm = valid ? sm[p] : 1.0;
     const double Gm = fp.G * bm;  // (Config.G * b.m) is evaluated first (BHA:256)
     const double soft2 = fp.soft2, theta2 = fp.theta2;
+    const double s2root = g.s2[0];
     const uint32_t self = (uint32_t)p;
     double fx = 0.0, fy = 0.0;
     uint32_t nvis = 0, niters = 0;
@@ -108,7 +109,10 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
             contrib = active && ((meta & NODE_BODY_MASK) != self);
             open = false;
         } else {
-            const bool acc = g.s2[meta & NODE_DEPTH_MASK] < theta2 * d2;  // BHA:226-228
+            // s2 = (h_d * 2.0)^2 with h_d = h_0 / 2^d exactly, so s2 = s2_0 * 4^-d exactly
+            // (a power-of-two scaling commutes with rounding): one v_ldexp, no table load.
+            const double s2 = __builtin_ldexp(s2root, -2 * (int)(meta & NODE_DEPTH_MASK));
+            const bool acc = s2 < theta2 * d2;  // BHA:226-228
             contrib = active && acc;
             open = active && !acc;
         }
