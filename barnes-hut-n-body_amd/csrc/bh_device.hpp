@@ -29,6 +29,14 @@ constexpr uint32_t NODE_SKIP = 1u << 30;        // mass == 0.0: never visited (B
 constexpr uint32_t NODE_BODY_MASK = (1u << 30) - 1;  // leaf: Morton-sorted body position
 constexpr uint32_t NODE_DEPTH_MASK = 0xFFu;     // internal: depth (root = 0)
 constexpr int NODE_JMASK_SHIFT = 8;             // jitter cell: which children got subdivided
+constexpr uint32_t NODE_SPAN = 1u << 12;        // internal: body range crosses a COM chunk
+
+// Centre-of-mass chunking (tree_build.hip): nodes inside a 2^COM_CHUNK_SHIFT-body chunk of
+// the Morton order are finished by one workgroup; the rest are listed per level.
+constexpr int COM_CHUNK_SHIFT = 10;
+__host__ __device__ inline uint32_t span_stride_for(int64_t n) {
+    return (uint32_t)((n >> COM_CHUNK_SHIFT) + 2);
+}
 
 constexpr int MAX_DEPTH_TAB = 40;
 
@@ -63,6 +71,9 @@ struct TreeBuffers {
     uint32_t *cnt, *base;  // node slots per sorted body; exclusive scan (n + 1 entries)
     Node *nodes;
     uint32_t *scalars;     // [0] = node count T, [1] = error flags
+    uint32_t *span_cnt;    // [J + 1] chunk-spanning internal nodes per level
+    uint32_t *span_list;   // [(J + 1) * span_stride]
+    uint32_t span_stride;
     void *cub_tmp;
     size_t cub_bytes;
 };

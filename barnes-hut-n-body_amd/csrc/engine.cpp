@@ -63,6 +63,7 @@ struct bh_engine {
     uint32_t *cnt = nullptr, *base = nullptr;
     Node *nodes = nullptr;
     size_t node_cap = 0;
+    uint32_t *span_cnt = nullptr, *span_list = nullptr;
     uint32_t *scalars = nullptr;  // [0] unused, [1] error flags, [2] heavy count, [3] pair count
     uint32_t *visits32 = nullptr;
     uint32_t *wave_iters = nullptr;  // per-wave union of visited nodes (diagnostics)
@@ -77,6 +78,10 @@ struct bh_engine {
     double *mupd_mass = nullptr, *hmass = nullptr;
     uint32_t mcap = 0;
     int64_t heavy_count = -1;  // -1: unknown (recompute)
+    std::vector<uint32_t> h_heavy;  // host copy of the ordered heavy list
+    std::vector<double> h_hmass;    // and of the heavy bodies' masses
+    void *pin = nullptr;            // pinned staging for the merge mailbox / uploads
+    size_t pin_bytes = 0;
 
     void *cub_tmp = nullptr;
     size_t cub_bytes = 0;
@@ -220,6 +225,8 @@ int ensure_capacity(bh_engine *e, int64_t n) {
     size_t ncap = node_capacity(e->cap, J);
     if (ncap > e->node_cap || J != e->J_alloc) {
         TRY(dev_alloc(e, e->nodes, ncap));
+        TRY(dev_alloc(e, e->span_cnt, (size_t)J + 2));
+        TRY(dev_alloc(e, e->span_list, (size_t)(J + 2) * span_stride_for(e->cap)));
         e->node_cap = ncap;
         e->J_alloc = J;
     }
@@ -250,6 +257,9 @@ TreeBuffers tree_buffers(bh_engine *e) {
     b.base = e->base;
     b.nodes = e->nodes;
     b.scalars = e->scalars;
+    b.span_cnt = e->span_cnt;
+    b.span_list = e->span_list;
+    b.span_stride = span_stride_for(e->cap);
     b.cub_tmp = e->cub_tmp;
     b.cub_bytes = e->cub_bytes;
     return b;
@@ -335,90 +345,125 @@ int check_tree_flags(bh_engine *e) {
 }
 
 // ---- merge rule (BHA:463-532) ---------------------------------------------------------
+// Heavy bodies (m > mergeMaxMass) only ever gain mass and are few, so the host keeps their
+// ordered index list and masses; the device finds candidate pairs (d^2 < minD^2) with one
+// kernel and posts them to a small mailbox that is copied back with ONE async copy into
+// pinned memory — one host round trip per step.  The host replays the reference's
+// sequential rule exactly over those pairs and the device applies removals by compaction.
+constexpr uint32_t kMailboxPairs = 2048;
+
+int pinned_reserve(bh_engine *e, size_t bytes) {
+    if (bytes <= e->pin_bytes) return BH_OK;
+    if (e->pin) (void)hipHostFree(e->pin);
+    e->pin = nullptr;
+    size_t nb = std::max<size_t>(bytes, 1 << 16);
+    HIPCHK(e, hipHostMalloc(&e->pin, nb, hipHostMallocDefault));
+    e->pin_bytes = nb;
+    return BH_OK;
+}
+
+int refresh_heavy_list(bh_engine *e) {  // ordered list of m > mergeMaxMass (BHA:474)
+    const int64_t n = e->n;
+    HIPCHK(e, heavy_list(e->m, n, e->p.merge_max_mass, e->heavy, e->scalars + 2, e->cub_tmp,
+                         e->cub_bytes, e->stream));
+    uint32_t hc = 0;
+    HIPCHK(e, hipMemcpyAsync(&hc, e->scalars + 2, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                             e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    e->h_heavy.resize(hc);
+    e->h_hmass.resize(hc);
+    if (hc > 0) {
+        if (e->mcap < hc) {
+            e->mcap = hc * 2;
+            TRY(dev_alloc(e, e->hmass, e->mcap));
+        }
+        gather_doubles(e->heavy, hc, e->m, e->hmass, e->stream);
+        HIPCHK(e, hipMemcpyAsync(e->h_heavy.data(), e->heavy, sizeof(uint32_t) * hc,
+                                 hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->h_hmass.data(), e->hmass, sizeof(double) * hc,
+                                 hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+    }
+    e->heavy_count = hc;
+    return BH_OK;
+}
+
 int merge(bh_engine *e) {
     if (e->p.merge_min_dist <= 0.0 || e->n <= 1) return BH_OK;  // BHA:465
     TRY(mark(e, -1));
     const int64_t n = e->n;
-    if (e->heavy_count < 0) {
-        HIPCHK(e, heavy_list(e->m, n, e->p.merge_max_mass, e->heavy, e->scalars + 2, e->cub_tmp,
-                             e->cub_bytes, e->stream));
-        uint32_t hc = 0;
-        HIPCHK(e, hipMemcpyAsync(&hc, e->scalars + 2, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                 e->stream));
-        HIPCHK(e, hipStreamSynchronize(e->stream));
-        e->heavy_count = hc;
-    }
+    if (e->heavy_count < 0) TRY(refresh_heavy_list(e));
     const uint32_t H = (uint32_t)e->heavy_count;
     if (H == 0) {
         TRY(mark(e, 3));
         return BH_OK;
     }
     const double minD2 = e->p.merge_min_dist * e->p.merge_min_dist;  // BHA:468
+    if (e->pair_cap == 0) {
+        e->pair_cap = 1u << 16;
+        TRY(dev_alloc(e, e->pairs, e->pair_cap + 1));
+    }
+    // mailbox = pairs[0] (count in .k) followed by up to pair_cap pairs
+    MergePair *box = e->pairs;
+    const size_t fast_bytes = sizeof(MergePair) * (1 + kMailboxPairs);
+    TRY(pinned_reserve(e, std::max(fast_bytes, sizeof(MergePair) * (1 + (size_t)e->pair_cap))));
     uint32_t count = 0;
     for (;;) {
-        if (e->pair_cap == 0) {
-            e->pair_cap = 1u << 16;
-            TRY(dev_alloc(e, e->pairs, e->pair_cap));
-        }
-        merge_candidates(n, e->x, e->y, e->m, e->heavy, H, minD2, e->pairs, e->pair_cap,
-                         e->scalars + 3, e->stream);
+        merge_candidates(n, e->x, e->y, e->m, e->heavy, H, minD2, box + 1, e->pair_cap,
+                         &box->k, e->stream);
         HIPCHK(e, hipGetLastError());
-        HIPCHK(e, hipMemcpyAsync(&count, e->scalars + 3, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                 e->stream));
-        HIPCHK(e, hipStreamSynchronize(e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->pin, box, fast_bytes, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));  // the one round trip of the step
+        count = reinterpret_cast<MergePair *>(e->pin)->k;
         if (count <= e->pair_cap) break;
         e->pair_cap = count + (count >> 1);
-        TRY(dev_alloc(e, e->pairs, e->pair_cap));
+        TRY(dev_alloc(e, e->pairs, e->pair_cap + 1));
+        box = e->pairs;
+        TRY(pinned_reserve(e, sizeof(MergePair) * (1 + (size_t)e->pair_cap)));
     }
     if (count == 0) {
         TRY(mark(e, 3));
         return BH_OK;
     }
-    // Sequential replay of BHA:470-531 over the (few) candidate pairs.
-    std::vector<MergePair> pr(count);
-    std::vector<uint32_t> hv(H);
-    std::vector<double> hm(H);
-    HIPCHK(e, hipMemcpyAsync(pr.data(), e->pairs, sizeof(MergePair) * count, hipMemcpyDeviceToHost,
-                             e->stream));
-    HIPCHK(e, hipMemcpyAsync(hv.data(), e->heavy, sizeof(uint32_t) * H, hipMemcpyDeviceToHost,
-                             e->stream));
-    if (e->mcap < std::max<uint32_t>(H, count)) {
-        e->mcap = std::max<uint32_t>(H, count) * 2;
-        TRY(dev_alloc(e, e->mdead, e->mcap));
-        TRY(dev_alloc(e, e->mupd, e->mcap));
-        TRY(dev_alloc(e, e->mupd_mass, e->mcap));
-        TRY(dev_alloc(e, e->hmass, e->mcap));
+    if (count > kMailboxPairs) {
+        HIPCHK(e, hipMemcpyAsync(e->pin, box, sizeof(MergePair) * (1 + (size_t)count),
+                                 hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
     }
-    gather_doubles(e->heavy, H, e->m, e->hmass, e->stream);
-    HIPCHK(e, hipMemcpyAsync(hm.data(), e->hmass, sizeof(double) * H, hipMemcpyDeviceToHost,
-                             e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    const MergePair *pp = reinterpret_cast<const MergePair *>(e->pin) + 1;
+    std::vector<MergePair> pr(pp, pp + count);
     std::sort(pr.begin(), pr.end(), [](const MergePair &a, const MergePair &b) {
         return a.k != b.k ? a.k < b.k : a.j < b.j;
     });
-    std::unordered_map<uint32_t, double> cur_mass;  // heavy bodies' running masses
-    for (uint32_t k = 0; k < H; ++k) cur_mass[hv[k]] = hm[k];
+    // Sequential replay of BHA:470-531.  Heavy bodies are visited in list order; a heavy body
+    // eaten earlier is skipped; victims are absorbed in descending index order (BHA:514-519).
+    const std::vector<uint32_t> &hv = e->h_heavy;
+    std::unordered_map<uint32_t, uint32_t> heavy_pos;
+    for (uint32_t k = 0; k < H; ++k) heavy_pos[hv[k]] = k;
+    std::vector<double> cur = e->h_hmass;
+    std::vector<char> heavy_dead(H, 0);
     std::unordered_set<uint32_t> dead;
     std::vector<uint32_t> dead_list;
     size_t pi = 0;
     for (uint32_t k = 0; k < H; ++k) {
         size_t pe = pi;
         while (pe < pr.size() && pr[pe].k == k) ++pe;
-        const uint32_t hi = hv[k];
-        if (dead.count(hi) == 0) {  // bi still in the list; m only grew, still > mergeMaxMass
-            double mi = cur_mass[hi];
-            bool any = false;
-            for (size_t q = pe; q > pi; --q) {  // victims in descending j (BHA:514)
+        if (!heavy_dead[k]) {  // bi still in the list; its mass only grew: still heavy
+            double mi = cur[k];
+            for (size_t q = pe; q > pi; --q) {
                 const MergePair &c = pr[q - 1];
                 if (dead.count(c.j)) continue;
-                auto it = cur_mass.find(c.j);
-                double mj = (it != cur_mass.end()) ? it->second : c.mj;
+                auto it = heavy_pos.find(c.j);
+                double mj = c.mj;
+                if (it != heavy_pos.end()) {  // a heavy victim carries its grown mass
+                    mj = cur[it->second];
+                    heavy_dead[it->second] = 1;
+                }
                 mi += mj;  // BHA:518
                 dead.insert(c.j);
                 dead_list.push_back(c.j);
-                any = true;
             }
-            if (any) cur_mass[hi] = mi;
+            cur[k] = mi;
         }
         pi = pe;
     }
@@ -426,38 +471,69 @@ int merge(bh_engine *e) {
         TRY(mark(e, 3));
         return BH_OK;
     }
+    std::sort(dead_list.begin(), dead_list.end());
+    // upload: dead list | updated heavy (index, mass) | new heavy list, from pinned memory
     std::vector<uint32_t> upd;
     std::vector<double> upd_mass;
+    std::vector<uint32_t> new_heavy;
+    std::vector<double> new_hmass;
     for (uint32_t k = 0; k < H; ++k) {
-        uint32_t hi = hv[k];
-        if (dead.count(hi)) continue;
-        if (cur_mass[hi] != hm[k] || std::signbit(cur_mass[hi]) != std::signbit(hm[k])) {
+        if (heavy_dead[k]) continue;
+        const uint32_t hi = hv[k];
+        if (std::memcmp(&cur[k], &e->h_hmass[k], sizeof(double)) != 0) {
             upd.push_back(hi);
-            upd_mass.push_back(cur_mass[hi]);
+            upd_mass.push_back(cur[k]);
         }
+        // index after removal of every dead body before it (list order is preserved)
+        uint32_t shift = (uint32_t)(std::lower_bound(dead_list.begin(), dead_list.end(), hi) -
+                                    dead_list.begin());
+        new_heavy.push_back(hi - shift);
+        new_hmass.push_back(cur[k]);
     }
-    HIPCHK(e, hipMemcpyAsync(e->mdead, dead_list.data(), sizeof(uint32_t) * dead_list.size(),
-                             hipMemcpyHostToDevice, e->stream));
-    if (!upd.empty()) {
-        HIPCHK(e, hipMemcpyAsync(e->mupd, upd.data(), sizeof(uint32_t) * upd.size(),
-                                 hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->mupd_mass, upd_mass.data(), sizeof(double) * upd.size(),
-                                 hipMemcpyHostToDevice, e->stream));
+    const uint32_t nd = (uint32_t)dead_list.size(), nu = (uint32_t)upd.size(),
+                   nh = (uint32_t)new_heavy.size();
+    if (e->mcap < std::max<uint32_t>(std::max(nd, nu), std::max<uint32_t>(nh, 1))) {
+        e->mcap = std::max<uint32_t>(std::max(nd, nu), std::max<uint32_t>(nh, 1)) * 2;
+        TRY(dev_alloc(e, e->mdead, e->mcap));
+        TRY(dev_alloc(e, e->mupd, e->mcap));
+        TRY(dev_alloc(e, e->mupd_mass, e->mcap));
+        TRY(dev_alloc(e, e->hmass, e->mcap));
+    }
+    size_t up_bytes = 4 * (size_t)nd + 4 * (size_t)nu + 8 * (size_t)nu + 4 * (size_t)nh + 64;
+    TRY(pinned_reserve(e, up_bytes + sizeof(MergePair) * (1 + (size_t)count)));
+    char *u = static_cast<char *>(e->pin);
+    uint32_t *u_dead = reinterpret_cast<uint32_t *>(u);
+    uint32_t *u_upd = u_dead + nd;
+    uint32_t *u_heavy = u_upd + nu;
+    double *u_mass = reinterpret_cast<double *>(
+        u + (((4 * (size_t)(nd + nu + nh)) + 7) & ~(size_t)7));
+    std::memcpy(u_dead, dead_list.data(), 4 * (size_t)nd);
+    std::memcpy(u_upd, upd.data(), 4 * (size_t)nu);
+    std::memcpy(u_heavy, new_heavy.data(), 4 * (size_t)nh);
+    std::memcpy(u_mass, upd_mass.data(), 8 * (size_t)nu);
+    HIPCHK(e, hipMemcpyAsync(e->mdead, u_dead, 4 * (size_t)nd, hipMemcpyHostToDevice, e->stream));
+    if (nu) {
+        HIPCHK(e, hipMemcpyAsync(e->mupd, u_upd, 4 * (size_t)nu, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->mupd_mass, u_mass, 8 * (size_t)nu, hipMemcpyHostToDevice,
+                                 e->stream));
     }
     HIPCHK(e, hipMemsetD32Async((hipDeviceptr_t)e->keep, 1, (size_t)n, e->stream));
-    apply_merge((uint32_t)dead_list.size(), e->mdead, (uint32_t)upd.size(), e->mupd, e->mupd_mass,
-                e->keep, e->m, e->stream);
+    apply_merge(nd, e->mdead, nu, e->mupd, e->mupd_mass, e->keep, e->m, e->stream);
     const double *src[5] = {e->x, e->y, e->vx, e->vy, e->m};
     double *dst[5] = {e->alt[0], e->alt[1], e->alt[2], e->alt[3], e->alt[4]};
     HIPCHK(e, compact_bodies(n, e->keep, src, dst, e->pos, nullptr, e->cub_tmp, e->cub_bytes,
                              e->stream));
+    if (nh) HIPCHK(e, hipMemcpyAsync(e->heavy, u_heavy, 4 * (size_t)nh, hipMemcpyHostToDevice,
+                                     e->stream));
     std::swap(e->x, e->alt[0]);
     std::swap(e->y, e->alt[1]);
     std::swap(e->vx, e->alt[2]);
     std::swap(e->vy, e->alt[3]);
     std::swap(e->m, e->alt[4]);
-    e->n = n - (int64_t)dead_list.size();
-    e->heavy_count = -1;    // indices shifted: rebuild the ordered heavy list lazily
+    e->n = n - (int64_t)nd;
+    e->h_heavy = std::move(new_heavy);
+    e->h_hmass = std::move(new_hmass);
+    e->heavy_count = nh;
     e->tree_valid = false;  // BHA:526
     TRY(mark(e, 3));
     return BH_OK;
@@ -643,11 +719,13 @@ void bh_destroy(bh_engine *e) {
     void *ptrs[] = {e->x, e->y, e->vx, e->vy, e->m, e->alt[0], e->alt[1], e->alt[2], e->alt[3],
                     e->alt[4], e->ax, e->ay, e->a_sorted, e->keys, e->keys_s, e->idx, e->perm,
                     e->sx, e->sy, e->sm, e->cpl, e->cnt, e->base, e->nodes, e->scalars,
+                    e->span_cnt, e->span_list,
                     e->visits32, e->wave_iters, e->heavy, e->keep, e->pos, e->pairs, e->mdead, e->mupd,
                     e->mupd_mass, e->hmass, e->cub_tmp};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     for (hipEvent_t ev : e->ev) (void)hipEventDestroy(ev);
+    if (e->pin) (void)hipHostFree(e->pin);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
 }

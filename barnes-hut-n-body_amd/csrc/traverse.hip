@@ -30,7 +30,7 @@ typedef double double4_t __attribute__((ext_vector_type(4)));
 // v_div_fmas scaling) and the special-value fix-ups (v_cmp_class / v_div_fixup) removed.
 // For a finite normal operand in [2^-600, 2^600] those removed steps are identities (no
 // scaling is triggered, no special value occurs), so the results are bit-identical to the
-// full sequences; callers take this path only when every lane's operand is in that range.
+// full sequences; a wave takes this path only when lane_fast_ok() holds for all its lanes.
 __device__ __forceinline__ double sqrt_rn_inrange(double x) {
     double y = __builtin_amdgcn_rsq(x);
     double g = x * y;
@@ -55,36 +55,22 @@ __device__ __forceinline__ double rcp_rn_inrange(double b) {
     return __builtin_fma(r, y, y);
 }
 
-__device__ __forceinline__ bool in_fast_range(double x) {
-    return x >= 0x1p-600 && x <= 0x1p600;
+// Wave-uniform precondition for the exact fast paths: every tree node's centre of mass lies
+// within the root cell or 2e-3 of it (a convex combination of inserted bodies; a jittered
+// leaf body moved by at most 2 x 1e-3), so |comX|, |comY| < 2^31 always.  If the lane's own
+// body is finite with |x|, |y| < 2^250 and soft2 is in [2^-600, 2^500], every dist2 of the
+// traversal is in [soft2, 2^503] and both sqrt and the reciprocals stay in the range where
+// sqrt_rn_inrange / rcp_rn_inrange equal the full IEEE sequences.
+__device__ __forceinline__ bool lane_fast_ok(double bx, double by, double soft2) {
+    return __builtin_fabs(bx) < 0x1p250 && __builtin_fabs(by) < 0x1p250 && soft2 >= 0x1p-600 &&
+           soft2 <= 0x1p500;
 }
 
-template <bool SORTED_OUT, bool COUNT>
-__global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
-                                                 const uint32_t *__restrict__ d_T,
-                                                 const double *__restrict__ sx,
-                                                 const double *__restrict__ sy,
-                                                 const double *__restrict__ sm,
-                                                 const uint32_t *__restrict__ perm, int64_t lo,
-                                                 int64_t hi, ForceParams fp, Geometry g,
-                                                 double *__restrict__ ax, double *__restrict__ ay,
-                                                 double *__restrict__ a_sorted,
-                                                 uint32_t *__restrict__ visits,
-                                                 uint32_t *__restrict__ wave_iters) {
-    const int64_t p = lo + (int64_t)blockIdx.x * TB + threadIdx.x;
-    const bool valid = p < hi;
-    const double bx = valid ? sx[p] : 0.0;
-    const double by = valid ? sy[p] : 0.0;
-    const double bm = valid ? sm[p] : 1.0;
-    const double Gm = fp.G * bm;  // (Config.G * b.m) is evaluated first (BHA:256)
-    const double soft2 = fp.soft2, theta2 = fp.theta2;
-    const double s2root = g.s2[0];
-    const uint32_t self = (uint32_t)p;
-    double fx = 0.0, fy = 0.0;
-    uint32_t nvis = 0, niters = 0;
-    // lane is active for node `cur` iff cur >= resume; invalid lanes never are.
-    uint32_t resume = valid ? 0u : 0xFFFFFFFFu;
-    const uint32_t T = __builtin_amdgcn_readfirstlane(*d_T);
+template <bool FAST, bool COUNT>
+__device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T, double bx,
+                                     double by, double Gm, double soft2, double theta2,
+                                     double s2root, uint32_t self, uint32_t resume, double &fx,
+                                     double &fy, uint32_t &nvis, uint32_t &niters) {
     uint32_t cur = 0;
     while (cur < T) {
         const double4_t raw = *reinterpret_cast<const double4_t *>(nodes + cur);
@@ -116,10 +102,9 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
             contrib = active && acc;
             open = active && !acc;
         }
-        const bool all_fast = __ballot(contrib && !in_fast_range(d2)) == 0ull;
         if (contrib) {  // BHA:250-259, expression order as written
             double invR, invR2;
-            if (all_fast) {
+            if (FAST) {
                 invR = rcp_rn_inrange(sqrt_rn_inrange(d2));
                 invR2 = rcp_rn_inrange(d2);
             } else {
@@ -134,6 +119,41 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
         const bool any_open = __ballot(open) != 0ull;  // wave-uniform
         cur = any_open ? cur + 1 : next;
     }
+}
+
+template <bool SORTED_OUT, bool COUNT>
+__global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
+                                                 const uint32_t *__restrict__ d_T,
+                                                 const double *__restrict__ sx,
+                                                 const double *__restrict__ sy,
+                                                 const double *__restrict__ sm,
+                                                 const uint32_t *__restrict__ perm, int64_t lo,
+                                                 int64_t hi, ForceParams fp, Geometry g,
+                                                 double *__restrict__ ax, double *__restrict__ ay,
+                                                 double *__restrict__ a_sorted,
+                                                 uint32_t *__restrict__ visits,
+                                                 uint32_t *__restrict__ wave_iters) {
+    const int64_t p = lo + (int64_t)blockIdx.x * TB + threadIdx.x;
+    const bool valid = p < hi;
+    const double bx = valid ? sx[p] : 0.0;
+    const double by = valid ? sy[p] : 0.0;
+    const double bm = valid ? sm[p] : 1.0;
+    const double Gm = fp.G * bm;  // (Config.G * b.m) is evaluated first (BHA:256)
+    const double soft2 = fp.soft2, theta2 = fp.theta2;
+    const double s2root = g.s2[0];
+    const uint32_t self = (uint32_t)p;
+    double fx = 0.0, fy = 0.0;
+    uint32_t nvis = 0, niters = 0;
+    // lane is active for node `cur` iff cur >= resume; invalid lanes never are.
+    const uint32_t resume = valid ? 0u : 0xFFFFFFFFu;
+    const uint32_t T = __builtin_amdgcn_readfirstlane(*d_T);
+    const bool fast = __ballot(valid && !lane_fast_ok(bx, by, soft2)) == 0ull;
+    if (fast)
+        walk<true, COUNT>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx, fy, nvis,
+                          niters);
+    else
+        walk<false, COUNT>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx, fy, nvis,
+                           niters);
     if (COUNT && (threadIdx.x & 63) == 0) wave_iters[(p - lo) >> 6] = niters;
     if (!valid) return;
     const double rax = fx / bm;  // BHA:390-391

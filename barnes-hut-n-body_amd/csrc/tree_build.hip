@@ -18,7 +18,9 @@
 //   exclusive scan                 -> base (pre-order slot of each sorted body's nodes)
 //   k_emit    internal node skeletons (depth, next) + leaf records
 //   k_jitter  replay of BHA:125-156 inside each jitter cell
-//   k_com[L]  L = J..0: centre of mass bottom-up, children 0..3 in order (BHA:184-200)
+//   k_com_local  centre of mass bottom-up (children 0..3 in order, BHA:184-200) for every
+//                node inside a 1024-body chunk, all levels in one launch
+//   k_com_span[L] the few chunk-spanning nodes, one small launch per level L = J..0
 #include <hipcub/hipcub.hpp>
 
 #include "bh_device.hpp"
@@ -131,7 +133,10 @@ __global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, const uint64_t *_
                                              const double *__restrict__ sx,
                                              const double *__restrict__ sy,
                                              const double *__restrict__ sm,
-                                             Node *__restrict__ nodes) {
+                                             Node *__restrict__ nodes,
+                                             uint32_t *__restrict__ span_cnt,
+                                             uint32_t *__restrict__ span_list,
+                                             uint32_t span_stride) {
     int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (a >= n) return;
     uint64_t k = keys_s[a];
@@ -141,15 +146,32 @@ __global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, const uint64_t *_
     uint32_t b0 = base[a];
     int64_t end = a;
     for (int L = cc; L > cp; --L) {  // deepest first: ends are nested
-        int shift = 2 * (J - L);
-        end = run_end(keys_s, n, end, shift, k >> shift);
+        // last body of the depth-L cell: first b >= end with c(b) < L.  A short scan of the
+        // 1-byte c array settles the (many) small deep cells; big cells gallop on the keys.
+        int64_t b = end;
+        int steps = 0;
+        while (steps < 24 && (int)cpl[b] >= L) {
+            ++b;
+            ++steps;
+        }
+        if ((int)cpl[b] >= L) {
+            int shift = 2 * (J - L);
+            b = run_end(keys_s, n, b, shift, k >> shift);
+        }
+        end = b;
+        const bool span = (a >> COM_CHUNK_SHIFT) != (end >> COM_CHUNK_SHIFT);
+        const uint32_t ni = b0 + (uint32_t)(L - cp - 1);
         Node nd;
         nd.comX = 0.0;
         nd.comY = 0.0;
         nd.mass = 0.0;
         nd.next = base[end + 1];
-        nd.meta = (uint32_t)L;
-        nodes[b0 + (uint32_t)(L - cp - 1)] = nd;
+        nd.meta = (uint32_t)L | (span ? NODE_SPAN : 0u);
+        nodes[ni] = nd;
+        if (span) {
+            uint32_t slot = atomicAdd(&span_cnt[L], 1u);
+            span_list[(size_t)L * span_stride + slot] = ni;
+        }
     }
     uint32_t li = b0 + (uint32_t)max(0, cc - cp);
     double mm = sm[a];
@@ -288,21 +310,12 @@ __global__ __launch_bounds__(TB) void k_jitter(int64_t n, Geometry g,
     }
     // remember which children were subdivided (for getTreeForDebug/visitQuads)
     uint32_t ni = base[a] + (uint32_t)(J - cp - 1);
-    nodes[ni].meta = (uint32_t)J | (jmask << NODE_JMASK_SHIFT);
+    nodes[ni].meta |= jmask << NODE_JMASK_SHIFT;
 }
 
-// BHA:173-202 for the internal nodes at depth L.
-__global__ __launch_bounds__(TB) void k_com(int64_t n, int L, Geometry g,
-                                            const uint64_t *__restrict__ keys_s,
-                                            const int8_t *__restrict__ cpl,
-                                            const uint32_t *__restrict__ base, Node *nodes) {
-    int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (a >= n) return;
-    int cc = (int)cpl[a];
-    if (cc < L) return;
-    int cp = a > 0 ? (int)cpl[a - 1] : -1;
-    if (cp >= L) return;
-    uint32_t ni = base[a] + (uint32_t)(L - cp - 1);
+// BHA:173-202 for one internal node: children 0..3 in pre-order, skipping mass <= 0.
+__device__ __forceinline__ void node_com(Node *nodes, uint32_t ni, const Geometry &g,
+                                         uint64_t key, int L) {
     Node nd = nodes[ni];
     double mSum = 0.0, cx = 0.0, cy = 0.0;
     uint32_t c = ni + 1;
@@ -320,10 +333,69 @@ __global__ __launch_bounds__(TB) void k_com(int64_t n, int L, Geometry g,
         nd.comX = cx / mSum;
         nd.comY = cy / mSum;
     } else {  // BHA:197-199 (never visited: mass == 0)
-        cell_centre(g, keys_s[a], L, nd.comX, nd.comY);
+        cell_centre(g, key, L, nd.comX, nd.comY);
         nd.meta |= NODE_SKIP;
     }
     nodes[ni] = nd;
+}
+
+// Every internal node whose body range lies inside one COM_CHUNK-body chunk, all levels
+// bottom-up in ONE launch: a workgroup owns a chunk, levels are separated by barriers
+// (children written by this workgroup are visible to it after __syncthreads).
+constexpr int COM_TB = 256;
+constexpr int COM_PER_THREAD = (1 << COM_CHUNK_SHIFT) / COM_TB;
+
+__global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
+                                                      const uint64_t *__restrict__ keys_s,
+                                                      const int8_t *__restrict__ cpl,
+                                                      const uint32_t *__restrict__ base,
+                                                      Node *nodes) {
+    const int64_t c0 = (int64_t)blockIdx.x << COM_CHUNK_SHIFT;
+    const int64_t a0 = c0 + (int64_t)threadIdx.x * COM_PER_THREAD;
+    int cps[COM_PER_THREAD], ccs[COM_PER_THREAD];
+    int lmax = -1;
+#pragma unroll
+    for (int i = 0; i < COM_PER_THREAD; ++i) {
+        const int64_t a = a0 + i;
+        int cp = -1, cc = -1;
+        if (a < n) {
+            cp = a > 0 ? (int)cpl[a - 1] : -1;
+            cc = (int)cpl[a];
+        }
+        cps[i] = cp;
+        ccs[i] = cc;
+        lmax = max(lmax, cc);
+    }
+    __shared__ int s_lmax;
+    if (threadIdx.x == 0) s_lmax = -1;
+    __syncthreads();
+    atomicMax(&s_lmax, lmax);
+    __syncthreads();
+    const int top = s_lmax;
+    for (int L = top; L >= 0; --L) {
+#pragma unroll
+        for (int i = 0; i < COM_PER_THREAD; ++i) {
+            if (ccs[i] >= L && cps[i] < L) {
+                const int64_t a = a0 + i;
+                const uint32_t ni = base[a] + (uint32_t)(L - cps[i] - 1);
+                if (!(nodes[ni].meta & NODE_SPAN)) node_com(nodes, ni, g, keys_s[a], L);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// The nodes whose range crosses a chunk boundary (at most one per boundary per level):
+// one small launch per level over a compact list.
+__global__ __launch_bounds__(TB) void k_com_span(int L, Geometry g,
+                                                 const uint32_t *__restrict__ span_cnt,
+                                                 const uint32_t *__restrict__ span_list,
+                                                 uint32_t span_stride, Node *nodes) {
+    const uint32_t cnt = span_cnt[L];
+    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < cnt; i += gridDim.x * TB) {
+        const uint32_t ni = span_list[(size_t)L * span_stride + i];
+        node_com(nodes, ni, g, 0ull, L);
+    }
 }
 
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + TB - 1) / TB); }
@@ -353,11 +425,17 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     bytes = b.cub_bytes;
     st = hipcub::DeviceScan::ExclusiveSum(b.cub_tmp, bytes, b.cnt, b.base, (int)(n + 1), s);
     if (st != hipSuccess) return st;
-    k_emit<<<grid_for(n), TB, 0, s>>>(n, g.J, b.keys_s, b.cpl, b.base, b.sx, b.sy, b.sm, b.nodes);
+    st = hipMemsetAsync(b.span_cnt, 0, sizeof(uint32_t) * (g.J + 1), s);
+    if (st != hipSuccess) return st;
+    k_emit<<<grid_for(n), TB, 0, s>>>(n, g.J, b.keys_s, b.cpl, b.base, b.sx, b.sy, b.sm, b.nodes,
+                                      b.span_cnt, b.span_list, b.span_stride);
     k_jitter<<<grid_for(n), TB, 0, s>>>(n, g, b.keys_s, b.cpl, b.base, b.sx, b.sy, b.sm, b.x, b.y,
                                         b.perm, b.nodes, b.scalars + 1);
+    k_com_local<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), COM_TB, 0, s>>>(
+        n, g, b.keys_s, b.cpl, b.base, b.nodes);
+    const unsigned span_grid = (b.span_stride + TB - 1) / TB;
     for (int L = g.J; L >= 0; --L)
-        k_com<<<grid_for(n), TB, 0, s>>>(n, L, g, b.keys_s, b.cpl, b.base, b.nodes);
+        k_com_span<<<span_grid, TB, 0, s>>>(L, g, b.span_cnt, b.span_list, b.span_stride, b.nodes);
     return hipGetLastError();
 }
 
