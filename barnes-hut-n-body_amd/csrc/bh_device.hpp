@@ -74,6 +74,7 @@ struct TreeBuffers {
     uint32_t *span_cnt;    // [J + 1] chunk-spanning internal nodes per level
     uint32_t *span_list;   // [(J + 1) * span_stride]
     uint32_t span_stride;
+    uint4 *span_children;  // [(J + 1) * span_stride]
     void *cub_tmp;
     size_t cub_bytes;
 };

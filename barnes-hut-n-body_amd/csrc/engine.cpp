@@ -64,6 +64,7 @@ struct bh_engine {
     Node *nodes = nullptr;
     size_t node_cap = 0;
     uint32_t *span_cnt = nullptr, *span_list = nullptr;
+    uint4 *span_children = nullptr;
     uint32_t *scalars = nullptr;  // [0] unused, [1] error flags, [2] heavy count, [3] pair count
     uint32_t *visits32 = nullptr;
     uint32_t *wave_iters = nullptr;  // per-wave union of visited nodes (diagnostics)
@@ -206,7 +207,7 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(dev_alloc(e, e->sx, cap));
         TRY(dev_alloc(e, e->sy, cap));
         TRY(dev_alloc(e, e->sm, cap));
-        TRY(dev_alloc(e, e->cpl, cap));
+        TRY(dev_alloc(e, e->cpl, cap + 32));  // slack for word-wise scans
         TRY(dev_alloc(e, e->cnt, cap + 1));
         TRY(dev_alloc(e, e->base, cap + 1));
         TRY(dev_alloc(e, e->visits32, cap));
@@ -227,6 +228,7 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(dev_alloc(e, e->nodes, ncap));
         TRY(dev_alloc(e, e->span_cnt, (size_t)J + 2));
         TRY(dev_alloc(e, e->span_list, (size_t)(J + 2) * span_stride_for(e->cap)));
+        TRY(dev_alloc(e, e->span_children, (size_t)(J + 2) * span_stride_for(e->cap)));
         e->node_cap = ncap;
         e->J_alloc = J;
     }
@@ -260,6 +262,7 @@ TreeBuffers tree_buffers(bh_engine *e) {
     b.span_cnt = e->span_cnt;
     b.span_list = e->span_list;
     b.span_stride = span_stride_for(e->cap);
+    b.span_children = e->span_children;
     b.cub_tmp = e->cub_tmp;
     b.cub_bytes = e->cub_bytes;
     return b;
@@ -362,6 +365,16 @@ int pinned_reserve(bh_engine *e, size_t bytes) {
     return BH_OK;
 }
 
+int merge_bufs(bh_engine *e, uint32_t need) {  // dead / update / mass staging on the device
+    if (need <= e->mcap && e->mdead) return BH_OK;
+    e->mcap = std::max<uint32_t>(need, 64) * 2;
+    TRY(dev_alloc(e, e->mdead, e->mcap));
+    TRY(dev_alloc(e, e->mupd, e->mcap));
+    TRY(dev_alloc(e, e->mupd_mass, e->mcap));
+    TRY(dev_alloc(e, e->hmass, e->mcap));
+    return BH_OK;
+}
+
 int refresh_heavy_list(bh_engine *e) {  // ordered list of m > mergeMaxMass (BHA:474)
     const int64_t n = e->n;
     HIPCHK(e, heavy_list(e->m, n, e->p.merge_max_mass, e->heavy, e->scalars + 2, e->cub_tmp,
@@ -373,10 +386,7 @@ int refresh_heavy_list(bh_engine *e) {  // ordered list of m > mergeMaxMass (BHA
     e->h_heavy.resize(hc);
     e->h_hmass.resize(hc);
     if (hc > 0) {
-        if (e->mcap < hc) {
-            e->mcap = hc * 2;
-            TRY(dev_alloc(e, e->hmass, e->mcap));
-        }
+        TRY(merge_bufs(e, hc));
         gather_doubles(e->heavy, hc, e->m, e->hmass, e->stream);
         HIPCHK(e, hipMemcpyAsync(e->h_heavy.data(), e->heavy, sizeof(uint32_t) * hc,
                                  hipMemcpyDeviceToHost, e->stream));
@@ -492,13 +502,7 @@ int merge(bh_engine *e) {
     }
     const uint32_t nd = (uint32_t)dead_list.size(), nu = (uint32_t)upd.size(),
                    nh = (uint32_t)new_heavy.size();
-    if (e->mcap < std::max<uint32_t>(std::max(nd, nu), std::max<uint32_t>(nh, 1))) {
-        e->mcap = std::max<uint32_t>(std::max(nd, nu), std::max<uint32_t>(nh, 1)) * 2;
-        TRY(dev_alloc(e, e->mdead, e->mcap));
-        TRY(dev_alloc(e, e->mupd, e->mcap));
-        TRY(dev_alloc(e, e->mupd_mass, e->mcap));
-        TRY(dev_alloc(e, e->hmass, e->mcap));
-    }
+    TRY(merge_bufs(e, std::max<uint32_t>(std::max(nd, nu), nh)));
     size_t up_bytes = 4 * (size_t)nd + 4 * (size_t)nu + 8 * (size_t)nu + 4 * (size_t)nh + 64;
     TRY(pinned_reserve(e, up_bytes + sizeof(MergePair) * (1 + (size_t)count)));
     char *u = static_cast<char *>(e->pin);
@@ -719,7 +723,7 @@ void bh_destroy(bh_engine *e) {
     void *ptrs[] = {e->x, e->y, e->vx, e->vy, e->m, e->alt[0], e->alt[1], e->alt[2], e->alt[3],
                     e->alt[4], e->ax, e->ay, e->a_sorted, e->keys, e->keys_s, e->idx, e->perm,
                     e->sx, e->sy, e->sm, e->cpl, e->cnt, e->base, e->nodes, e->scalars,
-                    e->span_cnt, e->span_list,
+                    e->span_cnt, e->span_list, e->span_children,
                     e->visits32, e->wave_iters, e->heavy, e->keep, e->pos, e->pairs, e->mdead, e->mupd,
                     e->mupd_mass, e->hmass, e->cub_tmp};
     for (void *q : ptrs)

@@ -20,8 +20,9 @@
 //   k_jitter  replay of BHA:125-156 inside each jitter cell
 //   k_com_local  centre of mass bottom-up (children 0..3 in order, BHA:184-200) for every
 //                node inside a 1024-body chunk, all levels in one launch
-//   k_com_span[L] the few chunk-spanning nodes, one small launch per level L = J..0
+//   k_com_span   the few chunk-spanning nodes, levels J..0, one workgroup
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include "bh_device.hpp"
 
@@ -111,6 +112,23 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
     cnt[a] = (k == SENT) ? 0u : 1u + (uint32_t)max(0, c_cur - c_prev);
 }
 
+// First b >= from with c(b) < L, looking at most at the 3 aligned 8-byte words of c that
+// start at `from`'s word; -1 if not found there.  c(n-1) == -1 bounds every search, and the
+// c array is allocated with 16 bytes of slack so whole-word loads stay in bounds.
+__device__ __forceinline__ int64_t scan_cpl(const int8_t *__restrict__ cpl, int64_t from, int L) {
+    const int64_t w0 = from & ~(int64_t)7;
+    for (int w = 0; w < 3; ++w) {
+        const uint64_t word = *reinterpret_cast<const uint64_t *>(cpl + w0 + 8 * w);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            const int64_t idx = w0 + 8 * w + k;
+            const int c = (int)(int8_t)(word >> (8 * k));
+            if (idx >= from && c < L) return idx;
+        }
+    }
+    return -1;
+}
+
 // Largest index e >= from with (keys_s[e] >> shift) == pref (keys_s[from] matches).
 __device__ __forceinline__ int64_t run_end(const uint64_t *__restrict__ keys_s, int64_t n,
                                            int64_t from, int shift, uint64_t pref) {
@@ -148,13 +166,9 @@ __global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, const uint64_t *_
     for (int L = cc; L > cp; --L) {  // deepest first: ends are nested
         // last body of the depth-L cell: first b >= end with c(b) < L.  A short scan of the
         // 1-byte c array settles the (many) small deep cells; big cells gallop on the keys.
-        int64_t b = end;
-        int steps = 0;
-        while (steps < 24 && (int)cpl[b] >= L) {
-            ++b;
-            ++steps;
-        }
-        if ((int)cpl[b] >= L) {
+        int64_t b = scan_cpl(cpl, end, L);
+        if (b < 0) {
+            b = end;
             int shift = 2 * (J - L);
             b = run_end(keys_s, n, b, shift, k >> shift);
         }
@@ -339,62 +353,177 @@ __device__ __forceinline__ void node_com(Node *nodes, uint32_t ni, const Geometr
     nodes[ni] = nd;
 }
 
-// Every internal node whose body range lies inside one COM_CHUNK-body chunk, all levels
-// bottom-up in ONE launch: a workgroup owns a chunk, levels are separated by barriers
-// (children written by this workgroup are visible to it after __syncthreads).
+// Every internal node whose body range lies inside one COM chunk (2^COM_CHUNK_SHIFT bodies
+// of the Morton order) is finished here, all levels bottom-up in ONE launch: a workgroup owns
+// a chunk, stages the chunk's pre-order slot range [base[c0], base[c1]) in LDS (a local
+// node's whole subtree lives in that range), walks children at LDS latency, and separates
+// levels with barriers.  Chunks whose range exceeds the LDS capacity use global memory.
 constexpr int COM_TB = 256;
 constexpr int COM_PER_THREAD = (1 << COM_CHUNK_SHIFT) / COM_TB;
+constexpr int COM_CAP = 2560;  // nodes staged per chunk (2.5 per body; deep chains spill)
+constexpr uint32_t LDS_SPAN = 1u << 31;
 
 __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
                                                       const uint64_t *__restrict__ keys_s,
                                                       const int8_t *__restrict__ cpl,
                                                       const uint32_t *__restrict__ base,
                                                       Node *nodes) {
+    __shared__ double s_m[COM_CAP], s_x[COM_CAP], s_y[COM_CAP];
+    __shared__ uint32_t s_next[COM_CAP];
+    __shared__ int s_lmax;
     const int64_t c0 = (int64_t)blockIdx.x << COM_CHUNK_SHIFT;
+    const int64_t c1 = min(c0 + (1 << COM_CHUNK_SHIFT), n);
     const int64_t a0 = c0 + (int64_t)threadIdx.x * COM_PER_THREAD;
     int cps[COM_PER_THREAD], ccs[COM_PER_THREAD];
+    uint32_t bases[COM_PER_THREAD];
     int lmax = -1;
 #pragma unroll
     for (int i = 0; i < COM_PER_THREAD; ++i) {
         const int64_t a = a0 + i;
         int cp = -1, cc = -1;
+        uint32_t ba = 0;
         if (a < n) {
             cp = a > 0 ? (int)cpl[a - 1] : -1;
             cc = (int)cpl[a];
+            ba = base[a];
         }
         cps[i] = cp;
         ccs[i] = cc;
+        bases[i] = ba;
         lmax = max(lmax, cc);
     }
-    __shared__ int s_lmax;
     if (threadIdx.x == 0) s_lmax = -1;
+    const uint32_t S0 = base[c0], S1 = base[c1];
+    const uint32_t cnt = S1 - S0;
+    const bool lds = cnt <= (uint32_t)COM_CAP;
     __syncthreads();
     atomicMax(&s_lmax, lmax);
+    if (lds) {
+        for (uint32_t i = threadIdx.x; i < cnt; i += COM_TB) {
+            const Node nd = nodes[S0 + i];
+            s_m[i] = nd.mass;
+            s_x[i] = nd.comX;
+            s_y[i] = nd.comY;
+            s_next[i] = (nd.next - S0) | ((!(nd.meta & NODE_LEAF) && (nd.meta & NODE_SPAN)) ? LDS_SPAN : 0u);
+        }
+    }
     __syncthreads();
     const int top = s_lmax;
     for (int L = top; L >= 0; --L) {
 #pragma unroll
         for (int i = 0; i < COM_PER_THREAD; ++i) {
-            if (ccs[i] >= L && cps[i] < L) {
-                const int64_t a = a0 + i;
-                const uint32_t ni = base[a] + (uint32_t)(L - cps[i] - 1);
-                if (!(nodes[ni].meta & NODE_SPAN)) node_com(nodes, ni, g, keys_s[a], L);
+            if (ccs[i] < L || cps[i] >= L) continue;
+            const int64_t a = a0 + i;
+            const uint32_t ni = bases[i] + (uint32_t)(L - cps[i] - 1);
+            if (lds) {
+                const uint32_t li = ni - S0;
+                const uint32_t nx = s_next[li];
+                if (nx & LDS_SPAN) continue;  // finished by k_com_span
+                double mSum = 0.0, cx = 0.0, cy = 0.0;
+                uint32_t c = li + 1;
+                while (c < nx) {  // children 0..3 in pre-order (BHA:189-192)
+                    const double cm = s_m[c];
+                    if (cm > 0.0) {
+                        mSum += cm;
+                        cx += s_x[c] * cm;
+                        cy += s_y[c] * cm;
+                    }
+                    c = max(s_next[c] & ~LDS_SPAN, c + 1);
+                }
+                double ox, oy;
+                if (mSum > 0.0) {
+                    ox = cx / mSum;
+                    oy = cy / mSum;
+                } else {
+                    cell_centre(g, keys_s[a], L, ox, oy);
+                }
+                s_m[li] = mSum;
+                s_x[li] = ox;
+                s_y[li] = oy;
+                Node *dst = nodes + ni;
+                dst->comX = ox;
+                dst->comY = oy;
+                dst->mass = mSum;
+                if (!(mSum > 0.0)) dst->meta |= NODE_SKIP;
+            } else if (!(nodes[ni].meta & NODE_SPAN)) {
+                node_com(nodes, ni, g, keys_s[a], L);
             }
         }
         __syncthreads();
     }
 }
 
-// The nodes whose range crosses a chunk boundary (at most one per boundary per level):
-// one small launch per level over a compact list.
-__global__ __launch_bounds__(TB) void k_com_span(int L, Geometry g,
-                                                 const uint32_t *__restrict__ span_cnt,
-                                                 const uint32_t *__restrict__ span_list,
-                                                 uint32_t span_stride, Node *nodes) {
+// Children (pre-order indices, up to 4) of every chunk-spanning node, found in parallel so
+// the level-by-level pass below issues independent loads only.
+__global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__restrict__ span_cnt,
+                                                      const uint32_t *__restrict__ span_list,
+                                                      uint32_t span_stride,
+                                                      const Node *__restrict__ nodes,
+                                                      uint4 *__restrict__ span_children) {
+    const uint32_t L = blockIdx.y;
     const uint32_t cnt = span_cnt[L];
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < cnt; i += gridDim.x * TB) {
-        const uint32_t ni = span_list[(size_t)L * span_stride + i];
-        node_com(nodes, ni, g, 0ull, L);
+        const size_t slot = (size_t)L * span_stride + i;
+        const uint32_t ni = span_list[slot];
+        const uint32_t end = nodes[ni].next;
+        uint32_t ch[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        uint32_t c = ni + 1;
+        for (int k = 0; k < 4 && c < end; ++k) {
+            ch[k] = c;
+            c = max(nodes[c].next, c + 1);
+        }
+        span_children[slot] = make_uint4(ch[0], ch[1], ch[2], ch[3]);
+    }
+}
+
+// All chunk-spanning nodes, levels J..0, by ONE workgroup (levels separated by barriers;
+// its own global writes are visible to it).  Few nodes: at most one per chunk boundary and
+// level.
+constexpr int SPAN_TB = 1024;
+__global__ __launch_bounds__(SPAN_TB) void k_com_span(int J, const uint32_t *__restrict__ span_cnt,
+                                                      const uint32_t *__restrict__ span_list,
+                                                      uint32_t span_stride,
+                                                      const uint4 *__restrict__ span_children,
+                                                      Node *nodes) {
+    for (int L = J; L >= 0; --L) {
+        const uint32_t cnt = span_cnt[L];
+        for (uint32_t i = threadIdx.x; i < cnt; i += SPAN_TB) {
+            const size_t slot = (size_t)L * span_stride + i;
+            const uint32_t ni = span_list[slot];
+            const uint4 ch = span_children[slot];
+            const uint32_t cs[4] = {ch.x, ch.y, ch.z, ch.w};
+            double cm[4], cxs[4], cys[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {  // independent loads
+                cm[k] = 0.0;
+                cxs[k] = 0.0;
+                cys[k] = 0.0;
+                if (cs[k] != 0xFFFFFFFFu) {
+                    const Node c = nodes[cs[k]];
+                    cm[k] = c.mass;
+                    cxs[k] = c.comX;
+                    cys[k] = c.comY;
+                }
+            }
+            double mSum = 0.0, cx = 0.0, cy = 0.0;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {  // BHA:189-192, children 0..3 in order
+                if (cs[k] != 0xFFFFFFFFu && cm[k] > 0.0) {
+                    mSum += cm[k];
+                    cx += cxs[k] * cm[k];
+                    cy += cys[k] * cm[k];
+                }
+            }
+            Node *dst = nodes + ni;
+            dst->mass = mSum;
+            if (mSum > 0.0) {
+                dst->comX = cx / mSum;
+                dst->comY = cy / mSum;
+            } else {  // massless: never visited (the cell centre is not recorded here)
+                dst->meta |= NODE_SKIP;
+            }
+        }
+        __syncthreads();
     }
 }
 
@@ -402,11 +531,17 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + TB - 1) / TB); }
 
 }  // namespace
 
+// rocprim's default sends n <= 2^20 items to a merge sort (~20 kernels at n = 1e6); the
+// stable LSD onesweep radix sort over the 2J+1 key bits is several times cheaper here.
+using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                              rocprim::default_config, 0>;
+
 size_t tree_cub_bytes(int64_t n, int J) {
     size_t sort_bytes = 0, scan_bytes = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, sort_bytes, (uint64_t *)nullptr, (uint64_t *)nullptr,
-                                       (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n, 0,
-                                       2 * J + 1);
+    (void)rocprim::radix_sort_pairs<SortConfig>(nullptr, sort_bytes, (uint64_t *)nullptr,
+                                                (uint64_t *)nullptr, (uint32_t *)nullptr,
+                                                (uint32_t *)nullptr, (size_t)n, 0u,
+                                                (unsigned)(2 * J + 1));
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
                                      (int)(n + 1));
     return sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
@@ -417,8 +552,8 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     hipError_t st;
     k_morton<<<grid_for(n), TB, 0, s>>>(n, b.x, b.y, g, b.keys, b.idx);
     size_t bytes = b.cub_bytes;
-    st = hipcub::DeviceRadixSort::SortPairs(b.cub_tmp, bytes, b.keys, b.keys_s, b.idx, b.perm,
-                                            (int)n, 0, 2 * g.J + 1, s);
+    st = rocprim::radix_sort_pairs<SortConfig>(b.cub_tmp, bytes, b.keys, b.keys_s, b.idx, b.perm,
+                                               (size_t)n, 0u, (unsigned)(2 * g.J + 1), s);
     if (st != hipSuccess) return st;
     k_prep<<<grid_for(n + 1), TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.x, b.y, b.m, b.sx, b.sy, b.sm,
                                           b.cpl, b.cnt);
@@ -433,9 +568,10 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
                                         b.perm, b.nodes, b.scalars + 1);
     k_com_local<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), COM_TB, 0, s>>>(
         n, g, b.keys_s, b.cpl, b.base, b.nodes);
-    const unsigned span_grid = (b.span_stride + TB - 1) / TB;
-    for (int L = g.J; L >= 0; --L)
-        k_com_span<<<span_grid, TB, 0, s>>>(L, g, b.span_cnt, b.span_list, b.span_stride, b.nodes);
+    k_span_children<<<dim3((b.span_stride + TB - 1) / TB, g.J + 1), TB, 0, s>>>(
+        g.J, b.span_cnt, b.span_list, b.span_stride, b.nodes, b.span_children);
+    k_com_span<<<1, SPAN_TB, 0, s>>>(g.J, b.span_cnt, b.span_list, b.span_stride, b.span_children,
+                                     b.nodes);
     return hipGetLastError();
 }
 
