@@ -35,7 +35,7 @@ EXPORTED_SYMBOLS = (
     "bh_last_error", "bh_set_params", "bh_get_params", "bh_reset_bodies", "bh_step",
     "bh_num_bodies", "bh_get_bodies", "bh_compute_accelerations", "bh_get_quads",
     "bh_last_timings", "bh_last_tree_nodes", "bh_traverse_kernel_ms", "bh_set_profiling",
-    "bh_synchronize", "bh_shard_range", "bh_traversal_stats", "bh_scene_galaxy_disk", "bh_scene_kepler_disk", "bh_scene_uniform",
+    "bh_synchronize", "bh_shard_range", "bh_traversal_stats", "bh_last_removed", "bh_scene_galaxy_disk", "bh_scene_kepler_disk", "bh_scene_uniform",
 )
 
 
@@ -101,6 +101,7 @@ def load_library(path: str | None = None):
     lib.bh_set_profiling.argtypes = [_VP, ctypes.c_int]
     lib.bh_synchronize.argtypes = [_VP]
     lib.bh_traversal_stats.argtypes = [_VP, _I64P, _I64P, _I64P]
+    lib.bh_last_removed.argtypes = [_VP, _I64P, ctypes.c_int64, _I64P]
     lib.bh_shard_range.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, _I64P, _I64P]
     lib.bh_scene_galaxy_disk.argtypes = (
         [ctypes.c_int32] + [ctypes.c_double] * 6 + [ctypes.c_int32, ctypes.c_int64]
@@ -210,6 +211,17 @@ class Engine:
         self._check(self._lib.bh_compute_accelerations(
             self._h, _dp(ax), _dp(ay), vis.ctypes.data_as(_I64P) if visits else None))
         return (ax, ay, vis) if visits else (ax, ay)
+
+    def last_removed(self):
+        """Indices (list before the last step() call) removed by the merge rule, ascending."""
+        need = ctypes.c_int64(0)
+        rc = self._lib.bh_last_removed(self._h, None, 0, ctypes.byref(need))
+        if rc not in (BH_OK, BH_E_CAPACITY):
+            self._check(rc)
+        out = np.empty(need.value, dtype=np.int64)
+        self._check(self._lib.bh_last_removed(self._h, out.ctypes.data_as(_I64P), need.value,
+                                              ctypes.byref(need)))
+        return out
 
     def get_quads(self):
         need = ctypes.c_int64(0)
@@ -327,14 +339,15 @@ class PhysicsEngine:
         self._eng.reset_bodies(*(np.array([getattr(b, f) for b in bs], dtype=np.float64)
                                  for f in ("x", "y", "vx", "vy", "m")))
 
-    def _pull(self):
+    def _pull(self, after_step=False):
         x, y, vx, vy, m = self._eng.get_bodies()
         n = len(x)
         bs = self._bodies
-        if n != len(bs):
-            # merge: the reference removes victims from the same list, keeping order;
-            # the survivors' identities are the kept indices in order.
-            del bs[n:]
+        if after_step:
+            for j in self._eng.last_removed()[::-1]:  # BHA:519 removeAt on the caller's list
+                del bs[int(j)]
+        if len(bs) != n:
+            raise RuntimeError("engine and caller body lists diverged")
         for i in range(n):
             b = bs[i]
             b.x, b.y, b.vx, b.vy, b.m = float(x[i]), float(y[i]), float(vx[i]), float(vy[i]), float(m[i])
@@ -343,7 +356,7 @@ class PhysicsEngine:
         self._eng.set_params(self._params())
         self._push()
         self._eng.step(1)
-        self._pull()
+        self._pull(after_step=True)
 
     def get_bodies(self):  # BHA:335
         return self._bodies

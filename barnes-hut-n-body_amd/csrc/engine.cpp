@@ -15,6 +15,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <iterator>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -79,6 +80,7 @@ struct bh_engine {
     double *mupd_mass = nullptr, *hmass = nullptr;
     uint32_t mcap = 0;
     int64_t heavy_count = -1;  // -1: unknown (recompute)
+    std::vector<std::vector<uint32_t>> step_dead;  // per-step removals of the last bh_step
     std::vector<uint32_t> h_heavy;  // host copy of the ordered heavy list
     std::vector<double> h_hmass;    // and of the heavy bodies' masses
     void *pin = nullptr;            // pinned staging for the merge mailbox / uploads
@@ -535,6 +537,7 @@ int merge(bh_engine *e) {
     std::swap(e->vy, e->alt[3]);
     std::swap(e->m, e->alt[4]);
     e->n = n - (int64_t)nd;
+    e->step_dead.push_back(dead_list);
     e->h_heavy = std::move(new_heavy);
     e->h_hmass = std::move(new_hmass);
     e->heavy_count = nh;
@@ -789,6 +792,7 @@ int bh_step(bh_engine *e, int32_t k) {
     e->ev_used = 0;
     e->timings_pending = false;
     HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
+    e->step_dead.clear();
     for (int32_t s = 0; s < k; ++s) TRY(step_once(e));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     if (e->n > 0 && k > 0) TRY(check_tree_flags(e));
@@ -879,6 +883,33 @@ int bh_get_quads(bh_engine *e, double *cx, double *cy, double *h, int64_t cap, i
     if (w.rc != BH_OK) return w.rc;
     if (n_out) *n_out = w.k;
     return w.k > cap ? BH_E_CAPACITY : BH_OK;
+}
+
+int bh_last_removed(const bh_engine *e, int64_t *idx, int64_t cap, int64_t *n_out) {
+    if (!e || cap < 0 || (cap > 0 && !idx)) return BH_E_INVALID;
+    // compose the per-step removal lists into indices of the list before the call
+    std::vector<int64_t> orig;  // sorted
+    for (const auto &dl : e->step_dead) {
+        std::vector<int64_t> add;
+        size_t r = 0;
+        int64_t shift = 0;
+        for (uint32_t d : dl) {  // d ascending: index among the survivors so far
+            int64_t o = (int64_t)d + shift;
+            while (r < orig.size() && orig[r] <= o) {
+                ++r;
+                ++shift;
+                o = (int64_t)d + shift;
+            }
+            add.push_back(o);
+        }
+        std::vector<int64_t> merged;
+        std::merge(orig.begin(), orig.end(), add.begin(), add.end(), std::back_inserter(merged));
+        orig.swap(merged);
+    }
+    if (n_out) *n_out = (int64_t)orig.size();
+    if ((int64_t)orig.size() > cap) return BH_E_CAPACITY;
+    for (size_t i = 0; i < orig.size(); ++i) idx[i] = orig[i];
+    return BH_OK;
 }
 
 int bh_last_timings(const bh_engine *e, double *out5) {

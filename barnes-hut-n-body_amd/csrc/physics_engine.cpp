@@ -59,12 +59,20 @@ void PhysicsEngine::pushBodies() {
 
 // Write results back into the SAME Body objects (the reference mutates in place,
 // BHA:414-432) and shrink the list after a merge (BHA:519).
-void PhysicsEngine::pullBodies() {
+void PhysicsEngine::pullBodies(bool afterStep) {
+    if (afterStep) {  // BHA:519: remove the merged-away bodies from the caller's own list
+        int64_t cnt = 0;
+        int rc = bh_last_removed(eng_, nullptr, 0, &cnt);
+        if (rc != BH_OK && rc != BH_E_CAPACITY) check(rc);
+        std::vector<int64_t> rem((size_t)cnt);
+        check(bh_last_removed(eng_, rem.data(), cnt, &cnt));
+        for (auto it = rem.rbegin(); it != rem.rend(); ++it) bodies_->erase(bodies_->begin() + *it);
+    }
     const int64_t n = bh_num_bodies(eng_);
     std::vector<double> x(n), y(n), vx(n), vy(n), m(n);
     int64_t got = 0;
     check(bh_get_bodies(eng_, x.data(), y.data(), vx.data(), vy.data(), m.data(), n, &got));
-    bodies_->resize((size_t)got);
+    if ((int64_t)bodies_->size() != got) throw std::runtime_error("engine and caller lists diverged");
     for (int64_t i = 0; i < got; ++i) (*bodies_)[(size_t)i] = Body{x[i], y[i], vx[i], vy[i], m[i]};
 }
 
@@ -72,7 +80,7 @@ void PhysicsEngine::step() {
     pushParams();
     pushBodies();  // the caller may have edited bodies between frames
     check(bh_step(eng_, 1));
-    pullBodies();
+    pullBodies(true);
 }
 
 const std::vector<Body> &PhysicsEngine::getBodies() const { return *bodies_; }
@@ -92,7 +100,7 @@ BHTree PhysicsEngine::getTreeForDebug() {
     check(bh_get_quads(eng_, cx.data(), cy.data(), h.data(), need, &got));
     std::vector<Quad> quads((size_t)got);
     for (int64_t i = 0; i < got; ++i) quads[(size_t)i] = Quad{cx[i], cy[i], h[i]};
-    pullBodies();  // building a fresh tree can jitter positions (BHA:146-151)
+    pullBodies(false);  // building a fresh tree can jitter positions (BHA:146-151)
     return BHTree(std::move(quads));
 }
 

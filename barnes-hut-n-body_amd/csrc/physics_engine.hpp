@@ -79,7 +79,7 @@ public:
 private:
     void pushParams();
     void pushBodies();
-    void pullBodies();
+    void pullBodies(bool afterStep);
     void check(int rc) const;
 
     std::vector<Body> *bodies_;

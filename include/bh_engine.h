@@ -94,6 +94,11 @@ int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, do
  * mass == 0 test, BHA:216) — the V of the roofline byte model. */
 int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visits);
 
+/* Indices (into the list as it was before the last bh_step call, ascending) of the bodies the
+ * merge rule removed during that call — what a shim needs to apply BHA:519's removeAt to the
+ * caller's own list and keep Body identity.  BH_E_CAPACITY + *n_out if cap is too small. */
+int bh_last_removed(const bh_engine *e, int64_t *idx, int64_t cap, int64_t *n_out);
+
 /* getTreeForDebug().visitQuads{} (BHA:265-274,329-332): pre-order list of every cell
  * (cx, cy, h) of the last tree, or of a freshly built one if the cache was dropped
  * (after resetBodies or a merge, BHA:348,526).  BH_E_CAPACITY + *n_out if cap too small. */

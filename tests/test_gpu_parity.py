@@ -234,3 +234,39 @@ def test_c3_1e6_full_size_sampled():
     eng.step(1)
     ref.step(1)
     _assert_state_equal(eng, ref)
+
+
+def test_physics_engine_mirror_preserves_body_identity():
+    """The Kotlin-surface mirror (bh_amd.PhysicsEngine) driven like NBodyPanel: step() updates
+    the caller's own Body objects in place and removes merged-away bodies from the caller's
+    list (BHA:414-432, 519); survivors are the same objects the reference keeps."""
+    from oracle import py_oracle
+    bx = [1000.0, 1007.9, 1008.1, 1000.0, 1003.0, 1500.0, 1504.0, 1200.0]
+    by = [400.0, 400.0, 400.0, 406.0, 403.0, 300.0, 300.0, 200.0]
+    bm = [5000.0, 1.0, 1.0, 2.0, 4500.0, 10.0, 9000.0, 3.0]
+    f = scenes.uniform(200, 0.5, seed=9)
+    arrs = (np.concatenate([bx, f[0]]), np.concatenate([by, f[1]]), np.concatenate([np.zeros(8), f[2]]),
+            np.concatenate([np.zeros(8), f[3]]), np.concatenate([bm, f[4]]))
+    saved = bh_amd.Config.theta
+    bh_amd.Config.theta = 0.5
+    try:
+        bodies = [bh_amd.Body(*(float(a[i]) for a in arrs)) for i in range(len(arrs[0]))]
+        origin = {id(b): i for i, b in enumerate(bodies)}
+        eng = bh_amd.PhysicsEngine(bodies)
+        cfg = dict(G=80.0, dt=0.005, theta=0.5, soft2=1.0, width_px=2400, height_px=800,
+                   merge_max_mass=4000.0, merge_min_dist=8.0)
+        ref = py_oracle.make_engine(*arrs, cfg)
+        ref_origin = {id(b): i for i, b in enumerate(ref.bodies)}
+        for _ in range(15):
+            eng.step()
+            ref.step()
+        assert eng.get_bodies() is bodies
+        assert [origin[id(b)] for b in bodies] == [ref_origin[id(b)] for b in ref.bodies]
+        assert len(bodies) < len(arrs[0])
+        for b, r in zip(bodies, ref.bodies):
+            assert (b.x, b.y, b.vx, b.vy, b.m) == (r.x, r.y, r.vx, r.vy, r.m)
+        quads = []
+        eng.get_tree_for_debug().visit_quads(lambda q: quads.append(q))
+        assert quads[0] == bh_amd.Quad(1200.0, 400.0, 1202.0)
+    finally:
+        bh_amd.Config.theta = saved
