@@ -1,11 +1,18 @@
 // Device-side data layout shared by the engine's HIP translation units.
 //
-// The quadtree of the reference (BHA:95-202, a pointer tree of BHTree objects) is held in
-// HBM as ONE flat array of 32-byte node records in depth-first PRE-ORDER with the
-// reference's child order 0..3 (BHA:73-81 NW,NE,SW,SE == ascending Morton digit).
-// Only non-empty cells are stored: accumulateForce returns on mass == 0 (BHA:216), so an
-// empty cell contributes nothing and is never descended.  Each record carries `next`, the
-// pre-order index just past its subtree, so the traversal is stackless:
+// Bodies live in HBM as SoA fp64 arrays in MORTON ("slot") order — the order of the last
+// tree build — plus `cidx`, each body's index in the caller's list (the reference's
+// List<Body> order, which the jitter replay and the merge rule depend on).  Every build
+// sorts, then permutes the state into the new order (nearly sequential: bodies move little
+// between builds), so the traversal reads and writes coalesced and consecutive lanes hold
+// spatial neighbours.
+//
+// The quadtree of the reference (BHA:95-202, a pointer tree of BHTree objects) is ONE flat
+// array of 32-byte node records in depth-first PRE-ORDER with the reference's child order
+// 0..3 (BHA:73-81 NW,NE,SW,SE == ascending Morton digit).  Only non-empty cells are stored:
+// accumulateForce returns on mass == 0 (BHA:216), so an empty cell contributes nothing and is
+// never descended.  Each record carries `next`, the pre-order index just past its subtree, so
+// the traversal is stackless:
 //     open    -> cur + 1      (first child)
 //     skip    -> next         (accepted, leaf, or nobody in the wave opened it)
 #pragma once
@@ -24,12 +31,12 @@ struct __attribute__((aligned(32))) Node {
 static_assert(sizeof(Node) == 32, "node record must be 32 bytes");
 
 // meta bits
-constexpr uint32_t NODE_LEAF = 1u << 31;        // leaf holding one body (BHA:97)
-constexpr uint32_t NODE_SKIP = 1u << 30;        // mass == 0.0: never visited (BHA:216)
-constexpr uint32_t NODE_BODY_MASK = (1u << 30) - 1;  // leaf: Morton-sorted body position
-constexpr uint32_t NODE_DEPTH_MASK = 0xFFu;     // internal: depth (root = 0)
-constexpr int NODE_JMASK_SHIFT = 8;             // jitter cell: which children got subdivided
-constexpr uint32_t NODE_SPAN = 1u << 12;        // internal: body range crosses a COM chunk
+constexpr uint32_t NODE_LEAF = 1u << 31;             // leaf holding one body (BHA:97)
+constexpr uint32_t NODE_SKIP = 1u << 30;             // mass == 0.0: never visited (BHA:216)
+constexpr uint32_t NODE_BODY_MASK = (1u << 30) - 1;  // leaf: body slot (Morton position)
+constexpr uint32_t NODE_DEPTH_MASK = 0xFFu;          // internal: depth (root = 0)
+constexpr int NODE_JMASK_SHIFT = 8;                  // jitter cell: children that got subdivided
+constexpr uint32_t NODE_SPAN = 1u << 12;             // internal: body range crosses a COM chunk
 
 // Centre-of-mass chunking (tree_build.hip): nodes inside a 2^COM_CHUNK_SHIFT-body chunk of
 // the Morton order are finished by one workgroup; the rest are listed per level.
@@ -38,15 +45,19 @@ __host__ __device__ inline uint32_t span_stride_for(int64_t n) {
     return (uint32_t)((n >> COM_CHUNK_SHIFT) + 2);
 }
 
+// Cell-start table: first sorted body of every depth-D0 cell, so the end of any node at
+// depth <= D0 is one load, and deeper searches stay inside one depth-D0 cell.
+constexpr int CELL_TABLE_MAX_DEPTH = 10;
+
 constexpr int MAX_DEPTH_TAB = 40;
 
 // Root cell and per-depth geometry, computed on the host exactly as the reference does:
 // root Quad(W/2, H/2, max(W,H)/2 + 2) (BHA:360-361); child h = h / 2.0 (BHA:74).
 struct Geometry {
     double root_cx, root_cy, root_h;
-    int J;                        // first depth whose h < 1e-3: the jitter depth (BHA:146)
-    double h[MAX_DEPTH_TAB];      // h at depth d
-    double s2[MAX_DEPTH_TAB];     // (h*2.0)^2 at depth d (BHA:226)
+    int J;                     // first depth whose h < 1e-3: the jitter depth (BHA:146)
+    double h[MAX_DEPTH_TAB];   // h at depth d
+    double s2[MAX_DEPTH_TAB];  // (h*2.0)^2 at depth d (BHA:226)
 };
 
 // Key of a body outside the root cell (never inserted, BHA:126): sorts after every
@@ -58,19 +69,23 @@ struct ForceParams {
     double G, soft2, theta2;
 };
 
+// Body state in slot order.
+struct BodyState {
+    double *x, *y, *vx, *vy, *m;
+    uint32_t *cidx;  // caller (list) index
+};
+
 // ---- launchers (tree_build.hip) --------------------------------------------------
 struct TreeBuffers {
-    // inputs: positions in caller order (mutated by the jitter), masses
-    double *x, *y;
-    const double *m;
-    // workspace
+    BodyState src;  // state before the build (previous slot order)
+    BodyState dst;  // receives the state in the new Morton order (positions may be jittered)
     uint64_t *keys, *keys_s;
     uint32_t *idx, *perm;
-    double *sx, *sy, *sm;  // Morton-sorted copies (sm: mass)
     int8_t *cpl;           // c(a): common digit count between sorted keys a, a+1; -1 at ends
     uint32_t *cnt, *base;  // node slots per sorted body; exclusive scan (n + 1 entries)
+    uint32_t *cell_start;  // [4^D0 + 1] first sorted body of each depth-D0 cell
     Node *nodes;
-    uint32_t *scalars;     // [0] = node count T, [1] = error flags
+    uint32_t *scalars;     // [1] = error flags
     uint32_t *span_cnt;    // [J + 1] chunk-spanning internal nodes per level
     uint32_t *span_list;   // [(J + 1) * span_stride]
     uint32_t span_stride;
@@ -79,44 +94,50 @@ struct TreeBuffers {
     size_t cub_bytes;
 };
 
+int cell_table_depth(int J, int64_t n);
 size_t tree_cub_bytes(int64_t n, int J);
 hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStream_t s);
 
 // ---- launchers (traverse.hip) ----------------------------------------------------
-// Accelerations for Morton-sorted positions [lo, hi).  If a_sorted == nullptr the result
-// F/m is scattered to ax/ay in caller order through perm; otherwise it is written
-// interleaved (ax, ay) to a_sorted[2p], a_sorted[2p+1] for the multi-GPU all-gather.
-void traverse(const Node *nodes, const uint32_t *d_T, const double *sx, const double *sy,
-              const double *sm, const uint32_t *perm, int64_t lo, int64_t hi, const Geometry &g,
-              const ForceParams &fp, double *ax, double *ay, double *a_sorted, uint32_t *visits,
-              uint32_t *wave_iters, hipStream_t s);
-void scatter_sorted_acc(const double *a_sorted, const uint32_t *perm, int64_t n, double *ax,
-                        double *ay, hipStream_t s);
+// Accelerations F/m of slots [lo, hi), written interleaved to a2[2p], a2[2p+1].
+void traverse(const Node *nodes, const uint32_t *d_T, const double *x, const double *y,
+              const double *m, int64_t lo, int64_t hi, const Geometry &g, const ForceParams &fp,
+              double *a2, uint32_t *visits, uint32_t *wave_iters, hipStream_t s);
 
 // ---- launchers (integrate.hip) ---------------------------------------------------
-void kick_drift(int64_t n, const double *ax, const double *ay, double *x, double *y, double *vx,
-                double *vy, double dtHalf, double dt, hipStream_t s);
-void kick(int64_t n, const double *ax, const double *ay, double *vx, double *vy, double dtHalf,
-          hipStream_t s);
+void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
+                double dtHalf, double dt, hipStream_t s);
+void kick(int64_t n, const double *a2, double *vx, double *vy, double dtHalf, hipStream_t s);
+void iota_u32(uint32_t *p, int64_t n, hipStream_t s);
+// caller-order copies: dst_k[cidx[s]] = src_k[s]
+void scatter_to_caller(int64_t n, const uint32_t *cidx, int k, const double *const *src,
+                       double *const *dst, hipStream_t s);
+void scatter_acc_to_caller(int64_t n, const uint32_t *cidx, const double *a2, double *ax,
+                           double *ay, hipStream_t s);
 
 struct MergePair {
-    uint32_t k;  // heavy list position
-    uint32_t j;  // victim candidate body index
-    double mj;   // candidate mass
+    uint32_t h_cidx, v_cidx;  // heavy body and candidate victim, caller indices
+    uint32_t h_slot, v_slot;
+    double h_mass, v_mass;
 };
-size_t merge_cub_bytes(int64_t n);
-// Ordered list of bodies with m > thr (BHA:474); returns via d_count.
-hipError_t heavy_list(const double *m, int64_t n, double thr, uint32_t *heavy, uint32_t *d_count,
-                void *tmp, size_t tmp_bytes, hipStream_t s);
+// mailbox header (pairs[0] reinterpreted): pair count, heavy count
+struct MergeHeader {
+    uint32_t pairs, heavies, pad0, pad1;
+    double pad2, pad3;
+};
+static_assert(sizeof(MergeHeader) == sizeof(MergePair), "mailbox header size");
+// heavy = m > thr (BHA:474) -> slot list (any order); then the distance test (BHA:493-501)
 void merge_candidates(int64_t n, const double *x, const double *y, const double *m,
-                      const uint32_t *heavy, uint32_t H, double minD2, MergePair *pairs,
-                      uint32_t cap, uint32_t *d_count, hipStream_t s);
-// Remove flagged bodies (keep[i] == 0) preserving order; writes compacted arrays to dst.
-hipError_t compact_bodies(int64_t n, const uint32_t *keep, const double *const src[5], double *const dst[5],
-                    uint32_t *pos, uint32_t *d_count, void *tmp, size_t tmp_bytes, hipStream_t s);
-// keep[dead[i]] = 0; m[upd_idx[i]] = upd_mass[i]
-void apply_merge(uint32_t n_dead, const uint32_t *dead, uint32_t n_upd, const uint32_t *upd_idx,
-                 const double *upd_mass, uint32_t *keep, double *m, hipStream_t s);
-void gather_doubles(const uint32_t *idx, uint32_t cnt, const double *src, double *dst, hipStream_t s);
+                      const uint32_t *cidx, double thr, double minD2, uint32_t *heavy,
+                      MergePair *box, uint32_t cap, hipStream_t s);
+void apply_merge(uint32_t n_dead, const uint32_t *dead_slots, uint32_t n_upd,
+                 const uint32_t *upd_slots, const double *upd_mass, uint32_t *keep, double *m,
+                 hipStream_t s);
+size_t compact_cub_bytes(int64_t n);
+// Remove slots with keep == 0 preserving order; caller indices are renumbered past the
+// removed ones (dead_cidx sorted ascending, n_dead entries).
+hipError_t compact_state(int64_t n, const uint32_t *keep, const BodyState &src,
+                         const BodyState &dst, const uint32_t *dead_cidx, uint32_t n_dead,
+                         uint32_t *pos, void *tmp, size_t tmp_bytes, hipStream_t s);
 
 }  // namespace bh

@@ -1,24 +1,24 @@
 // Engine host code and the C-ABI (include/bh_engine.h).
 //
-// Replaces PhysicsEngine (BHA:287-532).  The engine owns SoA fp64 body arrays in HBM in the
-// caller's list order, a Morton-ordered workspace for the tree, and one HIP stream.  A step
-// is the reference's step() (BHA:405-439) as a fixed sequence of kernels on that stream;
-// the only host round trips are the merge rule's (BHA:463-532) candidate count when heavy
-// bodies exist, and the copy-in / copy-out calls.
+// Replaces PhysicsEngine (BHA:287-532).  The engine owns the body state in HBM as SoA fp64
+// arrays in Morton ("slot") order plus each body's caller-list index (cidx), the tree
+// workspace, and one HIP stream.  A step is the reference's step() (BHA:405-439) as a fixed
+// kernel sequence on that stream; the only host round trip is the merge rule's (BHA:463-532)
+// candidate mailbox, and only while heavy bodies exist.
 //
 // Multi-GPU (bh_create_dist): every rank holds the full replicated state and builds the
 // same tree (deterministically, so the jitter mutates every replica identically); force
 // evaluation is sharded by contiguous Morton ranges and the accelerations are all-gathered
-// with RCCL over xGMI, after which every rank integrates the full set.  The merge rule is
-// replicated (identical inputs, identical outcome) and needs no exchange.
+// in place with RCCL over xGMI, after which every rank integrates the full set.  The merge
+// rule is replicated (identical inputs, identical outcome) and needs no exchange.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
 #include <algorithm>
-#include <iterator>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <iterator>
 #include <string>
 #include <unordered_map>
 #include <unordered_set>
@@ -30,14 +30,7 @@
 using namespace bh;
 
 namespace {
-
 constexpr int kPhases = 5;  // build, traverse, integrate, merge, allgather
-
-struct DevArray {
-    void *p = nullptr;
-    size_t bytes = 0;
-};
-
 }  // namespace
 
 struct bh_engine {
@@ -48,25 +41,25 @@ struct bh_engine {
     int rank = 0, world = 1;
     ncclComm_t comm = nullptr;
 
-    int64_t n = 0;    // live bodies
-    int64_t cap = 0;  // allocated bodies
-    int J_alloc = -1; // J the node array was sized for
+    int64_t n = 0;     // live bodies
+    int64_t cap = 0;   // allocated bodies
+    int J_alloc = -1;  // J the node array was sized for
 
-    double *x = nullptr, *y = nullptr, *vx = nullptr, *vy = nullptr, *m = nullptr;
-    double *alt[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};  // compaction targets
-    double *ax = nullptr, *ay = nullptr;
-    double *a_sorted = nullptr;
+    BodyState st{};   // current state, slot (Morton) order
+    BodyState alt{};  // second buffer: build / compaction target, copy-out staging
+    double *a2 = nullptr;  // interleaved accelerations (slot order), 2 * chunk * world
+    double *ax = nullptr, *ay = nullptr;  // caller-order copy-out staging
 
     uint64_t *keys = nullptr, *keys_s = nullptr;
     uint32_t *idx = nullptr, *perm = nullptr;
-    double *sx = nullptr, *sy = nullptr, *sm = nullptr;
     int8_t *cpl = nullptr;
     uint32_t *cnt = nullptr, *base = nullptr;
+    uint32_t *cell_start = nullptr;
     Node *nodes = nullptr;
     size_t node_cap = 0;
     uint32_t *span_cnt = nullptr, *span_list = nullptr;
     uint4 *span_children = nullptr;
-    uint32_t *scalars = nullptr;  // [0] unused, [1] error flags, [2] heavy count, [3] pair count
+    uint32_t *scalars = nullptr;  // [1] tree error flags
     uint32_t *visits32 = nullptr;
     uint32_t *wave_iters = nullptr;  // per-wave union of visited nodes (diagnostics)
     int64_t stat_lane_visits = 0, stat_wave_iters = 0, stat_waves = 0;
@@ -74,26 +67,24 @@ struct bh_engine {
     // merge
     uint32_t *heavy = nullptr;
     uint32_t *keep = nullptr, *pos = nullptr;
-    MergePair *pairs = nullptr;
-    uint32_t pair_cap = 0;
-    uint32_t *mdead = nullptr, *mupd = nullptr;
-    double *mupd_mass = nullptr, *hmass = nullptr;
+    MergePair *box = nullptr;  // mailbox: header + pairs
+    uint32_t box_cap = 0;
+    uint32_t *mdead = nullptr, *mupd = nullptr, *mdead_cidx = nullptr;
+    double *mupd_mass = nullptr;
     uint32_t mcap = 0;
-    int64_t heavy_count = -1;  // -1: unknown (recompute)
-    std::vector<std::vector<uint32_t>> step_dead;  // per-step removals of the last bh_step
-    std::vector<uint32_t> h_heavy;  // host copy of the ordered heavy list
-    std::vector<double> h_hmass;    // and of the heavy bodies' masses
-    void *pin = nullptr;            // pinned staging for the merge mailbox / uploads
+    bool heavy_possible = true;  // false once a step saw no heavy body (heavies never appear)
+    std::vector<std::vector<uint32_t>> step_dead;  // per-step removals (caller indices)
+    void *pin = nullptr;  // pinned staging for the mailbox / uploads
     size_t pin_bytes = 0;
 
     void *cub_tmp = nullptr;
     size_t cub_bytes = 0;
 
-    bool tree_valid = false;  // lastTree (BHA:304)
+    bool tree_valid = false;  // lastTree (BHA:304): keys_s / cpl / base / nodes are current
 
     // profiling
     bool profiling = false;
-    std::vector<hipEvent_t> ev;  // pairs (start, stop) per phase interval
+    std::vector<hipEvent_t> ev;
     std::vector<int> ev_phase;
     size_t ev_used = 0;
     double phase_ms[kPhases] = {0, 0, 0, 0, 0};
@@ -172,43 +163,38 @@ int dev_alloc(bh_engine *e, T *&ptr, size_t count) {
     return BH_OK;
 }
 
+int alloc_state(bh_engine *e, BodyState &s, size_t cap) {
+    TRY(dev_alloc(e, s.x, cap));
+    TRY(dev_alloc(e, s.y, cap));
+    TRY(dev_alloc(e, s.vx, cap));
+    TRY(dev_alloc(e, s.vy, cap));
+    TRY(dev_alloc(e, s.m, cap));
+    TRY(dev_alloc(e, s.cidx, cap));
+    return BH_OK;
+}
+
 size_t node_capacity(int64_t n, int J) {
     // T = sum_a (1 + max(0, c(a) - c(a-1))) <= n + (J+1) * (n/2 + 2)
     return (size_t)n + (size_t)(J + 1) * ((size_t)n / 2 + 2) + 16;
 }
 
+// Capacity for n bodies.  Growing drops the live state (callers reset it); a change of the
+// jitter depth J only re-sizes the tree workspace.
 int ensure_capacity(bh_engine *e, int64_t n) {
     const int J = e->geo.J;
     if (n <= e->cap && J == e->J_alloc) return BH_OK;
-    int64_t cap = std::max<int64_t>(n, std::max<int64_t>(e->cap, 1));
-    if (n > e->cap) {
-        // keep the live state across a growth
-        std::vector<double> keep5[5];
-        if (e->n > 0 && e->x) {
-            double *src[5] = {e->x, e->y, e->vx, e->vy, e->m};
-            for (int k = 0; k < 5; ++k) {
-                keep5[k].resize((size_t)e->n);
-                HIPCHK(e, hipMemcpy(keep5[k].data(), src[k], sizeof(double) * e->n,
-                                    hipMemcpyDeviceToHost));
-            }
-        }
-        TRY(dev_alloc(e, e->x, cap));
-        TRY(dev_alloc(e, e->y, cap));
-        TRY(dev_alloc(e, e->vx, cap));
-        TRY(dev_alloc(e, e->vy, cap));
-        TRY(dev_alloc(e, e->m, cap));
-        for (int k = 0; k < 5; ++k) TRY(dev_alloc(e, e->alt[k], cap));
+    const int64_t cap = std::max<int64_t>(n, std::max<int64_t>(e->cap, 1));
+    if (n > e->cap || !e->st.x) {
+        TRY(alloc_state(e, e->st, cap));
+        TRY(alloc_state(e, e->alt, cap));
+        const int64_t chunk = (cap + e->world - 1) / e->world;
+        TRY(dev_alloc(e, e->a2, 2 * chunk * e->world));
         TRY(dev_alloc(e, e->ax, cap));
         TRY(dev_alloc(e, e->ay, cap));
-        int64_t chunk = (cap + e->world - 1) / e->world;
-        TRY(dev_alloc(e, e->a_sorted, 2 * chunk * e->world));
         TRY(dev_alloc(e, e->keys, cap));
         TRY(dev_alloc(e, e->keys_s, cap));
         TRY(dev_alloc(e, e->idx, cap));
         TRY(dev_alloc(e, e->perm, cap));
-        TRY(dev_alloc(e, e->sx, cap));
-        TRY(dev_alloc(e, e->sy, cap));
-        TRY(dev_alloc(e, e->sm, cap));
         TRY(dev_alloc(e, e->cpl, cap + 32));  // slack for word-wise scans
         TRY(dev_alloc(e, e->cnt, cap + 1));
         TRY(dev_alloc(e, e->base, cap + 1));
@@ -217,12 +203,6 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(dev_alloc(e, e->heavy, cap));
         TRY(dev_alloc(e, e->keep, cap));
         TRY(dev_alloc(e, e->pos, cap));
-        if (e->n > 0 && !keep5[0].empty()) {
-            double *dst[5] = {e->x, e->y, e->vx, e->vy, e->m};
-            for (int k = 0; k < 5; ++k)
-                HIPCHK(e, hipMemcpy(dst[k], keep5[k].data(), sizeof(double) * e->n,
-                                    hipMemcpyHostToDevice));
-        }
         e->cap = cap;
     }
     size_t ncap = node_capacity(e->cap, J);
@@ -231,10 +211,12 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(dev_alloc(e, e->span_cnt, (size_t)J + 2));
         TRY(dev_alloc(e, e->span_list, (size_t)(J + 2) * span_stride_for(e->cap)));
         TRY(dev_alloc(e, e->span_children, (size_t)(J + 2) * span_stride_for(e->cap)));
+        TRY(dev_alloc(e, e->cell_start,
+                      ((size_t)1 << (2 * std::min(J, CELL_TABLE_MAX_DEPTH))) + 2));
         e->node_cap = ncap;
         e->J_alloc = J;
     }
-    size_t cb = std::max(tree_cub_bytes(e->cap, J), merge_cub_bytes(e->cap));
+    size_t cb = std::max(tree_cub_bytes(e->cap, J), compact_cub_bytes(e->cap));
     if (cb > e->cub_bytes) {
         if (e->cub_tmp) (void)hipFree(e->cub_tmp);
         e->cub_tmp = nullptr;
@@ -246,19 +228,16 @@ int ensure_capacity(bh_engine *e, int64_t n) {
 
 TreeBuffers tree_buffers(bh_engine *e) {
     TreeBuffers b;
-    b.x = e->x;
-    b.y = e->y;
-    b.m = e->m;
+    b.src = e->st;
+    b.dst = e->alt;
     b.keys = e->keys;
     b.keys_s = e->keys_s;
     b.idx = e->idx;
     b.perm = e->perm;
-    b.sx = e->sx;
-    b.sy = e->sy;
-    b.sm = e->sm;
     b.cpl = e->cpl;
     b.cnt = e->cnt;
     b.base = e->base;
+    b.cell_start = e->cell_start;
     b.nodes = e->nodes;
     b.scalars = e->scalars;
     b.span_cnt = e->span_cnt;
@@ -307,31 +286,39 @@ int collect_timings(bh_engine *e) {
     return BH_OK;
 }
 
+// ---- buildTree() (BHA:359-366): sort + build; the state moves to the new Morton order ----
+int build(bh_engine *e) {
+    const int64_t n = e->n;
+    HIPCHK(e, tree_build(tree_buffers(e), n, e->geo, e->stream));
+    if (n > 0) std::swap(e->st, e->alt);
+    e->tree_valid = true;
+    return BH_OK;
+}
+
 // ---- one force evaluation: buildTree() + computeAccelerations() (BHA:359-395) -------------
 int evaluate(bh_engine *e, uint32_t *visits) {
     const int64_t n = e->n;
     TRY(mark(e, -1));
-    HIPCHK(e, tree_build(tree_buffers(e), n, e->geo, e->stream));
+    TRY(build(e));
     TRY(mark(e, 0));
     ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};  // BHA:378
     const uint32_t *d_T = e->base + n;
     if (e->world == 1 || visits) {
-        traverse(e->nodes, d_T, e->sx, e->sy, e->sm, e->perm, 0, n, e->geo, fp, e->ax, e->ay,
-                 nullptr, visits, e->wave_iters, e->stream);
+        traverse(e->nodes, d_T, e->st.x, e->st.y, e->st.m, 0, n, e->geo, fp, e->a2, visits,
+                 e->wave_iters, e->stream);
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
     } else {
-        int64_t chunk = (n + e->world - 1) / e->world;
+        const int64_t chunk = (n + e->world - 1) / e->world;
         int64_t lo = 0, hi = 0;
         bh_shard_range(n, e->rank, e->world, &lo, &hi);
-        traverse(e->nodes, d_T, e->sx, e->sy, e->sm, e->perm, lo, hi, e->geo, fp, e->ax, e->ay,
-                 e->a_sorted, nullptr, nullptr, e->stream);
+        traverse(e->nodes, d_T, e->st.x, e->st.y, e->st.m, lo, hi, e->geo, fp, e->a2, nullptr,
+                 nullptr, e->stream);
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
-        NCCLCHK(e, ncclAllGather(e->a_sorted + 2 * e->rank * chunk, e->a_sorted, (size_t)(2 * chunk),
+        // in place: rank r's chunk already sits at a2 + 2 * r * chunk
+        NCCLCHK(e, ncclAllGather(e->a2 + 2 * e->rank * chunk, e->a2, (size_t)(2 * chunk),
                                  ncclDouble, e->comm, e->stream));
-        scatter_sorted_acc(e->a_sorted, e->perm, n, e->ax, e->ay, e->stream);
-        HIPCHK(e, hipGetLastError());
         TRY(mark(e, 4));
     }
     return BH_OK;
@@ -350,11 +337,12 @@ int check_tree_flags(bh_engine *e) {
 }
 
 // ---- merge rule (BHA:463-532) ---------------------------------------------------------
-// Heavy bodies (m > mergeMaxMass) only ever gain mass and are few, so the host keeps their
-// ordered index list and masses; the device finds candidate pairs (d^2 < minD^2) with one
-// kernel and posts them to a small mailbox that is copied back with ONE async copy into
-// pinned memory — one host round trip per step.  The host replays the reference's
-// sequential rule exactly over those pairs and the device applies removals by compaction.
+// The device lists heavy bodies (m > mergeMaxMass) and every (heavy, body) pair closer than
+// mergeMinDist into a small mailbox that comes back with ONE async copy into pinned memory:
+// one host round trip per step.  The host replays the reference's sequential rule exactly
+// over those pairs (list order = caller index), the device applies the removals by an
+// order-preserving compaction.  Heavy bodies only gain mass and never appear, so once a step
+// sees none the rule is skipped until the bodies or mergeMaxMass change.
 constexpr uint32_t kMailboxPairs = 2048;
 
 int pinned_reserve(bh_engine *e, size_t bytes) {
@@ -367,180 +355,134 @@ int pinned_reserve(bh_engine *e, size_t bytes) {
     return BH_OK;
 }
 
-int merge_bufs(bh_engine *e, uint32_t need) {  // dead / update / mass staging on the device
+int merge_bufs(bh_engine *e, uint32_t need) {
     if (need <= e->mcap && e->mdead) return BH_OK;
     e->mcap = std::max<uint32_t>(need, 64) * 2;
     TRY(dev_alloc(e, e->mdead, e->mcap));
+    TRY(dev_alloc(e, e->mdead_cidx, e->mcap));
     TRY(dev_alloc(e, e->mupd, e->mcap));
     TRY(dev_alloc(e, e->mupd_mass, e->mcap));
-    TRY(dev_alloc(e, e->hmass, e->mcap));
-    return BH_OK;
-}
-
-int refresh_heavy_list(bh_engine *e) {  // ordered list of m > mergeMaxMass (BHA:474)
-    const int64_t n = e->n;
-    HIPCHK(e, heavy_list(e->m, n, e->p.merge_max_mass, e->heavy, e->scalars + 2, e->cub_tmp,
-                         e->cub_bytes, e->stream));
-    uint32_t hc = 0;
-    HIPCHK(e, hipMemcpyAsync(&hc, e->scalars + 2, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                             e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    e->h_heavy.resize(hc);
-    e->h_hmass.resize(hc);
-    if (hc > 0) {
-        TRY(merge_bufs(e, hc));
-        gather_doubles(e->heavy, hc, e->m, e->hmass, e->stream);
-        HIPCHK(e, hipMemcpyAsync(e->h_heavy.data(), e->heavy, sizeof(uint32_t) * hc,
-                                 hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->h_hmass.data(), e->hmass, sizeof(double) * hc,
-                                 hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(e, hipStreamSynchronize(e->stream));
-    }
-    e->heavy_count = hc;
     return BH_OK;
 }
 
 int merge(bh_engine *e) {
-    if (e->p.merge_min_dist <= 0.0 || e->n <= 1) return BH_OK;  // BHA:465
+    if (e->p.merge_min_dist <= 0.0 || e->n <= 1 || !e->heavy_possible) return BH_OK;  // BHA:465
     TRY(mark(e, -1));
     const int64_t n = e->n;
-    if (e->heavy_count < 0) TRY(refresh_heavy_list(e));
-    const uint32_t H = (uint32_t)e->heavy_count;
-    if (H == 0) {
-        TRY(mark(e, 3));
-        return BH_OK;
-    }
     const double minD2 = e->p.merge_min_dist * e->p.merge_min_dist;  // BHA:468
-    if (e->pair_cap == 0) {
-        e->pair_cap = 1u << 16;
-        TRY(dev_alloc(e, e->pairs, e->pair_cap + 1));
+    if (e->box_cap == 0) {
+        e->box_cap = 1u << 16;
+        TRY(dev_alloc(e, e->box, e->box_cap + 1));
     }
-    // mailbox = pairs[0] (count in .k) followed by up to pair_cap pairs
-    MergePair *box = e->pairs;
     const size_t fast_bytes = sizeof(MergePair) * (1 + kMailboxPairs);
-    TRY(pinned_reserve(e, std::max(fast_bytes, sizeof(MergePair) * (1 + (size_t)e->pair_cap))));
-    uint32_t count = 0;
+    TRY(pinned_reserve(e, sizeof(MergePair) * (1 + (size_t)e->box_cap)));
+    uint32_t count = 0, heavies = 0;
     for (;;) {
-        merge_candidates(n, e->x, e->y, e->m, e->heavy, H, minD2, box + 1, e->pair_cap,
-                         &box->k, e->stream);
+        merge_candidates(n, e->st.x, e->st.y, e->st.m, e->st.cidx, e->p.merge_max_mass, minD2,
+                         e->heavy, e->box, e->box_cap, e->stream);
         HIPCHK(e, hipGetLastError());
-        HIPCHK(e, hipMemcpyAsync(e->pin, box, fast_bytes, hipMemcpyDeviceToHost, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->pin, e->box, fast_bytes, hipMemcpyDeviceToHost, e->stream));
         HIPCHK(e, hipStreamSynchronize(e->stream));  // the one round trip of the step
-        count = reinterpret_cast<MergePair *>(e->pin)->k;
-        if (count <= e->pair_cap) break;
-        e->pair_cap = count + (count >> 1);
-        TRY(dev_alloc(e, e->pairs, e->pair_cap + 1));
-        box = e->pairs;
-        TRY(pinned_reserve(e, sizeof(MergePair) * (1 + (size_t)e->pair_cap)));
+        const MergeHeader *h = reinterpret_cast<const MergeHeader *>(e->pin);
+        count = h->pairs;
+        heavies = h->heavies;
+        if (count <= e->box_cap) break;
+        e->box_cap = count + (count >> 1);
+        TRY(dev_alloc(e, e->box, e->box_cap + 1));
+        TRY(pinned_reserve(e, sizeof(MergePair) * (1 + (size_t)e->box_cap)));
     }
+    if (heavies == 0) e->heavy_possible = false;
     if (count == 0) {
         TRY(mark(e, 3));
         return BH_OK;
     }
     if (count > kMailboxPairs) {
-        HIPCHK(e, hipMemcpyAsync(e->pin, box, sizeof(MergePair) * (1 + (size_t)count),
+        HIPCHK(e, hipMemcpyAsync(e->pin, e->box, sizeof(MergePair) * (1 + (size_t)count),
                                  hipMemcpyDeviceToHost, e->stream));
         HIPCHK(e, hipStreamSynchronize(e->stream));
     }
     const MergePair *pp = reinterpret_cast<const MergePair *>(e->pin) + 1;
     std::vector<MergePair> pr(pp, pp + count);
     std::sort(pr.begin(), pr.end(), [](const MergePair &a, const MergePair &b) {
-        return a.k != b.k ? a.k < b.k : a.j < b.j;
+        return a.h_cidx != b.h_cidx ? a.h_cidx < b.h_cidx : a.v_cidx < b.v_cidx;
     });
-    // Sequential replay of BHA:470-531.  Heavy bodies are visited in list order; a heavy body
-    // eaten earlier is skipped; victims are absorbed in descending index order (BHA:514-519).
-    const std::vector<uint32_t> &hv = e->h_heavy;
-    std::unordered_map<uint32_t, uint32_t> heavy_pos;
-    for (uint32_t k = 0; k < H; ++k) heavy_pos[hv[k]] = k;
-    std::vector<double> cur = e->h_hmass;
-    std::vector<char> heavy_dead(H, 0);
+    // Sequential replay of BHA:470-531: heavy bodies in list order; one already absorbed is
+    // skipped; victims absorbed in descending list index (BHA:514-519); a heavy victim
+    // carries the mass it has grown to.
+    std::unordered_map<uint32_t, double> mass;    // current masses of involved bodies
+    std::unordered_map<uint32_t, uint32_t> slot;  // caller index -> slot
+    for (const MergePair &c : pr) {
+        if (!mass.count(c.h_cidx)) mass[c.h_cidx] = c.h_mass;
+        if (!mass.count(c.v_cidx)) mass[c.v_cidx] = c.v_mass;
+        slot[c.h_cidx] = c.h_slot;
+        slot[c.v_cidx] = c.v_slot;
+    }
     std::unordered_set<uint32_t> dead;
-    std::vector<uint32_t> dead_list;
-    size_t pi = 0;
-    for (uint32_t k = 0; k < H; ++k) {
+    std::vector<uint32_t> dead_cidx;
+    std::vector<uint32_t> grown;  // heavy caller indices whose mass changed
+    for (size_t pi = 0; pi < pr.size();) {
         size_t pe = pi;
-        while (pe < pr.size() && pr[pe].k == k) ++pe;
-        if (!heavy_dead[k]) {  // bi still in the list; its mass only grew: still heavy
-            double mi = cur[k];
+        const uint32_t hi = pr[pi].h_cidx;
+        while (pe < pr.size() && pr[pe].h_cidx == hi) ++pe;
+        if (!dead.count(hi)) {  // bi still in the list; its mass only grew: still heavy
+            double mi = mass[hi];
+            bool any = false;
             for (size_t q = pe; q > pi; --q) {
-                const MergePair &c = pr[q - 1];
-                if (dead.count(c.j)) continue;
-                auto it = heavy_pos.find(c.j);
-                double mj = c.mj;
-                if (it != heavy_pos.end()) {  // a heavy victim carries its grown mass
-                    mj = cur[it->second];
-                    heavy_dead[it->second] = 1;
-                }
-                mi += mj;  // BHA:518
-                dead.insert(c.j);
-                dead_list.push_back(c.j);
+                const uint32_t vj = pr[q - 1].v_cidx;
+                if (dead.count(vj)) continue;
+                mi += mass[vj];  // BHA:518
+                dead.insert(vj);
+                dead_cidx.push_back(vj);
+                any = true;
             }
-            cur[k] = mi;
+            if (any) {
+                mass[hi] = mi;
+                grown.push_back(hi);
+            }
         }
         pi = pe;
     }
-    if (dead_list.empty()) {
+    if (dead_cidx.empty()) {
         TRY(mark(e, 3));
         return BH_OK;
     }
-    std::sort(dead_list.begin(), dead_list.end());
-    // upload: dead list | updated heavy (index, mass) | new heavy list, from pinned memory
-    std::vector<uint32_t> upd;
+    std::sort(dead_cidx.begin(), dead_cidx.end());
+    std::vector<uint32_t> dead_slot, upd_slot;
     std::vector<double> upd_mass;
-    std::vector<uint32_t> new_heavy;
-    std::vector<double> new_hmass;
-    for (uint32_t k = 0; k < H; ++k) {
-        if (heavy_dead[k]) continue;
-        const uint32_t hi = hv[k];
-        if (std::memcmp(&cur[k], &e->h_hmass[k], sizeof(double)) != 0) {
-            upd.push_back(hi);
-            upd_mass.push_back(cur[k]);
+    for (uint32_t c : dead_cidx) dead_slot.push_back(slot[c]);
+    for (uint32_t h : grown)
+        if (!dead.count(h)) {
+            upd_slot.push_back(slot[h]);
+            upd_mass.push_back(mass[h]);
         }
-        // index after removal of every dead body before it (list order is preserved)
-        uint32_t shift = (uint32_t)(std::lower_bound(dead_list.begin(), dead_list.end(), hi) -
-                                    dead_list.begin());
-        new_heavy.push_back(hi - shift);
-        new_hmass.push_back(cur[k]);
-    }
-    const uint32_t nd = (uint32_t)dead_list.size(), nu = (uint32_t)upd.size(),
-                   nh = (uint32_t)new_heavy.size();
-    TRY(merge_bufs(e, std::max<uint32_t>(std::max(nd, nu), nh)));
-    size_t up_bytes = 4 * (size_t)nd + 4 * (size_t)nu + 8 * (size_t)nu + 4 * (size_t)nh + 64;
-    TRY(pinned_reserve(e, up_bytes + sizeof(MergePair) * (1 + (size_t)count)));
+    const uint32_t nd = (uint32_t)dead_cidx.size(), nu = (uint32_t)upd_slot.size();
+    TRY(merge_bufs(e, std::max(nd, nu)));
+    // upload from pinned memory (the mailbox bytes were consumed above)
+    TRY(pinned_reserve(e, 4 * (size_t)(2 * nd + nu) + 8 * (size_t)nu + 64));
     char *u = static_cast<char *>(e->pin);
-    uint32_t *u_dead = reinterpret_cast<uint32_t *>(u);
-    uint32_t *u_upd = u_dead + nd;
-    uint32_t *u_heavy = u_upd + nu;
-    double *u_mass = reinterpret_cast<double *>(
-        u + (((4 * (size_t)(nd + nu + nh)) + 7) & ~(size_t)7));
-    std::memcpy(u_dead, dead_list.data(), 4 * (size_t)nd);
-    std::memcpy(u_upd, upd.data(), 4 * (size_t)nu);
-    std::memcpy(u_heavy, new_heavy.data(), 4 * (size_t)nh);
+    double *u_mass = reinterpret_cast<double *>(u);
+    uint32_t *u_dslot = reinterpret_cast<uint32_t *>(u + 8 * (size_t)nu);
+    uint32_t *u_dcidx = u_dslot + nd;
+    uint32_t *u_uslot = u_dcidx + nd;
     std::memcpy(u_mass, upd_mass.data(), 8 * (size_t)nu);
-    HIPCHK(e, hipMemcpyAsync(e->mdead, u_dead, 4 * (size_t)nd, hipMemcpyHostToDevice, e->stream));
+    std::memcpy(u_dslot, dead_slot.data(), 4 * (size_t)nd);
+    std::memcpy(u_dcidx, dead_cidx.data(), 4 * (size_t)nd);
+    std::memcpy(u_uslot, upd_slot.data(), 4 * (size_t)nu);
+    HIPCHK(e, hipMemcpyAsync(e->mdead, u_dslot, 4 * (size_t)nd, hipMemcpyHostToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(e->mdead_cidx, u_dcidx, 4 * (size_t)nd, hipMemcpyHostToDevice,
+                             e->stream));
     if (nu) {
-        HIPCHK(e, hipMemcpyAsync(e->mupd, u_upd, 4 * (size_t)nu, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->mupd, u_uslot, 4 * (size_t)nu, hipMemcpyHostToDevice, e->stream));
         HIPCHK(e, hipMemcpyAsync(e->mupd_mass, u_mass, 8 * (size_t)nu, hipMemcpyHostToDevice,
                                  e->stream));
     }
     HIPCHK(e, hipMemsetD32Async((hipDeviceptr_t)e->keep, 1, (size_t)n, e->stream));
-    apply_merge(nd, e->mdead, nu, e->mupd, e->mupd_mass, e->keep, e->m, e->stream);
-    const double *src[5] = {e->x, e->y, e->vx, e->vy, e->m};
-    double *dst[5] = {e->alt[0], e->alt[1], e->alt[2], e->alt[3], e->alt[4]};
-    HIPCHK(e, compact_bodies(n, e->keep, src, dst, e->pos, nullptr, e->cub_tmp, e->cub_bytes,
-                             e->stream));
-    if (nh) HIPCHK(e, hipMemcpyAsync(e->heavy, u_heavy, 4 * (size_t)nh, hipMemcpyHostToDevice,
-                                     e->stream));
-    std::swap(e->x, e->alt[0]);
-    std::swap(e->y, e->alt[1]);
-    std::swap(e->vx, e->alt[2]);
-    std::swap(e->vy, e->alt[3]);
-    std::swap(e->m, e->alt[4]);
+    apply_merge(nd, e->mdead, nu, e->mupd, e->mupd_mass, e->keep, e->st.m, e->stream);
+    HIPCHK(e, compact_state(n, e->keep, e->st, e->alt, e->mdead_cidx, nd, e->pos, e->cub_tmp,
+                            e->cub_bytes, e->stream));
+    std::swap(e->st, e->alt);
     e->n = n - (int64_t)nd;
-    e->step_dead.push_back(dead_list);
-    e->h_heavy = std::move(new_heavy);
-    e->h_hmass = std::move(new_hmass);
-    e->heavy_count = nh;
+    e->step_dead.push_back(dead_cidx);
     e->tree_valid = false;  // BHA:526
     TRY(mark(e, 3));
     return BH_OK;
@@ -553,12 +495,12 @@ int step_once(bh_engine *e) {
     if (n > 0) {
         TRY(evaluate(e, nullptr));  // a(t)
         TRY(mark(e, -1));
-        kick_drift(n, e->ax, e->ay, e->x, e->y, e->vx, e->vy, dtHalf, e->p.dt, e->stream);
+        kick_drift(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->p.dt, e->stream);
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 2));
         TRY(evaluate(e, nullptr));  // a(t+dt)
         TRY(mark(e, -1));
-        kick(n, e->ax, e->ay, e->vx, e->vy, dtHalf, e->stream);
+        kick(n, e->a2, e->st.vx, e->st.vy, dtHalf, e->stream);
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 2));
         e->tree_valid = true;  // lastTree = root (BHA:435)
@@ -633,12 +575,12 @@ struct QuadWalker {
 };
 
 void set_defaults(bh_params *p) {
-    p->G = 80.0;               // CFG:11
-    p->dt = 0.005;             // CFG:14
-    p->theta = 0.30;           // CFG:23
-    p->soft2 = 1.0 * 1.0;      // CFG:17,20
-    p->width_px = 2400;        // CFG:5
-    p->height_px = 800;        // CFG:8
+    p->G = 80.0;                 // CFG:11
+    p->dt = 0.005;               // CFG:14
+    p->theta = 0.30;             // CFG:23
+    p->soft2 = 1.0 * 1.0;        // CFG:17,20
+    p->width_px = 2400;          // CFG:5
+    p->height_px = 800;          // CFG:8
     p->merge_max_mass = 4000.0;  // BHA:315
     p->merge_min_dist = 8.0;     // BHA:321 = Config.MIN_R (CFG:35)
 }
@@ -657,6 +599,12 @@ int engine_init(bh_engine *e, const bh_params *p, int device) {
     HIPCHK(e, hipMemset(e->scalars, 0, 16 * sizeof(uint32_t)));
     TRY(ensure_capacity(e, 1));
     return BH_OK;
+}
+
+void free_state(BodyState &s) {
+    void *p[] = {s.x, s.y, s.vx, s.vy, s.m, s.cidx};
+    for (void *q : p)
+        if (q) (void)hipFree(q);
 }
 
 }  // namespace
@@ -723,12 +671,12 @@ void bh_destroy(bh_engine *e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->comm) (void)ncclCommDestroy(e->comm);
-    void *ptrs[] = {e->x, e->y, e->vx, e->vy, e->m, e->alt[0], e->alt[1], e->alt[2], e->alt[3],
-                    e->alt[4], e->ax, e->ay, e->a_sorted, e->keys, e->keys_s, e->idx, e->perm,
-                    e->sx, e->sy, e->sm, e->cpl, e->cnt, e->base, e->nodes, e->scalars,
-                    e->span_cnt, e->span_list, e->span_children,
-                    e->visits32, e->wave_iters, e->heavy, e->keep, e->pos, e->pairs, e->mdead, e->mupd,
-                    e->mupd_mass, e->hmass, e->cub_tmp};
+    free_state(e->st);
+    free_state(e->alt);
+    void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->idx, e->perm, e->cpl, e->cnt,
+                    e->base, e->cell_start, e->nodes, e->span_cnt, e->span_list,
+                    e->span_children, e->scalars, e->visits32, e->wave_iters, e->heavy, e->keep,
+                    e->pos, e->box, e->mdead, e->mdead_cidx, e->mupd, e->mupd_mass, e->cub_tmp};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     for (hipEvent_t ev : e->ev) (void)hipEventDestroy(ev);
@@ -744,13 +692,17 @@ int bh_set_params(bh_engine *e, const bh_params *p) {
     Geometry g;
     TRY(make_geometry(*p, g, e->err));
     HIPCHK(e, hipSetDevice(e->device));
-    bool geo_changed = std::memcmp(&g, &e->geo, sizeof(g)) != 0;
-    if (p->merge_max_mass != e->p.merge_max_mass) e->heavy_count = -1;
+    const bool geo_changed = std::memcmp(&g, &e->geo, sizeof(g)) != 0;
+    if (p->merge_max_mass != e->p.merge_max_mass || p->merge_min_dist != e->p.merge_min_dist)
+        e->heavy_possible = true;
     e->p = *p;
-    e->geo = g;
     if (geo_changed) {
+        e->geo = g;
         e->tree_valid = false;
-        TRY(ensure_capacity(e, e->n));
+        if (g.J != e->J_alloc) {  // tree workspace sized for another depth; the state stays
+            HIPCHK(e, hipStreamSynchronize(e->stream));
+            TRY(ensure_capacity(e, e->n));
+        }
     }
     return BH_OK;
 }
@@ -770,18 +722,20 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     }
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    e->n = 0;  // old state is replaced, do not preserve it across a growth
     TRY(ensure_capacity(e, n));
-    if (n > 0) {
-        HIPCHK(e, hipMemcpyAsync(e->x, x, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->y, y, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->vx, vx, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->vy, vy, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->m, m, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
+    if (n > 0) {  // slot order = caller order until the first build
+        HIPCHK(e, hipMemcpyAsync(e->st.x, x, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->st.y, y, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->st.vx, vx, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->st.vy, vy, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->st.m, m, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
+        iota_u32(e->st.cidx, n, e->stream);
+        HIPCHK(e, hipGetLastError());
     }
     HIPCHK(e, hipStreamSynchronize(e->stream));
     e->n = n;
-    e->heavy_count = -1;
+    e->heavy_possible = true;
+    e->step_dead.clear();
     e->tree_valid = false;  // BHA:348
     return BH_OK;
 }
@@ -808,12 +762,18 @@ int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, do
     if (n_out) *n_out = e->n;
     if (cap < e->n) return BH_E_CAPACITY;
     HIPCHK(e, hipSetDevice(e->device));
-    double *dst[5] = {x, y, vx, vy, m};
-    double *src[5] = {e->x, e->y, e->vx, e->vy, e->m};
-    for (int k = 0; k < 5; ++k)
-        if (dst[k] && e->n > 0)
-            HIPCHK(e, hipMemcpyAsync(dst[k], src[k], sizeof(double) * e->n, hipMemcpyDeviceToHost,
-                                     e->stream));
+    const int64_t n = e->n;
+    if (n > 0) {  // back to caller (list) order, staged in the second state buffer
+        const double *src[5] = {e->st.x, e->st.y, e->st.vx, e->st.vy, e->st.m};
+        double *stage[5] = {e->alt.x, e->alt.y, e->alt.vx, e->alt.vy, e->alt.m};
+        scatter_to_caller(n, e->st.cidx, 5, src, stage, e->stream);
+        HIPCHK(e, hipGetLastError());
+        double *dst[5] = {x, y, vx, vy, m};
+        for (int k = 0; k < 5; ++k)
+            if (dst[k])
+                HIPCHK(e, hipMemcpyAsync(dst[k], stage[k], sizeof(double) * n,
+                                         hipMemcpyDeviceToHost, e->stream));
+    }
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return BH_OK;
 }
@@ -827,17 +787,19 @@ int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visi
     HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
     if (n > 0) {
         TRY(evaluate(e, visits ? e->visits32 : nullptr));
-        e->tree_valid = true;
+        scatter_acc_to_caller(n, e->st.cidx, e->a2, e->ax, e->ay, e->stream);
+        HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipStreamSynchronize(e->stream));
         TRY(check_tree_flags(e));
         if (ax) HIPCHK(e, hipMemcpy(ax, e->ax, sizeof(double) * n, hipMemcpyDeviceToHost));
         if (ay) HIPCHK(e, hipMemcpy(ay, e->ay, sizeof(double) * n, hipMemcpyDeviceToHost));
         if (visits) {
-            std::vector<uint32_t> v((size_t)n);
+            std::vector<uint32_t> v((size_t)n), c((size_t)n);
             HIPCHK(e, hipMemcpy(v.data(), e->visits32, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
+            HIPCHK(e, hipMemcpy(c.data(), e->st.cidx, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
             int64_t lane_sum = 0;
             for (int64_t i = 0; i < n; ++i) {
-                visits[i] = v[(size_t)i];
+                visits[c[(size_t)i]] = v[(size_t)i];
                 lane_sum += v[(size_t)i];
             }
             const int64_t waves = (n + 63) / 64;
@@ -845,7 +807,7 @@ int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visi
             HIPCHK(e, hipMemcpy(wi.data(), e->wave_iters, sizeof(uint32_t) * waves,
                                 hipMemcpyDeviceToHost));
             int64_t wsum = 0;
-            for (uint32_t c : wi) wsum += c;
+            for (uint32_t w : wi) wsum += w;
             e->stat_lane_visits = lane_sum;
             e->stat_wave_iters = wsum;
             e->stat_waves = waves;
@@ -860,16 +822,14 @@ int bh_get_quads(bh_engine *e, double *cx, double *cy, double *h, int64_t cap, i
     HIPCHK(e, hipSetDevice(e->device));
     const int64_t n = e->n;
     if (!e->tree_valid) {  // getTreeForDebug builds a fresh tree (BHA:329-332)
-        if (n > 0) {
-            HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
-            HIPCHK(e, tree_build(tree_buffers(e), n, e->geo, e->stream));
-            TRY(check_tree_flags(e));
-        }
-        e->tree_valid = true;
+        HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
+        TRY(build(e));
+        if (n > 0) TRY(check_tree_flags(e));
     }
     std::vector<uint64_t> keys((size_t)n);
     std::vector<int8_t> cpl((size_t)n);
     std::vector<uint32_t> base((size_t)n + 1);
+    HIPCHK(e, hipStreamSynchronize(e->stream));
     if (n > 0) {
         HIPCHK(e, hipMemcpy(keys.data(), e->keys_s, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
         HIPCHK(e, hipMemcpy(cpl.data(), e->cpl, n, hipMemcpyDeviceToHost));

@@ -1,5 +1,5 @@
-// Kick-drift-kick integration (BHA:410-432) and the device side of the merge rule
-// (BHA:463-532).  All elementwise, coalesced, in caller (list) order.
+// Kick-drift-kick integration (BHA:410-432), caller-order copies, and the device side of the
+// merge rule (BHA:463-532).  All elementwise and coalesced over the slot (Morton) order.
 #include <hipcub/hipcub.hpp>
 
 #include "bh_device.hpp"
@@ -10,18 +10,20 @@ namespace {
 constexpr int TB = 256;
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + TB - 1) / TB); }
 
+typedef double double2_t __attribute__((ext_vector_type(2)));
+
 // BHA:412-422 fused: v += a * dtHalf; x += v * DT.  The reference runs the kick loop over
 // all bodies and then the drift loop; per body the operations are identical.
-__global__ __launch_bounds__(TB) void k_kick_drift(int64_t n, const double *__restrict__ ax,
-                                                   const double *__restrict__ ay,
+__global__ __launch_bounds__(TB) void k_kick_drift(int64_t n, const double *__restrict__ a2,
                                                    double *__restrict__ x, double *__restrict__ y,
                                                    double *__restrict__ vx,
                                                    double *__restrict__ vy, double dtHalf,
                                                    double dt) {
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
-    double vxi = vx[i] + ax[i] * dtHalf;
-    double vyi = vy[i] + ay[i] * dtHalf;
+    const double2_t a = *reinterpret_cast<const double2_t *>(a2 + 2 * i);
+    double vxi = vx[i] + a.x * dtHalf;
+    double vyi = vy[i] + a.y * dtHalf;
     vx[i] = vxi;
     vy[i] = vyi;
     x[i] = x[i] + vxi * dt;
@@ -29,132 +31,174 @@ __global__ __launch_bounds__(TB) void k_kick_drift(int64_t n, const double *__re
 }
 
 // BHA:429-432
-__global__ __launch_bounds__(TB) void k_kick(int64_t n, const double *__restrict__ ax,
-                                             const double *__restrict__ ay,
+__global__ __launch_bounds__(TB) void k_kick(int64_t n, const double *__restrict__ a2,
                                              double *__restrict__ vx, double *__restrict__ vy,
                                              double dtHalf) {
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
-    vx[i] = vx[i] + ax[i] * dtHalf;
-    vy[i] = vy[i] + ay[i] * dtHalf;
+    const double2_t a = *reinterpret_cast<const double2_t *>(a2 + 2 * i);
+    vx[i] = vx[i] + a.x * dtHalf;
+    vy[i] = vy[i] + a.y * dtHalf;
 }
 
-struct HeavyPred {
-    const double *m;
-    double thr;
-    __host__ __device__ bool operator()(const uint32_t &i) const { return m[i] > thr; }
+__global__ __launch_bounds__(TB) void k_iota(uint32_t *__restrict__ p, int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i < n) p[i] = (uint32_t)i;
+}
+
+struct Ptrs5 {
+    const double *src[5];
+    double *dst[5];
 };
 
-// BHA:493-501: for every heavy body k (list order) and every body j != heavy[k]:
-// dx*dx + dy*dy < minD2 (dx = bj.x - bi.x).  Candidates are appended in arbitrary order;
-// the host sorts and replays them in the reference's sequential order.
-__global__ __launch_bounds__(TB) void k_merge_candidates(int64_t n, const double *__restrict__ x,
-                                                         const double *__restrict__ y,
-                                                         const double *__restrict__ m,
-                                                         const uint32_t *__restrict__ heavy,
-                                                         uint32_t H, double minD2,
-                                                         MergePair *__restrict__ pairs,
-                                                         uint32_t cap, uint32_t *d_count) {
+__global__ __launch_bounds__(TB) void k_scatter_caller(int64_t n, const uint32_t *__restrict__ cidx,
+                                                       int k, Ptrs5 p) {
+    int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t o = cidx[i];
+    for (int j = 0; j < k; ++j) p.dst[j][o] = p.src[j][i];
+}
+
+__global__ __launch_bounds__(TB) void k_scatter_acc(int64_t n, const uint32_t *__restrict__ cidx,
+                                                    const double *__restrict__ a2,
+                                                    double *__restrict__ ax,
+                                                    double *__restrict__ ay) {
+    int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t o = cidx[i];
+    ax[o] = a2[2 * i];
+    ay[o] = a2[2 * i + 1];
+}
+
+// heavy bodies: m > mergeMaxMass (BHA:474), appended in any order (the host replays in list
+// order using the caller indices carried by every candidate pair)
+__global__ __launch_bounds__(TB) void k_heavy(int64_t n, const double *__restrict__ m, double thr,
+                                              uint32_t *__restrict__ heavy, MergeHeader *hdr) {
+    int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= n) return;
+    if (m[i] > thr) heavy[atomicAdd(&hdr->heavies, 1u)] = (uint32_t)i;
+}
+
+// BHA:493-501: for every heavy body h and every body j != h: dx*dx + dy*dy < minD2 with
+// dx = bj.x - bi.x.  Pairs are appended in any order; the host sorts and replays them.
+__global__ __launch_bounds__(TB) void k_candidates(int64_t n, const double *__restrict__ x,
+                                                   const double *__restrict__ y,
+                                                   const double *__restrict__ m,
+                                                   const uint32_t *__restrict__ cidx,
+                                                   const uint32_t *__restrict__ heavy,
+                                                   double minD2, MergePair *box, uint32_t cap) {
     int64_t j = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (j >= n) return;
-    double xj = x[j], yj = y[j];
+    MergeHeader *hdr = reinterpret_cast<MergeHeader *>(box);
+    const uint32_t H = __builtin_amdgcn_readfirstlane(
+        __hip_atomic_load(&hdr->heavies, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (j >= n || H == 0) return;
+    const double xj = x[j], yj = y[j];
     for (uint32_t k = 0; k < H; ++k) {
-        uint32_t hi = heavy[k];
-        if ((int64_t)hi == j) continue;
-        double dx = xj - x[hi];
-        double dy = yj - y[hi];
+        const uint32_t hs = heavy[k];
+        if ((int64_t)hs == j) continue;
+        const double dx = xj - x[hs];
+        const double dy = yj - y[hs];
         if (dx * dx + dy * dy < minD2) {
-            uint32_t slot = atomicAdd(d_count, 1u);
-            if (slot < cap) pairs[slot] = MergePair{k, (uint32_t)j, m[j]};
+            const uint32_t slot = atomicAdd(&hdr->pairs, 1u);
+            if (slot < cap) box[1 + slot] = MergePair{cidx[hs], cidx[j], hs, (uint32_t)j, m[hs], m[j]};
         }
     }
 }
 
-__global__ __launch_bounds__(TB) void k_compact_scatter(int64_t n, const uint32_t *__restrict__ keep,
-                                                        const uint32_t *__restrict__ pos,
-                                                        const double *s0, const double *s1,
-                                                        const double *s2, const double *s3,
-                                                        const double *s4, double *d0, double *d1,
-                                                        double *d2, double *d3, double *d4) {
-    int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (i >= n || !keep[i]) return;
-    uint32_t o = pos[i];
-    d0[o] = s0[i];
-    d1[o] = s1[i];
-    d2[o] = s2[i];
-    d3[o] = s3[i];
-    d4[o] = s4[i];
-}
-
 __global__ __launch_bounds__(TB) void k_apply_merge(uint32_t n_dead, const uint32_t *__restrict__ dead,
-                                                    uint32_t n_upd, const uint32_t *__restrict__ upd_idx,
+                                                    uint32_t n_upd, const uint32_t *__restrict__ upd,
                                                     const double *__restrict__ upd_mass,
-                                                    uint32_t *__restrict__ keep, double *__restrict__ m) {
+                                                    uint32_t *__restrict__ keep,
+                                                    double *__restrict__ m) {
     uint32_t i = blockIdx.x * TB + threadIdx.x;
     if (i < n_dead) keep[dead[i]] = 0u;
-    if (i < n_upd) m[upd_idx[i]] = upd_mass[i];
+    if (i < n_upd) m[upd[i]] = upd_mass[i];  // BHA:518 bi.m += bj.m (final value)
 }
 
-__global__ __launch_bounds__(TB) void k_gather(const uint32_t *__restrict__ idx, uint32_t cnt,
-                                               const double *__restrict__ src, double *__restrict__ dst) {
-    uint32_t i = blockIdx.x * TB + threadIdx.x;
-    if (i < cnt) dst[i] = src[idx[i]];
+// compaction (BHA:519 removeAt), order preserved; list indices shift past removed ones
+__global__ __launch_bounds__(TB) void k_compact(int64_t n, const uint32_t *__restrict__ keep,
+                                                const uint32_t *__restrict__ pos, BodyState src,
+                                                BodyState dst, const uint32_t *__restrict__ dead_cidx,
+                                                uint32_t n_dead) {
+    int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= n || !keep[i]) return;
+    const uint32_t o = pos[i];
+    dst.x[o] = src.x[i];
+    dst.y[o] = src.y[i];
+    dst.vx[o] = src.vx[i];
+    dst.vy[o] = src.vy[i];
+    dst.m[o] = src.m[i];
+    const uint32_t c = src.cidx[i];
+    uint32_t lo = 0, hi = n_dead;  // number of removed list indices below c
+    while (lo < hi) {
+        uint32_t mid = (lo + hi) >> 1;
+        if (dead_cidx[mid] < c) lo = mid + 1; else hi = mid;
+    }
+    dst.cidx[o] = c - lo;
 }
 
 }  // namespace
 
-void apply_merge(uint32_t n_dead, const uint32_t *dead, uint32_t n_upd, const uint32_t *upd_idx,
-                 const double *upd_mass, uint32_t *keep, double *m, hipStream_t s) {
-    uint32_t c = n_dead > n_upd ? n_dead : n_upd;
-    if (c) k_apply_merge<<<(c + TB - 1) / TB, TB, 0, s>>>(n_dead, dead, n_upd, upd_idx, upd_mass, keep, m);
+void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
+                double dtHalf, double dt, hipStream_t s) {
+    if (n > 0) k_kick_drift<<<grid_for(n), TB, 0, s>>>(n, a2, x, y, vx, vy, dtHalf, dt);
 }
 
-void gather_doubles(const uint32_t *idx, uint32_t cnt, const double *src, double *dst, hipStream_t s) {
-    if (cnt) k_gather<<<(cnt + TB - 1) / TB, TB, 0, s>>>(idx, cnt, src, dst);
+void kick(int64_t n, const double *a2, double *vx, double *vy, double dtHalf, hipStream_t s) {
+    if (n > 0) k_kick<<<grid_for(n), TB, 0, s>>>(n, a2, vx, vy, dtHalf);
 }
 
-void kick_drift(int64_t n, const double *ax, const double *ay, double *x, double *y, double *vx,
-                double *vy, double dtHalf, double dt, hipStream_t s) {
-    if (n > 0) k_kick_drift<<<grid_for(n), TB, 0, s>>>(n, ax, ay, x, y, vx, vy, dtHalf, dt);
+void iota_u32(uint32_t *p, int64_t n, hipStream_t s) {
+    if (n > 0) k_iota<<<grid_for(n), TB, 0, s>>>(p, n);
 }
 
-void kick(int64_t n, const double *ax, const double *ay, double *vx, double *vy, double dtHalf,
-          hipStream_t s) {
-    if (n > 0) k_kick<<<grid_for(n), TB, 0, s>>>(n, ax, ay, vx, vy, dtHalf);
+void scatter_to_caller(int64_t n, const uint32_t *cidx, int k, const double *const *src,
+                       double *const *dst, hipStream_t s) {
+    if (n <= 0) return;
+    Ptrs5 p{};
+    for (int j = 0; j < k && j < 5; ++j) {
+        p.src[j] = src[j];
+        p.dst[j] = dst[j];
+    }
+    k_scatter_caller<<<grid_for(n), TB, 0, s>>>(n, cidx, k < 5 ? k : 5, p);
 }
 
-size_t merge_cub_bytes(int64_t n) {
-    size_t a = 0, b = 0;
-    hipcub::CountingInputIterator<uint32_t> it(0);
-    (void)hipcub::DeviceSelect::If(nullptr, a, it, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n,
-                             HeavyPred{nullptr, 0.0});
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint32_t *)nullptr, (uint32_t *)nullptr, (int)n);
-    return a > b ? a : b;
-}
-
-hipError_t heavy_list(const double *m, int64_t n, double thr, uint32_t *heavy, uint32_t *d_count,
-                      void *tmp, size_t tmp_bytes, hipStream_t s) {
-    hipcub::CountingInputIterator<uint32_t> it(0);
-    return hipcub::DeviceSelect::If(tmp, tmp_bytes, it, heavy, d_count, (int)n, HeavyPred{m, thr}, s);
+void scatter_acc_to_caller(int64_t n, const uint32_t *cidx, const double *a2, double *ax,
+                           double *ay, hipStream_t s) {
+    if (n > 0) k_scatter_acc<<<grid_for(n), TB, 0, s>>>(n, cidx, a2, ax, ay);
 }
 
 void merge_candidates(int64_t n, const double *x, const double *y, const double *m,
-                      const uint32_t *heavy, uint32_t H, double minD2, MergePair *pairs,
-                      uint32_t cap, uint32_t *d_count, hipStream_t s) {
-    (void)hipMemsetAsync(d_count, 0, sizeof(uint32_t), s);
-    if (n > 0 && H > 0)
-        k_merge_candidates<<<grid_for(n), TB, 0, s>>>(n, x, y, m, heavy, H, minD2, pairs, cap,
-                                                      d_count);
+                      const uint32_t *cidx, double thr, double minD2, uint32_t *heavy,
+                      MergePair *box, uint32_t cap, hipStream_t s) {
+    (void)hipMemsetAsync(box, 0, sizeof(MergeHeader), s);
+    if (n <= 0) return;
+    MergeHeader *hdr = reinterpret_cast<MergeHeader *>(box);
+    k_heavy<<<grid_for(n), TB, 0, s>>>(n, m, thr, heavy, hdr);
+    k_candidates<<<grid_for(n), TB, 0, s>>>(n, x, y, m, cidx, heavy, minD2, box, cap);
 }
 
-hipError_t compact_bodies(int64_t n, const uint32_t *keep, const double *const src[5],
-                          double *const dst[5], uint32_t *pos, uint32_t *d_count, void *tmp,
-                          size_t tmp_bytes, hipStream_t s) {
-    (void)d_count;
+void apply_merge(uint32_t n_dead, const uint32_t *dead_slots, uint32_t n_upd,
+                 const uint32_t *upd_slots, const double *upd_mass, uint32_t *keep, double *m,
+                 hipStream_t s) {
+    uint32_t c = n_dead > n_upd ? n_dead : n_upd;
+    if (c) k_apply_merge<<<(c + TB - 1) / TB, TB, 0, s>>>(n_dead, dead_slots, n_upd, upd_slots,
+                                                          upd_mass, keep, m);
+}
+
+size_t compact_cub_bytes(int64_t n) {
+    size_t b = 0;
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                           (int)n);
+    return b;
+}
+
+hipError_t compact_state(int64_t n, const uint32_t *keep, const BodyState &src,
+                         const BodyState &dst, const uint32_t *dead_cidx, uint32_t n_dead,
+                         uint32_t *pos, void *tmp, size_t tmp_bytes, hipStream_t s) {
     hipError_t st = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, keep, pos, (int)n, s);
     if (st != hipSuccess) return st;
-    k_compact_scatter<<<grid_for(n), TB, 0, s>>>(n, keep, pos, src[0], src[1], src[2], src[3],
-                                                 src[4], dst[0], dst[1], dst[2], dst[3], dst[4]);
+    k_compact<<<grid_for(n), TB, 0, s>>>(n, keep, pos, src, dst, dead_cidx, n_dead);
     return hipGetLastError();
 }
 

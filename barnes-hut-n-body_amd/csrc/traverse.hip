@@ -121,23 +121,21 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
     }
 }
 
-template <bool SORTED_OUT, bool COUNT>
+template <bool COUNT>
 __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
                                                  const uint32_t *__restrict__ d_T,
-                                                 const double *__restrict__ sx,
-                                                 const double *__restrict__ sy,
-                                                 const double *__restrict__ sm,
-                                                 const uint32_t *__restrict__ perm, int64_t lo,
+                                                 const double *__restrict__ x,
+                                                 const double *__restrict__ y,
+                                                 const double *__restrict__ m, int64_t lo,
                                                  int64_t hi, ForceParams fp, Geometry g,
-                                                 double *__restrict__ ax, double *__restrict__ ay,
-                                                 double *__restrict__ a_sorted,
+                                                 double *__restrict__ a2,
                                                  uint32_t *__restrict__ visits,
                                                  uint32_t *__restrict__ wave_iters) {
     const int64_t p = lo + (int64_t)blockIdx.x * TB + threadIdx.x;
     const bool valid = p < hi;
-    const double bx = valid ? sx[p] : 0.0;
-    const double by = valid ? sy[p] : 0.0;
-    const double bm = valid ? sm[p] : 1.0;
+    const double bx = valid ? x[p] : 0.0;
+    const double by = valid ? y[p] : 0.0;
+    const double bm = valid ? m[p] : 1.0;
     const double Gm = fp.G * bm;  // (Config.G * b.m) is evaluated first (BHA:256)
     const double soft2 = fp.soft2, theta2 = fp.theta2;
     const double s2root = g.s2[0];
@@ -156,53 +154,28 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
                            niters);
     if (COUNT && (threadIdx.x & 63) == 0) wave_iters[(p - lo) >> 6] = niters;
     if (!valid) return;
-    const double rax = fx / bm;  // BHA:390-391
-    const double ray = fy / bm;
-    if (SORTED_OUT) {
-        a_sorted[2 * p] = rax;
-        a_sorted[2 * p + 1] = ray;
-    } else {
-        const uint32_t o = perm[p];
-        ax[o] = rax;
-        ay[o] = ray;
-    }
-    if (COUNT) visits[perm[p]] = nvis;
-}
-
-__global__ __launch_bounds__(TB) void k_scatter(const double *__restrict__ a_sorted,
-                                                const uint32_t *__restrict__ perm, int64_t n,
-                                                double *__restrict__ ax, double *__restrict__ ay) {
-    int64_t p = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (p >= n) return;
-    uint32_t o = perm[p];
-    ax[o] = a_sorted[2 * p];
-    ay[o] = a_sorted[2 * p + 1];
+    // BHA:390-391, interleaved (ax, ay): coalesced 16-byte stores in Morton order
+    typedef double double2_t __attribute__((ext_vector_type(2)));
+    double2_t acc;
+    acc.x = fx / bm;
+    acc.y = fy / bm;
+    *reinterpret_cast<double2_t *>(a2 + 2 * p) = acc;
+    if (COUNT) visits[p] = nvis;
 }
 
 }  // namespace
 
-void traverse(const Node *nodes, const uint32_t *d_T, const double *sx, const double *sy,
-              const double *sm, const uint32_t *perm, int64_t lo, int64_t hi, const Geometry &g,
-              const ForceParams &fp, double *ax, double *ay, double *a_sorted, uint32_t *visits,
-              uint32_t *wave_iters, hipStream_t s) {
+void traverse(const Node *nodes, const uint32_t *d_T, const double *x, const double *y,
+              const double *m, int64_t lo, int64_t hi, const Geometry &g, const ForceParams &fp,
+              double *a2, uint32_t *visits, uint32_t *wave_iters, hipStream_t s) {
     if (hi <= lo) return;
     unsigned grid = (unsigned)((hi - lo + TB - 1) / TB);
-    if (visits) {
-        k_traverse<false, true><<<grid, TB, 0, s>>>(nodes, d_T, sx, sy, sm, perm, lo, hi, fp, g, ax,
-                                                    ay, a_sorted, visits, wave_iters);
-    } else if (a_sorted) {
-        k_traverse<true, false><<<grid, TB, 0, s>>>(nodes, d_T, sx, sy, sm, perm, lo, hi, fp, g, ax,
-                                                    ay, a_sorted, visits, wave_iters);
-    } else {
-        k_traverse<false, false><<<grid, TB, 0, s>>>(nodes, d_T, sx, sy, sm, perm, lo, hi, fp, g, ax,
-                                                     ay, a_sorted, visits, wave_iters);
-    }
-}
-
-void scatter_sorted_acc(const double *a_sorted, const uint32_t *perm, int64_t n, double *ax,
-                        double *ay, hipStream_t s) {
-    if (n <= 0) return;
-    k_scatter<<<(unsigned)((n + TB - 1) / TB), TB, 0, s>>>(a_sorted, perm, n, ax, ay);
+    if (visits)
+        k_traverse<true><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2, visits,
+                                             wave_iters);
+    else
+        k_traverse<false><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2, visits,
+                                              wave_iters);
 }
 
 }  // namespace bh

@@ -9,15 +9,17 @@
 // the reference — the deterministic jitter applied when a cell with h < 1e-3 is subdivided
 // (BHA:146-151), which mutates positions and can drop bodies — is confined to the cells at
 // the first depth J with h < 1e-3 that hold >= 2 bodies.  Those "jitter cells" are replayed
-// exactly, in body-index order, by one thread each (k_jitter) after a STABLE sort.
+// exactly, in caller-list order, by one thread each (k_jitter).
 //
 // Pipeline (all on one stream, no host synchronisation):
-//   k_morton  keys (2 bits per level, J levels) + identity payload
-//   radix sort (stable)            -> keys_s, perm
-//   k_prep    gather sorted x,y,m; c(a) = common digit count of neighbours; slot counts
-//   exclusive scan                 -> base (pre-order slot of each sorted body's nodes)
-//   k_emit    internal node skeletons (depth, next) + leaf records
-//   k_jitter  replay of BHA:125-156 inside each jitter cell
+//   k_morton     keys (2 bits per level, J levels) + slot payload
+//   radix sort   (stable)                    -> keys_s, perm
+//   k_prep       state permuted into the new Morton order; c(a) = common digit count of
+//                neighbours; node slot counts
+//   exclusive scan                            -> base (pre-order slot of each body's nodes)
+//   k_cells      first sorted body of every depth-D0 cell
+//   k_emit       internal node skeletons (depth, next) + leaf records
+//   k_jitter     replay of BHA:125-156 inside each jitter cell
 //   k_com_local  centre of mass bottom-up (children 0..3 in order, BHA:184-200) for every
 //                node inside a 1024-body chunk, all levels in one launch
 //   k_com_span   the few chunk-spanning nodes, levels J..0, one workgroup
@@ -81,12 +83,9 @@ __global__ __launch_bounds__(TB) void k_morton(int64_t n, const double *__restri
 }
 
 __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *__restrict__ keys_s,
-                                             const uint32_t *__restrict__ perm,
-                                             const double *__restrict__ x,
-                                             const double *__restrict__ y,
-                                             const double *__restrict__ m, double *__restrict__ sx,
-                                             double *__restrict__ sy, double *__restrict__ sm,
-                                             int8_t *__restrict__ cpl, uint32_t *__restrict__ cnt) {
+                                             const uint32_t *__restrict__ perm, BodyState src,
+                                             BodyState dst, int8_t *__restrict__ cpl,
+                                             uint32_t *__restrict__ cnt) {
     int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (a > n) return;
     if (a == n) {
@@ -95,10 +94,13 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
     }
     const uint64_t SENT = sentinel_key(J);
     uint64_t k = keys_s[a];
-    uint32_t i = perm[a];
-    sx[a] = x[i];
-    sy[a] = y[i];
-    sm[a] = m[i];
+    uint32_t i = perm[a];  // nearly the identity: the state is kept in the last Morton order
+    dst.x[a] = src.x[i];
+    dst.y[a] = src.y[i];
+    dst.vx[a] = src.vx[i];
+    dst.vy[a] = src.vy[i];
+    dst.m[a] = src.m[i];
+    dst.cidx[a] = src.cidx[i];
     int c_cur = -1, c_prev = -1;
     if (k != SENT) {
         if (a + 1 < n) {
@@ -112,9 +114,26 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
     cnt[a] = (k == SENT) ? 0u : 1u + (uint32_t)max(0, c_cur - c_prev);
 }
 
+// First sorted body of every depth-D0 cell (bins 0 .. 4^D0; the sentinel's prefix is 4^D0,
+// so bin 4^D0 starts at the first out-of-root body, i.e. at the in-root count).
+__global__ __launch_bounds__(TB) void k_cells(int64_t n, int J, int D0,
+                                              const uint64_t *__restrict__ keys_s,
+                                              uint32_t *__restrict__ cell_start) {
+    const int64_t bin = (int64_t)blockIdx.x * TB + threadIdx.x;
+    const int64_t nbins = (int64_t)1 << (2 * D0);
+    if (bin > nbins) return;
+    const int shift = 2 * (J - D0);
+    int64_t lo = 0, hi = n;  // first index with (key >> shift) >= bin
+    while (lo < hi) {
+        int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)(keys_s[mid] >> shift) < bin) lo = mid + 1; else hi = mid;
+    }
+    cell_start[bin] = (uint32_t)lo;
+}
+
 // First b >= from with c(b) < L, looking at most at the 3 aligned 8-byte words of c that
 // start at `from`'s word; -1 if not found there.  c(n-1) == -1 bounds every search, and the
-// c array is allocated with 16 bytes of slack so whole-word loads stay in bounds.
+// c array is allocated with 32 bytes of slack so whole-word loads stay in bounds.
 __device__ __forceinline__ int64_t scan_cpl(const int8_t *__restrict__ cpl, int64_t from, int L) {
     const int64_t w0 = from & ~(int64_t)7;
     for (int w = 0; w < 3; ++w) {
@@ -129,15 +148,15 @@ __device__ __forceinline__ int64_t scan_cpl(const int8_t *__restrict__ cpl, int6
     return -1;
 }
 
-// Largest index e >= from with (keys_s[e] >> shift) == pref (keys_s[from] matches).
-__device__ __forceinline__ int64_t run_end(const uint64_t *__restrict__ keys_s, int64_t n,
+// Largest e in [from, limit] with (keys_s[e] >> shift) == pref (keys_s[from] matches).
+__device__ __forceinline__ int64_t run_end(const uint64_t *__restrict__ keys_s, int64_t limit,
                                            int64_t from, int shift, uint64_t pref) {
     int64_t lo = from, step = 1;
-    while (lo + step < n && (keys_s[lo + step] >> shift) == pref) {
+    while (lo + step <= limit && (keys_s[lo + step] >> shift) == pref) {
         lo += step;
         step <<= 1;
     }
-    int64_t hi = min(lo + step, n);  // keys_s[hi] does not match (or hi == n)
+    int64_t hi = min(lo + step, limit + 1);  // keys_s[hi] does not match (or hi > limit)
     while (hi - lo > 1) {
         int64_t mid = lo + ((hi - lo) >> 1);
         if ((keys_s[mid] >> shift) == pref) lo = mid; else hi = mid;
@@ -145,32 +164,39 @@ __device__ __forceinline__ int64_t run_end(const uint64_t *__restrict__ keys_s, 
     return lo;
 }
 
-__global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, const uint64_t *__restrict__ keys_s,
+__global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, int D0,
+                                             const uint64_t *__restrict__ keys_s,
                                              const int8_t *__restrict__ cpl,
                                              const uint32_t *__restrict__ base,
-                                             const double *__restrict__ sx,
-                                             const double *__restrict__ sy,
-                                             const double *__restrict__ sm,
+                                             const uint32_t *__restrict__ cell_start,
+                                             const double *__restrict__ x,
+                                             const double *__restrict__ y,
+                                             const double *__restrict__ m,
                                              Node *__restrict__ nodes,
                                              uint32_t *__restrict__ span_cnt,
                                              uint32_t *__restrict__ span_list,
                                              uint32_t span_stride) {
     int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (a >= n) return;
-    uint64_t k = keys_s[a];
+    const uint64_t k = keys_s[a];
     if (k == sentinel_key(J)) return;
-    int cp = a > 0 ? (int)cpl[a - 1] : -1;
-    int cc = (int)cpl[a];
-    uint32_t b0 = base[a];
+    const int cp = a > 0 ? (int)cpl[a - 1] : -1;
+    const int cc = (int)cpl[a];
+    const uint32_t b0 = base[a];
+    const int shift0 = 2 * (J - D0);
     int64_t end = a;
     for (int L = cc; L > cp; --L) {  // deepest first: ends are nested
-        // last body of the depth-L cell: first b >= end with c(b) < L.  A short scan of the
-        // 1-byte c array settles the (many) small deep cells; big cells gallop on the keys.
-        int64_t b = scan_cpl(cpl, end, L);
-        if (b < 0) {
-            b = end;
-            int shift = 2 * (J - L);
-            b = run_end(keys_s, n, b, shift, k >> shift);
+        int64_t b;
+        if (L <= D0) {  // one load: the next depth-L cell starts at a depth-D0 cell start
+            const uint64_t nextcell = ((k >> (2 * (J - L))) + 1) << (2 * (D0 - L));
+            b = (int64_t)cell_start[nextcell] - 1;
+        } else {  // inside a's depth-D0 cell: short scan of c, then bounded galloping
+            b = scan_cpl(cpl, end, L);
+            if (b < 0) {
+                const int64_t limit = (int64_t)cell_start[(k >> shift0) + 1] - 1;
+                const int shift = 2 * (J - L);
+                b = run_end(keys_s, limit, end, shift, k >> shift);
+            }
         }
         end = b;
         const bool span = (a >> COM_CHUNK_SHIFT) != (end >> COM_CHUNK_SHIFT);
@@ -187,11 +213,11 @@ __global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, const uint64_t *_
             span_list[(size_t)L * span_stride + slot] = ni;
         }
     }
-    uint32_t li = b0 + (uint32_t)max(0, cc - cp);
-    double mm = sm[a];
+    const uint32_t li = b0 + (uint32_t)max(0, cc - cp);
+    const double mm = m[a];
     Node leaf;
-    leaf.comX = sx[a];  // BHA:176-178
-    leaf.comY = sy[a];
+    leaf.comX = x[a];  // BHA:176-178
+    leaf.comY = y[a];
     leaf.mass = mm;
     leaf.next = li + 1;
     leaf.meta = NODE_LEAF | (uint32_t)a | (mm == 0.0 ? NODE_SKIP : 0u);
@@ -200,22 +226,20 @@ __global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, const uint64_t *_
 
 // ---- exact replay of BHA:125-156 inside one jitter cell (depth J, h_J < 1e-3) ---------
 struct JitterCtx {
-    double *sx, *sy, *x, *y;
-    const uint32_t *perm;
+    double *x, *y;
     uint32_t *err;
 };
 
-// BHA:146-151: x += (lsb(x)==0 ? +eps : -eps); y += (lsb(y)==0 ? -eps : +eps)
+// BHA:146-151: x += (lsb(x)==0 ? +eps : -eps); y += (lsb(y)==0 ? -eps : +eps).  The
+// mutation is permanent in the reference (the Body object is shared): it is applied to the
+// body state itself.
 __device__ __forceinline__ void jitter(const JitterCtx &c, int64_t j) {
     const double eps = 1e-3;
-    double px = c.sx[j], py = c.sy[j];
+    double px = c.x[j], py = c.y[j];
     px += ((__double_as_longlong(px) & 1ll) == 0) ? +eps : -eps;
     py += ((__double_as_longlong(py) & 1ll) == 0) ? -eps : +eps;
-    c.sx[j] = px;
-    c.sy[j] = py;
-    uint32_t o = c.perm[j];
-    c.x[o] = px;  // the mutation is permanent in the reference (Body is shared)
-    c.y[o] = py;
+    c.x[j] = px;
+    c.y[j] = py;
 }
 
 // insertIntoChild on a depth-(J+1) cell: the body is jittered and must then land in a
@@ -223,21 +247,45 @@ __device__ __forceinline__ void jitter(const JitterCtx &c, int64_t j) {
 // (BHA:126).  If geometry ever allowed it we flag instead of guessing.
 __device__ void into_child_deep(const JitterCtx &c, int64_t j, double qcx, double qcy, double qh) {
     jitter(c, j);
-    double px = c.sx[j], py = c.sy[j];
+    double px = c.x[j], py = c.y[j];
     double hh = qh / 2.0;
     double gcx = (px < qcx) ? qcx - hh : qcx + hh;
     double gcy = (py < qcy) ? qcy - hh : qcy + hh;
     if (quad_contains(gcx, gcy, hh, px, py)) atomicOr(c.err, 1u);
 }
 
+// in-place heapsort of ord[0..k) by key cidx[ord[i]] (caller-list order of a jitter run)
+__device__ void sort_by_cidx(uint32_t *ord, int64_t k, const uint32_t *__restrict__ cidx) {
+    auto sift = [&](int64_t root, int64_t end) {
+        while (2 * root + 1 < end) {
+            int64_t child = 2 * root + 1;
+            if (child + 1 < end && cidx[ord[child]] < cidx[ord[child + 1]]) ++child;
+            if (cidx[ord[root]] < cidx[ord[child]]) {
+                uint32_t t = ord[root];
+                ord[root] = ord[child];
+                ord[child] = t;
+                root = child;
+            } else {
+                return;
+            }
+        }
+    };
+    for (int64_t st = k / 2 - 1; st >= 0; --st) sift(st, k);
+    for (int64_t end = k - 1; end > 0; --end) {
+        uint32_t t = ord[0];
+        ord[0] = ord[end];
+        ord[end] = t;
+        sift(0, end);
+    }
+}
+
 __global__ __launch_bounds__(TB) void k_jitter(int64_t n, Geometry g,
                                                const uint64_t *__restrict__ keys_s,
                                                const int8_t *__restrict__ cpl,
-                                               const uint32_t *__restrict__ base, double *sx,
-                                               double *sy, const double *__restrict__ sm,
-                                               double *x, double *y,
-                                               const uint32_t *__restrict__ perm, Node *nodes,
-                                               uint32_t *err) {
+                                               const uint32_t *__restrict__ base, double *x,
+                                               double *y, const double *__restrict__ m,
+                                               const uint32_t *__restrict__ cidx,
+                                               uint32_t *scratch, Node *nodes, uint32_t *err) {
     int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (a >= n) return;
     const int J = g.J;
@@ -245,22 +293,27 @@ __global__ __launch_bounds__(TB) void k_jitter(int64_t n, Geometry g,
     int cp = a > 0 ? (int)cpl[a - 1] : -1;
     if (cp == J) return;  // not the first body of its jitter cell
     int64_t b = a;
-    while (b < n && (int)cpl[b] == J) ++b;  // run = sorted bodies a..b (index order: stable sort)
+    while (b < n && (int)cpl[b] == J) ++b;  // run = sorted bodies a..b
+    const int64_t k = b - a + 1;
 
-    JitterCtx c{sx, sy, x, y, perm, err};
+    // BHA:363 inserts in list order: order the run by caller index
+    uint32_t *ord = scratch + a;
+    for (int64_t i = 0; i < k; ++i) ord[i] = (uint32_t)(a + i);
+    sort_by_cidx(ord, k, cidx);
+
+    JitterCtx c{x, y, err};
     double ccx, ccy;
     cell_centre(g, keys_s[a], J, ccx, ccy);
-    const double hJ = g.h[J];
     const double hc = g.h[J + 1];
 
-    // state of the 4 children: -1 empty, >= 0 leaf body (sorted pos), -2 subdivided
+    // state of the 4 children: -1 empty, >= 0 leaf body (slot), -2 subdivided
     int64_t ch[4] = {-1, -1, -1, -1};
     int64_t occ = -1;
     bool sub = false;
 
     auto into_child = [&](int64_t j) {  // BHA:145-156 on the jitter cell
         jitter(c, j);
-        double px = c.sx[j], py = c.sy[j];
+        double px = c.x[j], py = c.y[j];
         int ix = (px < ccx) ? 0 : 1;
         int iy = (py < ccy) ? 0 : 2;
         int q = ix + iy;
@@ -279,7 +332,8 @@ __global__ __launch_bounds__(TB) void k_jitter(int64_t n, Geometry g,
         into_child_deep(c, j, qcx, qcy, hc);  // BHA:136
     };
 
-    for (int64_t j = a; j <= b; ++j) {  // BHA:363 insertion in list order
+    for (int64_t i = 0; i < k; ++i) {
+        const int64_t j = ord[i];
         if (!sub && occ < 0) {
             occ = j;
             continue;
@@ -292,28 +346,26 @@ __global__ __launch_bounds__(TB) void k_jitter(int64_t n, Geometry g,
         }
         into_child(j);
     }
-    (void)hJ;
 
-    // Write the cell's children into its k = b - a + 1 contiguous slots, child order 0..3.
+    // Write the cell's children into its k contiguous slots, child order 0..3.
     uint32_t s0 = base[a] + (uint32_t)(J - cp);
-    uint32_t k = (uint32_t)(b - a + 1);
     uint32_t w = 0;
     uint32_t jmask = 0;
     for (int q = 0; q < 4; ++q) {
         if (ch[q] == -2) jmask |= 1u << q;
         if (ch[q] < 0) continue;
         int64_t j = ch[q];
-        double mm = sm[j];
+        double mm = m[j];
         Node leaf;
-        leaf.comX = sx[j];
-        leaf.comY = sy[j];
+        leaf.comX = x[j];
+        leaf.comY = y[j];
         leaf.mass = mm;
         leaf.next = s0 + w + 1;
         leaf.meta = NODE_LEAF | (uint32_t)j | (mm == 0.0 ? NODE_SKIP : 0u);
         nodes[s0 + w] = leaf;
         ++w;
     }
-    for (; w < k; ++w) {
+    for (; w < (uint32_t)k; ++w) {
         Node dead;
         dead.comX = 0.0;
         dead.comY = 0.0;
@@ -536,36 +588,45 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + TB - 1) / TB); }
 // a forced onesweep (6 passes x 25 us + lookback-state memsets, ~230 us), so keep the default.
 using SortConfig = rocprim::default_config;
 
+int cell_table_depth(int J, int64_t n) {
+    int d = 1;  // smallest depth with 4^d >= n, capped
+    while (d < CELL_TABLE_MAX_DEPTH && ((int64_t)1 << (2 * d)) < n) ++d;
+    return d < J ? d : J;
+}
+
 size_t tree_cub_bytes(int64_t n, int J) {
     size_t sort_bytes = 0, scan_bytes = 0;
     (void)rocprim::radix_sort_pairs<SortConfig>(nullptr, sort_bytes, (uint64_t *)nullptr,
                                                 (uint64_t *)nullptr, (uint32_t *)nullptr,
                                                 (uint32_t *)nullptr, (size_t)n, 0u,
                                                 (unsigned)(2 * J + 1));
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                     (int)(n + 1));
+    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint32_t *)nullptr,
+                                           (uint32_t *)nullptr, (int)(n + 1));
     return sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
 }
 
 hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStream_t s) {
     if (n <= 0) return hipMemsetAsync(b.base, 0, sizeof(uint32_t), s);
     hipError_t st;
-    k_morton<<<grid_for(n), TB, 0, s>>>(n, b.x, b.y, g, b.keys, b.idx);
+    const int D0 = cell_table_depth(g.J, n);
+    k_morton<<<grid_for(n), TB, 0, s>>>(n, b.src.x, b.src.y, g, b.keys, b.idx);
     size_t bytes = b.cub_bytes;
     st = rocprim::radix_sort_pairs<SortConfig>(b.cub_tmp, bytes, b.keys, b.keys_s, b.idx, b.perm,
                                                (size_t)n, 0u, (unsigned)(2 * g.J + 1), s);
     if (st != hipSuccess) return st;
-    k_prep<<<grid_for(n + 1), TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.x, b.y, b.m, b.sx, b.sy, b.sm,
-                                          b.cpl, b.cnt);
+    k_prep<<<grid_for(n + 1), TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.src, b.dst, b.cpl, b.cnt);
     bytes = b.cub_bytes;
     st = hipcub::DeviceScan::ExclusiveSum(b.cub_tmp, bytes, b.cnt, b.base, (int)(n + 1), s);
     if (st != hipSuccess) return st;
+    k_cells<<<grid_for(((int64_t)1 << (2 * D0)) + 1), TB, 0, s>>>(n, g.J, D0, b.keys_s,
+                                                                  b.cell_start);
     st = hipMemsetAsync(b.span_cnt, 0, sizeof(uint32_t) * (g.J + 1), s);
     if (st != hipSuccess) return st;
-    k_emit<<<grid_for(n), TB, 0, s>>>(n, g.J, b.keys_s, b.cpl, b.base, b.sx, b.sy, b.sm, b.nodes,
-                                      b.span_cnt, b.span_list, b.span_stride);
-    k_jitter<<<grid_for(n), TB, 0, s>>>(n, g, b.keys_s, b.cpl, b.base, b.sx, b.sy, b.sm, b.x, b.y,
-                                        b.perm, b.nodes, b.scalars + 1);
+    k_emit<<<grid_for(n), TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cpl, b.base, b.cell_start, b.dst.x,
+                                      b.dst.y, b.dst.m, b.nodes, b.span_cnt, b.span_list,
+                                      b.span_stride);
+    k_jitter<<<grid_for(n), TB, 0, s>>>(n, g, b.keys_s, b.cpl, b.base, b.dst.x, b.dst.y, b.dst.m,
+                                        b.dst.cidx, b.idx, b.nodes, b.scalars + 1);
     k_com_local<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), COM_TB, 0, s>>>(
         n, g, b.keys_s, b.cpl, b.base, b.nodes);
     k_span_children<<<dim3((b.span_stride + TB - 1) / TB, g.J + 1), TB, 0, s>>>(
