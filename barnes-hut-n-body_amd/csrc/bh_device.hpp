@@ -47,7 +47,7 @@ __host__ __device__ inline uint32_t span_stride_for(int64_t n) {
 
 // Cell-start table: first sorted body of every depth-D0 cell, so the end of any node at
 // depth <= D0 is one load, and deeper searches stay inside one depth-D0 cell.
-constexpr int CELL_TABLE_MAX_DEPTH = 10;
+constexpr int CELL_TABLE_MAX_DEPTH = 8;
 
 constexpr int MAX_DEPTH_TAB = 40;
 
@@ -86,8 +86,7 @@ struct TreeBuffers {
     uint32_t *cell_start;  // [4^D0 + 1] first sorted body of each depth-D0 cell
     Node *nodes;
     uint32_t *scalars;     // [1] = error flags
-    uint32_t *span_cnt;    // [J + 1] chunk-spanning internal nodes per level
-    uint32_t *span_list;   // [(J + 1) * span_stride]
+    uint32_t *span_list;   // [(J + 1) * span_stride]: chunk-spanning node per (level, boundary)
     uint32_t span_stride;
     uint4 *span_children;  // [(J + 1) * span_stride]
     void *cub_tmp;

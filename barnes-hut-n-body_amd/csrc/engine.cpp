@@ -240,7 +240,6 @@ TreeBuffers tree_buffers(bh_engine *e) {
     b.cell_start = e->cell_start;
     b.nodes = e->nodes;
     b.scalars = e->scalars;
-    b.span_cnt = e->span_cnt;
     b.span_list = e->span_list;
     b.span_stride = span_stride_for(e->cap);
     b.span_children = e->span_children;

@@ -172,10 +172,7 @@ __global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, int D0,
                                              const double *__restrict__ x,
                                              const double *__restrict__ y,
                                              const double *__restrict__ m,
-                                             Node *__restrict__ nodes,
-                                             uint32_t *__restrict__ span_cnt,
-                                             uint32_t *__restrict__ span_list,
-                                             uint32_t span_stride) {
+                                             Node *__restrict__ nodes) {
     int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (a >= n) return;
     const uint64_t k = keys_s[a];
@@ -208,10 +205,6 @@ __global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, int D0,
         nd.next = base[end + 1];
         nd.meta = (uint32_t)L | (span ? NODE_SPAN : 0u);
         nodes[ni] = nd;
-        if (span) {
-            uint32_t slot = atomicAdd(&span_cnt[L], 1u);
-            span_list[(size_t)L * span_stride + slot] = ni;
-        }
     }
     const uint32_t li = b0 + (uint32_t)max(0, cc - cp);
     const double mm = m[a];
@@ -412,8 +405,12 @@ __device__ __forceinline__ void node_com(Node *nodes, uint32_t ni, const Geometr
 // levels with barriers.  Chunks whose range exceeds the LDS capacity use global memory.
 constexpr int COM_TB = 256;
 constexpr int COM_PER_THREAD = (1 << COM_CHUNK_SHIFT) / COM_TB;
-constexpr int COM_CAP = 2560;  // nodes staged per chunk (2.5 per body; deep chains spill)
+constexpr int COM_CAP = 2048;  // nodes staged per chunk (C3 at 1e6: ~1.7 per body, max 1814)
+constexpr int COM_LOAD_BATCH = 4;
 constexpr uint32_t LDS_SPAN = 1u << 31;
+constexpr uint32_t LDS_LEAF = 1u << 30;
+constexpr uint32_t LDS_NEXT_MASK = LDS_LEAF - 1;
+constexpr uint16_t NO_CHILD = 0xFFFFu;
 
 __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
                                                       const uint64_t *__restrict__ keys_s,
@@ -422,6 +419,7 @@ __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
                                                       Node *nodes) {
     __shared__ double s_m[COM_CAP], s_x[COM_CAP], s_y[COM_CAP];
     __shared__ uint32_t s_next[COM_CAP];
+    __shared__ ushort4 s_ch[COM_CAP];  // child offsets of internal nodes (NO_CHILD-padded)
     __shared__ int s_lmax;
     const int64_t c0 = (int64_t)blockIdx.x << COM_CHUNK_SHIFT;
     const int64_t c1 = min(c0 + (1 << COM_CHUNK_SHIFT), n);
@@ -451,12 +449,40 @@ __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
     __syncthreads();
     atomicMax(&s_lmax, lmax);
     if (lds) {
+        // stage the chunk's pre-order range; loads issued in batches (independent)
+        for (uint32_t i0 = threadIdx.x; i0 < cnt; i0 += COM_TB * COM_LOAD_BATCH) {
+            Node nd[COM_LOAD_BATCH];
+#pragma unroll
+            for (int k = 0; k < COM_LOAD_BATCH; ++k) {
+                const uint32_t i = i0 + k * COM_TB;
+                if (i < cnt) nd[k] = nodes[S0 + i];
+            }
+#pragma unroll
+            for (int k = 0; k < COM_LOAD_BATCH; ++k) {
+                const uint32_t i = i0 + k * COM_TB;
+                if (i < cnt) {
+                    s_m[i] = nd[k].mass;
+                    s_x[i] = nd[k].comX;
+                    s_y[i] = nd[k].comY;
+                    const bool leaf = nd[k].meta & NODE_LEAF;
+                    s_next[i] = (nd[k].next - S0) | (leaf ? LDS_LEAF : 0u) |
+                                ((!leaf && (nd[k].meta & NODE_SPAN)) ? LDS_SPAN : 0u);
+                }
+            }
+        }
+        __syncthreads();
+        // child offsets of every staged local internal node, found once, in parallel
         for (uint32_t i = threadIdx.x; i < cnt; i += COM_TB) {
-            const Node nd = nodes[S0 + i];
-            s_m[i] = nd.mass;
-            s_x[i] = nd.comX;
-            s_y[i] = nd.comY;
-            s_next[i] = (nd.next - S0) | ((!(nd.meta & NODE_LEAF) && (nd.meta & NODE_SPAN)) ? LDS_SPAN : 0u);
+            const uint32_t nx = s_next[i];
+            if (nx & (LDS_LEAF | LDS_SPAN)) continue;
+            const uint32_t end = nx & LDS_NEXT_MASK;
+            uint16_t ch[4] = {NO_CHILD, NO_CHILD, NO_CHILD, NO_CHILD};
+            uint32_t c = i + 1;
+            for (int k = 0; k < 4 && c < end; ++k) {
+                ch[k] = (uint16_t)c;
+                c = max(s_next[c] & LDS_NEXT_MASK, c + 1);
+            }
+            s_ch[i] = make_ushort4(ch[0], ch[1], ch[2], ch[3]);
         }
     }
     __syncthreads();
@@ -469,18 +495,19 @@ __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
             const uint32_t ni = bases[i] + (uint32_t)(L - cps[i] - 1);
             if (lds) {
                 const uint32_t li = ni - S0;
-                const uint32_t nx = s_next[li];
-                if (nx & LDS_SPAN) continue;  // finished by k_com_span
+                if (s_next[li] & LDS_SPAN) continue;  // finished by k_com_span
+                const ushort4 chv = s_ch[li];
+                const uint16_t cs[4] = {chv.x, chv.y, chv.z, chv.w};
                 double mSum = 0.0, cx = 0.0, cy = 0.0;
-                uint32_t c = li + 1;
-                while (c < nx) {  // children 0..3 in pre-order (BHA:189-192)
-                    const double cm = s_m[c];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {  // children 0..3 in pre-order (BHA:189-192)
+                    if (cs[k] == NO_CHILD) continue;
+                    const double cm = s_m[cs[k]];
                     if (cm > 0.0) {
                         mSum += cm;
-                        cx += s_x[c] * cm;
-                        cy += s_y[c] * cm;
+                        cx += s_x[cs[k]] * cm;
+                        cy += s_y[cs[k]] * cm;
                     }
-                    c = max(s_next[c] & ~LDS_SPAN, c + 1);
                 }
                 double ox, oy;
                 if (mSum > 0.0) {
@@ -505,18 +532,61 @@ __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
     }
 }
 
+// The nodes crossing the boundary between chunk k and k+1 (bodies b = end of chunk k and
+// b+1) are exactly b's ancestors at depths 0..c(b); each chunk-spanning node is listed once,
+// by the boundary of the chunk it starts in: span_list[L * stride + k] (or NO_SPAN).
+constexpr uint32_t NO_SPAN = 0xFFFFFFFFu;
+
+__global__ __launch_bounds__(TB) void k_span_find(int64_t n, int J, int D0,
+                                                  const uint64_t *__restrict__ keys_s,
+                                                  const int8_t *__restrict__ cpl,
+                                                  const uint32_t *__restrict__ base,
+                                                  const uint32_t *__restrict__ cell_start,
+                                                  uint32_t *__restrict__ span_list,
+                                                  uint32_t span_stride) {
+    const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (k >= (int64_t)span_stride) return;
+    const int64_t chunk0 = k << COM_CHUNK_SHIFT;
+    const int64_t b = chunk0 + (1 << COM_CHUNK_SHIFT) - 1;
+    const int cb = (b + 1 < n) ? (int)cpl[b] : -1;
+    const uint64_t key = (b < n) ? keys_s[b] : 0ull;
+    for (int L = 0; L <= J; ++L) {
+        uint32_t out = NO_SPAN;
+        if (L <= cb) {
+            // first body of b's depth-L cell
+            int64_t aL;
+            if (L <= D0) {
+                aL = cell_start[(key >> (2 * (J - L))) << (2 * (D0 - L))];
+            } else {
+                const int shift = 2 * (J - L);
+                const uint64_t pref = key >> shift;
+                int64_t lo = cell_start[key >> (2 * (J - D0))], hi = b;
+                while (lo < hi) {
+                    const int64_t mid = (lo + hi) >> 1;
+                    if ((keys_s[mid] >> shift) < pref) lo = mid + 1; else hi = mid;
+                }
+                aL = lo;
+            }
+            if (aL >= chunk0) {  // starts in chunk k: this boundary owns it
+                const int cp = aL > 0 ? (int)cpl[aL - 1] : -1;
+                out = base[aL] + (uint32_t)(L - cp - 1);
+            }
+        }
+        span_list[(size_t)L * span_stride + k] = out;
+    }
+}
+
 // Children (pre-order indices, up to 4) of every chunk-spanning node, found in parallel so
 // the level-by-level pass below issues independent loads only.
-__global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__restrict__ span_cnt,
-                                                      const uint32_t *__restrict__ span_list,
+__global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__restrict__ span_list,
                                                       uint32_t span_stride,
                                                       const Node *__restrict__ nodes,
                                                       uint4 *__restrict__ span_children) {
     const uint32_t L = blockIdx.y;
-    const uint32_t cnt = span_cnt[L];
-    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < cnt; i += gridDim.x * TB) {
+    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < span_stride; i += gridDim.x * TB) {
         const size_t slot = (size_t)L * span_stride + i;
         const uint32_t ni = span_list[slot];
+        if (ni == NO_SPAN) continue;
         const uint32_t end = nodes[ni].next;
         uint32_t ch[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
         uint32_t c = ni + 1;
@@ -532,16 +602,15 @@ __global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__r
 // its own global writes are visible to it).  Few nodes: at most one per chunk boundary and
 // level.
 constexpr int SPAN_TB = 1024;
-__global__ __launch_bounds__(SPAN_TB) void k_com_span(int J, const uint32_t *__restrict__ span_cnt,
-                                                      const uint32_t *__restrict__ span_list,
+__global__ __launch_bounds__(SPAN_TB) void k_com_span(int J, const uint32_t *__restrict__ span_list,
                                                       uint32_t span_stride,
                                                       const uint4 *__restrict__ span_children,
                                                       Node *nodes) {
     for (int L = J; L >= 0; --L) {
-        const uint32_t cnt = span_cnt[L];
-        for (uint32_t i = threadIdx.x; i < cnt; i += SPAN_TB) {
+        for (uint32_t i = threadIdx.x; i < span_stride; i += SPAN_TB) {
             const size_t slot = (size_t)L * span_stride + i;
             const uint32_t ni = span_list[slot];
+            if (ni == NO_SPAN) continue;
             const uint4 ch = span_children[slot];
             const uint32_t cs[4] = {ch.x, ch.y, ch.z, ch.w};
             double cm[4], cxs[4], cys[4];
@@ -620,18 +689,18 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     if (st != hipSuccess) return st;
     k_cells<<<grid_for(((int64_t)1 << (2 * D0)) + 1), TB, 0, s>>>(n, g.J, D0, b.keys_s,
                                                                   b.cell_start);
-    st = hipMemsetAsync(b.span_cnt, 0, sizeof(uint32_t) * (g.J + 1), s);
-    if (st != hipSuccess) return st;
     k_emit<<<grid_for(n), TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cpl, b.base, b.cell_start, b.dst.x,
-                                      b.dst.y, b.dst.m, b.nodes, b.span_cnt, b.span_list,
-                                      b.span_stride);
+                                      b.dst.y, b.dst.m, b.nodes);
     k_jitter<<<grid_for(n), TB, 0, s>>>(n, g, b.keys_s, b.cpl, b.base, b.dst.x, b.dst.y, b.dst.m,
                                         b.dst.cidx, b.idx, b.nodes, b.scalars + 1);
     k_com_local<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), COM_TB, 0, s>>>(
         n, g, b.keys_s, b.cpl, b.base, b.nodes);
+    k_span_find<<<(b.span_stride + TB - 1) / TB, TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cpl, b.base,
+                                                            b.cell_start, b.span_list,
+                                                            b.span_stride);
     k_span_children<<<dim3((b.span_stride + TB - 1) / TB, g.J + 1), TB, 0, s>>>(
-        g.J, b.span_cnt, b.span_list, b.span_stride, b.nodes, b.span_children);
-    k_com_span<<<1, SPAN_TB, 0, s>>>(g.J, b.span_cnt, b.span_list, b.span_stride, b.span_children,
+        g.J, b.span_list, b.span_stride, b.nodes, b.span_children);
+    k_com_span<<<1, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
                                      b.nodes);
     return hipGetLastError();
 }
