@@ -35,7 +35,8 @@ EXPORTED_SYMBOLS = (
     "bh_last_error", "bh_set_params", "bh_get_params", "bh_reset_bodies", "bh_step",
     "bh_num_bodies", "bh_get_bodies", "bh_compute_accelerations", "bh_get_quads",
     "bh_last_timings", "bh_last_tree_nodes", "bh_traverse_kernel_ms", "bh_set_profiling",
-    "bh_synchronize", "bh_shard_range", "bh_traversal_stats", "bh_last_removed", "bh_scene_galaxy_disk", "bh_scene_kepler_disk", "bh_scene_uniform",
+    "bh_synchronize", "bh_shard_range", "bh_traversal_stats", "bh_last_removed",
+    "bh_selftest_fast_math", "bh_scene_galaxy_disk", "bh_scene_kepler_disk", "bh_scene_uniform",
 )
 
 
@@ -103,6 +104,7 @@ def load_library(path: str | None = None):
     lib.bh_traversal_stats.argtypes = [_VP, _I64P, _I64P, _I64P]
     lib.bh_last_removed.argtypes = [_VP, _I64P, ctypes.c_int64, _I64P]
     lib.bh_shard_range.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, _I64P, _I64P]
+    lib.bh_selftest_fast_math.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, _I64P]
     lib.bh_scene_galaxy_disk.argtypes = (
         [ctypes.c_int32] + [ctypes.c_double] * 6 + [ctypes.c_int32, ctypes.c_int64]
         + [ctypes.c_double] * 9 + [_D] * 5)
@@ -137,6 +139,16 @@ def shard_range(n: int, rank: int, world: int):
     if rc != BH_OK:
         raise BhError(rc, "bh_shard_range: invalid arguments")
     return lo.value, hi.value
+
+
+def selftest_fast_math(n: int, seed: int = 1, device: int = 0) -> int:
+    """Mismatches of the traversal's exact in-range sqrt/reciprocal sequences against IEEE
+    sqrt, 1/sqrt, 1/x over n generated operands (bh_selftest_fast_math); 0 expected."""
+    bad = ctypes.c_int64(-1)
+    rc = load_library().bh_selftest_fast_math(int(device), int(n), int(seed), ctypes.byref(bad))
+    if rc != BH_OK:
+        raise BhError(rc, "bh_selftest_fast_math failed")
+    return bad.value
 
 
 def comm_unique_id() -> bytes:

@@ -75,6 +75,15 @@ struct BodyState {
     uint32_t *cidx;  // caller (list) index
 };
 
+// A chunk-spanning node's children, gathered once its local children are final: per child
+// either a reference to another span node (SPAN_REF | owner boundary) with zero values, or
+// the child's (mass, comX*mass, comY*mass) — zeros for mass <= 0 (BHA:189-192 skip those;
+// adding +0.0 leaves the running sums bit-identical).
+struct __attribute__((aligned(16))) SpanSlot {
+    uint32_t ch[4];
+    double v[4][3];
+};
+
 // ---- launchers (tree_build.hip) --------------------------------------------------
 struct TreeBuffers {
     BodyState src;  // state before the build (previous slot order)
@@ -88,7 +97,7 @@ struct TreeBuffers {
     uint32_t *scalars;     // [1] = error flags
     uint32_t *span_list;   // [(J + 1) * span_stride]: chunk-spanning node per (level, boundary)
     uint32_t span_stride;
-    uint4 *span_children;  // [(J + 1) * span_stride]
+    struct SpanSlot *span_children;  // [(J + 1) * span_stride]
     void *cub_tmp;
     size_t cub_bytes;
 };
@@ -102,6 +111,25 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
 void traverse(const Node *nodes, const uint32_t *d_T, const double *x, const double *y,
               const double *m, int64_t lo, int64_t hi, const Geometry &g, const ForceParams &fp,
               double *a2, uint32_t *visits, uint32_t *wave_iters, hipStream_t s);
+
+// Exactness check of the traversal's in-range sqrt/reciprocal sequences against the IEEE
+// operations on n generated operands; adds the mismatch count to *d_bad.
+hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_bad, hipStream_t s);
+
+// ---- launchers (direct.hip): theta = 0 all-pairs ---------------------------------
+// Non-empty leaves of the last tree in pre-order (the reference's theta = 0 summation order).
+struct LeafList {
+    double *xy;      // interleaved (x, y)
+    double *m;
+    uint32_t *slot;  // body slot (self-skip)
+};
+size_t leaf_select_bytes(int64_t node_cap);
+hipError_t leaf_list_build(const Node *nodes, const uint32_t *d_T, int64_t node_cap,
+                           uint8_t *flags, uint32_t *sel, uint32_t *d_count, const LeafList &L,
+                           int64_t n, void *tmp, size_t tmp_bytes, hipStream_t s);
+void direct_forces(const LeafList &L, const uint32_t *d_count, const double *x, const double *y,
+                   const double *m, int64_t lo, int64_t hi, double G, double soft2, double *a2,
+                   hipStream_t s);
 
 // ---- launchers (integrate.hip) ---------------------------------------------------
 void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,

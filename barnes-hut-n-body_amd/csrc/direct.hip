@@ -1,0 +1,163 @@
+// θ = 0 force evaluation as a direct all-pairs sum.
+//
+// At θ = 0 the reference's criterion `s2 < 0 * dist2` (BHA:226-228) never accepts, so
+// accumulateForce (BHA:215-239) recurses to every leaf: each body's force is the point force
+// of every non-empty (mass != 0, BHA:216) leaf except its own (BHA:219), summed in the tree's
+// depth-first pre-order.  Here that leaf sequence is extracted once per build (a stable
+// compaction of the pre-order node array) and the O(N^2) sum runs as an LDS-tiled kernel:
+// a workgroup stages 1024 leaves (x, y, m, slot) in LDS with coalesced loads, every lane (one
+// body) reads them as broadcasts in sequence order — the reference's order, so the result is
+// bit-identical to the tree walk — with no criterion, cursor or ballot in the loop.  Bound by
+// fp64 VALU issue (one v_rsq_f64 and ~35 fp64 ops per interaction).
+#include <hipcub/hipcub.hpp>
+
+#include "bh_device.hpp"
+#include "fastmath.hpp"
+
+namespace bh {
+namespace {
+
+constexpr int TB = 256;
+constexpr int TILE = 1024;
+
+__global__ __launch_bounds__(TB) void k_leaf_flags(const Node *__restrict__ nodes,
+                                                   const uint32_t *__restrict__ d_T,
+                                                   uint8_t *__restrict__ flags, int64_t cap) {
+    const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= cap) return;
+    const uint32_t T = *d_T;
+    uint8_t f = 0;
+    if (i < (int64_t)T) {
+        const uint32_t meta = nodes[i].meta;
+        f = (meta & NODE_LEAF) && !(meta & NODE_SKIP);  // BHA:216 (mass == 0 never visited)
+    }
+    flags[i] = f;
+}
+
+__global__ __launch_bounds__(TB) void k_leaf_gather(const Node *__restrict__ nodes,
+                                                    const uint32_t *__restrict__ sel,
+                                                    const uint32_t *__restrict__ d_count,
+                                                    LeafList L) {
+    const uint32_t i = blockIdx.x * TB + threadIdx.x;
+    if (i >= *d_count) return;
+    const Node nd = nodes[sel[i]];
+    L.xy[2 * i] = nd.comX;  // leaf: the body's own x, y, m (BHA:176-178)
+    L.xy[2 * i + 1] = nd.comY;
+    L.m[i] = nd.mass;
+    L.slot[i] = nd.meta & NODE_BODY_MASK;
+}
+
+typedef double double2_t __attribute__((ext_vector_type(2)));
+
+template <bool FAST>
+__device__ __forceinline__ void pair_force(double px, double py, double pm, double bx, double by,
+                                           double Gm, double soft2, double &fx, double &fy) {
+    const double dx = px - bx;  // BHA:251-258, expression order as written
+    const double dy = py - by;
+    const double r2 = dx * dx + dy * dy + soft2;
+    double invR, invR2;
+    if (FAST) {
+        double h;
+        const double r = sqrt_rn_inrange_h(r2, h);
+        invR = rcp_rn_seeded(r, h + h);
+        invR2 = rcp_rn_seeded(r2, invR * invR);
+    } else {
+        invR = 1.0 / sqrt(r2);
+        invR2 = 1.0 / r2;
+    }
+    const double f = Gm * pm * invR2;
+    fx += f * dx * invR;
+    fy += f * dy * invR;
+}
+
+template <bool FAST>
+__device__ __forceinline__ void sum_tile(const double2_t *s_xy, const double *s_m,
+                                         const uint32_t *s_slot, int cnt, double bx, double by,
+                                         double Gm, double soft2, uint32_t self, double &fx,
+                                         double &fy) {
+    int j = 0;
+    for (; j + 4 <= cnt; j += 4) {
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+            const double2_t p = s_xy[j + u];
+            if (s_slot[j + u] != self) pair_force<FAST>(p.x, p.y, s_m[j + u], bx, by, Gm, soft2, fx, fy);
+        }
+    }
+    for (; j < cnt; ++j) {
+        const double2_t p = s_xy[j];
+        if (s_slot[j] != self) pair_force<FAST>(p.x, p.y, s_m[j], bx, by, Gm, soft2, fx, fy);
+    }
+}
+
+__global__ __launch_bounds__(TB) void k_direct(LeafList L, const uint32_t *__restrict__ d_count,
+                                               const double *__restrict__ x,
+                                               const double *__restrict__ y,
+                                               const double *__restrict__ m, int64_t lo,
+                                               int64_t hi, double G, double soft2,
+                                               double *__restrict__ a2) {
+    __shared__ double2_t s_xy[TILE];
+    __shared__ double s_m[TILE];
+    __shared__ uint32_t s_slot[TILE];
+    const int64_t p = lo + (int64_t)blockIdx.x * TB + threadIdx.x;
+    const bool valid = p < hi;
+    const double bx = valid ? x[p] : 0.0;
+    const double by = valid ? y[p] : 0.0;
+    const double bm = valid ? m[p] : 1.0;
+    const double Gm = G * bm;  // (Config.G * b.m) first (BHA:256)
+    const uint32_t self = valid ? (uint32_t)p : 0xFFFFFFFFu;
+    const bool fast = __ballot(valid && !lane_fast_ok(bx, by, soft2)) == 0ull;
+    const uint32_t nl = *d_count;
+    double fx = 0.0, fy = 0.0;
+    for (uint32_t t0 = 0; t0 < nl; t0 += TILE) {
+        const int cnt = (int)min((uint32_t)TILE, nl - t0);
+        __syncthreads();
+        for (int i = threadIdx.x; i < cnt; i += TB) {
+            s_xy[i] = *reinterpret_cast<const double2_t *>(L.xy + 2 * (t0 + i));
+            s_m[i] = L.m[t0 + i];
+            s_slot[i] = L.slot[t0 + i];
+        }
+        __syncthreads();
+        if (fast)
+            sum_tile<true>(s_xy, s_m, s_slot, cnt, bx, by, Gm, soft2, self, fx, fy);
+        else
+            sum_tile<false>(s_xy, s_m, s_slot, cnt, bx, by, Gm, soft2, self, fx, fy);
+    }
+    if (!valid) return;
+    double2_t acc;
+    acc.x = fx / bm;  // BHA:390-391
+    acc.y = fy / bm;
+    *reinterpret_cast<double2_t *>(a2 + 2 * p) = acc;
+}
+
+}  // namespace
+
+size_t leaf_select_bytes(int64_t node_cap) {
+    size_t b = 0;
+    (void)hipcub::DeviceSelect::Flagged(nullptr, b, hipcub::CountingInputIterator<uint32_t>(0),
+                                        (const uint8_t *)nullptr, (uint32_t *)nullptr,
+                                        (uint32_t *)nullptr, (int)node_cap);
+    return b;
+}
+
+hipError_t leaf_list_build(const Node *nodes, const uint32_t *d_T, int64_t node_cap,
+                           uint8_t *flags, uint32_t *sel, uint32_t *d_count, const LeafList &L,
+                           int64_t n, void *tmp, size_t tmp_bytes, hipStream_t s) {
+    if (node_cap <= 0) return hipSuccess;
+    k_leaf_flags<<<(unsigned)((node_cap + TB - 1) / TB), TB, 0, s>>>(nodes, d_T, flags, node_cap);
+    hipError_t st = hipcub::DeviceSelect::Flagged(tmp, tmp_bytes,
+                                                  hipcub::CountingInputIterator<uint32_t>(0), flags,
+                                                  sel, d_count, (int)node_cap, s);
+    if (st != hipSuccess) return st;
+    if (n > 0) k_leaf_gather<<<(unsigned)((n + TB - 1) / TB), TB, 0, s>>>(nodes, sel, d_count, L);
+    return hipGetLastError();
+}
+
+void direct_forces(const LeafList &L, const uint32_t *d_count, const double *x, const double *y,
+                   const double *m, int64_t lo, int64_t hi, double G, double soft2, double *a2,
+                   hipStream_t s) {
+    if (hi <= lo) return;
+    k_direct<<<(unsigned)((hi - lo + TB - 1) / TB), TB, 0, s>>>(L, d_count, x, y, m, lo, hi, G,
+                                                              soft2, a2);
+}
+
+}  // namespace bh

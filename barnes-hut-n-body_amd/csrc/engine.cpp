@@ -57,8 +57,8 @@ struct bh_engine {
     uint32_t *cell_start = nullptr;
     Node *nodes = nullptr;
     size_t node_cap = 0;
-    uint32_t *span_cnt = nullptr, *span_list = nullptr;
-    uint4 *span_children = nullptr;
+    uint32_t *span_list = nullptr;
+    bh::SpanSlot *span_children = nullptr;
     uint32_t *scalars = nullptr;  // [1] tree error flags
     uint32_t *visits32 = nullptr;
     uint32_t *wave_iters = nullptr;  // per-wave union of visited nodes (diagnostics)
@@ -79,6 +79,15 @@ struct bh_engine {
 
     void *cub_tmp = nullptr;
     size_t cub_bytes = 0;
+
+    // theta = 0 all-pairs path (direct.hip), allocated on first use
+    uint8_t *leaf_flags = nullptr;
+    uint32_t *leaf_sel = nullptr, *leaf_count = nullptr;
+    LeafList leaves{nullptr, nullptr, nullptr};
+    void *leaf_tmp = nullptr;
+    size_t leaf_tmp_bytes = 0;
+    size_t leaf_node_cap = 0;  // node capacity the flags were sized for
+    int64_t leaf_cap = 0;
 
     bool tree_valid = false;  // lastTree (BHA:304): keys_s / cpl / base / nodes are current
 
@@ -208,7 +217,6 @@ int ensure_capacity(bh_engine *e, int64_t n) {
     size_t ncap = node_capacity(e->cap, J);
     if (ncap > e->node_cap || J != e->J_alloc) {
         TRY(dev_alloc(e, e->nodes, ncap));
-        TRY(dev_alloc(e, e->span_cnt, (size_t)J + 2));
         TRY(dev_alloc(e, e->span_list, (size_t)(J + 2) * span_stride_for(e->cap)));
         TRY(dev_alloc(e, e->span_children, (size_t)(J + 2) * span_stride_for(e->cap)));
         TRY(dev_alloc(e, e->cell_start,
@@ -294,7 +302,30 @@ int build(bh_engine *e) {
     return BH_OK;
 }
 
+// theta = 0 workspace: flags per node slot, selected indices and the leaf list per body.
+int ensure_direct(bh_engine *e) {
+    if (e->leaf_node_cap == e->node_cap && e->leaf_cap == e->cap) return BH_OK;
+    TRY(dev_alloc(e, e->leaf_flags, e->node_cap));
+    TRY(dev_alloc(e, e->leaf_sel, (size_t)e->node_cap));
+    TRY(dev_alloc(e, e->leaf_count, 1));
+    TRY(dev_alloc(e, e->leaves.xy, 2 * (size_t)e->cap));
+    TRY(dev_alloc(e, e->leaves.m, (size_t)e->cap));
+    TRY(dev_alloc(e, e->leaves.slot, (size_t)e->cap));
+    const size_t tb = leaf_select_bytes((int64_t)e->node_cap);
+    if (e->leaf_tmp) (void)hipFree(e->leaf_tmp);
+    e->leaf_tmp = nullptr;
+    HIPCHK(e, hipMalloc(&e->leaf_tmp, tb));
+    e->leaf_tmp_bytes = tb;
+    e->leaf_node_cap = e->node_cap;
+    e->leaf_cap = e->cap;
+    return BH_OK;
+}
+
 // ---- one force evaluation: buildTree() + computeAccelerations() (BHA:359-395) -------------
+// theta == 0 (config C5): the criterion never accepts (BHA:226-228), so the force is the
+// direct sum over the tree's non-empty leaves in pre-order -- run by the all-pairs kernel
+// (direct.hip) on the leaf list instead of the tree walk; bit-identical either way.  The
+// visit-counting diagnostic keeps the walk (it counts internal nodes too).
 int evaluate(bh_engine *e, uint32_t *visits) {
     const int64_t n = e->n;
     TRY(mark(e, -1));
@@ -302,6 +333,25 @@ int evaluate(bh_engine *e, uint32_t *visits) {
     TRY(mark(e, 0));
     ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};  // BHA:378
     const uint32_t *d_T = e->base + n;
+    if (fp.theta2 == 0.0 && !visits) {
+        TRY(ensure_direct(e));
+        HIPCHK(e, leaf_list_build(e->nodes, d_T, (int64_t)e->node_cap, e->leaf_flags, e->leaf_sel,
+                                  e->leaf_count, e->leaves, n, e->leaf_tmp, e->leaf_tmp_bytes,
+                                  e->stream));
+        int64_t lo = 0, hi = n;
+        if (e->world > 1) bh_shard_range(n, e->rank, e->world, &lo, &hi);
+        direct_forces(e->leaves, e->leaf_count, e->st.x, e->st.y, e->st.m, lo, hi, fp.G,
+                      fp.soft2, e->a2, e->stream);
+        HIPCHK(e, hipGetLastError());
+        TRY(mark(e, 1));
+        if (e->world > 1) {
+            const int64_t chunk = (n + e->world - 1) / e->world;
+            NCCLCHK(e, ncclAllGather(e->a2 + 2 * e->rank * chunk, e->a2, (size_t)(2 * chunk),
+                                     ncclDouble, e->comm, e->stream));
+            TRY(mark(e, 4));
+        }
+        return BH_OK;
+    }
     if (e->world == 1 || visits) {
         traverse(e->nodes, d_T, e->st.x, e->st.y, e->st.m, 0, n, e->geo, fp, e->a2, visits,
                  e->wave_iters, e->stream);
@@ -673,9 +723,11 @@ void bh_destroy(bh_engine *e) {
     free_state(e->st);
     free_state(e->alt);
     void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->idx, e->perm, e->cpl, e->cnt,
-                    e->base, e->cell_start, e->nodes, e->span_cnt, e->span_list,
+                    e->base, e->cell_start, e->nodes, e->span_list,
                     e->span_children, e->scalars, e->visits32, e->wave_iters, e->heavy, e->keep,
-                    e->pos, e->box, e->mdead, e->mdead_cidx, e->mupd, e->mupd_mass, e->cub_tmp};
+                    e->pos, e->box, e->mdead, e->mdead_cidx, e->mupd, e->mupd_mass, e->cub_tmp,
+                    e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaves.xy, e->leaves.m,
+                    e->leaves.slot, e->leaf_tmp};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     for (hipEvent_t ev : e->ev) (void)hipEventDestroy(ev);
@@ -912,6 +964,21 @@ int bh_shard_range(int64_t n, int rank, int world, int64_t *lo, int64_t *hi) {
     const int64_t chunk = (n + world - 1) / world;
     *lo = std::min<int64_t>(n, (int64_t)rank * chunk);
     *hi = std::min<int64_t>(n, *lo + chunk);
+    return BH_OK;
+}
+
+int bh_selftest_fast_math(int device, int64_t n, uint64_t seed, int64_t *mismatches) {
+    if (!mismatches || n < 0) return BH_E_INVALID;
+    *mismatches = -1;
+    unsigned long long *d_bad = nullptr, h_bad = 0;
+    if (hipSetDevice(device) != hipSuccess) return BH_E_DEVICE;
+    if (hipMalloc((void **)&d_bad, sizeof(*d_bad)) != hipSuccess) return BH_E_DEVICE;
+    bool ok = hipMemset(d_bad, 0, sizeof(*d_bad)) == hipSuccess &&
+              bh::selftest_fast_math(n, seed, d_bad, nullptr) == hipSuccess &&
+              hipMemcpy(&h_bad, d_bad, sizeof(h_bad), hipMemcpyDeviceToHost) == hipSuccess;
+    (void)hipFree(d_bad);
+    if (!ok) return BH_E_DEVICE;
+    *mismatches = (int64_t)h_bad;
     return BH_OK;
 }
 

@@ -16,6 +16,7 @@
 // interaction), not by HBM: the node stream is shared by 64 lanes and served from the
 // scalar cache / L2.  See DESIGN.md for the roofline accounting.
 #include "bh_device.hpp"
+#include "fastmath.hpp"
 
 namespace bh {
 namespace {
@@ -23,48 +24,6 @@ namespace {
 constexpr int TB = 256;
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
-
-// ---- exact fast paths for RN(sqrt(x)) and RN(1/x) ------------------------------------
-// These are the instruction sequences the compiler emits for IEEE sqrt(double) and
-// 1.0 / double on gfx950, with the operand-range scaling (v_cmp + v_ldexp / v_div_scale /
-// v_div_fmas scaling) and the special-value fix-ups (v_cmp_class / v_div_fixup) removed.
-// For a finite normal operand in [2^-600, 2^600] those removed steps are identities (no
-// scaling is triggered, no special value occurs), so the results are bit-identical to the
-// full sequences; a wave takes this path only when lane_fast_ok() holds for all its lanes.
-__device__ __forceinline__ double sqrt_rn_inrange(double x) {
-    double y = __builtin_amdgcn_rsq(x);
-    double g = x * y;
-    double h = y * 0.5;
-    double r = __builtin_fma(-h, g, 0.5);
-    g = __builtin_fma(g, r, g);
-    h = __builtin_fma(h, r, h);
-    double d = __builtin_fma(-g, g, x);
-    g = __builtin_fma(d, h, g);
-    d = __builtin_fma(-g, g, x);
-    g = __builtin_fma(d, h, g);
-    return g;
-}
-
-__device__ __forceinline__ double rcp_rn_inrange(double b) {
-    double y = __builtin_amdgcn_rcp(b);
-    double e = __builtin_fma(-b, y, 1.0);
-    y = __builtin_fma(y, e, y);
-    e = __builtin_fma(-b, y, 1.0);
-    y = __builtin_fma(y, e, y);
-    double r = __builtin_fma(-b, y, 1.0);  // q = 1.0 * y = y exactly
-    return __builtin_fma(r, y, y);
-}
-
-// Wave-uniform precondition for the exact fast paths: every tree node's centre of mass lies
-// within the root cell or 2e-3 of it (a convex combination of inserted bodies; a jittered
-// leaf body moved by at most 2 x 1e-3), so |comX|, |comY| < 2^31 always.  If the lane's own
-// body is finite with |x|, |y| < 2^250 and soft2 is in [2^-600, 2^500], every dist2 of the
-// traversal is in [soft2, 2^503] and both sqrt and the reciprocals stay in the range where
-// sqrt_rn_inrange / rcp_rn_inrange equal the full IEEE sequences.
-__device__ __forceinline__ bool lane_fast_ok(double bx, double by, double soft2) {
-    return __builtin_fabs(bx) < 0x1p250 && __builtin_fabs(by) < 0x1p250 && soft2 >= 0x1p-600 &&
-           soft2 <= 0x1p500;
-}
 
 template <bool FAST, bool COUNT>
 __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T, double bx,
@@ -105,8 +64,10 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
         if (contrib) {  // BHA:250-259, expression order as written
             double invR, invR2;
             if (FAST) {
-                invR = rcp_rn_inrange(sqrt_rn_inrange(d2));
-                invR2 = rcp_rn_inrange(d2);
+                double h;
+                const double r = sqrt_rn_inrange_h(d2, h);
+                invR = rcp_rn_seeded(r, h + h);
+                invR2 = rcp_rn_seeded(d2, invR * invR);
             } else {
                 invR = 1.0 / sqrt(d2);
                 invR2 = 1.0 / d2;
@@ -163,7 +124,54 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     if (COUNT) visits[p] = nvis;
 }
 
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+// Operands d2 in the fast-path range [2^-600, 2^503]: random; mantissas near 1.0 / near 2.0;
+// squares of random doubles +- a few ulp (sqrt ties region); the physical range [1, 2^24).
+__global__ __launch_bounds__(TB) void k_selftest_math(int64_t n, uint64_t seed,
+                                                      unsigned long long *bad) {
+    uint32_t local = 0;
+    for (int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * TB) {
+        const uint64_t r0 = mix64(seed ^ (uint64_t)i), r1 = mix64(r0);
+        const int kind = (int)(r1 >> 62);
+        uint64_t mant = r0 & ((1ull << 52) - 1);
+        int ex = (int)(r1 % 1104) - 600;  // [-600, 503]
+        if (kind == 1) mant = (r1 & 1) ? (mant & 0xFFF) : (((1ull << 52) - 1) ^ (mant & 0xFFF));
+        double d2;
+        if (kind == 2) {
+            const double s0 = __builtin_ldexp(__longlong_as_double((long long)((1023ull << 52) | mant)),
+                                              ex / 2);
+            d2 = __longlong_as_double(__double_as_longlong(s0 * s0) + (long long)((r1 >> 8) % 5) - 2);
+        } else {
+            if (kind == 3) ex = (int)(r1 % 24);
+            d2 = __builtin_ldexp(__longlong_as_double((long long)((1023ull << 52) | mant)), ex);
+        }
+        if (!(d2 >= 0x1p-600 && d2 <= 0x1p503)) continue;
+        double h;
+        const double sr = sqrt_rn_inrange_h(d2, h);
+        const double invR = rcp_rn_seeded(sr, h + h);
+        const double invR2 = rcp_rn_seeded(d2, invR * invR);
+        const double wantR = 1.0 / sqrt(d2), wantR2 = 1.0 / d2;
+        if (__double_as_longlong(sr) != __double_as_longlong(sqrt(d2))) ++local;
+        if (__double_as_longlong(invR) != __double_as_longlong(wantR)) ++local;
+        if (__double_as_longlong(invR2) != __double_as_longlong(wantR2)) ++local;
+        if (__double_as_longlong(rcp_rn_inrange(d2)) != __double_as_longlong(wantR2)) ++local;
+    }
+    if (local) atomicAdd(bad, (unsigned long long)local);
+}
+
 }  // namespace
+
+hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_bad, hipStream_t s) {
+    k_selftest_math<<<4096, TB, 0, s>>>(n, seed, d_bad);
+    return hipGetLastError();
+}
 
 void traverse(const Node *nodes, const uint32_t *d_T, const double *x, const double *y,
               const double *m, int64_t lo, int64_t hi, const Geometry &g, const ForceParams &fp,

@@ -410,14 +410,15 @@ constexpr int COM_LOAD_BATCH = 4;
 constexpr uint32_t LDS_SPAN = 1u << 31;
 constexpr uint32_t LDS_LEAF = 1u << 30;
 constexpr uint32_t LDS_NEXT_MASK = LDS_LEAF - 1;
-constexpr uint16_t NO_CHILD = 0xFFFFu;
+constexpr uint16_t NO_CHILD = (uint16_t)COM_CAP;  // the massless pad entry
+constexpr uint16_t SPAN_CHILD = 0xFFFFu;         // s_ch.x of a chunk-spanning node
 
 __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
                                                       const uint64_t *__restrict__ keys_s,
                                                       const int8_t *__restrict__ cpl,
                                                       const uint32_t *__restrict__ base,
                                                       Node *nodes) {
-    __shared__ double s_m[COM_CAP], s_x[COM_CAP], s_y[COM_CAP];
+    __shared__ double s_m[COM_CAP + 1], s_x[COM_CAP + 1], s_y[COM_CAP + 1];  // [COM_CAP]: pad
     __shared__ uint32_t s_next[COM_CAP];
     __shared__ ushort4 s_ch[COM_CAP];  // child offsets of internal nodes (NO_CHILD-padded)
     __shared__ int s_lmax;
@@ -464,17 +465,27 @@ __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
                     s_m[i] = nd[k].mass;
                     s_x[i] = nd[k].comX;
                     s_y[i] = nd[k].comY;
-                    const bool leaf = nd[k].meta & NODE_LEAF;
+                    // leaves and dead jitter slots (SKIP before COM) have no children
+                    const bool leaf = nd[k].meta & (NODE_LEAF | NODE_SKIP);
                     s_next[i] = (nd[k].next - S0) | (leaf ? LDS_LEAF : 0u) |
                                 ((!leaf && (nd[k].meta & NODE_SPAN)) ? LDS_SPAN : 0u);
                 }
             }
         }
         __syncthreads();
+        if (threadIdx.x == 0) {
+            s_m[COM_CAP] = 0.0;
+            s_x[COM_CAP] = 0.0;
+            s_y[COM_CAP] = 0.0;
+        }
         // child offsets of every staged local internal node, found once, in parallel
         for (uint32_t i = threadIdx.x; i < cnt; i += COM_TB) {
             const uint32_t nx = s_next[i];
-            if (nx & (LDS_LEAF | LDS_SPAN)) continue;
+            if (nx & LDS_LEAF) continue;
+            if (nx & LDS_SPAN) {
+                s_ch[i] = make_ushort4(SPAN_CHILD, SPAN_CHILD, SPAN_CHILD, SPAN_CHILD);
+                continue;
+            }
             const uint32_t end = nx & LDS_NEXT_MASK;
             uint16_t ch[4] = {NO_CHILD, NO_CHILD, NO_CHILD, NO_CHILD};
             uint32_t c = i + 1;
@@ -487,26 +498,43 @@ __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
     }
     __syncthreads();
     const int top = s_lmax;
+    // level masks: bit i set when body a0+i owns a depth-L node (cp < L <= cc)
     for (int L = top; L >= 0; --L) {
+        uint32_t mask = 0;
 #pragma unroll
-        for (int i = 0; i < COM_PER_THREAD; ++i) {
-            if (ccs[i] < L || cps[i] >= L) continue;
-            const int64_t a = a0 + i;
-            const uint32_t ni = bases[i] + (uint32_t)(L - cps[i] - 1);
-            if (lds) {
-                const uint32_t li = ni - S0;
-                if (s_next[li] & LDS_SPAN) continue;  // finished by k_com_span
+        for (int i = 0; i < COM_PER_THREAD; ++i)
+            if (ccs[i] >= L && cps[i] < L) mask |= 1u << i;
+        if (lds) {
+            while (mask) {  // usually one node per lane and level
+                const int i = __builtin_ctz(mask);
+                mask &= mask - 1;
+                int cpi = cps[0];
+                uint32_t bi = bases[0];
+#pragma unroll
+                for (int q = 1; q < COM_PER_THREAD; ++q)
+                    if (i == q) {
+                        cpi = cps[q];
+                        bi = bases[q];
+                    }
+                const uint32_t li = bi + (uint32_t)(L - cpi - 1) - S0;
                 const ushort4 chv = s_ch[li];
+                if (chv.x == SPAN_CHILD) continue;  // finished by k_com_span
+                // all four children fetched at once (absent ones read the massless pad)
                 const uint16_t cs[4] = {chv.x, chv.y, chv.z, chv.w};
+                double cm[4], ccx[4], ccy[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    cm[k] = s_m[cs[k]];
+                    ccx[k] = s_x[cs[k]];
+                    ccy[k] = s_y[cs[k]];
+                }
                 double mSum = 0.0, cx = 0.0, cy = 0.0;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {  // children 0..3 in pre-order (BHA:189-192)
-                    if (cs[k] == NO_CHILD) continue;
-                    const double cm = s_m[cs[k]];
-                    if (cm > 0.0) {
-                        mSum += cm;
-                        cx += s_x[cs[k]] * cm;
-                        cy += s_y[cs[k]] * cm;
+                    if (cm[k] > 0.0) {
+                        mSum += cm[k];
+                        cx += ccx[k] * cm[k];
+                        cy += ccy[k] * cm[k];
                     }
                 }
                 double ox, oy;
@@ -514,21 +542,37 @@ __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
                     ox = cx / mSum;
                     oy = cy / mSum;
                 } else {
-                    cell_centre(g, keys_s[a], L, ox, oy);
+                    cell_centre(g, keys_s[a0 + i], L, ox, oy);
                 }
                 s_m[li] = mSum;
                 s_x[li] = ox;
                 s_y[li] = oy;
-                Node *dst = nodes + ni;
-                dst->comX = ox;
-                dst->comY = oy;
-                dst->mass = mSum;
-                if (!(mSum > 0.0)) dst->meta |= NODE_SKIP;
-            } else if (!(nodes[ni].meta & NODE_SPAN)) {
-                node_com(nodes, ni, g, keys_s[a], L);
             }
+            // only LDS traffic inside the level loop: wait on LDS, not on stores
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+            __builtin_amdgcn_s_barrier();
+        } else {
+            while (mask) {
+                const int i = __builtin_ctz(mask);
+                mask &= mask - 1;
+                const uint32_t ni = bases[i] + (uint32_t)(L - cps[i] - 1);
+                if (!(nodes[ni].meta & NODE_SPAN)) node_com(nodes, ni, g, keys_s[a0 + i], L);
+            }
+            __syncthreads();
         }
+    }
+    if (lds) {  // write the chunk's local internal nodes back once
         __syncthreads();
+        for (uint32_t i = threadIdx.x; i < cnt; i += COM_TB) {
+            const uint32_t nx = s_next[i];
+            if (nx & (LDS_LEAF | LDS_SPAN)) continue;
+            Node *dst = nodes + S0 + i;
+            const double mSum = s_m[i];
+            dst->comX = s_x[i];
+            dst->comY = s_y[i];
+            dst->mass = mSum;
+            if (!(mSum > 0.0)) dst->meta |= NODE_SKIP;
+        }
     }
 }
 
@@ -536,6 +580,7 @@ __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
 // b+1) are exactly b's ancestors at depths 0..c(b); each chunk-spanning node is listed once,
 // by the boundary of the chunk it starts in: span_list[L * stride + k] (or NO_SPAN).
 constexpr uint32_t NO_SPAN = 0xFFFFFFFFu;
+constexpr uint32_t SPAN_REF = 1u << 31;  // child list entry: owner slot of a span child
 
 __global__ __launch_bounds__(TB) void k_span_find(int64_t n, int J, int D0,
                                                   const uint64_t *__restrict__ keys_s,
@@ -543,106 +588,202 @@ __global__ __launch_bounds__(TB) void k_span_find(int64_t n, int J, int D0,
                                                   const uint32_t *__restrict__ base,
                                                   const uint32_t *__restrict__ cell_start,
                                                   uint32_t *__restrict__ span_list,
-                                                  uint32_t span_stride) {
+                                                  uint32_t span_stride, Node *nodes) {
     const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
+    const int L = blockIdx.y;
     if (k >= (int64_t)span_stride) return;
     const int64_t chunk0 = k << COM_CHUNK_SHIFT;
     const int64_t b = chunk0 + (1 << COM_CHUNK_SHIFT) - 1;
     const int cb = (b + 1 < n) ? (int)cpl[b] : -1;
-    const uint64_t key = (b < n) ? keys_s[b] : 0ull;
-    for (int L = 0; L <= J; ++L) {
-        uint32_t out = NO_SPAN;
-        if (L <= cb) {
-            // first body of b's depth-L cell
-            int64_t aL;
-            if (L <= D0) {
-                aL = cell_start[(key >> (2 * (J - L))) << (2 * (D0 - L))];
-            } else {
-                const int shift = 2 * (J - L);
-                const uint64_t pref = key >> shift;
-                int64_t lo = cell_start[key >> (2 * (J - D0))], hi = b;
-                while (lo < hi) {
-                    const int64_t mid = (lo + hi) >> 1;
-                    if ((keys_s[mid] >> shift) < pref) lo = mid + 1; else hi = mid;
-                }
-                aL = lo;
+    uint32_t out = NO_SPAN;
+    if (L <= cb) {
+        const uint64_t key = keys_s[b];
+        int64_t aL;  // first body of b's depth-L cell
+        if (L <= D0) {
+            aL = cell_start[(key >> (2 * (J - L))) << (2 * (D0 - L))];
+        } else {
+            const int shift = 2 * (J - L);
+            const uint64_t pref = key >> shift;
+            int64_t lo = cell_start[key >> (2 * (J - D0))], hi = b;
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if ((keys_s[mid] >> shift) < pref) lo = mid + 1; else hi = mid;
             }
-            if (aL >= chunk0) {  // starts in chunk k: this boundary owns it
-                const int cp = aL > 0 ? (int)cpl[aL - 1] : -1;
-                out = base[aL] + (uint32_t)(L - cp - 1);
-            }
+            aL = lo;
         }
-        span_list[(size_t)L * span_stride + k] = out;
+        if (aL >= chunk0) {  // starts in chunk k: this boundary owns it
+            const int cp = aL > 0 ? (int)cpl[aL - 1] : -1;
+            out = base[aL] + (uint32_t)(L - cp - 1);
+            // the owner slot rides in the (not yet computed) comX of the span node, so its
+            // parent's child list can refer to the slot (k_span_children)
+            nodes[out].comX = __longlong_as_double((long long)k);
+        }
     }
+    span_list[(size_t)L * span_stride + k] = out;
 }
 
-// Children (pre-order indices, up to 4) of every chunk-spanning node, found in parallel so
-// the level-by-level pass below issues independent loads only.
+// Children of every chunk-spanning node with the values of the local ones (final after
+// k_com_local), gathered in parallel so the level-by-level pass below reads one
+// independent record per level.
 __global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__restrict__ span_list,
                                                       uint32_t span_stride,
                                                       const Node *__restrict__ nodes,
-                                                      uint4 *__restrict__ span_children) {
+                                                      SpanSlot *__restrict__ span_children) {
     const uint32_t L = blockIdx.y;
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < span_stride; i += gridDim.x * TB) {
         const size_t slot = (size_t)L * span_stride + i;
         const uint32_t ni = span_list[slot];
-        if (ni == NO_SPAN) continue;
-        const uint32_t end = nodes[ni].next;
-        uint32_t ch[4] = {0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        SpanSlot out;
+        const uint32_t end = ni != NO_SPAN ? nodes[ni].next : 0u;  // empty slot: no children
         uint32_t c = ni + 1;
-        for (int k = 0; k < 4 && c < end; ++k) {
-            ch[k] = c;
-            c = max(nodes[c].next, c + 1);
+        for (int k = 0; k < 4; ++k) {
+            out.ch[k] = 0xFFFFFFFFu;
+            out.v[k][0] = 0.0;
+            out.v[k][1] = 0.0;
+            out.v[k][2] = 0.0;
+            if (c >= end) continue;
+            const Node cn = nodes[c];
+            if (!(cn.meta & NODE_LEAF) && (cn.meta & NODE_SPAN)) {
+                out.ch[k] = SPAN_REF | (uint32_t)__double_as_longlong(cn.comX);
+            } else {
+                out.ch[k] = c;
+                if (cn.mass > 0.0) {
+                    out.v[k][0] = cn.mass;
+                    out.v[k][1] = cn.comX * cn.mass;
+                    out.v[k][2] = cn.comY * cn.mass;
+                }
+            }
+            c = max(cn.next, c + 1);
         }
-        span_children[slot] = make_uint4(ch[0], ch[1], ch[2], ch[3]);
+        span_children[slot] = out;
     }
 }
 
-// All chunk-spanning nodes, levels J..0, by ONE workgroup (levels separated by barriers;
-// its own global writes are visible to it).  Few nodes: at most one per chunk boundary and
-// level.
+// All chunk-spanning nodes, levels J..0, by ONE workgroup; thread k owns boundary k.  The
+// previous level's results live in LDS (a span child is referenced by its owner slot); the
+// per-level records are loaded two levels ahead, and stores to global stay in flight across
+// the LDS-only barriers.  Requires span_stride <= SPAN_LDS; larger trees use
+// k_com_span_global.
 constexpr int SPAN_TB = 1024;
+constexpr int SPAN_LDS = SPAN_TB;  // boundaries held in LDS (one per thread)
+
+struct SpanRegs {
+    uint32_t ni;
+    uint32_t ch[4];
+    double v[4][3];
+};
+
+__device__ __forceinline__ void load_span(SpanRegs &r, const uint32_t *span_list,
+                                          const SpanSlot *span_children, size_t slot) {
+    r.ni = span_list[slot];
+    const SpanSlot q = span_children[slot];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        r.ch[k] = q.ch[k];
+        r.v[k][0] = q.v[k][0];
+        r.v[k][1] = q.v[k][1];
+        r.v[k][2] = q.v[k][2];
+    }
+}
+
+// One level of k_com_span with the record R of this level; R is then refilled with the
+// record three levels up the loop (fixed register roles: no copies of in-flight loads).
+__device__ __forceinline__ void span_level(int L, SpanRegs &R, uint32_t k, uint32_t kk,
+                                           uint32_t span_stride, const uint32_t *span_list,
+                                           const SpanSlot *span_children, Node *nodes,
+                                           double (*r_m)[SPAN_LDS], double (*r_x)[SPAN_LDS],
+                                           double (*r_y)[SPAN_LDS]) {
+    const int cur = L & 1, prev = cur ^ 1;
+    if (R.ni != NO_SPAN && k < span_stride) {
+        double mSum = 0.0, cx = 0.0, cy = 0.0;  // children 0..3 in order (BHA:189-192)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            if (R.ch[c] != 0xFFFFFFFFu && (R.ch[c] & SPAN_REF)) {
+                const uint32_t s2 = R.ch[c] & ~SPAN_REF;
+                const double cm = r_m[prev][s2];
+                if (cm > 0.0) {
+                    mSum += cm;
+                    cx += r_x[prev][s2] * cm;
+                    cy += r_y[prev][s2] * cm;
+                }
+            } else {  // local child (or none): precomputed, zeros when skipped
+                mSum += R.v[c][0];
+                cx += R.v[c][1];
+                cy += R.v[c][2];
+            }
+        }
+        double ox = 0.0, oy = 0.0;
+        if (mSum > 0.0) {
+            ox = cx / mSum;
+            oy = cy / mSum;
+        }
+        r_m[cur][k] = mSum;
+        r_x[cur][k] = ox;
+        r_y[cur][k] = oy;
+        Node *dst = nodes + R.ni;
+        dst->mass = mSum;
+        dst->comX = ox;  // massless: never visited (the cell centre is not recorded)
+        dst->comY = oy;
+        if (!(mSum > 0.0)) dst->meta |= NODE_SKIP;
+    }
+    if (L >= 3) load_span(R, span_list, span_children, (size_t)(L - 3) * span_stride + kk);
+    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): LDS results visible; loads/stores fly on
+    __builtin_amdgcn_s_barrier();
+}
+
 __global__ __launch_bounds__(SPAN_TB) void k_com_span(int J, const uint32_t *__restrict__ span_list,
                                                       uint32_t span_stride,
-                                                      const uint4 *__restrict__ span_children,
+                                                      const SpanSlot *__restrict__ span_children,
                                                       Node *nodes) {
+    __shared__ double r_m[2][SPAN_LDS], r_x[2][SPAN_LDS], r_y[2][SPAN_LDS];
+    const uint32_t k = threadIdx.x;
+    const uint32_t kk = k < span_stride ? k : 0;  // threads past the table mirror slot 0
+    SpanRegs R0, R1, R2;
+    load_span(R0, span_list, span_children, (size_t)J * span_stride + kk);
+    if (J >= 1) load_span(R1, span_list, span_children, (size_t)(J - 1) * span_stride + kk);
+    if (J >= 2) load_span(R2, span_list, span_children, (size_t)(J - 2) * span_stride + kk);
+    for (int L = J; L >= 0; L -= 3) {
+        span_level(L, R0, k, kk, span_stride, span_list, span_children, nodes, r_m, r_x, r_y);
+        if (L < 1) break;
+        span_level(L - 1, R1, k, kk, span_stride, span_list, span_children, nodes, r_m, r_x, r_y);
+        if (L < 2) break;
+        span_level(L - 2, R2, k, kk, span_stride, span_list, span_children, nodes, r_m, r_x, r_y);
+    }
+}
+
+// Same, for trees too large for the LDS variant: results through global memory.
+__global__ __launch_bounds__(SPAN_TB) void k_com_span_global(int J,
+                                                             const uint32_t *__restrict__ span_list,
+                                                             uint32_t span_stride,
+                                                             const SpanSlot *__restrict__ span_children,
+                                                             Node *nodes) {
     for (int L = J; L >= 0; --L) {
-        for (uint32_t i = threadIdx.x; i < span_stride; i += SPAN_TB) {
-            const size_t slot = (size_t)L * span_stride + i;
+        for (uint32_t k = threadIdx.x; k < span_stride; k += SPAN_TB) {
+            const size_t slot = (size_t)L * span_stride + k;
             const uint32_t ni = span_list[slot];
             if (ni == NO_SPAN) continue;
-            const uint4 ch = span_children[slot];
-            const uint32_t cs[4] = {ch.x, ch.y, ch.z, ch.w};
-            double cm[4], cxs[4], cys[4];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {  // independent loads
-                cm[k] = 0.0;
-                cxs[k] = 0.0;
-                cys[k] = 0.0;
-                if (cs[k] != 0xFFFFFFFFu) {
-                    const Node c = nodes[cs[k]];
-                    cm[k] = c.mass;
-                    cxs[k] = c.comX;
-                    cys[k] = c.comY;
-                }
-            }
+            const SpanSlot q = span_children[slot];
             double mSum = 0.0, cx = 0.0, cy = 0.0;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {  // BHA:189-192, children 0..3 in order
-                if (cs[k] != 0xFFFFFFFFu && cm[k] > 0.0) {
-                    mSum += cm[k];
-                    cx += cxs[k] * cm[k];
-                    cy += cys[k] * cm[k];
+            for (int c = 0; c < 4; ++c) {
+                if (q.ch[c] != 0xFFFFFFFFu && (q.ch[c] & SPAN_REF)) {
+                    const Node cn =
+                        nodes[span_list[(size_t)(L + 1) * span_stride + (q.ch[c] & ~SPAN_REF)]];
+                    if (cn.mass > 0.0) {
+                        mSum += cn.mass;
+                        cx += cn.comX * cn.mass;
+                        cy += cn.comY * cn.mass;
+                    }
+                } else {
+                    mSum += q.v[c][0];
+                    cx += q.v[c][1];
+                    cy += q.v[c][2];
                 }
             }
             Node *dst = nodes + ni;
             dst->mass = mSum;
-            if (mSum > 0.0) {
-                dst->comX = cx / mSum;
-                dst->comY = cy / mSum;
-            } else {  // massless: never visited (the cell centre is not recorded here)
-                dst->meta |= NODE_SKIP;
-            }
+            dst->comX = mSum > 0.0 ? cx / mSum : 0.0;
+            dst->comY = mSum > 0.0 ? cy / mSum : 0.0;
+            if (!(mSum > 0.0)) dst->meta |= NODE_SKIP;
         }
         __syncthreads();
     }
@@ -695,13 +836,17 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
                                         b.dst.cidx, b.idx, b.nodes, b.scalars + 1);
     k_com_local<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), COM_TB, 0, s>>>(
         n, g, b.keys_s, b.cpl, b.base, b.nodes);
-    k_span_find<<<(b.span_stride + TB - 1) / TB, TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cpl, b.base,
-                                                            b.cell_start, b.span_list,
-                                                            b.span_stride);
-    k_span_children<<<dim3((b.span_stride + TB - 1) / TB, g.J + 1), TB, 0, s>>>(
-        g.J, b.span_list, b.span_stride, b.nodes, b.span_children);
-    k_com_span<<<1, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
-                                     b.nodes);
+    const dim3 span_grid((b.span_stride + TB - 1) / TB, g.J + 1);
+    k_span_find<<<span_grid, TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cpl, b.base, b.cell_start,
+                                         b.span_list, b.span_stride, b.nodes);
+    k_span_children<<<span_grid, TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.nodes,
+                                             b.span_children);
+    if (b.span_stride <= (uint32_t)SPAN_LDS)
+        k_com_span<<<1, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
+                                         b.nodes);
+    else
+        k_com_span_global<<<1, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
+                                                b.nodes);
     return hipGetLastError();
 }
 

@@ -130,6 +130,12 @@ int bh_set_profiling(bh_engine *e, int enabled);
  * 2 * ceil(n / world) doubles per rank).  Host-only; used by the engine itself. */
 int bh_shard_range(int64_t n, int rank, int world, int64_t *lo, int64_t *hi);
 
+/* Diagnostic: checks, on HIP device `device`, the traversal's reduced-range exact sequences
+ * for sqrt(d2), 1/sqrt(d2) and 1/d2 (traverse.hip) bit-for-bit against the IEEE operations on
+ * n generated operands (random, near powers of two, near perfect squares, physical range);
+ * *mismatches receives the number of differing results (0 expected). */
+int bh_selftest_fast_math(int device, int64_t n, uint64_t seed, int64_t *mismatches);
+
 /* Block until all device work of this engine is complete. */
 int bh_synchronize(bh_engine *e);
 

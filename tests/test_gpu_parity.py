@@ -236,6 +236,18 @@ def test_c3_1e6_full_size_sampled():
     _assert_state_equal(eng, ref)
 
 
+def test_c3x2_2e6_global_span_path():
+    """2e6 bodies: more chunk boundaries than the LDS span pass holds, so the chunk-spanning
+    nodes go through the global-memory variant (tree_build.hip k_com_span_global)."""
+    arrs = scenes.config_scene("c3x2")
+    assert len(arrs[0]) > (1024 << 10)
+    eng, ref = _pair(arrs, theta=0.5)
+    _assert_acc_equal(eng, ref)
+    eng.step(1)
+    ref.step(1)
+    _assert_state_equal(eng, ref)
+
+
 def test_physics_engine_mirror_preserves_body_identity():
     """The Kotlin-surface mirror (bh_amd.PhysicsEngine) driven like NBodyPanel: step() updates
     the caller's own Body objects in place and removes merged-away bodies from the caller's
@@ -270,3 +282,9 @@ def test_physics_engine_mirror_preserves_body_identity():
         assert quads[0] == bh_amd.Quad(1200.0, 400.0, 1202.0)
     finally:
         bh_amd.Config.theta = saved
+
+
+def test_fast_math_sequences_exact():
+    """The traversal's reduced sqrt / seeded-reciprocal sequences (traverse.hip) equal IEEE
+    sqrt, 1.0/sqrt and 1.0/x bit-for-bit on 2^26 operands across the fast-path range."""
+    assert bh_amd.selftest_fast_math(1 << 26, seed=20261015) == 0
