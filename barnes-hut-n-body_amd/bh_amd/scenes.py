@@ -95,6 +95,8 @@ def config_scene(name: str):
         return two_disks(800_000, 200_000)
     if name == "c4":
         return uniform(10_000_000, 0.5, seed=4)
+    if name == "c5":  # theta = 0 direct-sum configuration
+        return uniform(262_144, 0.5, seed=5)
     if name.startswith("c3x"):  # weak-scaling family: c3x<k> = k copies' worth of bodies
         k = int(name[3:])
         return two_disks(800_000 * k, 200_000 * k)

@@ -70,22 +70,39 @@ __device__ __forceinline__ void pair_force(double px, double py, double pm, doub
     fy += f * dy * invR;
 }
 
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+// One staged leaf: (x, y, m, slot bits).
 template <bool FAST>
-__device__ __forceinline__ void sum_tile(const double2_t *s_xy, const double *s_m,
-                                         const uint32_t *s_slot, int cnt, double bx, double by,
+__device__ __forceinline__ void sum_tile(const double4_t *s_rec, int cnt, double bx, double by,
                                          double Gm, double soft2, uint32_t self, double &fx,
                                          double &fy) {
+    constexpr int U = 4;
     int j = 0;
-    for (; j + 4 <= cnt; j += 4) {
+    for (; j + U <= cnt; j += U) {
+        double4_t r[U];
 #pragma unroll
-        for (int u = 0; u < 4; ++u) {
-            const double2_t p = s_xy[j + u];
-            if (s_slot[j + u] != self) pair_force<FAST>(p.x, p.y, s_m[j + u], bx, by, Gm, soft2, fx, fy);
+        for (int u = 0; u < U; ++u) r[u] = s_rec[j + u];  // broadcast reads, issued together
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const bool other = (uint32_t)__double_as_longlong(r[u].w) != self;  // BHA:219
+            if (FAST) {
+                // self-skip without a branch: the own leaf enters with mass +0.0, so its term
+                // is an exact +-0.0 and fx, fy (never -0.0) are unchanged -- valid because the
+                // fast path guarantees finite Gm and r2 >= soft2 > 0
+                pair_force<true>(r[u].x, r[u].y, other ? r[u].z : 0.0, bx, by, Gm, soft2, fx, fy);
+            } else if (other) {
+                pair_force<false>(r[u].x, r[u].y, r[u].z, bx, by, Gm, soft2, fx, fy);
+            }
         }
     }
     for (; j < cnt; ++j) {
-        const double2_t p = s_xy[j];
-        if (s_slot[j] != self) pair_force<FAST>(p.x, p.y, s_m[j], bx, by, Gm, soft2, fx, fy);
+        const double4_t r = s_rec[j];
+        const bool other = (uint32_t)__double_as_longlong(r.w) != self;
+        if (FAST)
+            pair_force<true>(r.x, r.y, other ? r.z : 0.0, bx, by, Gm, soft2, fx, fy);
+        else if (other)
+            pair_force<false>(r.x, r.y, r.z, bx, by, Gm, soft2, fx, fy);
     }
 }
 
@@ -95,9 +112,7 @@ __global__ __launch_bounds__(TB) void k_direct(LeafList L, const uint32_t *__res
                                                const double *__restrict__ m, int64_t lo,
                                                int64_t hi, double G, double soft2,
                                                double *__restrict__ a2) {
-    __shared__ double2_t s_xy[TILE];
-    __shared__ double s_m[TILE];
-    __shared__ uint32_t s_slot[TILE];
+    __shared__ double4_t s_rec[TILE];
     const int64_t p = lo + (int64_t)blockIdx.x * TB + threadIdx.x;
     const bool valid = p < hi;
     const double bx = valid ? x[p] : 0.0;
@@ -105,22 +120,27 @@ __global__ __launch_bounds__(TB) void k_direct(LeafList L, const uint32_t *__res
     const double bm = valid ? m[p] : 1.0;
     const double Gm = G * bm;  // (Config.G * b.m) first (BHA:256)
     const uint32_t self = valid ? (uint32_t)p : 0xFFFFFFFFu;
-    const bool fast = __ballot(valid && !lane_fast_ok(bx, by, soft2)) == 0ull;
+    const bool fast =
+        __ballot(valid && !(lane_fast_ok(bx, by, soft2) && __builtin_isfinite(Gm))) == 0ull;
     const uint32_t nl = *d_count;
     double fx = 0.0, fy = 0.0;
     for (uint32_t t0 = 0; t0 < nl; t0 += TILE) {
         const int cnt = (int)min((uint32_t)TILE, nl - t0);
         __syncthreads();
         for (int i = threadIdx.x; i < cnt; i += TB) {
-            s_xy[i] = *reinterpret_cast<const double2_t *>(L.xy + 2 * (t0 + i));
-            s_m[i] = L.m[t0 + i];
-            s_slot[i] = L.slot[t0 + i];
+            const double2_t q = *reinterpret_cast<const double2_t *>(L.xy + 2 * (t0 + i));
+            double4_t r;
+            r.x = q.x;
+            r.y = q.y;
+            r.z = L.m[t0 + i];
+            r.w = __longlong_as_double((long long)L.slot[t0 + i]);
+            s_rec[i] = r;
         }
         __syncthreads();
         if (fast)
-            sum_tile<true>(s_xy, s_m, s_slot, cnt, bx, by, Gm, soft2, self, fx, fy);
+            sum_tile<true>(s_rec, cnt, bx, by, Gm, soft2, self, fx, fy);
         else
-            sum_tile<false>(s_xy, s_m, s_slot, cnt, bx, by, Gm, soft2, self, fx, fy);
+            sum_tile<false>(s_rec, cnt, bx, by, Gm, soft2, self, fx, fy);
     }
     if (!valid) return;
     double2_t acc;

@@ -25,6 +25,8 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "barnes-hut-n-body_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
+FP64_VEC_PEAK_TF = 78.6  # MI355X FP64 vector peak, AMD spec sheet (not in the local guide)
+FLOP_PER_INTERACTION = 20  # SURVEY §8d C5 convention (sqrt and divisions counted as 1)
 NODE_BYTES = 32        # one fp64 node record (comX, comY, mass, s2/next) — SURVEY §8d
 BODY_EVAL_BYTES = 40   # body read (x, y, m) + acceleration write (ax, ay) per evaluation
 
@@ -34,8 +36,9 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c3", help="c3 (default), c2, c4, c1_code, c1_baseline")
-    ap.add_argument("--theta", type=float, default=0.5)
+    ap.add_argument("--config", default="c3",
+                    help="c3 (default), c2, c4, c5 (theta=0 all-pairs), c1_code, c1_baseline")
+    ap.add_argument("--theta", type=float, default=None, help="default 0.5 (c5: 0.0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
@@ -55,11 +58,15 @@ WORKLOAD_DESC = {
     "c4": "uniform cloud N=1e7 over 2400x800, m=0.5",
     "c1_code": "defaultBodies(): two galaxy disks 10000 + 2500",
     "c1_baseline": "BASELINE 'R' scene: two galaxy disks 2 x 1000",
+    "c5": "uniform cloud N=262144, theta=0: direct all-pairs sum in tree leaf order",
 }
 
 
 def main():
     args = parse()
+    if args.theta is None:
+        args.theta = 0.0 if args.config == "c5" else 0.5
+    direct = args.theta == 0.0
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -89,14 +96,16 @@ def main():
 
     # V-bar: mean non-empty nodes visited per body per evaluation on this scene,
     # counted by the engine on a separate instance so the timed state is untouched.
-    probe = bh_amd.Engine(params, device=local_rank)
-    probe.reset_bodies(*arrs)
-    _, _, vis = probe.compute_accelerations(visits=True)
-    vbar = float(np.mean(vis)) if len(vis) else 0.0
-    lane_visits, wave_iters, waves = probe.traversal_stats()
-    lane_eff = lane_visits / (64.0 * wave_iters) if wave_iters else 0.0
-    probe.close()
-    del probe
+    vbar = lane_eff = 0.0
+    if not direct:
+        probe = bh_amd.Engine(params, device=local_rank)
+        probe.reset_bodies(*arrs)
+        _, _, vis = probe.compute_accelerations(visits=True)
+        vbar = float(np.mean(vis)) if len(vis) else 0.0
+        lane_visits, wave_iters, waves = probe.traversal_stats()
+        lane_eff = lane_visits / (64.0 * wave_iters) if wave_iters else 0.0
+        probe.close()
+        del probe
 
     eng.reset_bodies(*arrs)
     if args.warmup > 0:
@@ -129,27 +138,67 @@ def main():
     value = bodies * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / max(args.steps, 1)
 
-    # Roofline of the dominant kernel (traversal): algorithmic bytes per launch / duration.
+    # Roofline of the dominant kernel: algorithmic bytes (traversal) or flops (theta = 0
+    # all-pairs) per launch / its average duration on the engine's stream.
     bodies_per_launch = bodies / world
-    bytes_per_launch = (NODE_BYTES * vbar + BODY_EVAL_BYTES) * bodies_per_launch
-    achieved = bytes_per_launch / (trav_ms * 1e-3) / 1e9 if trav_ms > 0 else 0.0
-    roofline = {
-        "bound": "hbm",
-        "achieved": round(achieved, 1),
-        "peak": HBM_PEAK_GBS,
-        "unit": "GB/s",
-        "frac": round(achieved / HBM_PEAK_GBS, 4),
-        "traffic": None,
-        "kernel": "k_traverse",
-        "kernel_avg_ms": round(trav_ms, 4),
-        "launches": trav_launches,
-        "vbar_nodes_per_body_eval": round(vbar, 2),
-        "wave_lane_efficiency": round(lane_eff, 4),
-        "bytes_per_launch": round(bytes_per_launch),
-    }
+    if direct:
+        flops_per_launch = FLOP_PER_INTERACTION * bodies_per_launch * (bodies - 1)
+        achieved = flops_per_launch / (trav_ms * 1e-3) / 1e12 if trav_ms > 0 else 0.0
+        roofline = {
+            "bound": "valu",
+            "achieved": round(achieved, 2),
+            "peak": FP64_VEC_PEAK_TF,
+            "unit": "TFLOP/s",
+            "frac": round(achieved / FP64_VEC_PEAK_TF, 4),
+            "traffic": None,
+            "kernel": "k_direct",
+            "kernel_avg_ms": round(trav_ms, 4),
+            "launches": trav_launches,
+            "flops_per_launch": round(flops_per_launch),
+            "interactions_per_s": round(flops_per_launch / FLOP_PER_INTERACTION / (trav_ms * 1e-3))
+            if trav_ms > 0 else 0,
+        }
+    else:
+        bytes_per_launch = (NODE_BYTES * vbar + BODY_EVAL_BYTES) * bodies_per_launch
+        achieved = bytes_per_launch / (trav_ms * 1e-3) / 1e9 if trav_ms > 0 else 0.0
+        roofline = {
+            "bound": "hbm",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBS, 4),
+            "traffic": None,
+            "kernel": "k_traverse",
+            "kernel_avg_ms": round(trav_ms, 4),
+            "launches": trav_launches,
+            "vbar_nodes_per_body_eval": round(vbar, 2),
+            "wave_lane_efficiency": round(lane_eff, 4),
+            "bytes_per_launch": round(bytes_per_launch),
+        }
 
     cpu_baseline = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and world == 1 and not args.no_cpu_baseline and direct:
+        # theta = 0: one evaluation of a body subsample through the oracle's tree walk (every
+        # leaf visited), scaled to body-steps/s (2 evaluations per step)
+        import oracle
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        ref = oracle.Oracle(*arrs, theta=0.0, threads=threads)
+        sample = np.arange(0, n0, max(1, n0 // 4096), dtype=np.int64)
+        c0 = time.perf_counter()
+        ref.accelerations(subset=sample)
+        c1 = time.perf_counter()
+        cpu_baseline = {
+            "value": round(len(sample) / (2.0 * (c1 - c0)), 1),
+            "unit": "body-steps/s",
+            "cores": threads,
+            "kind": "port",
+            "sample": f"one theta=0 evaluation of {len(sample)} of {n0} bodies (every leaf of the "
+                      f"tree) with the C restatement (oracle/bh_oracle.c), scaled by 2 "
+                      f"evaluations per step; includes the serial tree build",
+            "seconds": round(c1 - c0, 3),
+        }
+        ref.close()
+    elif rank == 0 and world == 1 and not args.no_cpu_baseline:
         import oracle
         threads = args.cpu_threads or min(16, os.cpu_count() or 1)
         ref = oracle.Oracle(*arrs, theta=args.theta, threads=threads)
@@ -171,7 +220,8 @@ def main():
 
     if rank == 0:
         line = {
-            "metric": "body-steps/sec at N=1e6, theta=0.5; achieved HBM GB/s vs roofline",
+            "metric": "body-steps/sec at N=1e6, theta=0.5; achieved HBM GB/s vs roofline"
+            if args.config == "c3" else f"body-steps/sec ({args.config}, theta={args.theta})",
             "value": round(value, 1),
             "unit": "body-steps/s",
             "n_gpus": world,

@@ -288,3 +288,49 @@ def test_fast_math_sequences_exact():
     """The traversal's reduced sqrt / seeded-reciprocal sequences (traverse.hip) equal IEEE
     sqrt, 1.0/sqrt and 1.0/x bit-for-bit on 2^26 operands across the fast-path range."""
     assert bh_amd.selftest_fast_math(1 << 26, seed=20261015) == 0
+
+
+def _theta0_mixed_scene():
+    """Two disks plus coincident pairs (jitter), out-of-root, zero- and negative-mass bodies."""
+    x, y, vx, vy, m = (a.copy() for a in scenes.two_disks(2500, 600))
+    rng = np.random.default_rng(21)
+    dup = rng.choice(len(x), 30, replace=False)
+    ex = np.concatenate([x[dup], x[dup[:10]] + 3e-4, [-5.0, 2403.0, 700.0]])
+    ey = np.concatenate([y[dup], y[dup[:10]] - 2e-4, [300.0, 100.0, 900.0]])
+    em = np.concatenate([np.full(40, 1.0), [2.0, 2.0, 2.0]])
+    x, y, m = np.concatenate([x, ex]), np.concatenate([y, ey]), np.concatenate([m, em])
+    vx = np.concatenate([vx, np.zeros(len(ex))])
+    vy = np.concatenate([vy, np.zeros(len(ex))])
+    m[[7, 99]] = 0.0   # never visited as leaves; their own a = 0/0
+    m[[13]] = -1.5     # visited, negative contribution
+    perm = rng.permutation(len(x))
+    return tuple(a[perm] for a in (x, y, vx, vy, m))
+
+
+def test_theta0_direct_all_pairs():
+    """theta = 0 runs the all-pairs kernel over the tree's leaf list (direct.hip): bit-identical
+    to the oracle's tree walk (every leaf, pre-order), incl. jitter, out-of-root, zero and
+    negative masses; then full steps through the same path."""
+    arrs = _theta0_mixed_scene()
+    eng, ref = _pair(arrs, theta=0.0, merge_min_dist=0.0)
+    ax, ay = eng.compute_accelerations()        # no visit counts -> the direct kernel
+    rax, ray = ref.accelerations()
+    assert np.array_equal(ax, rax, equal_nan=True) and np.array_equal(ay, ray, equal_nan=True)
+    fin = np.isfinite(rax)
+    assert fin.sum() == len(rax) - 2
+    assert bits_equal(ax[fin], rax[fin]) and bits_equal(ay[fin], ray[fin])
+    _assert_state_equal(eng, ref, nan_ok=True)  # the jitter mutation
+    eng2, ref2 = _pair(scenes.two_disks(3000, 700), theta=0.0)
+    eng2.step(3)
+    ref2.step(3)
+    _assert_state_equal(eng2, ref2)
+
+
+def test_theta0_direct_c5_sampled():
+    """C5 geometry at 1/8 scale (uniform cloud, 32768 bodies): one theta = 0 evaluation, every
+    body bit-identical to the oracle."""
+    arrs = scenes.uniform(32_768, 0.5, seed=5)
+    eng, ref = _pair(arrs, theta=0.0)
+    ax, ay = eng.compute_accelerations()
+    rax, ray = ref.accelerations()
+    assert bits_equal(ax, rax) and bits_equal(ay, ray)
