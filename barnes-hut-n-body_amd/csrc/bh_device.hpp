@@ -72,8 +72,9 @@ struct ForceParams {
 // Body state in slot order.
 struct BodyState {
     double *x, *y, *vx, *vy, *m;
-    uint32_t *cidx;  // caller (list) index
+    uint32_t *cidx;  // caller (list) index; CIDX_DEAD marks a merged-away body until compaction
 };
+constexpr uint32_t CIDX_DEAD = 1u << 31;
 
 // A chunk-spanning node's children, gathered once its local children are final: per child
 // either a reference to another span node (SPAN_REF | owner boundary) with zero values, or
@@ -153,18 +154,20 @@ struct MergeHeader {
     double pad2, pad3;
 };
 static_assert(sizeof(MergeHeader) == sizeof(MergePair), "mailbox header size");
-// heavy = m > thr (BHA:474) -> slot list (any order); then the distance test (BHA:493-501)
+// heavy = live m > thr (BHA:474) -> slot list (any order); then the distance test (BHA:493-501)
 void merge_candidates(int64_t n, const double *x, const double *y, const double *m,
                       const uint32_t *cidx, double thr, double minD2, uint32_t *heavy,
                       MergePair *box, uint32_t cap, hipStream_t s);
-void apply_merge(uint32_t n_dead, const uint32_t *dead_slots, uint32_t n_upd,
-                 const uint32_t *upd_slots, const double *upd_mass, uint32_t *keep, double *m,
-                 hipStream_t s);
+// Sequential merge rule on the device (one workgroup): removals become tombstones
+// (cidx |= CIDX_DEAD) logged in dlog[scal[2]++]; scal[3] = pair count if the mailbox overflowed.
+// skeys/sidx: scratch of cap entries (lists longer than the LDS sort).
+void merge_replay(const MergePair *box, uint32_t cap, double *m, uint32_t *cidx, uint32_t *scal,
+                  uint32_t *dlog, uint64_t *skeys, uint32_t *sidx, hipStream_t s);
 size_t compact_cub_bytes(int64_t n);
-// Remove slots with keep == 0 preserving order; caller indices are renumbered past the
-// removed ones (dead_cidx sorted ascending, n_dead entries).
-hipError_t compact_state(int64_t n, const uint32_t *keep, const BodyState &src,
-                         const BodyState &dst, const uint32_t *dead_cidx, uint32_t n_dead,
-                         uint32_t *pos, void *tmp, size_t tmp_bytes, hipStream_t s);
+// Remove tombstoned slots preserving order; caller indices are renumbered past the removed
+// ones (dead_cidx sorted ascending, n_dead entries).  keep, pos: n-entry scratch.
+hipError_t compact_state(int64_t n, uint32_t *keep, const BodyState &src, const BodyState &dst,
+                         const uint32_t *dead_cidx, uint32_t n_dead, uint32_t *pos, void *tmp,
+                         size_t tmp_bytes, hipStream_t s);
 
 }  // namespace bh

@@ -67,14 +67,17 @@ struct bh_engine {
     // merge
     uint32_t *heavy = nullptr;
     uint32_t *keep = nullptr, *pos = nullptr;
-    MergePair *box = nullptr;  // mailbox: header + pairs
+    MergePair *box = nullptr;  // candidate pairs: header + pairs
     uint32_t box_cap = 0;
-    uint32_t *mdead = nullptr, *mupd = nullptr, *mdead_cidx = nullptr;
-    double *mupd_mass = nullptr;
-    uint32_t mcap = 0;
+    uint32_t *dlog = nullptr;        // removal log of the running bh_step call (caller indices)
+    uint32_t *dead_sorted = nullptr; // the log sorted, for the compaction's renumbering
+    uint64_t *rkeys = nullptr;       // replay sort scratch (long candidate lists)
+    uint32_t *ridx = nullptr;
+    int64_t dlog_cap = 0;
     bool heavy_possible = true;  // false once a step saw no heavy body (heavies never appear)
-    std::vector<std::vector<uint32_t>> step_dead;  // per-step removals (caller indices)
-    void *pin = nullptr;  // pinned staging for the mailbox / uploads
+    bool merge_ran = false;      // the running bh_step call launched the merge rule
+    std::vector<int64_t> removed;  // removals of the last bh_step call, ascending (BHA:519)
+    void *pin = nullptr;  // pinned staging for small read-backs
     size_t pin_bytes = 0;
 
     void *cub_tmp = nullptr;
@@ -386,14 +389,13 @@ int check_tree_flags(bh_engine *e) {
 }
 
 // ---- merge rule (BHA:463-532) ---------------------------------------------------------
-// The device lists heavy bodies (m > mergeMaxMass) and every (heavy, body) pair closer than
-// mergeMinDist into a small mailbox that comes back with ONE async copy into pinned memory:
-// one host round trip per step.  The host replays the reference's sequential rule exactly
-// over those pairs (list order = caller index), the device applies the removals by an
-// order-preserving compaction.  Heavy bodies only gain mass and never appear, so once a step
-// sees none the rule is skipped until the bodies or mergeMaxMass change.
-constexpr uint32_t kMailboxPairs = 2048;
-
+// Entirely on the device, no host round trip: heavy bodies (m > mergeMaxMass) and every
+// (heavy, body) pair closer than mergeMinDist are collected in parallel, then one workgroup
+// replays the reference's sequential rule over the pairs sorted by caller index
+// (integrate.hip k_merge_replay).  Removed bodies become tombstones that leave the tree, the
+// candidate search and the output at once; the state is compacted once per bh_step call
+// (finish_merges).  Heavy bodies only gain mass and never appear, so once a call ends with
+// none the rule is skipped until the bodies or mergeMaxMass change.
 int pinned_reserve(bh_engine *e, size_t bytes) {
     if (bytes <= e->pin_bytes) return BH_OK;
     if (e->pin) (void)hipHostFree(e->pin);
@@ -404,136 +406,69 @@ int pinned_reserve(bh_engine *e, size_t bytes) {
     return BH_OK;
 }
 
-int merge_bufs(bh_engine *e, uint32_t need) {
-    if (need <= e->mcap && e->mdead) return BH_OK;
-    e->mcap = std::max<uint32_t>(need, 64) * 2;
-    TRY(dev_alloc(e, e->mdead, e->mcap));
-    TRY(dev_alloc(e, e->mdead_cidx, e->mcap));
-    TRY(dev_alloc(e, e->mupd, e->mcap));
-    TRY(dev_alloc(e, e->mupd_mass, e->mcap));
+int merge_bufs(bh_engine *e) {
+    const uint32_t cap = (uint32_t)std::max<int64_t>(1 << 16, e->cap);
+    if (!e->box || e->box_cap < cap) {
+        e->box_cap = cap;
+        TRY(dev_alloc(e, e->box, (size_t)cap + 1));
+        TRY(dev_alloc(e, e->rkeys, cap));
+        TRY(dev_alloc(e, e->ridx, cap));
+    }
+    if (e->dlog_cap < e->cap) {  // at most every body is removed within one call
+        TRY(dev_alloc(e, e->dlog, (size_t)e->cap + 1));
+        TRY(dev_alloc(e, e->dead_sorted, (size_t)e->cap + 1));
+        e->dlog_cap = e->cap;
+    }
     return BH_OK;
 }
 
 int merge(bh_engine *e) {
     if (e->p.merge_min_dist <= 0.0 || e->n <= 1 || !e->heavy_possible) return BH_OK;  // BHA:465
     TRY(mark(e, -1));
-    const int64_t n = e->n;
+    TRY(merge_bufs(e));
     const double minD2 = e->p.merge_min_dist * e->p.merge_min_dist;  // BHA:468
-    if (e->box_cap == 0) {
-        e->box_cap = 1u << 16;
-        TRY(dev_alloc(e, e->box, e->box_cap + 1));
+    merge_candidates(e->n, e->st.x, e->st.y, e->st.m, e->st.cidx, e->p.merge_max_mass, minD2,
+                     e->heavy, e->box, e->box_cap, e->stream);
+    merge_replay(e->box, e->box_cap, e->st.m, e->st.cidx, e->scalars, e->dlog, e->rkeys, e->ridx,
+                 e->stream);
+    HIPCHK(e, hipGetLastError());
+    e->merge_ran = true;
+    TRY(mark(e, 3));
+    return BH_OK;
+}
+
+// End of a bh_step call (the stream is idle): read the removal count, compact the state and
+// renumber caller indices; record the removals for bh_last_removed.
+int finish_merges(bh_engine *e) {
+    e->removed.clear();
+    if (!e->merge_ran) return BH_OK;
+    e->merge_ran = false;
+    TRY(pinned_reserve(e, 64));
+    uint32_t *h = static_cast<uint32_t *>(e->pin);
+    HIPCHK(e, hipMemcpyAsync(h, e->scalars, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(h + 4, e->box, sizeof(MergeHeader), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    const uint32_t nd = h[2], overflow = h[3];
+    const MergeHeader hdr = *reinterpret_cast<const MergeHeader *>(h + 4);
+    if (overflow) {
+        e->err = "merge rule: " + std::to_string(overflow) + " candidate pairs in one step exceed "
+                 "the mailbox capacity " + std::to_string(e->box_cap);
+        return BH_E_CAPACITY;
     }
-    const size_t fast_bytes = sizeof(MergePair) * (1 + kMailboxPairs);
-    TRY(pinned_reserve(e, sizeof(MergePair) * (1 + (size_t)e->box_cap)));
-    uint32_t count = 0, heavies = 0;
-    for (;;) {
-        merge_candidates(n, e->st.x, e->st.y, e->st.m, e->st.cidx, e->p.merge_max_mass, minD2,
-                         e->heavy, e->box, e->box_cap, e->stream);
-        HIPCHK(e, hipGetLastError());
-        HIPCHK(e, hipMemcpyAsync(e->pin, e->box, fast_bytes, hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(e, hipStreamSynchronize(e->stream));  // the one round trip of the step
-        const MergeHeader *h = reinterpret_cast<const MergeHeader *>(e->pin);
-        count = h->pairs;
-        heavies = h->heavies;
-        if (count <= e->box_cap) break;
-        e->box_cap = count + (count >> 1);
-        TRY(dev_alloc(e, e->box, e->box_cap + 1));
-        TRY(pinned_reserve(e, sizeof(MergePair) * (1 + (size_t)e->box_cap)));
-    }
-    if (heavies == 0) e->heavy_possible = false;
-    if (count == 0) {
-        TRY(mark(e, 3));
-        return BH_OK;
-    }
-    if (count > kMailboxPairs) {
-        HIPCHK(e, hipMemcpyAsync(e->pin, e->box, sizeof(MergePair) * (1 + (size_t)count),
-                                 hipMemcpyDeviceToHost, e->stream));
-        HIPCHK(e, hipStreamSynchronize(e->stream));
-    }
-    const MergePair *pp = reinterpret_cast<const MergePair *>(e->pin) + 1;
-    std::vector<MergePair> pr(pp, pp + count);
-    std::sort(pr.begin(), pr.end(), [](const MergePair &a, const MergePair &b) {
-        return a.h_cidx != b.h_cidx ? a.h_cidx < b.h_cidx : a.v_cidx < b.v_cidx;
-    });
-    // Sequential replay of BHA:470-531: heavy bodies in list order; one already absorbed is
-    // skipped; victims absorbed in descending list index (BHA:514-519); a heavy victim
-    // carries the mass it has grown to.
-    std::unordered_map<uint32_t, double> mass;    // current masses of involved bodies
-    std::unordered_map<uint32_t, uint32_t> slot;  // caller index -> slot
-    for (const MergePair &c : pr) {
-        if (!mass.count(c.h_cidx)) mass[c.h_cidx] = c.h_mass;
-        if (!mass.count(c.v_cidx)) mass[c.v_cidx] = c.v_mass;
-        slot[c.h_cidx] = c.h_slot;
-        slot[c.v_cidx] = c.v_slot;
-    }
-    std::unordered_set<uint32_t> dead;
-    std::vector<uint32_t> dead_cidx;
-    std::vector<uint32_t> grown;  // heavy caller indices whose mass changed
-    for (size_t pi = 0; pi < pr.size();) {
-        size_t pe = pi;
-        const uint32_t hi = pr[pi].h_cidx;
-        while (pe < pr.size() && pr[pe].h_cidx == hi) ++pe;
-        if (!dead.count(hi)) {  // bi still in the list; its mass only grew: still heavy
-            double mi = mass[hi];
-            bool any = false;
-            for (size_t q = pe; q > pi; --q) {
-                const uint32_t vj = pr[q - 1].v_cidx;
-                if (dead.count(vj)) continue;
-                mi += mass[vj];  // BHA:518
-                dead.insert(vj);
-                dead_cidx.push_back(vj);
-                any = true;
-            }
-            if (any) {
-                mass[hi] = mi;
-                grown.push_back(hi);
-            }
-        }
-        pi = pe;
-    }
-    if (dead_cidx.empty()) {
-        TRY(mark(e, 3));
-        return BH_OK;
-    }
-    std::sort(dead_cidx.begin(), dead_cidx.end());
-    std::vector<uint32_t> dead_slot, upd_slot;
-    std::vector<double> upd_mass;
-    for (uint32_t c : dead_cidx) dead_slot.push_back(slot[c]);
-    for (uint32_t h : grown)
-        if (!dead.count(h)) {
-            upd_slot.push_back(slot[h]);
-            upd_mass.push_back(mass[h]);
-        }
-    const uint32_t nd = (uint32_t)dead_cidx.size(), nu = (uint32_t)upd_slot.size();
-    TRY(merge_bufs(e, std::max(nd, nu)));
-    // upload from pinned memory (the mailbox bytes were consumed above)
-    TRY(pinned_reserve(e, 4 * (size_t)(2 * nd + nu) + 8 * (size_t)nu + 64));
-    char *u = static_cast<char *>(e->pin);
-    double *u_mass = reinterpret_cast<double *>(u);
-    uint32_t *u_dslot = reinterpret_cast<uint32_t *>(u + 8 * (size_t)nu);
-    uint32_t *u_dcidx = u_dslot + nd;
-    uint32_t *u_uslot = u_dcidx + nd;
-    std::memcpy(u_mass, upd_mass.data(), 8 * (size_t)nu);
-    std::memcpy(u_dslot, dead_slot.data(), 4 * (size_t)nd);
-    std::memcpy(u_dcidx, dead_cidx.data(), 4 * (size_t)nd);
-    std::memcpy(u_uslot, upd_slot.data(), 4 * (size_t)nu);
-    HIPCHK(e, hipMemcpyAsync(e->mdead, u_dslot, 4 * (size_t)nd, hipMemcpyHostToDevice, e->stream));
-    HIPCHK(e, hipMemcpyAsync(e->mdead_cidx, u_dcidx, 4 * (size_t)nd, hipMemcpyHostToDevice,
-                             e->stream));
-    if (nu) {
-        HIPCHK(e, hipMemcpyAsync(e->mupd, u_uslot, 4 * (size_t)nu, hipMemcpyHostToDevice, e->stream));
-        HIPCHK(e, hipMemcpyAsync(e->mupd_mass, u_mass, 8 * (size_t)nu, hipMemcpyHostToDevice,
-                                 e->stream));
-    }
-    HIPCHK(e, hipMemsetD32Async((hipDeviceptr_t)e->keep, 1, (size_t)n, e->stream));
-    apply_merge(nd, e->mdead, nu, e->mupd, e->mupd_mass, e->keep, e->st.m, e->stream);
-    HIPCHK(e, compact_state(n, e->keep, e->st, e->alt, e->mdead_cidx, nd, e->pos, e->cub_tmp,
+    if (hdr.heavies == 0) e->heavy_possible = false;
+    if (nd == 0) return BH_OK;
+    std::vector<uint32_t> dead(nd);
+    HIPCHK(e, hipMemcpy(dead.data(), e->dlog, 4 * (size_t)nd, hipMemcpyDeviceToHost));
+    std::sort(dead.begin(), dead.end());
+    HIPCHK(e, hipMemcpy(e->dead_sorted, dead.data(), 4 * (size_t)nd, hipMemcpyHostToDevice));
+    const int64_t n = e->n;
+    HIPCHK(e, compact_state(n, e->keep, e->st, e->alt, e->dead_sorted, nd, e->pos, e->cub_tmp,
                             e->cub_bytes, e->stream));
     std::swap(e->st, e->alt);
     e->n = n - (int64_t)nd;
-    e->step_dead.push_back(dead_cidx);
+    e->removed.assign(dead.begin(), dead.end());
     e->tree_valid = false;  // BHA:526
-    TRY(mark(e, 3));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
     return BH_OK;
 }
 
@@ -725,7 +660,7 @@ void bh_destroy(bh_engine *e) {
     void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->idx, e->perm, e->cpl, e->cnt,
                     e->base, e->cell_start, e->nodes, e->span_list,
                     e->span_children, e->scalars, e->visits32, e->wave_iters, e->heavy, e->keep,
-                    e->pos, e->box, e->mdead, e->mdead_cidx, e->mupd, e->mupd_mass, e->cub_tmp,
+                    e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->cub_tmp,
                     e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaves.xy, e->leaves.m,
                     e->leaves.slot, e->leaf_tmp};
     for (void *q : ptrs)
@@ -786,7 +721,7 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     HIPCHK(e, hipStreamSynchronize(e->stream));
     e->n = n;
     e->heavy_possible = true;
-    e->step_dead.clear();
+    e->removed.clear();
     e->tree_valid = false;  // BHA:348
     return BH_OK;
 }
@@ -796,11 +731,13 @@ int bh_step(bh_engine *e, int32_t k) {
     HIPCHK(e, hipSetDevice(e->device));
     e->ev_used = 0;
     e->timings_pending = false;
-    HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
-    e->step_dead.clear();
+    HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, 3 * sizeof(uint32_t), e->stream));
+    e->removed.clear();
+    e->merge_ran = false;
     for (int32_t s = 0; s < k; ++s) TRY(step_once(e));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     if (e->n > 0 && k > 0) TRY(check_tree_flags(e));
+    TRY(finish_merges(e));
     if (e->profiling) TRY(collect_timings(e));
     return BH_OK;
 }
@@ -898,28 +835,11 @@ int bh_get_quads(bh_engine *e, double *cx, double *cy, double *h, int64_t cap, i
 
 int bh_last_removed(const bh_engine *e, int64_t *idx, int64_t cap, int64_t *n_out) {
     if (!e || cap < 0 || (cap > 0 && !idx)) return BH_E_INVALID;
-    // compose the per-step removal lists into indices of the list before the call
-    std::vector<int64_t> orig;  // sorted
-    for (const auto &dl : e->step_dead) {
-        std::vector<int64_t> add;
-        size_t r = 0;
-        int64_t shift = 0;
-        for (uint32_t d : dl) {  // d ascending: index among the survivors so far
-            int64_t o = (int64_t)d + shift;
-            while (r < orig.size() && orig[r] <= o) {
-                ++r;
-                ++shift;
-                o = (int64_t)d + shift;
-            }
-            add.push_back(o);
-        }
-        std::vector<int64_t> merged;
-        std::merge(orig.begin(), orig.end(), add.begin(), add.end(), std::back_inserter(merged));
-        orig.swap(merged);
-    }
-    if (n_out) *n_out = (int64_t)orig.size();
-    if ((int64_t)orig.size() > cap) return BH_E_CAPACITY;
-    for (size_t i = 0; i < orig.size(); ++i) idx[i] = orig[i];
+    // caller indices are not renumbered inside a call, so the log is already relative to the
+    // list before the call
+    if (n_out) *n_out = (int64_t)e->removed.size();
+    if ((int64_t)e->removed.size() > cap) return BH_E_CAPACITY;
+    for (size_t i = 0; i < e->removed.size(); ++i) idx[i] = e->removed[i];
     return BH_OK;
 }
 

@@ -70,17 +70,18 @@ __global__ __launch_bounds__(TB) void k_scatter_acc(int64_t n, const uint32_t *_
     ay[o] = a2[2 * i + 1];
 }
 
-// heavy bodies: m > mergeMaxMass (BHA:474), appended in any order (the host replays in list
-// order using the caller indices carried by every candidate pair)
-__global__ __launch_bounds__(TB) void k_heavy(int64_t n, const double *__restrict__ m, double thr,
+// heavy bodies: m > mergeMaxMass (BHA:474), live ones only; appended in any order (the
+// replay below orders them by caller index)
+__global__ __launch_bounds__(TB) void k_heavy(int64_t n, const double *__restrict__ m,
+                                              const uint32_t *__restrict__ cidx, double thr,
                                               uint32_t *__restrict__ heavy, MergeHeader *hdr) {
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
-    if (m[i] > thr) heavy[atomicAdd(&hdr->heavies, 1u)] = (uint32_t)i;
+    if (m[i] > thr && !(cidx[i] & CIDX_DEAD)) heavy[atomicAdd(&hdr->heavies, 1u)] = (uint32_t)i;
 }
 
-// BHA:493-501: for every heavy body h and every body j != h: dx*dx + dy*dy < minD2 with
-// dx = bj.x - bi.x.  Pairs are appended in any order; the host sorts and replays them.
+// BHA:493-501: for every heavy body h and every live body j != h: dx*dx + dy*dy < minD2 with
+// dx = bj.x - bi.x.  Pairs are appended in any order; the replay sorts them.
 __global__ __launch_bounds__(TB) void k_candidates(int64_t n, const double *__restrict__ x,
                                                    const double *__restrict__ y,
                                                    const double *__restrict__ m,
@@ -92,6 +93,8 @@ __global__ __launch_bounds__(TB) void k_candidates(int64_t n, const double *__re
     const uint32_t H = __builtin_amdgcn_readfirstlane(
         __hip_atomic_load(&hdr->heavies, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
     if (j >= n || H == 0) return;
+    const uint32_t cj = cidx[j];
+    if (cj & CIDX_DEAD) return;
     const double xj = x[j], yj = y[j];
     for (uint32_t k = 0; k < H; ++k) {
         const uint32_t hs = heavy[k];
@@ -100,19 +103,141 @@ __global__ __launch_bounds__(TB) void k_candidates(int64_t n, const double *__re
         const double dy = yj - y[hs];
         if (dx * dx + dy * dy < minD2) {
             const uint32_t slot = atomicAdd(&hdr->pairs, 1u);
-            if (slot < cap) box[1 + slot] = MergePair{cidx[hs], cidx[j], hs, (uint32_t)j, m[hs], m[j]};
+            if (slot < cap) box[1 + slot] = MergePair{cidx[hs], cj, hs, (uint32_t)j, m[hs], m[j]};
         }
     }
 }
 
-__global__ __launch_bounds__(TB) void k_apply_merge(uint32_t n_dead, const uint32_t *__restrict__ dead,
-                                                    uint32_t n_upd, const uint32_t *__restrict__ upd,
-                                                    const double *__restrict__ upd_mass,
-                                                    uint32_t *__restrict__ keep,
-                                                    double *__restrict__ m) {
-    uint32_t i = blockIdx.x * TB + threadIdx.x;
-    if (i < n_dead) keep[dead[i]] = 0u;
-    if (i < n_upd) m[upd[i]] = upd_mass[i];  // BHA:518 bi.m += bj.m (final value)
+// Sequential replay of BHA:470-531 over candidate pairs sorted by (heavy, victim) caller
+// index: heavy bodies in list order, one already absorbed is skipped; victims absorbed in
+// descending list index (BHA:514-519), a heavy victim carrying the mass it has grown to;
+// m[h] += m[v] in that order (BHA:518).  Removal = tombstone (CIDX_DEAD; the body leaves the
+// tree, the candidate search and the output) plus an entry in the removal log; the host
+// compacts once per bh_step call.
+template <class K, class I>
+__device__ void replay_sorted(const MergePair *pairs, uint32_t count, K key, I idx, double *m,
+                              uint32_t *cidx, uint32_t *dlog, uint32_t &nd) {
+    for (uint32_t q = 0; q < count;) {
+        const uint32_t h = (uint32_t)(key(q) >> 32);
+        uint32_t qe = q;
+        while (qe < count && (uint32_t)(key(qe) >> 32) == h) ++qe;
+        const uint32_t hs = pairs[idx(q)].h_slot;
+        if (!(cidx[hs] & CIDX_DEAD)) {
+            double mi = m[hs];
+            bool any = false;
+            for (uint32_t r = qe; r > q; --r) {
+                const uint32_t vs = pairs[idx(r - 1)].v_slot;
+                const uint32_t cv = cidx[vs];
+                if (cv & CIDX_DEAD) continue;
+                mi += m[vs];  // BHA:518
+                dlog[nd++] = cv;
+                cidx[vs] = cv | CIDX_DEAD;
+                any = true;
+            }
+            if (any) m[hs] = mi;
+        }
+        q = qe;
+    }
+}
+
+constexpr int REPLAY_TB = 256;
+constexpr int REPLAY_LDS = 2048;
+
+__device__ __forceinline__ uint64_t pair_key(const MergePair &p) {
+    return ((uint64_t)p.h_cidx << 32) | p.v_cidx;
+}
+
+__global__ __launch_bounds__(REPLAY_TB) void k_merge_replay(const MergePair *__restrict__ box,
+                                                            uint32_t cap, double *m,
+                                                            uint32_t *cidx, uint32_t *scal,
+                                                            uint32_t *dlog, uint64_t *skeys,
+                                                            uint32_t *sidx) {
+    __shared__ uint64_t lk[REPLAY_LDS];
+    __shared__ uint32_t li[REPLAY_LDS];
+    const MergeHeader *hdr = reinterpret_cast<const MergeHeader *>(box);
+    const uint32_t count = hdr->pairs;
+    if (count == 0) return;
+    const MergePair *pairs = box + 1;
+    if (count > cap) {  // pairs were dropped: cannot replay exactly
+        if (threadIdx.x == 0) scal[3] = count;
+        return;
+    }
+    uint32_t nd = scal[2];
+    if (count <= REPLAY_LDS) {  // bitonic sort of (key, index) in LDS
+        uint32_t P = 1;
+        while (P < count) P <<= 1;
+        for (uint32_t i = threadIdx.x; i < P; i += REPLAY_TB) {
+            lk[i] = i < count ? pair_key(pairs[i]) : ~0ull;
+            li[i] = i;
+        }
+        __syncthreads();
+        for (uint32_t k = 2; k <= P; k <<= 1) {
+            for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+                for (uint32_t i = threadIdx.x; i < P; i += REPLAY_TB) {
+                    const uint32_t l = i ^ j;
+                    if (l > i) {
+                        const bool up = (i & k) == 0;
+                        if ((lk[i] > lk[l]) == up) {
+                            const uint64_t tk = lk[i];
+                            lk[i] = lk[l];
+                            lk[l] = tk;
+                            const uint32_t ti = li[i];
+                            li[i] = li[l];
+                            li[l] = ti;
+                        }
+                    }
+                }
+                __syncthreads();
+            }
+        }
+        if (threadIdx.x == 0) {
+            replay_sorted(
+                pairs, count, [&](uint32_t q) { return lk[q]; }, [&](uint32_t q) { return li[q]; },
+                m, cidx, dlog, nd);
+            scal[2] = nd;
+        }
+        return;
+    }
+    if (threadIdx.x != 0) return;  // large lists (rare): one-thread heapsort in global scratch
+    for (uint32_t i = 0; i < count; ++i) {
+        skeys[i] = pair_key(pairs[i]);
+        sidx[i] = i;
+    }
+    auto sift = [&](uint32_t root, uint32_t end) {
+        for (;;) {
+            uint32_t c = 2 * root + 1;
+            if (c >= end) return;
+            if (c + 1 < end && skeys[c] < skeys[c + 1]) ++c;
+            if (skeys[root] >= skeys[c]) return;
+            const uint64_t tk = skeys[root];
+            skeys[root] = skeys[c];
+            skeys[c] = tk;
+            const uint32_t ti = sidx[root];
+            sidx[root] = sidx[c];
+            sidx[c] = ti;
+            root = c;
+        }
+    };
+    for (uint32_t r = count / 2; r-- > 0;) sift(r, count);
+    for (uint32_t end = count; end-- > 1;) {
+        const uint64_t tk = skeys[0];
+        skeys[0] = skeys[end];
+        skeys[end] = tk;
+        const uint32_t ti = sidx[0];
+        sidx[0] = sidx[end];
+        sidx[end] = ti;
+        sift(0, end);
+    }
+    replay_sorted(
+        pairs, count, [&](uint32_t q) { return skeys[q]; }, [&](uint32_t q) { return sidx[q]; },
+        m, cidx, dlog, nd);
+    scal[2] = nd;
+}
+
+__global__ __launch_bounds__(TB) void k_keep(int64_t n, const uint32_t *__restrict__ cidx,
+                                             uint32_t *__restrict__ keep) {
+    int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i < n) keep[i] = (cidx[i] & CIDX_DEAD) ? 0u : 1u;
 }
 
 // compaction (BHA:519 removeAt), order preserved; list indices shift past removed ones
@@ -174,16 +299,13 @@ void merge_candidates(int64_t n, const double *x, const double *y, const double 
     (void)hipMemsetAsync(box, 0, sizeof(MergeHeader), s);
     if (n <= 0) return;
     MergeHeader *hdr = reinterpret_cast<MergeHeader *>(box);
-    k_heavy<<<grid_for(n), TB, 0, s>>>(n, m, thr, heavy, hdr);
+    k_heavy<<<grid_for(n), TB, 0, s>>>(n, m, cidx, thr, heavy, hdr);
     k_candidates<<<grid_for(n), TB, 0, s>>>(n, x, y, m, cidx, heavy, minD2, box, cap);
 }
 
-void apply_merge(uint32_t n_dead, const uint32_t *dead_slots, uint32_t n_upd,
-                 const uint32_t *upd_slots, const double *upd_mass, uint32_t *keep, double *m,
-                 hipStream_t s) {
-    uint32_t c = n_dead > n_upd ? n_dead : n_upd;
-    if (c) k_apply_merge<<<(c + TB - 1) / TB, TB, 0, s>>>(n_dead, dead_slots, n_upd, upd_slots,
-                                                          upd_mass, keep, m);
+void merge_replay(const MergePair *box, uint32_t cap, double *m, uint32_t *cidx, uint32_t *scal,
+                  uint32_t *dlog, uint64_t *skeys, uint32_t *sidx, hipStream_t s) {
+    k_merge_replay<<<1, REPLAY_TB, 0, s>>>(box, cap, m, cidx, scal, dlog, skeys, sidx);
 }
 
 size_t compact_cub_bytes(int64_t n) {
@@ -193,9 +315,10 @@ size_t compact_cub_bytes(int64_t n) {
     return b;
 }
 
-hipError_t compact_state(int64_t n, const uint32_t *keep, const BodyState &src,
-                         const BodyState &dst, const uint32_t *dead_cidx, uint32_t n_dead,
-                         uint32_t *pos, void *tmp, size_t tmp_bytes, hipStream_t s) {
+hipError_t compact_state(int64_t n, uint32_t *keep, const BodyState &src, const BodyState &dst,
+                         const uint32_t *dead_cidx, uint32_t n_dead, uint32_t *pos, void *tmp,
+                         size_t tmp_bytes, hipStream_t s) {
+    k_keep<<<grid_for(n), TB, 0, s>>>(n, src.cidx, keep);
     hipError_t st = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, keep, pos, (int)n, s);
     if (st != hipSuccess) return st;
     k_compact<<<grid_for(n), TB, 0, s>>>(n, keep, pos, src, dst, dead_cidx, n_dead);

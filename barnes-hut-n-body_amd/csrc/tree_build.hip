@@ -57,7 +57,8 @@ __device__ void cell_centre(const Geometry &g, uint64_t key, int L, double &cx, 
 }
 
 __global__ __launch_bounds__(TB) void k_morton(int64_t n, const double *__restrict__ x,
-                                               const double *__restrict__ y, Geometry g,
+                                               const double *__restrict__ y,
+                                               const uint32_t *__restrict__ cidx, Geometry g,
                                                uint64_t *__restrict__ keys,
                                                uint32_t *__restrict__ idx) {
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
@@ -65,8 +66,8 @@ __global__ __launch_bounds__(TB) void k_morton(int64_t n, const double *__restri
     double px = x[i], py = y[i];
     double cx = g.root_cx, cy = g.root_cy;
     uint64_t key;
-    if (!quad_contains(cx, cy, g.root_h, px, py)) {
-        key = sentinel_key(g.J);  // BHA:126 — not inserted
+    if (!quad_contains(cx, cy, g.root_h, px, py) || (cidx[i] & CIDX_DEAD)) {
+        key = sentinel_key(g.J);  // BHA:126 — not inserted (or merged away this call)
     } else {
         key = 0;
         for (int d = 0; d < g.J; ++d) {
@@ -819,7 +820,7 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     if (n <= 0) return hipMemsetAsync(b.base, 0, sizeof(uint32_t), s);
     hipError_t st;
     const int D0 = cell_table_depth(g.J, n);
-    k_morton<<<grid_for(n), TB, 0, s>>>(n, b.src.x, b.src.y, g, b.keys, b.idx);
+    k_morton<<<grid_for(n), TB, 0, s>>>(n, b.src.x, b.src.y, b.src.cidx, g, b.keys, b.idx);
     size_t bytes = b.cub_bytes;
     st = rocprim::radix_sort_pairs<SortConfig>(b.cub_tmp, bytes, b.keys, b.keys_s, b.idx, b.perm,
                                                (size_t)n, 0u, (unsigned)(2 * g.J + 1), s);
