@@ -45,6 +45,21 @@ def parse():
     return ap.parse_args()
 
 
+def measured_traffic(config, kernel):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of this workload
+    (profiles/hbm_traffic.json, written from rocprofv3 FETCH_SIZE/WRITE_SIZE passes by
+    tools/summarize_profile.py), or None."""
+    path = os.path.join(ROOT, "profiles", "hbm_traffic.json")
+    try:
+        with open(path) as fh:
+            ent = json.load(fh).get(config, {}).get(kernel)
+    except (OSError, ValueError):
+        return None, None
+    if not ent:
+        return None, None
+    return ent.get("hbm_bytes_per_launch"), ent.get("source")
+
+
 def scene_for(config, world):
     from bh_amd import scenes
     if config == "c3" and world > 1:
@@ -150,7 +165,7 @@ def main():
             "peak": FP64_VEC_PEAK_TF,
             "unit": "TFLOP/s",
             "frac": round(achieved / FP64_VEC_PEAK_TF, 4),
-            "traffic": None,
+            "traffic": measured_traffic(scene_name, "k_direct")[0],
             "kernel": "k_direct",
             "kernel_avg_ms": round(trav_ms, 4),
             "launches": trav_launches,
@@ -167,7 +182,8 @@ def main():
             "peak": HBM_PEAK_GBS,
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": None,
+            "traffic": measured_traffic(scene_name, "k_traverse")[0],
+            "traffic_source": measured_traffic(scene_name, "k_traverse")[1],
             "kernel": "k_traverse",
             "kernel_avg_ms": round(trav_ms, 4),
             "launches": trav_launches,
