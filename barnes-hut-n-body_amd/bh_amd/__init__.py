@@ -167,7 +167,7 @@ class Engine:
         self._lib = load_library()
         self._h = _VP()
         self.params = params if params is not None else default_params()
-        if world > 1:
+        if world > 1 or unique_id is not None:
             rc = self._lib.bh_create_dist(ctypes.byref(self.params), device, rank, world,
                                           unique_id, ctypes.byref(self._h))
         else:

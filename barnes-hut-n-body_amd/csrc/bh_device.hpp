@@ -44,6 +44,10 @@ constexpr int COM_CHUNK_SHIFT = 10;
 __host__ __device__ inline uint32_t span_stride_for(int64_t n) {
     return (uint32_t)((n >> COM_CHUNK_SHIFT) + 2);
 }
+// chunk boundaries are grouped by 1024 (one span workgroup each, tree_build.hip)
+__host__ __device__ inline uint32_t span_groups(uint32_t span_stride) {
+    return (span_stride + 1023) / 1024;
+}
 
 // Cell-start table: first sorted body of every depth-D0 cell, so the end of any node at
 // depth <= D0 is one load, and deeper searches stay inside one depth-D0 cell.
@@ -99,6 +103,7 @@ struct TreeBuffers {
     uint32_t *span_list;   // [(J + 1) * span_stride]: chunk-spanning node per (level, boundary)
     uint32_t span_stride;
     struct SpanSlot *span_children;  // [(J + 1) * span_stride]
+    uint32_t *super_list;  // [(J + 1) * span_groups]: group-crossing span node per (level, group)
     void *cub_tmp;
     size_t cub_bytes;
 };

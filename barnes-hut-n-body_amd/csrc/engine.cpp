@@ -57,7 +57,7 @@ struct bh_engine {
     uint32_t *cell_start = nullptr;
     Node *nodes = nullptr;
     size_t node_cap = 0;
-    uint32_t *span_list = nullptr;
+    uint32_t *span_list = nullptr, *super_list = nullptr;
     bh::SpanSlot *span_children = nullptr;
     uint32_t *scalars = nullptr;  // [1] tree error flags
     uint32_t *visits32 = nullptr;
@@ -222,6 +222,8 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(dev_alloc(e, e->nodes, ncap));
         TRY(dev_alloc(e, e->span_list, (size_t)(J + 2) * span_stride_for(e->cap)));
         TRY(dev_alloc(e, e->span_children, (size_t)(J + 2) * span_stride_for(e->cap)));
+        TRY(dev_alloc(e, e->super_list,
+                      (size_t)(J + 2) * span_groups(span_stride_for(e->cap))));
         TRY(dev_alloc(e, e->cell_start,
                       ((size_t)1 << (2 * std::min(J, CELL_TABLE_MAX_DEPTH))) + 2));
         e->node_cap = ncap;
@@ -254,6 +256,7 @@ TreeBuffers tree_buffers(bh_engine *e) {
     b.span_list = e->span_list;
     b.span_stride = span_stride_for(e->cap);
     b.span_children = e->span_children;
+    b.super_list = e->super_list;
     b.cub_tmp = e->cub_tmp;
     b.cub_bytes = e->cub_bytes;
     return b;
@@ -342,12 +345,12 @@ int evaluate(bh_engine *e, uint32_t *visits) {
                                   e->leaf_count, e->leaves, n, e->leaf_tmp, e->leaf_tmp_bytes,
                                   e->stream));
         int64_t lo = 0, hi = n;
-        if (e->world > 1) bh_shard_range(n, e->rank, e->world, &lo, &hi);
+        if (e->comm) bh_shard_range(n, e->rank, e->world, &lo, &hi);
         direct_forces(e->leaves, e->leaf_count, e->st.x, e->st.y, e->st.m, lo, hi, fp.G,
                       fp.soft2, e->a2, e->stream);
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
-        if (e->world > 1) {
+        if (e->comm) {
             const int64_t chunk = (n + e->world - 1) / e->world;
             NCCLCHK(e, ncclAllGather(e->a2 + 2 * e->rank * chunk, e->a2, (size_t)(2 * chunk),
                                      ncclDouble, e->comm, e->stream));
@@ -355,7 +358,7 @@ int evaluate(bh_engine *e, uint32_t *visits) {
         }
         return BH_OK;
     }
-    if (e->world == 1 || visits) {
+    if (!e->comm || visits) {
         traverse(e->nodes, d_T, e->st.x, e->st.y, e->st.m, 0, n, e->geo, fp, e->a2, visits,
                  e->wave_iters, e->stream);
         HIPCHK(e, hipGetLastError());
@@ -632,7 +635,7 @@ int bh_create_dist(const bh_params *p, int device, int rank, int world, const vo
     e->rank = rank;
     e->world = world;
     int rc = engine_init(e, p, device);
-    if (rc == BH_OK && world > 1) {
+    if (rc == BH_OK && unique_id) {  // world == 1 with an id: the RCCL path on one rank
         ncclUniqueId id;
         std::memcpy(&id, unique_id, sizeof(id));
         ncclResult_t nr = ncclCommInitRank(&e->comm, world, id, rank);
@@ -658,7 +661,7 @@ void bh_destroy(bh_engine *e) {
     free_state(e->st);
     free_state(e->alt);
     void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->idx, e->perm, e->cpl, e->cnt,
-                    e->base, e->cell_start, e->nodes, e->span_list,
+                    e->base, e->cell_start, e->nodes, e->span_list, e->super_list,
                     e->span_children, e->scalars, e->visits32, e->wave_iters, e->heavy, e->keep,
                     e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->cub_tmp,
                     e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaves.xy, e->leaves.m,

@@ -582,6 +582,10 @@ __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
 // by the boundary of the chunk it starts in: span_list[L * stride + k] (or NO_SPAN).
 constexpr uint32_t NO_SPAN = 0xFFFFFFFFu;
 constexpr uint32_t SPAN_REF = 1u << 31;  // child list entry: owner slot of a span child
+// span_list entry flag: the node also crosses a GROUP boundary (groups of SPAN_GROUP chunk
+// boundaries, finished by one workgroup each); such nodes are finished by k_com_span_top
+constexpr uint32_t SPAN_SUPER = 1u << 31;
+constexpr int SPAN_GROUP = 1024;
 
 __global__ __launch_bounds__(TB) void k_span_find(int64_t n, int J, int D0,
                                                   const uint64_t *__restrict__ keys_s,
@@ -589,7 +593,9 @@ __global__ __launch_bounds__(TB) void k_span_find(int64_t n, int J, int D0,
                                                   const uint32_t *__restrict__ base,
                                                   const uint32_t *__restrict__ cell_start,
                                                   uint32_t *__restrict__ span_list,
-                                                  uint32_t span_stride, Node *nodes) {
+                                                  uint32_t span_stride,
+                                                  uint32_t *__restrict__ super_list,
+                                                  uint32_t n_groups, Node *nodes) {
     const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
     const int L = blockIdx.y;
     if (k >= (int64_t)span_stride) return;
@@ -614,10 +620,17 @@ __global__ __launch_bounds__(TB) void k_span_find(int64_t n, int J, int D0,
         }
         if (aL >= chunk0) {  // starts in chunk k: this boundary owns it
             const int cp = aL > 0 ? (int)cpl[aL - 1] : -1;
-            out = base[aL] + (uint32_t)(L - cp - 1);
+            const uint32_t ni = base[aL] + (uint32_t)(L - cp - 1);
             // the owner slot rides in the (not yet computed) comX of the span node, so its
             // parent's child list can refer to the slot (k_span_children)
-            nodes[out].comX = __longlong_as_double((long long)k);
+            nodes[ni].comX = __longlong_as_double((long long)k);
+            // does the node also contain the first group boundary at or after chunk k?
+            const int64_t kG = (k / SPAN_GROUP) * SPAN_GROUP + SPAN_GROUP - 1;
+            const int64_t bG = (kG << COM_CHUNK_SHIFT) + (1 << COM_CHUNK_SHIFT) - 1;
+            const int shift = 2 * (J - L);
+            const bool super = bG + 1 < n && (keys_s[bG + 1] >> shift) == (key >> shift);
+            out = ni | (super ? SPAN_SUPER : 0u);
+            if (super) super_list[(size_t)L * n_groups + (uint32_t)(kG / SPAN_GROUP)] = (uint32_t)k;
         }
     }
     span_list[(size_t)L * span_stride + k] = out;
@@ -633,9 +646,10 @@ __global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__r
     const uint32_t L = blockIdx.y;
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < span_stride; i += gridDim.x * TB) {
         const size_t slot = (size_t)L * span_stride + i;
-        const uint32_t ni = span_list[slot];
+        const uint32_t e = span_list[slot];
+        const uint32_t ni = e & ~SPAN_SUPER;
         SpanSlot out;
-        const uint32_t end = ni != NO_SPAN ? nodes[ni].next : 0u;  // empty slot: no children
+        const uint32_t end = e != NO_SPAN ? nodes[ni].next : 0u;  // empty slot: no children
         uint32_t c = ni + 1;
         for (int k = 0; k < 4; ++k) {
             out.ch[k] = 0xFFFFFFFFu;
@@ -660,13 +674,13 @@ __global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__r
     }
 }
 
-// All chunk-spanning nodes, levels J..0, by ONE workgroup; thread k owns boundary k.  The
-// previous level's results live in LDS (a span child is referenced by its owner slot); the
-// per-level records are loaded two levels ahead, and stores to global stay in flight across
-// the LDS-only barriers.  Requires span_stride <= SPAN_LDS; larger trees use
-// k_com_span_global.
-constexpr int SPAN_TB = 1024;
-constexpr int SPAN_LDS = SPAN_TB;  // boundaries held in LDS (one per thread)
+// Chunk-spanning nodes, levels J..0: workgroup g owns the chunk boundaries
+// [g*SPAN_GROUP, (g+1)*SPAN_GROUP), thread = boundary, and finishes the span nodes that do
+// not cross a group boundary (their span children are then in the same group).  The previous
+// level's results live in LDS (a span child is referenced by its owner slot); each level's
+// records are loaded one level ahead; stores to global stay in flight across the LDS-only
+// barriers.
+constexpr int SPAN_TB = SPAN_GROUP;
 
 struct SpanRegs {
     uint32_t ni;
@@ -687,88 +701,81 @@ __device__ __forceinline__ void load_span(SpanRegs &r, const uint32_t *span_list
     }
 }
 
-// One level of k_com_span with the record R of this level; R is then refilled with the
-// record three levels up the loop (fixed register roles: no copies of in-flight loads).
-__device__ __forceinline__ void span_level(int L, SpanRegs &R, uint32_t k, uint32_t kk,
-                                           uint32_t span_stride, const uint32_t *span_list,
-                                           const SpanSlot *span_children, Node *nodes,
-                                           double (*r_m)[SPAN_LDS], double (*r_x)[SPAN_LDS],
-                                           double (*r_y)[SPAN_LDS]) {
-    const int cur = L & 1, prev = cur ^ 1;
-    if (R.ni != NO_SPAN && k < span_stride) {
-        double mSum = 0.0, cx = 0.0, cy = 0.0;  // children 0..3 in order (BHA:189-192)
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-            if (R.ch[c] != 0xFFFFFFFFu && (R.ch[c] & SPAN_REF)) {
-                const uint32_t s2 = R.ch[c] & ~SPAN_REF;
-                const double cm = r_m[prev][s2];
-                if (cm > 0.0) {
-                    mSum += cm;
-                    cx += r_x[prev][s2] * cm;
-                    cy += r_y[prev][s2] * cm;
-                }
-            } else {  // local child (or none): precomputed, zeros when skipped
-                mSum += R.v[c][0];
-                cx += R.v[c][1];
-                cy += R.v[c][2];
-            }
-        }
-        double ox = 0.0, oy = 0.0;
-        if (mSum > 0.0) {
-            ox = cx / mSum;
-            oy = cy / mSum;
-        }
-        r_m[cur][k] = mSum;
-        r_x[cur][k] = ox;
-        r_y[cur][k] = oy;
-        Node *dst = nodes + R.ni;
-        dst->mass = mSum;
-        dst->comX = ox;  // massless: never visited (the cell centre is not recorded)
-        dst->comY = oy;
-        if (!(mSum > 0.0)) dst->meta |= NODE_SKIP;
-    }
-    if (L >= 3) load_span(R, span_list, span_children, (size_t)(L - 3) * span_stride + kk);
-    __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): LDS results visible; loads/stores fly on
-    __builtin_amdgcn_s_barrier();
-}
-
 __global__ __launch_bounds__(SPAN_TB) void k_com_span(int J, const uint32_t *__restrict__ span_list,
                                                       uint32_t span_stride,
                                                       const SpanSlot *__restrict__ span_children,
                                                       Node *nodes) {
-    __shared__ double r_m[2][SPAN_LDS], r_x[2][SPAN_LDS], r_y[2][SPAN_LDS];
-    const uint32_t k = threadIdx.x;
-    const uint32_t kk = k < span_stride ? k : 0;  // threads past the table mirror slot 0
-    SpanRegs R0, R1, R2;
-    load_span(R0, span_list, span_children, (size_t)J * span_stride + kk);
-    if (J >= 1) load_span(R1, span_list, span_children, (size_t)(J - 1) * span_stride + kk);
-    if (J >= 2) load_span(R2, span_list, span_children, (size_t)(J - 2) * span_stride + kk);
-    for (int L = J; L >= 0; L -= 3) {
-        span_level(L, R0, k, kk, span_stride, span_list, span_children, nodes, r_m, r_x, r_y);
-        if (L < 1) break;
-        span_level(L - 1, R1, k, kk, span_stride, span_list, span_children, nodes, r_m, r_x, r_y);
-        if (L < 2) break;
-        span_level(L - 2, R2, k, kk, span_stride, span_list, span_children, nodes, r_m, r_x, r_y);
+    __shared__ double r_m[2][SPAN_GROUP], r_x[2][SPAN_GROUP], r_y[2][SPAN_GROUP];
+    const uint32_t g0 = blockIdx.x * SPAN_GROUP;
+    const uint32_t kl = threadIdx.x, k = g0 + kl;
+    const bool valid = k < span_stride;
+    const uint32_t kk = valid ? k : g0;  // threads past the table mirror the group's first slot
+    SpanRegs A;
+    load_span(A, span_list, span_children, (size_t)J * span_stride + kk);
+    for (int L = J; L >= 0; --L) {
+        const int cur = L & 1, prev = cur ^ 1;
+        const SpanRegs C = A;
+        if (L > 0) load_span(A, span_list, span_children, (size_t)(L - 1) * span_stride + kk);
+        if (valid && C.ni != NO_SPAN && !(C.ni & SPAN_SUPER)) {
+            double mSum = 0.0, cx = 0.0, cy = 0.0;  // children 0..3 in order (BHA:189-192)
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                if (C.ch[c] != 0xFFFFFFFFu && (C.ch[c] & SPAN_REF)) {
+                    const uint32_t s2 = (C.ch[c] & ~SPAN_REF) - g0;
+                    const double cm = r_m[prev][s2];
+                    if (cm > 0.0) {
+                        mSum += cm;
+                        cx += r_x[prev][s2] * cm;
+                        cy += r_y[prev][s2] * cm;
+                    }
+                } else {  // local child (or none): precomputed, zeros when skipped
+                    mSum += C.v[c][0];
+                    cx += C.v[c][1];
+                    cy += C.v[c][2];
+                }
+            }
+            double ox = 0.0, oy = 0.0;
+            if (mSum > 0.0) {
+                ox = cx / mSum;
+                oy = cy / mSum;
+            }
+            r_m[cur][kl] = mSum;
+            r_x[cur][kl] = ox;
+            r_y[cur][kl] = oy;
+            Node *dst = nodes + C.ni;
+            dst->mass = mSum;
+            dst->comX = ox;  // massless: never visited (the cell centre is not recorded)
+            dst->comY = oy;
+            if (!(mSum > 0.0)) dst->meta |= NODE_SKIP;
+        }
+        __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): LDS results visible; stores fly on
+        __builtin_amdgcn_s_barrier();
     }
 }
 
-// Same, for trees too large for the LDS variant: results through global memory.
-__global__ __launch_bounds__(SPAN_TB) void k_com_span_global(int J,
-                                                             const uint32_t *__restrict__ span_list,
-                                                             uint32_t span_stride,
-                                                             const SpanSlot *__restrict__ span_children,
-                                                             Node *nodes) {
+// The nodes that cross a group boundary (few: at most one per group boundary and level),
+// levels J..0, one workgroup, thread = group boundary.  Children come from the records
+// (local ones) or from the node array (span children: finished by k_com_span, or by this
+// kernel one level below).
+__global__ __launch_bounds__(SPAN_TB) void k_com_span_top(int J,
+                                                          const uint32_t *__restrict__ span_list,
+                                                          uint32_t span_stride,
+                                                          const SpanSlot *__restrict__ span_children,
+                                                          const uint32_t *__restrict__ super_list,
+                                                          uint32_t n_groups, Node *nodes) {
     for (int L = J; L >= 0; --L) {
-        for (uint32_t k = threadIdx.x; k < span_stride; k += SPAN_TB) {
-            const size_t slot = (size_t)L * span_stride + k;
-            const uint32_t ni = span_list[slot];
-            if (ni == NO_SPAN) continue;
+        for (uint32_t gi = threadIdx.x; gi < n_groups; gi += SPAN_TB) {
+            const uint32_t ko = super_list[(size_t)L * n_groups + gi];
+            if (ko == NO_SPAN) continue;
+            const size_t slot = (size_t)L * span_stride + ko;
+            const uint32_t ni = span_list[slot] & ~SPAN_SUPER;
             const SpanSlot q = span_children[slot];
             double mSum = 0.0, cx = 0.0, cy = 0.0;
             for (int c = 0; c < 4; ++c) {
                 if (q.ch[c] != 0xFFFFFFFFu && (q.ch[c] & SPAN_REF)) {
-                    const Node cn =
-                        nodes[span_list[(size_t)(L + 1) * span_stride + (q.ch[c] & ~SPAN_REF)]];
+                    const uint32_t ci =
+                        span_list[(size_t)(L + 1) * span_stride + (q.ch[c] & ~SPAN_REF)] & ~SPAN_SUPER;
+                    const Node cn = nodes[ci];
                     if (cn.mass > 0.0) {
                         mSum += cn.mass;
                         cx += cn.comX * cn.mass;
@@ -838,16 +845,21 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     k_com_local<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), COM_TB, 0, s>>>(
         n, g, b.keys_s, b.cpl, b.base, b.nodes);
     const dim3 span_grid((b.span_stride + TB - 1) / TB, g.J + 1);
+    const uint32_t n_groups = span_groups(b.span_stride);
+    if (n_groups > 1) {
+        st = hipMemsetAsync(b.super_list, 0xFF, sizeof(uint32_t) * (size_t)(g.J + 1) * n_groups, s);
+        if (st != hipSuccess) return st;
+    }
     k_span_find<<<span_grid, TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cpl, b.base, b.cell_start,
-                                         b.span_list, b.span_stride, b.nodes);
+                                         b.span_list, b.span_stride, b.super_list, n_groups,
+                                         b.nodes);
     k_span_children<<<span_grid, TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.nodes,
                                              b.span_children);
-    if (b.span_stride <= (uint32_t)SPAN_LDS)
-        k_com_span<<<1, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
-                                         b.nodes);
-    else
-        k_com_span_global<<<1, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
-                                                b.nodes);
+    k_com_span<<<n_groups, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
+                                            b.nodes);
+    if (n_groups > 1)
+        k_com_span_top<<<1, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
+                                             b.super_list, n_groups, b.nodes);
     return hipGetLastError();
 }
 

@@ -60,7 +60,8 @@ int bh_create(const bh_params *p, int device, bh_engine **out);
 /* Multi-GPU member: one process per GPU; `unique_id` is the 128-byte RCCL id produced by
  * bh_comm_unique_id() on rank 0 and broadcast by the caller (e.g. torch.distributed).
  * Every rank holds the full replicated state; force evaluation is sharded over ranks by
- * Morton-ordered body ranges and the accelerations are all-gathered over xGMI. */
+ * Morton-ordered body ranges and the accelerations are all-gathered over xGMI.  world == 1
+ * with a non-NULL id runs the same RCCL path on one rank (used to test it on one GPU). */
 int bh_create_dist(const bh_params *p, int device, int rank, int world, const void *unique_id,
                    bh_engine **out);
 int bh_comm_unique_id(void *out128);

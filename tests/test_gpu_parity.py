@@ -334,3 +334,21 @@ def test_theta0_direct_c5_sampled():
     ax, ay = eng.compute_accelerations()
     rax, ray = ref.accelerations()
     assert bits_equal(ax, rax) and bits_equal(ay, ray)
+
+
+def test_rccl_path_single_rank():
+    """The multi-GPU evaluation path (shard range, in-place ncclAllGather of (ax, ay) over an
+    RCCL communicator) on one rank: bit-identical to the oracle, tree walk and theta = 0."""
+    uid = bh_amd.comm_unique_id()
+    arrs = scenes.config_scene("c1_code")
+    for theta in (0.5, 0.0):
+        eng = bh_amd.Engine(bh_amd.default_params(theta=theta), device=0, rank=0, world=1,
+                            unique_id=uid)
+        eng.reset_bodies(*arrs)
+        ref = oracle.Oracle(*arrs, theta=theta)
+        eng.step(3)
+        ref.step(3)
+        _assert_state_equal(eng, ref)
+        eng.close()
+        ref.close()
+        uid = bh_amd.comm_unique_id()
