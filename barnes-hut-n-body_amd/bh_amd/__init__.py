@@ -37,6 +37,8 @@ EXPORTED_SYMBOLS = (
     "bh_last_timings", "bh_last_tree_nodes", "bh_traverse_kernel_ms", "bh_set_profiling",
     "bh_synchronize", "bh_shard_range", "bh_traversal_stats", "bh_last_removed",
     "bh_selftest_fast_math", "bh_scene_galaxy_disk", "bh_scene_kepler_disk", "bh_scene_uniform",
+    "bh_nbody3d_create", "bh_nbody3d_destroy", "bh_nbody3d_last_error", "bh_nbody3d_set",
+    "bh_nbody3d_step", "bh_nbody3d_accelerations", "bh_nbody3d_get", "bh_nbody3d_last_ms",
 )
 
 
@@ -105,6 +107,19 @@ def load_library(path: str | None = None):
     lib.bh_last_removed.argtypes = [_VP, _I64P, ctypes.c_int64, _I64P]
     lib.bh_shard_range.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, _I64P, _I64P]
     lib.bh_selftest_fast_math.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, _I64P]
+    _F = ctypes.POINTER(ctypes.c_float)
+    lib.bh_nbody3d_create.argtypes = [ctypes.c_int, ctypes.POINTER(_VP)]
+    lib.bh_nbody3d_destroy.argtypes = [_VP]
+    lib.bh_nbody3d_destroy.restype = None
+    lib.bh_nbody3d_last_error.argtypes = [_VP]
+    lib.bh_nbody3d_last_error.restype = ctypes.c_char_p
+    lib.bh_nbody3d_set.argtypes = [_VP, ctypes.c_int64] + [_F] * 7
+    lib.bh_nbody3d_step.argtypes = [_VP, ctypes.c_int32, ctypes.c_float, ctypes.c_float,
+                                    ctypes.c_float]
+    lib.bh_nbody3d_accelerations.argtypes = [_VP, ctypes.c_float, ctypes.c_float, _F, _F, _F]
+    lib.bh_nbody3d_get.argtypes = [_VP] + [_F] * 7 + [ctypes.c_int64, _I64P]
+    lib.bh_nbody3d_last_ms.argtypes = [_VP]
+    lib.bh_nbody3d_last_ms.restype = ctypes.c_double
     lib.bh_scene_galaxy_disk.argtypes = (
         [ctypes.c_int32] + [ctypes.c_double] * 6 + [ctypes.c_int32, ctypes.c_int64]
         + [ctypes.c_double] * 9 + [_D] * 5)
@@ -139,6 +154,66 @@ def shard_range(n: int, rank: int, world: int):
     if rc != BH_OK:
         raise BhError(rc, "bh_shard_range: invalid arguments")
     return lo.value, hi.value
+
+
+class NBody3D:
+    """fp32 3-D all-pairs engine with the physics of the reference's OpenGL compute shader
+    (gpu/GPU.kt:101-152: GpuNBody.simulate); see include/bh_engine.h bh_nbody3d_*."""
+
+    def __init__(self, device: int = 0):
+        self._lib = load_library()
+        self._h = _VP()
+        rc = self._lib.bh_nbody3d_create(int(device), ctypes.byref(self._h))
+        if rc != BH_OK:
+            raise BhError(rc, "bh_nbody3d_create failed")
+
+    def _check(self, rc, what):
+        if rc != BH_OK:
+            raise BhError(rc, f"{what}: {self._lib.bh_nbody3d_last_error(self._h).decode()}")
+
+    @staticmethod
+    def _f(a):
+        return np.ascontiguousarray(a, dtype=np.float32)
+
+    def set(self, x, y, z, vx, vy, vz, m):
+        arrs = [self._f(a) for a in (x, y, z, vx, vy, vz, m)]
+        self._keep = arrs
+        ptrs = [a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) for a in arrs]
+        self._check(self._lib.bh_nbody3d_set(self._h, len(arrs[0]), *ptrs), "bh_nbody3d_set")
+        self.n = len(arrs[0])
+
+    def step(self, k: int = 1, dt: float = 0.005, G: float = 80.0, softening: float = 1.0):
+        self._check(self._lib.bh_nbody3d_step(self._h, int(k), dt, G, softening),
+                    "bh_nbody3d_step")
+
+    def accelerations(self, G: float = 80.0, softening: float = 1.0):
+        out = [np.empty(self.n, dtype=np.float32) for _ in range(3)]
+        ptrs = [a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) for a in out]
+        self._check(self._lib.bh_nbody3d_accelerations(self._h, G, softening, *ptrs),
+                    "bh_nbody3d_accelerations")
+        return tuple(out)
+
+    def get(self):
+        out = [np.empty(self.n, dtype=np.float32) for _ in range(7)]
+        ptrs = [a.ctypes.data_as(ctypes.POINTER(ctypes.c_float)) for a in out]
+        got = ctypes.c_int64(0)
+        self._check(self._lib.bh_nbody3d_get(self._h, *ptrs, self.n, ctypes.byref(got)),
+                    "bh_nbody3d_get")
+        return tuple(out)
+
+    def last_ms(self) -> float:
+        return float(self._lib.bh_nbody3d_last_ms(self._h))
+
+    def close(self):
+        if getattr(self, "_h", None) and self._h.value:
+            self._lib.bh_nbody3d_destroy(self._h)
+            self._h = _VP()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def selftest_fast_math(n: int, seed: int = 1, device: int = 0) -> int:

@@ -156,6 +156,28 @@ int bh_scene_kepler_disk(int32_t n_total, int32_t clockwise, double radial_jitte
 int bh_scene_uniform(int32_t n, double m, int64_t seed, int32_t width_px, int32_t height_px,
                      double *ox, double *oy, double *ovx, double *ovy, double *om);
 
+/* ---- fp32 3-D all-pairs engine: the physics of the reference's OpenGL compute shader
+ * (gpu/GPU.kt:101-152 = "GPU").  a_i = sum_{j!=i} (G m_j) d / (d.d +
+ * softening^2)^{3/2} with the hardware reciprocal square root (GLSL inversesqrt, GPU:140),
+ * then v += a dt, x += v dt (GPU:145-146) — double-buffered instead of the reference's
+ * in-place race.  fp32 throughout; parity is a tolerance, not bit-identity. */
+typedef struct bh_nbody3d bh_nbody3d;
+int bh_nbody3d_create(int device, bh_nbody3d **out);
+void bh_nbody3d_destroy(bh_nbody3d *h);
+const char *bh_nbody3d_last_error(const bh_nbody3d *h);
+/* upload (replaces GpuNBody's SSBO upload of Body{x,y,z,vx,vy,vz,m}) */
+int bh_nbody3d_set(bh_nbody3d *h, int64_t n, const float *x, const float *y, const float *z,
+                   const float *vx, const float *vy, const float *vz, const float *m);
+/* GpuNBody.simulate(dt, g, softening) x k (GPU:411-422) */
+int bh_nbody3d_step(bh_nbody3d *h, int32_t k, float dt, float G, float softening);
+/* one evaluation of the accelerations of the current state (no integration) */
+int bh_nbody3d_accelerations(bh_nbody3d *h, float G, float softening, float *ax, float *ay,
+                             float *az);
+int bh_nbody3d_get(const bh_nbody3d *h, float *x, float *y, float *z, float *vx, float *vy,
+                   float *vz, float *m, int64_t cap, int64_t *n_out);
+/* device time (ms) of the last bh_nbody3d_step / bh_nbody3d_accelerations call */
+double bh_nbody3d_last_ms(const bh_nbody3d *h);
+
 #ifdef __cplusplus
 }
 #endif
