@@ -797,6 +797,72 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span_top(int J,
     }
 }
 
+// Hilbert index (J levels) of the cell with Morton key `key`: de-interleave, then the
+// classic quadrant walk with rotations.  Out-of-root / tombstone keys sort last.
+__device__ __forceinline__ uint64_t hilbert_of_morton(uint64_t key, int J) {
+    if (key >> (2 * J)) return ~0ull;
+    uint32_t x = 0, y = 0;
+    for (int b = 0; b < J; ++b) {
+        x |= (uint32_t)((key >> (2 * b)) & 1) << b;
+        y |= (uint32_t)((key >> (2 * b + 1)) & 1) << b;
+    }
+    uint64_t d = 0;
+    for (uint32_t s = 1u << (J - 1); s > 0; s >>= 1) {
+        const uint32_t rx = (x & s) ? 1u : 0u, ry = (y & s) ? 1u : 0u;
+        d += (uint64_t)s * s * ((3u * rx) ^ ry);
+        if (ry == 0) {
+            if (rx == 1) {
+                x = s - 1 - x;
+                y = s - 1 - y;
+            }
+            const uint32_t t = x;
+            x = y;
+            y = t;
+        }
+    }
+    return d;
+}
+
+// lane_perm: each LANE_WINDOW-slot window of the Morton order re-sorted by Hilbert index
+// (bitonic sort of (key, slot) in LDS, one workgroup per window).
+constexpr int LANE_TB = 1024;
+__global__ __launch_bounds__(LANE_TB) void k_lane_order(int64_t n, int J,
+                                                        const uint64_t *__restrict__ keys_s,
+                                                        uint32_t *__restrict__ lane_perm) {
+    __shared__ uint64_t sk[LANE_WINDOW];
+    __shared__ uint32_t sv[LANE_WINDOW];
+    const int64_t w0 = (int64_t)blockIdx.x * LANE_WINDOW;
+    for (int i = threadIdx.x; i < LANE_WINDOW; i += LANE_TB) {
+        const int64_t a = w0 + i;
+        sk[i] = a < n ? hilbert_of_morton(keys_s[a], J) : ~0ull;
+        sv[i] = (uint32_t)a;
+    }
+    __syncthreads();
+    for (int k = 2; k <= LANE_WINDOW; k <<= 1) {
+        for (int j = k >> 1; j > 0; j >>= 1) {
+            for (int i = threadIdx.x; i < LANE_WINDOW; i += LANE_TB) {
+                const int l = i ^ j;
+                if (l > i) {
+                    const bool up = (i & k) == 0;
+                    // ties (equal keys) ordered by slot, so the permutation is deterministic
+                    const bool gt = sk[i] > sk[l] || (sk[i] == sk[l] && sv[i] > sv[l]);
+                    if (gt == up) {
+                        const uint64_t tk = sk[i];
+                        sk[i] = sk[l];
+                        sk[l] = tk;
+                        const uint32_t tv = sv[i];
+                        sv[i] = sv[l];
+                        sv[l] = tv;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = threadIdx.x; i < LANE_WINDOW; i += LANE_TB)
+        if (w0 + i < n) lane_perm[w0 + i] = sv[i];
+}
+
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + TB - 1) / TB); }
 
 }  // namespace
@@ -842,6 +908,9 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
                                       b.dst.y, b.dst.m, b.nodes);
     k_jitter<<<grid_for(n), TB, 0, s>>>(n, g, b.keys_s, b.cpl, b.base, b.dst.x, b.dst.y, b.dst.m,
                                         b.dst.cidx, b.idx, b.nodes, b.scalars + 1);
+    if (b.lane_perm)
+        k_lane_order<<<(unsigned)((n + LANE_WINDOW - 1) / LANE_WINDOW), LANE_TB, 0, s>>>(
+            n, g.J, b.keys_s, b.lane_perm);
     k_com_local<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), COM_TB, 0, s>>>(
         n, g, b.keys_s, b.cpl, b.base, b.nodes);
     const dim3 span_grid((b.span_stride + TB - 1) / TB, g.J + 1);

@@ -473,6 +473,49 @@ void oracle_tree_stats(oracle_engine *e, int64_t *n_nodes, int64_t *n_nonempty) 
     *n_nonempty = ne;
 }
 
+/* Analysis helper (not part of the reference): the GPU traversal walks one pre-order cursor per
+ * wavefront over the UNION of its lanes' visit sets.  For groups of `group` consecutive bodies
+ * of `order`, count that union (nodes reached by at least one lane: the GPU's wave iterations)
+ * and the lanes' own visits; their ratio is the lane efficiency of that body ordering. */
+static int64_t union_walk(const Tree *t, const ForceCtx *c, int64_t node, const int64_t *bis,
+                          uint64_t mask, int64_t *lane_visits) {
+    const Node *nd = &t->nodes[node];
+    if (nd->mass == 0.0 || !mask) return 0; /* BHA:216 */
+    *lane_visits += __builtin_popcountll(mask);
+    if (nd->child < 0) return 1;
+    uint64_t open = 0;
+    for (uint64_t m = mask; m; m &= m - 1) {
+        const int l = __builtin_ctzll(m);
+        const Body *b = &t->bodies[bis[l]];
+        const double dx = nd->comX - b->x, dy = nd->comY - b->y;
+        const double dist2 = dx * dx + dy * dy + c->soft2;
+        const double hh = nd->q.h * 2.0, s2 = hh * hh;
+        if (!(s2 < c->theta2 * dist2)) open |= 1ull << l;
+    }
+    int64_t it = 1;
+    if (open)
+        for (int k = 0; k < 4; ++k) it += union_walk(t, c, nd->child + k, bis, open, lane_visits);
+    return it;
+}
+
+int64_t oracle_group_union(oracle_engine *e, const int64_t *order, int64_t count, int group,
+                           int64_t *lane_visits) {
+    if (group < 1 || group > 64) return -1;
+    if (!e->tree_valid) {
+        build_tree(e);
+        e->tree_valid = 1;
+    }
+    ForceCtx c = {e->p.G, e->p.soft2, e->p.theta * e->p.theta};
+    int64_t iters = 0, lv = 0;
+    for (int64_t g0 = 0; g0 < count; g0 += group) {
+        const int nb = (int)((count - g0) < group ? (count - g0) : group);
+        const uint64_t mask = nb == 64 ? ~0ull : ((1ull << nb) - 1);
+        iters += union_walk(&e->tree, &c, 0, order + g0, mask, &lv);
+    }
+    if (lane_visits) *lane_visits = lv;
+    return iters;
+}
+
 void oracle_destroy(oracle_engine *e) {
     if (!e) return;
     free(e->bodies);

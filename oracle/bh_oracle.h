@@ -35,6 +35,9 @@ int oracle_accel(oracle_engine *e, int64_t count, const int64_t *subset, double 
                  int64_t *visits);
 int64_t oracle_quads(oracle_engine *e, double *cx, double *cy, double *h, int64_t cap);
 void oracle_tree_stats(oracle_engine *e, int64_t *n_nodes, int64_t *n_nonempty);
+/* analysis: wave-union iterations of groups of `group` consecutive bodies of `order` */
+int64_t oracle_group_union(oracle_engine *e, const int64_t *order, int64_t count, int group,
+                           int64_t *lane_visits);
 void oracle_destroy(oracle_engine *e);
 
 #ifdef __cplusplus
