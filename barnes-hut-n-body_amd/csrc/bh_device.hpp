@@ -49,17 +49,6 @@ __host__ __device__ inline uint32_t span_groups(uint32_t span_stride) {
     return (span_stride + 1023) / 1024;
 }
 
-// Wavefront body order for the traversal: the Morton (slot) order re-sorted by Hilbert index
-// inside aligned windows of LANE_WINDOW slots (a permutation local to each window).  Lanes of
-// a wavefront then hold bodies along a continuous curve instead of across Z-order jumps: the
-// union of their interaction lists shrinks (C3: 5.7 % fewer wave iterations, measured with
-// oracle_group_union).  Shards are aligned to windows so a rank's lanes map to its own slots.
-constexpr int LANE_WINDOW = 4096;
-__host__ __device__ inline int64_t shard_chunk(int64_t n, int world) {
-    const int64_t c = (n + world - 1) / world;
-    return (c + LANE_WINDOW - 1) / LANE_WINDOW * LANE_WINDOW;
-}
-
 // Cell-start table: first sorted body of every depth-D0 cell, so the end of any node at
 // depth <= D0 is one load, and deeper searches stay inside one depth-D0 cell.
 constexpr int CELL_TABLE_MAX_DEPTH = 8;
@@ -115,7 +104,6 @@ struct TreeBuffers {
     uint32_t span_stride;
     struct SpanSlot *span_children;  // [(J + 1) * span_stride]
     uint32_t *super_list;  // [(J + 1) * span_groups]: group-crossing span node per (level, group)
-    uint32_t *lane_perm;   // [n]: slot of each traversal lane (see LANE_WINDOW)
     void *cub_tmp;
     size_t cub_bytes;
 };
@@ -125,12 +113,10 @@ size_t tree_cub_bytes(int64_t n, int J);
 hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStream_t s);
 
 // ---- launchers (traverse.hip) ----------------------------------------------------
-// Accelerations F/m of the bodies of lanes [lo, hi) (lane_perm: lane -> slot p, window-local),
-// written interleaved to a2[2p], a2[2p+1].
+// Accelerations F/m of slots [lo, hi), written interleaved to a2[2p], a2[2p+1].
 void traverse(const Node *nodes, const uint32_t *d_T, const double *x, const double *y,
-              const double *m, const uint32_t *lane_perm, int64_t lo, int64_t hi,
-              const Geometry &g, const ForceParams &fp, double *a2, uint32_t *visits,
-              uint32_t *wave_iters, hipStream_t s);
+              const double *m, int64_t lo, int64_t hi, const Geometry &g, const ForceParams &fp,
+              double *a2, uint32_t *visits, uint32_t *wave_iters, hipStream_t s);
 
 // Exactness check of the traversal's in-range sqrt/reciprocal sequences against the IEEE
 // operations on n generated operands; adds the mismatch count to *d_bad.

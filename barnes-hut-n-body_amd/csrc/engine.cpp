@@ -51,7 +51,7 @@ struct bh_engine {
     double *ax = nullptr, *ay = nullptr;  // caller-order copy-out staging
 
     uint64_t *keys = nullptr, *keys_s = nullptr;
-    uint32_t *idx = nullptr, *perm = nullptr, *lane_perm = nullptr;
+    uint32_t *idx = nullptr, *perm = nullptr;
     int8_t *cpl = nullptr;
     uint32_t *cnt = nullptr, *base = nullptr;
     uint32_t *cell_start = nullptr;
@@ -199,9 +199,8 @@ int ensure_capacity(bh_engine *e, int64_t n) {
     if (n > e->cap || !e->st.x) {
         TRY(alloc_state(e, e->st, cap));
         TRY(alloc_state(e, e->alt, cap));
-        const int64_t chunk = shard_chunk(cap, e->world);
+        const int64_t chunk = (cap + e->world - 1) / e->world;
         TRY(dev_alloc(e, e->a2, 2 * chunk * e->world));
-        TRY(dev_alloc(e, e->lane_perm, cap));
         TRY(dev_alloc(e, e->ax, cap));
         TRY(dev_alloc(e, e->ay, cap));
         TRY(dev_alloc(e, e->keys, cap));
@@ -258,7 +257,6 @@ TreeBuffers tree_buffers(bh_engine *e) {
     b.span_stride = span_stride_for(e->cap);
     b.span_children = e->span_children;
     b.super_list = e->super_list;
-    b.lane_perm = e->lane_perm;
     b.cub_tmp = e->cub_tmp;
     b.cub_bytes = e->cub_bytes;
     return b;
@@ -353,7 +351,7 @@ int evaluate(bh_engine *e, uint32_t *visits) {
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
         if (e->comm) {
-            const int64_t chunk = shard_chunk(n, e->world);
+            const int64_t chunk = (n + e->world - 1) / e->world;
             NCCLCHK(e, ncclAllGather(e->a2 + 2 * e->rank * chunk, e->a2, (size_t)(2 * chunk),
                                      ncclDouble, e->comm, e->stream));
             TRY(mark(e, 4));
@@ -361,17 +359,15 @@ int evaluate(bh_engine *e, uint32_t *visits) {
         return BH_OK;
     }
     if (!e->comm || visits) {
-        traverse(e->nodes, d_T, e->st.x, e->st.y, e->st.m, e->lane_perm, 0, n, e->geo, fp, e->a2,
-                 visits,
+        traverse(e->nodes, d_T, e->st.x, e->st.y, e->st.m, 0, n, e->geo, fp, e->a2, visits,
                  e->wave_iters, e->stream);
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
     } else {
-        const int64_t chunk = shard_chunk(n, e->world);
+        const int64_t chunk = (n + e->world - 1) / e->world;
         int64_t lo = 0, hi = 0;
         bh_shard_range(n, e->rank, e->world, &lo, &hi);
-        traverse(e->nodes, d_T, e->st.x, e->st.y, e->st.m, e->lane_perm, lo, hi, e->geo, fp, e->a2,
-                 nullptr,
+        traverse(e->nodes, d_T, e->st.x, e->st.y, e->st.m, lo, hi, e->geo, fp, e->a2, nullptr,
                  nullptr, e->stream);
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
@@ -664,7 +660,7 @@ void bh_destroy(bh_engine *e) {
     if (e->comm) (void)ncclCommDestroy(e->comm);
     free_state(e->st);
     free_state(e->alt);
-    void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->idx, e->perm, e->lane_perm, e->cpl, e->cnt,
+    void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->idx, e->perm, e->cpl, e->cnt,
                     e->base, e->cell_start, e->nodes, e->span_list, e->super_list,
                     e->span_children, e->scalars, e->visits32, e->wave_iters, e->heavy, e->keep,
                     e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->cub_tmp,
@@ -888,7 +884,7 @@ int bh_set_profiling(bh_engine *e, int enabled) {
 
 int bh_shard_range(int64_t n, int rank, int world, int64_t *lo, int64_t *hi) {
     if (n < 0 || world < 1 || rank < 0 || rank >= world || !lo || !hi) return BH_E_INVALID;
-    const int64_t chunk = shard_chunk(n, world);  // window-aligned (bh_device.hpp LANE_WINDOW)
+    const int64_t chunk = (n + world - 1) / world;
     *lo = std::min<int64_t>(n, (int64_t)rank * chunk);
     *hi = std::min<int64_t>(n, *lo + chunk);
     return BH_OK;

@@ -87,15 +87,13 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
                                                  const uint32_t *__restrict__ d_T,
                                                  const double *__restrict__ x,
                                                  const double *__restrict__ y,
-                                                 const double *__restrict__ m,
-                                                 const uint32_t *__restrict__ lane_perm,
-                                                 int64_t lo, int64_t hi, ForceParams fp, Geometry g,
+                                                 const double *__restrict__ m, int64_t lo,
+                                                 int64_t hi, ForceParams fp, Geometry g,
                                                  double *__restrict__ a2,
                                                  uint32_t *__restrict__ visits,
                                                  uint32_t *__restrict__ wave_iters) {
-    const int64_t lane = lo + (int64_t)blockIdx.x * TB + threadIdx.x;
-    const bool valid = lane < hi;
-    const int64_t p = valid ? (int64_t)lane_perm[lane] : lane;  // body slot of this lane
+    const int64_t p = lo + (int64_t)blockIdx.x * TB + threadIdx.x;
+    const bool valid = p < hi;
     const double bx = valid ? x[p] : 0.0;
     const double by = valid ? y[p] : 0.0;
     const double bm = valid ? m[p] : 1.0;
@@ -115,7 +113,7 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     else
         walk<false, COUNT>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx, fy, nvis,
                            niters);
-    if (COUNT && (threadIdx.x & 63) == 0) wave_iters[(lane - lo) >> 6] = niters;
+    if (COUNT && (threadIdx.x & 63) == 0) wave_iters[(p - lo) >> 6] = niters;
     if (!valid) return;
     // BHA:390-391, interleaved (ax, ay): coalesced 16-byte stores in Morton order
     typedef double double2_t __attribute__((ext_vector_type(2)));
@@ -176,16 +174,15 @@ hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_ba
 }
 
 void traverse(const Node *nodes, const uint32_t *d_T, const double *x, const double *y,
-              const double *m, const uint32_t *lane_perm, int64_t lo, int64_t hi,
-              const Geometry &g, const ForceParams &fp, double *a2, uint32_t *visits,
-              uint32_t *wave_iters, hipStream_t s) {
+              const double *m, int64_t lo, int64_t hi, const Geometry &g, const ForceParams &fp,
+              double *a2, uint32_t *visits, uint32_t *wave_iters, hipStream_t s) {
     if (hi <= lo) return;
     unsigned grid = (unsigned)((hi - lo + TB - 1) / TB);
     if (visits)
-        k_traverse<true><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lane_perm, lo, hi, fp, g, a2, visits,
+        k_traverse<true><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2, visits,
                                              wave_iters);
     else
-        k_traverse<false><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lane_perm, lo, hi, fp, g, a2, visits,
+        k_traverse<false><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2, visits,
                                               wave_iters);
 }
 

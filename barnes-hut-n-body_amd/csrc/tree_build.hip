@@ -132,23 +132,6 @@ __global__ __launch_bounds__(TB) void k_cells(int64_t n, int J, int D0,
     cell_start[bin] = (uint32_t)lo;
 }
 
-// First b >= from with c(b) < L, looking at most at the 3 aligned 8-byte words of c that
-// start at `from`'s word; -1 if not found there.  c(n-1) == -1 bounds every search, and the
-// c array is allocated with 32 bytes of slack so whole-word loads stay in bounds.
-__device__ __forceinline__ int64_t scan_cpl(const int8_t *__restrict__ cpl, int64_t from, int L) {
-    const int64_t w0 = from & ~(int64_t)7;
-    for (int w = 0; w < 3; ++w) {
-        const uint64_t word = *reinterpret_cast<const uint64_t *>(cpl + w0 + 8 * w);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            const int64_t idx = w0 + 8 * w + k;
-            const int c = (int)(int8_t)(word >> (8 * k));
-            if (idx >= from && c < L) return idx;
-        }
-    }
-    return -1;
-}
-
 // Largest e in [from, limit] with (keys_s[e] >> shift) == pref (keys_s[from] matches).
 __device__ __forceinline__ int64_t run_end(const uint64_t *__restrict__ keys_s, int64_t limit,
                                            int64_t from, int shift, uint64_t pref) {
@@ -165,6 +148,28 @@ __device__ __forceinline__ int64_t run_end(const uint64_t *__restrict__ keys_s, 
     return lo;
 }
 
+// c(j) + 1 of a window of EMIT_WIN sorted positions starting at the block's first body, in
+// LDS: a node's end is found by a word-wise SWAR scan of the window (most nodes end inside
+// it); only nodes that outrun the window gallop over the keys in global memory.
+constexpr int EMIT_WIN = 2048;
+
+// first j in [from, c0 + EMIT_WIN) with c(j) < L, or -1; w[i] = c(c0 + i) + 1 in [0, 42]
+__device__ __forceinline__ int64_t lds_scan(const uint64_t *w, int64_t c0, int64_t from, int L) {
+    const uint64_t ones = 0x0101010101010101ull, highs = 0x8080808080808080ull;
+    const uint64_t sub = ones * (uint64_t)(L + 1);
+    int64_t o = from - c0;
+    int wi = (int)(o >> 3);
+    // bytes before `from` are raised to 0x7F (>= L + 1): they neither match nor borrow
+    uint64_t pad = ~(~0ull << (8 * (o & 7))) & 0x7F7F7F7F7F7F7F7Full;
+    for (; wi < EMIT_WIN / 8; ++wi) {
+        const uint64_t x = w[wi] | pad;
+        const uint64_t t = (x - sub) & ~x & highs;  // lowest flag = first byte with c + 1 < L + 1
+        if (t) return c0 + 8 * (int64_t)wi + (__builtin_ctzll(t) >> 3);
+        pad = 0;
+    }
+    return -1;
+}
+
 __global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, int D0,
                                              const uint64_t *__restrict__ keys_s,
                                              const int8_t *__restrict__ cpl,
@@ -174,7 +179,17 @@ __global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, int D0,
                                              const double *__restrict__ y,
                                              const double *__restrict__ m,
                                              Node *__restrict__ nodes) {
-    int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
+    __shared__ uint64_t win[EMIT_WIN / 8];
+    const int64_t c0 = (int64_t)blockIdx.x * TB;
+    {
+        uint8_t *wb = reinterpret_cast<uint8_t *>(win);
+        for (int i = threadIdx.x; i < EMIT_WIN; i += TB) {
+            const int64_t j = c0 + i;
+            wb[i] = (uint8_t)(j < n ? (int)cpl[j] + 1 : 0);  // past the end: c = -1
+        }
+    }
+    __syncthreads();
+    const int64_t a = c0 + threadIdx.x;
     if (a >= n) return;
     const uint64_t k = keys_s[a];
     if (k == sentinel_key(J)) return;
@@ -188,12 +203,12 @@ __global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, int D0,
         if (L <= D0) {  // one load: the next depth-L cell starts at a depth-D0 cell start
             const uint64_t nextcell = ((k >> (2 * (J - L))) + 1) << (2 * (D0 - L));
             b = (int64_t)cell_start[nextcell] - 1;
-        } else {  // inside a's depth-D0 cell: short scan of c, then bounded galloping
-            b = scan_cpl(cpl, end, L);
-            if (b < 0) {
+        } else {  // inside a's depth-D0 cell: scan the LDS window, then bounded galloping
+            b = lds_scan(win, c0, end, L);
+            if (b < 0) {  // c >= L up to the window's end: the cell continues past it
                 const int64_t limit = (int64_t)cell_start[(k >> shift0) + 1] - 1;
                 const int shift = 2 * (J - L);
-                b = run_end(keys_s, limit, end, shift, k >> shift);
+                b = run_end(keys_s, limit, c0 + EMIT_WIN - 1, shift, k >> shift);
             }
         }
         end = b;
@@ -797,72 +812,6 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span_top(int J,
     }
 }
 
-// Hilbert index (J levels) of the cell with Morton key `key`: de-interleave, then the
-// classic quadrant walk with rotations.  Out-of-root / tombstone keys sort last.
-__device__ __forceinline__ uint64_t hilbert_of_morton(uint64_t key, int J) {
-    if (key >> (2 * J)) return ~0ull;
-    uint32_t x = 0, y = 0;
-    for (int b = 0; b < J; ++b) {
-        x |= (uint32_t)((key >> (2 * b)) & 1) << b;
-        y |= (uint32_t)((key >> (2 * b + 1)) & 1) << b;
-    }
-    uint64_t d = 0;
-    for (uint32_t s = 1u << (J - 1); s > 0; s >>= 1) {
-        const uint32_t rx = (x & s) ? 1u : 0u, ry = (y & s) ? 1u : 0u;
-        d += (uint64_t)s * s * ((3u * rx) ^ ry);
-        if (ry == 0) {
-            if (rx == 1) {
-                x = s - 1 - x;
-                y = s - 1 - y;
-            }
-            const uint32_t t = x;
-            x = y;
-            y = t;
-        }
-    }
-    return d;
-}
-
-// lane_perm: each LANE_WINDOW-slot window of the Morton order re-sorted by Hilbert index
-// (bitonic sort of (key, slot) in LDS, one workgroup per window).
-constexpr int LANE_TB = 1024;
-__global__ __launch_bounds__(LANE_TB) void k_lane_order(int64_t n, int J,
-                                                        const uint64_t *__restrict__ keys_s,
-                                                        uint32_t *__restrict__ lane_perm) {
-    __shared__ uint64_t sk[LANE_WINDOW];
-    __shared__ uint32_t sv[LANE_WINDOW];
-    const int64_t w0 = (int64_t)blockIdx.x * LANE_WINDOW;
-    for (int i = threadIdx.x; i < LANE_WINDOW; i += LANE_TB) {
-        const int64_t a = w0 + i;
-        sk[i] = a < n ? hilbert_of_morton(keys_s[a], J) : ~0ull;
-        sv[i] = (uint32_t)a;
-    }
-    __syncthreads();
-    for (int k = 2; k <= LANE_WINDOW; k <<= 1) {
-        for (int j = k >> 1; j > 0; j >>= 1) {
-            for (int i = threadIdx.x; i < LANE_WINDOW; i += LANE_TB) {
-                const int l = i ^ j;
-                if (l > i) {
-                    const bool up = (i & k) == 0;
-                    // ties (equal keys) ordered by slot, so the permutation is deterministic
-                    const bool gt = sk[i] > sk[l] || (sk[i] == sk[l] && sv[i] > sv[l]);
-                    if (gt == up) {
-                        const uint64_t tk = sk[i];
-                        sk[i] = sk[l];
-                        sk[l] = tk;
-                        const uint32_t tv = sv[i];
-                        sv[i] = sv[l];
-                        sv[l] = tv;
-                    }
-                }
-            }
-            __syncthreads();
-        }
-    }
-    for (int i = threadIdx.x; i < LANE_WINDOW; i += LANE_TB)
-        if (w0 + i < n) lane_perm[w0 + i] = sv[i];
-}
-
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + TB - 1) / TB); }
 
 }  // namespace
@@ -908,9 +857,6 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
                                       b.dst.y, b.dst.m, b.nodes);
     k_jitter<<<grid_for(n), TB, 0, s>>>(n, g, b.keys_s, b.cpl, b.base, b.dst.x, b.dst.y, b.dst.m,
                                         b.dst.cidx, b.idx, b.nodes, b.scalars + 1);
-    if (b.lane_perm)
-        k_lane_order<<<(unsigned)((n + LANE_WINDOW - 1) / LANE_WINDOW), LANE_TB, 0, s>>>(
-            n, g.J, b.keys_s, b.lane_perm);
     k_com_local<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), COM_TB, 0, s>>>(
         n, g, b.keys_s, b.cpl, b.base, b.nodes);
     const dim3 span_grid((b.span_stride + TB - 1) / TB, g.J + 1);

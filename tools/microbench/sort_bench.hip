@@ -5,6 +5,7 @@
 
 #include <cstdio>
 #include <cstdlib>
+#include <algorithm>
 #include <vector>
 
 #define CK(x)                                                                        \
@@ -16,8 +17,8 @@
         }                                                                            \
     } while (0)
 
-template <class Cfg>
-float run(const char *name, size_t n, unsigned bits, const uint64_t *k_in, uint64_t *k_out,
+template <class Cfg, class K>
+float run(const char *name, size_t n, unsigned bits, const K *k_in, K *k_out,
           const uint32_t *v_in, uint32_t *v_out, int reps) {
     size_t bytes = 0;
     CK(rocprim::radix_sort_pairs<Cfg>(nullptr, bytes, k_in, k_out, v_in, v_out, n, 0u, bits));
@@ -82,6 +83,30 @@ int main() {
         run<Onesweep<7>>("onesweep 7b", n, bits, k_in, k_out, v_in, v_out, reps);
         run<OnesweepBig<8>>("onesweep 8b 256x16", n, bits, k_in, k_out, v_in, v_out, reps);
         run<OnesweepBig<6>>("onesweep 6b 256x16", n, bits, k_in, k_out, v_in, v_out, reps);
+        // 32-bit keys (top 32 of the 43) + u32 payload; and the engine-like nearly sorted input
+        {
+            uint32_t *k32_in, *k32_out;
+            CK(hipMalloc(&k32_in, n * 4));
+            CK(hipMalloc(&k32_out, n * 4));
+            std::vector<uint32_t> h32(n);
+            for (size_t i = 0; i < n; ++i) h32[i] = (uint32_t)(hk[i] >> 11);
+            CK(hipMemcpy(k32_in, h32.data(), n * 4, hipMemcpyHostToDevice));
+            run<rocprim::default_config>("u32 keys default", n, 32, k32_in, k32_out, v_in, v_out, reps);
+            std::sort(h32.begin(), h32.end());
+            for (size_t i = 0; i + 1 < n; i += 7) std::swap(h32[i], h32[i + 1]);  // local disorder
+            CK(hipMemcpy(k32_in, h32.data(), n * 4, hipMemcpyHostToDevice));
+            run<rocprim::default_config>("u32 keys nearly sorted", n, 32, k32_in, k32_out, v_in, v_out, reps);
+            CK(hipFree(k32_in));
+            CK(hipFree(k32_out));
+        }
+        {
+            std::vector<uint64_t> hs = hk;
+            std::sort(hs.begin(), hs.end());
+            for (size_t i = 0; i + 1 < n; i += 7) std::swap(hs[i], hs[i + 1]);
+            CK(hipMemcpy(k_in, hs.data(), n * 8, hipMemcpyHostToDevice));
+            run<rocprim::default_config>("u64 nearly sorted", n, bits, k_in, k_out, v_in, v_out, reps);
+            CK(hipMemcpy(k_in, hk.data(), n * 8, hipMemcpyHostToDevice));
+        }
         // sorted-check of the last run
         std::vector<uint64_t> ok(n);
         CK(hipMemcpy(ok.data(), k_out, n * 8, hipMemcpyDeviceToHost));
