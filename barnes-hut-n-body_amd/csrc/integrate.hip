@@ -141,7 +141,9 @@ __device__ void replay_sorted(const MergePair *pairs, uint32_t count, K key, I i
 }
 
 constexpr int REPLAY_TB = 256;
-constexpr int REPLAY_LDS = 2048;
+constexpr int REPLAY_LDS = 2048;   // pairs sorted in LDS
+constexpr int REPLAY_FAST = 1024;  // pairs replayed entirely in LDS
+constexpr int REPLAY_HASH = 4096;  // >= 2 * REPLAY_FAST involved bodies, power of two
 
 __device__ __forceinline__ uint64_t pair_key(const MergePair &p) {
     return ((uint64_t)p.h_cidx << 32) | p.v_cidx;
@@ -154,6 +156,10 @@ __global__ __launch_bounds__(REPLAY_TB) void k_merge_replay(const MergePair *__r
                                                             uint32_t *sidx) {
     __shared__ uint64_t lk[REPLAY_LDS];
     __shared__ uint32_t li[REPLAY_LDS];
+    __shared__ uint32_t hkey[REPLAY_HASH], hcidx[REPLAY_HASH];
+    __shared__ double hmass[REPLAY_HASH];
+    __shared__ uint8_t hflag[REPLAY_HASH];
+    __shared__ uint16_t hh[REPLAY_FAST], hv[REPLAY_FAST];
     const MergeHeader *hdr = reinterpret_cast<const MergeHeader *>(box);
     const uint32_t count = hdr->pairs;
     if (count == 0) return;
@@ -190,11 +196,73 @@ __global__ __launch_bounds__(REPLAY_TB) void k_merge_replay(const MergePair *__r
                 __syncthreads();
             }
         }
-        if (threadIdx.x == 0) {
-            replay_sorted(
-                pairs, count, [&](uint32_t q) { return lk[q]; }, [&](uint32_t q) { return li[q]; },
-                m, cidx, dlog, nd);
+        if (count > REPLAY_FAST) {
+            if (threadIdx.x == 0) {
+                replay_sorted(
+                    pairs, count, [&](uint32_t q) { return lk[q]; },
+                    [&](uint32_t q) { return li[q]; }, m, cidx, dlog, nd);
+                scal[2] = nd;
+            }
+            return;
+        }
+        // Fast path: every involved body gets an LDS entry (open-addressing table keyed by
+        // slot, filled in parallel with its mass and caller index), so the sequential replay
+        // below touches LDS only; changed masses / tombstones are written back in parallel.
+        for (uint32_t i = threadIdx.x; i < REPLAY_HASH; i += REPLAY_TB) {
+            hkey[i] = 0xFFFFFFFFu;
+            hflag[i] = 0;
+        }
+        __syncthreads();
+        for (uint32_t q = threadIdx.x; q < 2 * count; q += REPLAY_TB) {
+            const MergePair &pr = pairs[li[q >> 1]];
+            const uint32_t slot = (q & 1) ? pr.v_slot : pr.h_slot;
+            uint32_t h = (slot * 2654435761u) & (REPLAY_HASH - 1);
+            for (;;) {
+                const uint32_t prev = atomicCAS(&hkey[h], 0xFFFFFFFFu, slot);
+                if (prev == 0xFFFFFFFFu) {  // new entry: this thread loads the body's state
+                    hmass[h] = m[slot];
+                    hcidx[h] = cidx[slot];
+                    break;
+                }
+                if (prev == slot) break;
+                h = (h + 1) & (REPLAY_HASH - 1);
+            }
+            if (q & 1) hv[q >> 1] = (uint16_t)h; else hh[q >> 1] = (uint16_t)h;
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {  // BHA:470-531 in list order, on LDS
+            for (uint32_t q = 0; q < count;) {
+                const uint32_t h = (uint32_t)(lk[q] >> 32);
+                uint32_t qe = q;
+                while (qe < count && (uint32_t)(lk[qe] >> 32) == h) ++qe;
+                const uint32_t eh = hh[q];
+                if (!(hcidx[eh] & CIDX_DEAD)) {
+                    double mi = hmass[eh];
+                    bool any = false;
+                    for (uint32_t r = qe; r > q; --r) {
+                        const uint32_t ev = hv[r - 1];
+                        const uint32_t cv = hcidx[ev];
+                        if (cv & CIDX_DEAD) continue;
+                        mi += hmass[ev];  // BHA:518
+                        dlog[nd++] = cv;
+                        hcidx[ev] = cv | CIDX_DEAD;
+                        hflag[ev] |= 2;
+                        any = true;
+                    }
+                    if (any) {
+                        hmass[eh] = mi;
+                        hflag[eh] |= 1;
+                    }
+                }
+                q = qe;
+            }
             scal[2] = nd;
+        }
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < REPLAY_HASH; i += REPLAY_TB) {
+            const uint32_t f = hflag[i];
+            if (f & 1) m[hkey[i]] = hmass[i];
+            if (f & 2) cidx[hkey[i]] = hcidx[i];
         }
         return;
     }
