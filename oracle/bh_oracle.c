@@ -477,12 +477,23 @@ void oracle_tree_stats(oracle_engine *e, int64_t *n_nodes, int64_t *n_nonempty) 
  * wavefront over the UNION of its lanes' visit sets.  For groups of `group` consecutive bodies
  * of `order`, count that union (nodes reached by at least one lane: the GPU's wave iterations)
  * and the lanes' own visits; their ratio is the lane efficiency of that body ordering. */
+static int64_t g_force_iters, g_contribs; /* analysis counters (single-threaded helper) */
+
 static int64_t union_walk(const Tree *t, const ForceCtx *c, int64_t node, const int64_t *bis,
                           uint64_t mask, int64_t *lane_visits) {
     const Node *nd = &t->nodes[node];
     if (nd->mass == 0.0 || !mask) return 0; /* BHA:216 */
     *lane_visits += __builtin_popcountll(mask);
-    if (nd->child < 0) return 1;
+    if (nd->child < 0) {
+        uint64_t contrib = 0;
+        for (uint64_t m = mask; m; m &= m - 1) {
+            const int l = __builtin_ctzll(m);
+            if (nd->body >= 0 && nd->body != bis[l]) contrib |= 1ull << l;
+        }
+        g_force_iters += contrib != 0;
+        g_contribs += __builtin_popcountll(contrib);
+        return 1;
+    }
     uint64_t open = 0;
     for (uint64_t m = mask; m; m &= m - 1) {
         const int l = __builtin_ctzll(m);
@@ -492,10 +503,18 @@ static int64_t union_walk(const Tree *t, const ForceCtx *c, int64_t node, const 
         const double hh = nd->q.h * 2.0, s2 = hh * hh;
         if (!(s2 < c->theta2 * dist2)) open |= 1ull << l;
     }
+    const uint64_t acc = mask & ~open;
+    g_force_iters += acc != 0;
+    g_contribs += __builtin_popcountll(acc);
     int64_t it = 1;
     if (open)
         for (int k = 0; k < 4; ++k) it += union_walk(t, c, nd->child + k, bis, open, lane_visits);
     return it;
+}
+
+void oracle_union_force_stats(int64_t *force_iters, int64_t *contribs) {
+    *force_iters = g_force_iters;
+    *contribs = g_contribs;
 }
 
 int64_t oracle_group_union(oracle_engine *e, const int64_t *order, int64_t count, int group,
@@ -507,6 +526,7 @@ int64_t oracle_group_union(oracle_engine *e, const int64_t *order, int64_t count
     }
     ForceCtx c = {e->p.G, e->p.soft2, e->p.theta * e->p.theta};
     int64_t iters = 0, lv = 0;
+    g_force_iters = g_contribs = 0;
     for (int64_t g0 = 0; g0 < count; g0 += group) {
         const int nb = (int)((count - g0) < group ? (count - g0) : group);
         const uint64_t mask = nb == 64 ? ~0ull : ((1ull << nb) - 1);

@@ -38,6 +38,8 @@ void oracle_tree_stats(oracle_engine *e, int64_t *n_nodes, int64_t *n_nonempty);
 /* analysis: wave-union iterations of groups of `group` consecutive bodies of `order` */
 int64_t oracle_group_union(oracle_engine *e, const int64_t *order, int64_t count, int group,
                            int64_t *lane_visits);
+/* of the last oracle_group_union: iterations with >= 1 contributing lane, contributions */
+void oracle_union_force_stats(int64_t *force_iters, int64_t *contribs);
 void oracle_destroy(oracle_engine *e);
 
 #ifdef __cplusplus
