@@ -67,6 +67,8 @@ struct Geometry {
 // Key of a body outside the root cell (never inserted, BHA:126): sorts after every
 // in-root key and differs from all of them at every prefix length.
 __host__ __device__ inline uint64_t sentinel_key(int J) { return 1ull << (2 * J); }
+// The build sorts the top 32 bits of the (2J+1)-bit keys and fixes the rare equal-prefix runs.
+__host__ __device__ inline int key32_shift(int J) { return 2 * J + 1 > 32 ? 2 * J + 1 - 32 : 0; }
 
 // Force-evaluation constants (BHA:225,253,256,378).
 struct ForceParams {
@@ -94,6 +96,7 @@ struct TreeBuffers {
     BodyState src;  // state before the build (previous slot order)
     BodyState dst;  // receives the state in the new Morton order (positions may be jittered)
     uint64_t *keys, *keys_s;
+    uint32_t *keys32, *keys32_s;  // sort keys (32-bit prefixes) before / after the sort
     uint32_t *idx, *perm;
     int8_t *cpl;           // c(a): common digit count between sorted keys a, a+1; -1 at ends
     uint32_t *cnt, *base;  // node slots per sorted body; exclusive scan (n + 1 entries)
@@ -117,6 +120,11 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
 void traverse(const Node *nodes, const uint32_t *d_T, const double *x, const double *y,
               const double *m, int64_t lo, int64_t hi, const Geometry &g, const ForceParams &fp,
               double *a2, uint32_t *visits, uint32_t *wave_iters, hipStream_t s);
+// ranks' Morton ranges are whole wavefronts (bh_shard_range)
+__host__ __device__ inline int64_t shard_chunk(int64_t n, int world) {
+    const int64_t c = (n + world - 1) / world;
+    return (c + 63) / 64 * 64;
+}
 
 // Exactness check of the traversal's in-range sqrt/reciprocal sequences against the IEEE
 // operations on n generated operands; adds the mismatch count to *d_bad.

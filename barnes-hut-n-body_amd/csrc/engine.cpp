@@ -51,6 +51,7 @@ struct bh_engine {
     double *ax = nullptr, *ay = nullptr;  // caller-order copy-out staging
 
     uint64_t *keys = nullptr, *keys_s = nullptr;
+    uint32_t *keys32 = nullptr, *keys32_s = nullptr;
     uint32_t *idx = nullptr, *perm = nullptr;
     int8_t *cpl = nullptr;
     uint32_t *cnt = nullptr, *base = nullptr;
@@ -199,12 +200,14 @@ int ensure_capacity(bh_engine *e, int64_t n) {
     if (n > e->cap || !e->st.x) {
         TRY(alloc_state(e, e->st, cap));
         TRY(alloc_state(e, e->alt, cap));
-        const int64_t chunk = (cap + e->world - 1) / e->world;
+        const int64_t chunk = shard_chunk(cap, e->world);
         TRY(dev_alloc(e, e->a2, 2 * chunk * e->world));
         TRY(dev_alloc(e, e->ax, cap));
         TRY(dev_alloc(e, e->ay, cap));
         TRY(dev_alloc(e, e->keys, cap));
         TRY(dev_alloc(e, e->keys_s, cap));
+        TRY(dev_alloc(e, e->keys32, cap));
+        TRY(dev_alloc(e, e->keys32_s, cap));
         TRY(dev_alloc(e, e->idx, cap));
         TRY(dev_alloc(e, e->perm, cap));
         TRY(dev_alloc(e, e->cpl, cap + 32));  // slack for word-wise scans
@@ -245,6 +248,8 @@ TreeBuffers tree_buffers(bh_engine *e) {
     b.dst = e->alt;
     b.keys = e->keys;
     b.keys_s = e->keys_s;
+    b.keys32 = e->keys32;
+    b.keys32_s = e->keys32_s;
     b.idx = e->idx;
     b.perm = e->perm;
     b.cpl = e->cpl;
@@ -351,7 +356,7 @@ int evaluate(bh_engine *e, uint32_t *visits) {
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
         if (e->comm) {
-            const int64_t chunk = (n + e->world - 1) / e->world;
+            const int64_t chunk = shard_chunk(n, e->world);
             NCCLCHK(e, ncclAllGather(e->a2 + 2 * e->rank * chunk, e->a2, (size_t)(2 * chunk),
                                      ncclDouble, e->comm, e->stream));
             TRY(mark(e, 4));
@@ -364,7 +369,7 @@ int evaluate(bh_engine *e, uint32_t *visits) {
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
     } else {
-        const int64_t chunk = (n + e->world - 1) / e->world;
+        const int64_t chunk = shard_chunk(n, e->world);
         int64_t lo = 0, hi = 0;
         bh_shard_range(n, e->rank, e->world, &lo, &hi);
         traverse(e->nodes, d_T, e->st.x, e->st.y, e->st.m, lo, hi, e->geo, fp, e->a2, nullptr,
@@ -660,7 +665,7 @@ void bh_destroy(bh_engine *e) {
     if (e->comm) (void)ncclCommDestroy(e->comm);
     free_state(e->st);
     free_state(e->alt);
-    void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->idx, e->perm, e->cpl, e->cnt,
+    void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->keys32, e->keys32_s, e->idx, e->perm, e->cpl, e->cnt,
                     e->base, e->cell_start, e->nodes, e->span_list, e->super_list,
                     e->span_children, e->scalars, e->visits32, e->wave_iters, e->heavy, e->keep,
                     e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->cub_tmp,
@@ -884,7 +889,7 @@ int bh_set_profiling(bh_engine *e, int enabled) {
 
 int bh_shard_range(int64_t n, int rank, int world, int64_t *lo, int64_t *hi) {
     if (n < 0 || world < 1 || rank < 0 || rank >= world || !lo || !hi) return BH_E_INVALID;
-    const int64_t chunk = (n + world - 1) / world;
+    const int64_t chunk = shard_chunk(n, world);  // whole wavefronts
     *lo = std::min<int64_t>(n, (int64_t)rank * chunk);
     *hi = std::min<int64_t>(n, *lo + chunk);
     return BH_OK;

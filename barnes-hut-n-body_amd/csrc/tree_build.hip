@@ -60,6 +60,7 @@ __global__ __launch_bounds__(TB) void k_morton(int64_t n, const double *__restri
                                                const double *__restrict__ y,
                                                const uint32_t *__restrict__ cidx, Geometry g,
                                                uint64_t *__restrict__ keys,
+                                               uint32_t *__restrict__ keys32,
                                                uint32_t *__restrict__ idx) {
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
@@ -80,7 +81,45 @@ __global__ __launch_bounds__(TB) void k_morton(int64_t n, const double *__restri
         }
     }
     keys[i] = key;
+    keys32[i] = (uint32_t)(key >> key32_shift(g.J));  // the sort key: top 32 of 2J+1 bits
     idx[i] = (uint32_t)i;
+}
+
+// After the 32-bit-prefix sort: keys_s = keys[perm] (k_key_gather), then every run of equal
+// prefixes (bodies sharing a depth-16 cell — short: at most 5 in C3) re-sorted by (full key,
+// original index) by the thread of its first element (k_key_fixup), so the result equals a
+// stable sort of the full keys.  The run of out-of-root / merged-away bodies (one shared
+// sentinel key) is already in index order and is left alone.
+__global__ __launch_bounds__(TB) void k_key_gather(int64_t n, const uint64_t *__restrict__ keys,
+                                                   const uint32_t *__restrict__ perm,
+                                                   uint64_t *__restrict__ keys_s) {
+    const int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (a < n) keys_s[a] = keys[perm[a]];
+}
+
+__global__ __launch_bounds__(TB) void k_key_fixup(int64_t n, int J,
+                                                  const uint32_t *__restrict__ keys32_s,
+                                                  uint64_t *__restrict__ keys_s,
+                                                  uint32_t *__restrict__ perm) {
+    const int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (a + 1 >= n) return;
+    const uint32_t k = keys32_s[a];
+    if (keys32_s[a + 1] != k || (a > 0 && keys32_s[a - 1] == k)) return;  // not a run start
+    if (k == (uint32_t)(sentinel_key(J) >> key32_shift(J))) return;        // sentinel run
+    int64_t e = a + 2;
+    while (e < n && keys32_s[e] == k) ++e;
+    for (int64_t i = a + 1; i < e; ++i) {  // insertion sort by (full key, original index)
+        const uint64_t ki = keys_s[i];
+        const uint32_t pi = perm[i];
+        int64_t j = i;
+        while (j > a && (keys_s[j - 1] > ki || (keys_s[j - 1] == ki && perm[j - 1] > pi))) {
+            keys_s[j] = keys_s[j - 1];
+            perm[j] = perm[j - 1];
+            --j;
+        }
+        keys_s[j] = ki;
+        perm[j] = pi;
+    }
 }
 
 __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *__restrict__ keys_s,
@@ -829,10 +868,10 @@ int cell_table_depth(int J, int64_t n) {
 
 size_t tree_cub_bytes(int64_t n, int J) {
     size_t sort_bytes = 0, scan_bytes = 0;
-    (void)rocprim::radix_sort_pairs<SortConfig>(nullptr, sort_bytes, (uint64_t *)nullptr,
-                                                (uint64_t *)nullptr, (uint32_t *)nullptr,
-                                                (uint32_t *)nullptr, (size_t)n, 0u,
-                                                (unsigned)(2 * J + 1));
+    (void)J;
+    (void)rocprim::radix_sort_pairs<SortConfig>(nullptr, sort_bytes, (uint32_t *)nullptr,
+                                                (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                (uint32_t *)nullptr, (size_t)n, 0u, 32u);
     (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint32_t *)nullptr,
                                            (uint32_t *)nullptr, (int)(n + 1));
     return sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
@@ -842,11 +881,14 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     if (n <= 0) return hipMemsetAsync(b.base, 0, sizeof(uint32_t), s);
     hipError_t st;
     const int D0 = cell_table_depth(g.J, n);
-    k_morton<<<grid_for(n), TB, 0, s>>>(n, b.src.x, b.src.y, b.src.cidx, g, b.keys, b.idx);
+    k_morton<<<grid_for(n), TB, 0, s>>>(n, b.src.x, b.src.y, b.src.cidx, g, b.keys, b.keys32,
+                                        b.idx);
     size_t bytes = b.cub_bytes;
-    st = rocprim::radix_sort_pairs<SortConfig>(b.cub_tmp, bytes, b.keys, b.keys_s, b.idx, b.perm,
-                                               (size_t)n, 0u, (unsigned)(2 * g.J + 1), s);
+    st = rocprim::radix_sort_pairs<SortConfig>(b.cub_tmp, bytes, b.keys32, b.keys32_s, b.idx,
+                                               b.perm, (size_t)n, 0u, 32u, s);
     if (st != hipSuccess) return st;
+    k_key_gather<<<grid_for(n), TB, 0, s>>>(n, b.keys, b.perm, b.keys_s);
+    k_key_fixup<<<grid_for(n), TB, 0, s>>>(n, g.J, b.keys32_s, b.keys_s, b.perm);
     k_prep<<<grid_for(n + 1), TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.src, b.dst, b.cpl, b.cnt);
     bytes = b.cub_bytes;
     st = hipcub::DeviceScan::ExclusiveSum(b.cub_tmp, bytes, b.cnt, b.base, (int)(n + 1), s);

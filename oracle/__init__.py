@@ -64,7 +64,8 @@ def load():
     lib.oracle_quads.argtypes = [ctypes.c_void_p, _D, _D, _D, ctypes.c_int64]
     lib.oracle_quads.restype = ctypes.c_int64
     lib.oracle_tree_stats.argtypes = [ctypes.c_void_p, _I64P, _I64P]
-    lib.oracle_group_union.argtypes = [ctypes.c_void_p, _I64P, ctypes.c_int64, ctypes.c_int, _I64P]
+    lib.oracle_group_union.argtypes = [ctypes.c_void_p, _I64P, ctypes.c_int64, ctypes.c_int, _I64P,
+                                       _I64P]
     lib.oracle_group_union.restype = ctypes.c_int64
     lib.oracle_destroy.argtypes = [ctypes.c_void_p]
     _lib = lib
@@ -143,13 +144,15 @@ class Oracle:
         self._lib.oracle_quads(self._h, _dp(cx), _dp(cy), _dp(h), n)
         return cx, cy, h
 
-    def group_union(self, order, group=64):
-        """(wave iterations, lane visits) of groups of `group` consecutive bodies of `order`."""
+    def group_union(self, order, group=64, per_group=False):
+        """(wave iterations, lane visits[, per-group iterations]) of groups of `group`
+        consecutive bodies of `order` (analysis helper, see bh_oracle.h)."""
         order = np.ascontiguousarray(order, dtype=np.int64)
         lv = ctypes.c_int64(0)
+        pg = np.zeros((len(order) + group - 1) // group, dtype=np.int64)
         it = self._lib.oracle_group_union(self._h, order.ctypes.data_as(_I64P), len(order),
-                                          int(group), ctypes.byref(lv))
-        return it, lv.value
+                                          int(group), ctypes.byref(lv), pg.ctypes.data_as(_I64P))
+        return (it, lv.value, pg) if per_group else (it, lv.value)
 
     def tree_stats(self):
         a = ctypes.c_int64(0)

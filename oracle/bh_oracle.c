@@ -518,7 +518,7 @@ void oracle_union_force_stats(int64_t *force_iters, int64_t *contribs) {
 }
 
 int64_t oracle_group_union(oracle_engine *e, const int64_t *order, int64_t count, int group,
-                           int64_t *lane_visits) {
+                           int64_t *lane_visits, int64_t *per_group) {
     if (group < 1 || group > 64) return -1;
     if (!e->tree_valid) {
         build_tree(e);
@@ -530,7 +530,9 @@ int64_t oracle_group_union(oracle_engine *e, const int64_t *order, int64_t count
     for (int64_t g0 = 0; g0 < count; g0 += group) {
         const int nb = (int)((count - g0) < group ? (count - g0) : group);
         const uint64_t mask = nb == 64 ? ~0ull : ((1ull << nb) - 1);
-        iters += union_walk(&e->tree, &c, 0, order + g0, mask, &lv);
+        const int64_t it = union_walk(&e->tree, &c, 0, order + g0, mask, &lv);
+        if (per_group) per_group[g0 / group] = it;
+        iters += it;
     }
     if (lane_visits) *lane_visits = lv;
     return iters;

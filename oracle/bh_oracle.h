@@ -37,7 +37,7 @@ int64_t oracle_quads(oracle_engine *e, double *cx, double *cy, double *h, int64_
 void oracle_tree_stats(oracle_engine *e, int64_t *n_nodes, int64_t *n_nonempty);
 /* analysis: wave-union iterations of groups of `group` consecutive bodies of `order` */
 int64_t oracle_group_union(oracle_engine *e, const int64_t *order, int64_t count, int group,
-                           int64_t *lane_visits);
+                           int64_t *lane_visits, int64_t *per_group);
 /* of the last oracle_group_union: iterations with >= 1 contributing lane, contributions */
 void oracle_union_force_stats(int64_t *force_iters, int64_t *contribs);
 void oracle_destroy(oracle_engine *e);

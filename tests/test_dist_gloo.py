@@ -62,7 +62,7 @@ def _worker(rank, world, port, out_dir):
     perm = morton_order(x, y)
     n = len(x)
     lo, hi = bh_amd.shard_range(n, rank, world)
-    chunk = (n + world - 1) // world
+    chunk = bh_amd.shard_range(n, 0, world)[1]  # whole wavefronts per rank (engine.cpp)
     ax, ay = ref.accelerations(subset=perm[lo:hi])  # this rank's Morton range
     send = np.zeros(2 * chunk)
     send[0:2 * (hi - lo):2] = ax
