@@ -21,7 +21,9 @@ import numpy as np
 from . import scenes  # noqa: F401  (re-export)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.normpath(os.path.join(_HERE, "..", "lib", "libbh_engine.so"))
+# BH_ENGINE_LIB selects another in-tree build of the library (A/B timing, tools/ab.sh)
+LIB_PATH = os.environ.get("BH_ENGINE_LIB") or os.path.normpath(
+    os.path.join(_HERE, "..", "lib", "libbh_engine.so"))
 
 BH_OK = 0
 BH_E_INVALID = -1
