@@ -40,7 +40,10 @@ constexpr uint32_t NODE_SPAN = 1u << 12;             // internal: body range cro
 
 // Centre-of-mass chunking (tree_build.hip): nodes inside a 2^COM_CHUNK_SHIFT-body chunk of
 // the Morton order are finished by one workgroup; the rest are listed per level.
-constexpr int COM_CHUNK_SHIFT = 10;
+#ifndef BH_COM_CHUNK_SHIFT
+#define BH_COM_CHUNK_SHIFT 10
+#endif
+constexpr int COM_CHUNK_SHIFT = BH_COM_CHUNK_SHIFT;
 __host__ __device__ inline uint32_t span_stride_for(int64_t n) {
     return (uint32_t)((n >> COM_CHUNK_SHIFT) + 2);
 }

@@ -30,11 +30,15 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
                                      double by, double Gm, double soft2, double theta2,
                                      double s2root, uint32_t self, uint32_t resume, double &fx,
                                      double &fy, uint32_t &nvis, uint32_t &niters) {
+    // s2root in a VGPR: v_ldexp_f64 then takes the uniform exponent straight from an SGPR
+    double s2root_v;
+    asm volatile("v_mov_b64 %0, %1" : "=v"(s2root_v) : "s"(s2root));
     uint32_t cur = 0;
     while (cur < T) {
         const double4_t raw = *reinterpret_cast<const double4_t *>(nodes + cur);
         const uint64_t w = (uint64_t)__double_as_longlong(raw.w);
-        const uint32_t meta = __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
+        uint32_t meta = __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
+        asm volatile("" : "+s"(meta));  // keep the flag tests scalar (s_bitcmp)
         uint32_t next = __builtin_amdgcn_readfirstlane((uint32_t)w);
         next = next > cur ? next : cur + 1;  // structural guard: the cursor always advances
         if (meta & NODE_SKIP) {              // mass == 0.0 (BHA:216), uniform
@@ -49,17 +53,21 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
         const double dx = raw.x - bx;  // BHA:223-225 == BHA:251-253
         const double dy = raw.y - by;
         const double d2 = dx * dx + dy * dy + soft2;
-        bool contrib, open;
+        bool contrib;
+        uint64_t open_m;  // lanes that open this node (wave-uniform mask)
         if (meta & NODE_LEAF) {  // BHA:217-221: skip self by identity
             contrib = active && ((meta & NODE_BODY_MASK) != self);
-            open = false;
+            open_m = 0;
         } else {
             // s2 = (h_d * 2.0)^2 with h_d = h_0 / 2^d exactly, so s2 = s2_0 * 4^-d exactly
             // (a power-of-two scaling commutes with rounding): one v_ldexp, no table load.
-            const double s2 = __builtin_ldexp(s2root, -2 * (int)(meta & NODE_DEPTH_MASK));
-            const bool acc = s2 < theta2 * d2;  // BHA:226-228
+            const double s2 = __builtin_ldexp(s2root_v, -2 * (int)(meta & NODE_DEPTH_MASK));
+            const double t2 = theta2 * d2;
+            const bool acc = s2 < t2;  // BHA:226-228
             contrib = active && acc;
-            open = active && !acc;
+            // ballot of the compare itself lands in an SGPR pair; masked by the active lanes
+            open_m = __builtin_amdgcn_ballot_w64(!(s2 < t2)) &
+                     __builtin_amdgcn_ballot_w64(cur >= resume);
         }
         if (contrib) {  // BHA:250-259, expression order as written
             double invR, invR2;
@@ -77,8 +85,7 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
             fy += f * dy * invR;
             resume = next;
         }
-        const bool any_open = __ballot(open) != 0ull;  // wave-uniform
-        cur = any_open ? cur + 1 : next;
+        cur = open_m != 0ull ? cur + 1 : next;  // descend iff some lane opened
     }
 }
 

@@ -460,7 +460,10 @@ __device__ __forceinline__ void node_com(Node *nodes, uint32_t ni, const Geometr
 // levels with barriers.  Chunks whose range exceeds the LDS capacity use global memory.
 constexpr int COM_TB = 256;
 constexpr int COM_PER_THREAD = (1 << COM_CHUNK_SHIFT) / COM_TB;
-constexpr int COM_CAP = 2048;  // nodes staged per chunk (C3 at 1e6: ~1.7 per body, max 1814)
+#ifndef BH_COM_CAP
+#define BH_COM_CAP 2048
+#endif
+constexpr int COM_CAP = BH_COM_CAP;  // nodes staged per chunk (C3 at 1e6, 1024-body chunks: max 1814)
 constexpr int COM_LOAD_BATCH = 4;
 constexpr uint32_t LDS_SPAN = 1u << 31;
 constexpr uint32_t LDS_LEAF = 1u << 30;
