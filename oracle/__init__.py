@@ -67,6 +67,12 @@ def load():
     lib.oracle_group_union.argtypes = [ctypes.c_void_p, _I64P, ctypes.c_int64, ctypes.c_int, _I64P,
                                        _I64P]
     lib.oracle_group_union.restype = ctypes.c_int64
+    lib.oracle_union_force_stats.argtypes = [_I64P, _I64P]
+    lib.oracle_union_force_stats.restype = None
+    lib.oracle_deferred_model.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.oracle_deferred_model.restype = None
+    lib.oracle_deferred_flushes.argtypes = []
+    lib.oracle_deferred_flushes.restype = ctypes.c_int64
     lib.oracle_destroy.argtypes = [ctypes.c_void_p]
     _lib = lib
     return lib
@@ -153,6 +159,23 @@ class Oracle:
         it = self._lib.oracle_group_union(self._h, order.ctypes.data_as(_I64P), len(order),
                                           int(group), ctypes.byref(lv), pg.ctypes.data_as(_I64P))
         return (it, lv.value, pg) if per_group else (it, lv.value)
+
+    def union_force_stats(self):
+        """(wave iterations with >= 1 contributing lane, contributions) of the last
+        group_union (analysis helper)."""
+        a, b = ctypes.c_int64(0), ctypes.c_int64(0)
+        self._lib.oracle_union_force_stats(ctypes.byref(a), ctypes.byref(b))
+        return a.value, b.value
+
+    def deferred_flushes(self, order, q, t, group=64):
+        """Force-block executions of the deferred-force model (per-lane FIFO of depth q,
+        flushed when one is full or >= t lanes have work) for waves of `order`."""
+        self._lib.oracle_deferred_model(int(q), int(t))
+        try:
+            self.group_union(order, group)
+            return int(self._lib.oracle_deferred_flushes())
+        finally:
+            self._lib.oracle_deferred_model(0, 0)
 
     def tree_stats(self):
         a = ctypes.c_int64(0)

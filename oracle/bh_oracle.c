@@ -479,6 +479,38 @@ void oracle_tree_stats(oracle_engine *e, int64_t *n_nodes, int64_t *n_nonempty) 
  * and the lanes' own visits; their ratio is the lane efficiency of that body ordering. */
 static int64_t g_force_iters, g_contribs; /* analysis counters (single-threaded helper) */
 
+/* Deferred-force model (analysis only): every lane queues its contributions (FIFO, depth
+ * g_sim_q); a "flush" runs the force math once for every lane with a non-empty queue.  A flush
+ * happens when some queue is full, or when at least g_sim_t lanes have work; the queues are
+ * drained at the end of the walk.  g_sim_flushes counts flushes (force-block executions). */
+static int g_sim_q, g_sim_t;
+static int g_sim_cnt[64];
+static int64_t g_sim_flushes;
+
+static void sim_push(uint64_t contrib) {
+    if (!g_sim_q) return;
+    int full = 0, nonempty = 0;
+    for (int l = 0; l < 64; ++l) {
+        if (contrib >> l & 1) ++g_sim_cnt[l];
+        full |= g_sim_cnt[l] >= g_sim_q;
+        nonempty += g_sim_cnt[l] > 0;
+    }
+    if (full || nonempty >= g_sim_t) {
+        ++g_sim_flushes;
+        for (int l = 0; l < 64; ++l)
+            if (g_sim_cnt[l] > 0) --g_sim_cnt[l];
+    }
+}
+
+static void sim_drain(void) {
+    int mx = 0;
+    for (int l = 0; l < 64; ++l) {
+        if (g_sim_cnt[l] > mx) mx = g_sim_cnt[l];
+        g_sim_cnt[l] = 0;
+    }
+    g_sim_flushes += mx;
+}
+
 static int64_t union_walk(const Tree *t, const ForceCtx *c, int64_t node, const int64_t *bis,
                           uint64_t mask, int64_t *lane_visits) {
     const Node *nd = &t->nodes[node];
@@ -492,6 +524,7 @@ static int64_t union_walk(const Tree *t, const ForceCtx *c, int64_t node, const 
         }
         g_force_iters += contrib != 0;
         g_contribs += __builtin_popcountll(contrib);
+        sim_push(contrib);
         return 1;
     }
     uint64_t open = 0;
@@ -506,6 +539,7 @@ static int64_t union_walk(const Tree *t, const ForceCtx *c, int64_t node, const 
     const uint64_t acc = mask & ~open;
     g_force_iters += acc != 0;
     g_contribs += __builtin_popcountll(acc);
+    sim_push(acc);
     int64_t it = 1;
     if (open)
         for (int k = 0; k < 4; ++k) it += union_walk(t, c, nd->child + k, bis, open, lane_visits);
@@ -516,6 +550,16 @@ void oracle_union_force_stats(int64_t *force_iters, int64_t *contribs) {
     *force_iters = g_force_iters;
     *contribs = g_contribs;
 }
+
+/* Configure the deferred-force model for the next oracle_group_union (q = 0: off). */
+void oracle_deferred_model(int q, int t) {
+    g_sim_q = q;
+    g_sim_t = t;
+    for (int l = 0; l < 64; ++l) g_sim_cnt[l] = 0;
+    g_sim_flushes = 0;
+}
+
+int64_t oracle_deferred_flushes(void) { return g_sim_flushes; }
 
 int64_t oracle_group_union(oracle_engine *e, const int64_t *order, int64_t count, int group,
                            int64_t *lane_visits, int64_t *per_group) {
@@ -531,6 +575,7 @@ int64_t oracle_group_union(oracle_engine *e, const int64_t *order, int64_t count
         const int nb = (int)((count - g0) < group ? (count - g0) : group);
         const uint64_t mask = nb == 64 ? ~0ull : ((1ull << nb) - 1);
         const int64_t it = union_walk(&e->tree, &c, 0, order + g0, mask, &lv);
+        if (g_sim_q) sim_drain();
         if (per_group) per_group[g0 / group] = it;
         iters += it;
     }

@@ -40,6 +40,10 @@ int64_t oracle_group_union(oracle_engine *e, const int64_t *order, int64_t count
                            int64_t *lane_visits, int64_t *per_group);
 /* of the last oracle_group_union: iterations with >= 1 contributing lane, contributions */
 void oracle_union_force_stats(int64_t *force_iters, int64_t *contribs);
+/* analysis: per-lane deferred-force queues of depth q, flushed when one is full or >= t lanes
+ * have work (q = 0: off); flush count of the next oracle_group_union */
+void oracle_deferred_model(int q, int t);
+int64_t oracle_deferred_flushes(void);
 void oracle_destroy(oracle_engine *e);
 
 #ifdef __cplusplus

@@ -1,14 +1,15 @@
 #!/usr/bin/env bash
-# A/B timing on one GPU box: bench.py alternately against two in-tree builds of the library
-# (barnes-hut-n-body_amd/lib/libA.so and libB.so, made by the caller), ROUNDS times each, so
-# box-to-box clock differences cancel.  Prints one line per run: label ms_per_step kernel_ms.
+# A/B timing on one GPU box: bench.py alternately against in-tree builds of the library
+# (barnes-hut-n-body_amd/lib/lib<L>.so for L in $LIBS, default "A B", made by the caller),
+# ROUNDS times each, so box-to-box clock differences cancel.  Prints one line per run:
+# label ms_per_step kernel_ms phases.
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 ROUNDS=${ROUNDS:-3}
 ARGS=${AB_ARGS:-"--steps 10 --warmup 2 --no-cpu-baseline"}
 for r in $(seq 1 $ROUNDS); do
-  for L in A B; do
+  for L in ${LIBS:-A B}; do
     BH_ENGINE_LIB=$PWD/barnes-hut-n-body_amd/lib/lib$L.so timeout -k 10 300 python bench.py $ARGS \
       > gpurun_out/ab_$L$r.log 2>&1 || { echo "run $L$r failed"; tail -3 gpurun_out/ab_$L$r.log; exit 1; }
     python - "$L" gpurun_out/ab_$L$r.log <<'PY'
