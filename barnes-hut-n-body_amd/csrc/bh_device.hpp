@@ -94,6 +94,25 @@ struct __attribute__((aligned(16))) SpanSlot {
     double v[4][3];
 };
 
+// Workgroup i of a launch runs on XCD i % 8 (8 XCDs, each with its own 4 MB L2).  For gathers
+// whose neighbouring blocks read overlapping lines, xcd_block() remaps the hardware block index
+// so that every XCD takes runs of BH_XCD_RUN consecutive logical blocks (0: identity; 16 is
+// ~1% faster for k_prep/k_key_gather/k_emit at C3 and C4 than the identity, A/B on one box).
+#ifndef BH_XCD_RUN
+#define BH_XCD_RUN 16
+#endif
+#ifdef __HIP__  // HIP translation units only (engine.cpp is host C++)
+__device__ __forceinline__ uint32_t xcd_block() {
+    uint32_t b = blockIdx.x;
+    if (BH_XCD_RUN > 0) {
+        constexpr uint32_t C = BH_XCD_RUN, G = 8 * C;
+        const uint32_t full = gridDim.x / G;
+        if (b < full * G) b = (b / 8 / C) * G + (b % 8) * C + (b / 8) % C;
+    }
+    return b;
+}
+#endif
+
 // ---- launchers (tree_build.hip) --------------------------------------------------
 struct TreeBuffers {
     BodyState src;  // state before the build (previous slot order)

@@ -45,31 +45,29 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
             cur = next;
             continue;
         }
-        const bool active = cur >= resume;
+        // lane masks in SGPRs straight from the compares; per-lane booleans via inverse ballot
+        const uint64_t act_m = __builtin_amdgcn_ballot_w64(cur >= resume);
         if (COUNT) {
-            nvis += active ? 1u : 0u;
+            nvis += __builtin_amdgcn_inverse_ballot_w64(act_m) ? 1u : 0u;
             niters += 1;
         }
         const double dx = raw.x - bx;  // BHA:223-225 == BHA:251-253
         const double dy = raw.y - by;
         const double d2 = dx * dx + dy * dy + soft2;
-        bool contrib;
-        uint64_t open_m;  // lanes that open this node (wave-uniform mask)
+        uint64_t contrib_m, open_m;  // lanes that take / open this node
         if (meta & NODE_LEAF) {  // BHA:217-221: skip self by identity
-            contrib = active && ((meta & NODE_BODY_MASK) != self);
+            contrib_m = act_m & __builtin_amdgcn_ballot_w64((meta & NODE_BODY_MASK) != self);
             open_m = 0;
         } else {
             // s2 = (h_d * 2.0)^2 with h_d = h_0 / 2^d exactly, so s2 = s2_0 * 4^-d exactly
             // (a power-of-two scaling commutes with rounding): one v_ldexp, no table load.
             const double s2 = __builtin_ldexp(s2root_v, -2 * (int)(meta & NODE_DEPTH_MASK));
             const double t2 = theta2 * d2;
-            const bool acc = s2 < t2;  // BHA:226-228
-            contrib = active && acc;
-            // ballot of the compare itself lands in an SGPR pair; masked by the active lanes
-            open_m = __builtin_amdgcn_ballot_w64(!(s2 < t2)) &
-                     __builtin_amdgcn_ballot_w64(cur >= resume);
+            const uint64_t acc_m = __builtin_amdgcn_ballot_w64(s2 < t2);  // BHA:226-228
+            contrib_m = act_m & acc_m;
+            open_m = act_m & ~acc_m;
         }
-        if (contrib) {  // BHA:250-259, expression order as written
+        if (__builtin_amdgcn_inverse_ballot_w64(contrib_m)) {  // BHA:250-259, order as written
             double invR, invR2;
             if (FAST) {
                 double h;

@@ -93,7 +93,7 @@ __global__ __launch_bounds__(TB) void k_morton(int64_t n, const double *__restri
 __global__ __launch_bounds__(TB) void k_key_gather(int64_t n, const uint64_t *__restrict__ keys,
                                                    const uint32_t *__restrict__ perm,
                                                    uint64_t *__restrict__ keys_s) {
-    const int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
+    const int64_t a = (int64_t)xcd_block() * TB + threadIdx.x;
     if (a < n) keys_s[a] = keys[perm[a]];
 }
 
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
                                              const uint32_t *__restrict__ perm, BodyState src,
                                              BodyState dst, int8_t *__restrict__ cpl,
                                              uint32_t *__restrict__ cnt) {
-    int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
+    int64_t a = (int64_t)xcd_block() * TB + threadIdx.x;
     if (a > n) return;
     if (a == n) {
         cnt[n] = 0;
@@ -219,7 +219,7 @@ __global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, int D0,
                                              const double *__restrict__ m,
                                              Node *__restrict__ nodes) {
     __shared__ uint64_t win[EMIT_WIN / 8];
-    const int64_t c0 = (int64_t)blockIdx.x * TB;
+    const int64_t c0 = (int64_t)xcd_block() * TB;
     {
         uint8_t *wb = reinterpret_cast<uint8_t *>(win);
         for (int i = threadIdx.x; i < EMIT_WIN; i += TB) {
@@ -858,10 +858,13 @@ inline unsigned grid_for(int64_t n) { return (unsigned)((n + TB - 1) / TB); }
 
 }  // namespace
 
-// Stable LSD radix sort over the 2J+1 key bits.  rocprim's default picks a merge sort for
-// n <= 2^20 and onesweep above; measured at n = 1e6 on MI355X the merge sort (~175 us) beats
-// a forced onesweep (6 passes x 25 us + lookback-state memsets, ~230 us), so keep the default.
-using SortConfig = rocprim::default_config;
+// Stable LSD radix sort of the 32-bit key prefixes.  rocprim's default picks a merge sort for
+// n <= BH_SORT_MERGE_LIMIT (2^20) and onesweep above.
+#ifndef BH_SORT_MERGE_LIMIT
+#define BH_SORT_MERGE_LIMIT (1024 * 1024)
+#endif
+using SortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                              rocprim::default_config, BH_SORT_MERGE_LIMIT>;
 
 int cell_table_depth(int J, int64_t n) {
     int d = 1;  // smallest depth with 4^d >= n, capped
