@@ -24,6 +24,21 @@ namespace {
 constexpr int TB = 256;
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
+
+// Node record through an explicit scalar load whose wait is placed by hand (nwait): the next
+// record is requested as soon as the cursor decision is made and waited for only after the
+// point-force block, so its latency hides behind that block's fp64 work.  (The compiler would
+// sink a plain load below the block, to its first use.)
+__device__ __forceinline__ u32x8 nload(const Node *p) {
+    u32x8 v;
+    asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
+    return v;
+}
+__device__ __forceinline__ void nwait(u32x8 &v) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(v)); }
+__device__ __forceinline__ double as_f64(uint32_t lo, uint32_t hi) {
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
 
 template <bool FAST, bool COUNT>
 __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T, double bx,
@@ -34,15 +49,20 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
     double s2root_v;
     asm volatile("v_mov_b64 %0, %1" : "=v"(s2root_v) : "s"(s2root));
     uint32_t cur = 0;
+    u32x8 rec = nload(nodes);  // T >= 1 whenever the loop runs
+    nwait(rec);
     while (cur < T) {
-        const double4_t raw = *reinterpret_cast<const double4_t *>(nodes + cur);
-        const uint64_t w = (uint64_t)__double_as_longlong(raw.w);
-        uint32_t meta = __builtin_amdgcn_readfirstlane((uint32_t)(w >> 32));
+        const double comX = as_f64(rec[0], rec[1]), comY = as_f64(rec[2], rec[3]);
+        const double mass = as_f64(rec[4], rec[5]);
+        uint32_t meta = rec[7];
         asm volatile("" : "+s"(meta));  // keep the flag tests scalar (s_bitcmp)
-        uint32_t next = __builtin_amdgcn_readfirstlane((uint32_t)w);
+        uint32_t next = rec[6];
         next = next > cur ? next : cur + 1;  // structural guard: the cursor always advances
         if (meta & NODE_SKIP) {              // mass == 0.0 (BHA:216), uniform
             cur = next;
+            u32x8 nrec = nload(nodes + (cur < T ? cur : 0u));
+            nwait(nrec);
+            rec = nrec;
             continue;
         }
         // lane masks in SGPRs straight from the compares; per-lane booleans via inverse ballot
@@ -51,8 +71,8 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
             nvis += __builtin_amdgcn_inverse_ballot_w64(act_m) ? 1u : 0u;
             niters += 1;
         }
-        const double dx = raw.x - bx;  // BHA:223-225 == BHA:251-253
-        const double dy = raw.y - by;
+        const double dx = comX - bx;  // BHA:223-225 == BHA:251-253
+        const double dy = comY - by;
         const double d2 = dx * dx + dy * dy + soft2;
         uint64_t contrib_m, open_m;  // lanes that take / open this node
         if (meta & NODE_LEAF) {  // BHA:217-221: skip self by identity
@@ -67,6 +87,8 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
             contrib_m = act_m & acc_m;
             open_m = act_m & ~acc_m;
         }
+        const uint32_t ncur = open_m != 0ull ? cur + 1 : next;  // descend iff some lane opened
+        u32x8 nrec = nload(nodes + (ncur < T ? ncur : 0u));
         if (__builtin_amdgcn_inverse_ballot_w64(contrib_m)) {  // BHA:250-259, order as written
             double invR, invR2;
             if (FAST) {
@@ -78,12 +100,14 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
                 invR = 1.0 / sqrt(d2);
                 invR2 = 1.0 / d2;
             }
-            const double f = Gm * raw.z * invR2;
+            const double f = Gm * mass * invR2;
             fx += f * dx * invR;
             fy += f * dy * invR;
             resume = next;
         }
-        cur = open_m != 0ull ? cur + 1 : next;  // descend iff some lane opened
+        nwait(nrec);
+        rec = nrec;
+        cur = ncur;
     }
 }
 
