@@ -74,6 +74,8 @@ struct bh_engine {
     uint32_t *dead_sorted = nullptr; // the log sorted, for the compaction's renumbering
     uint64_t *rkeys = nullptr;       // replay sort scratch (long candidate lists)
     uint32_t *ridx = nullptr;
+    uint32_t *mbits = nullptr;       // victim bitmap over caller indices (long lists)
+    uint32_t *mslot = nullptr;       // caller index -> slot of the victims
     int64_t dlog_cap = 0;
     bool heavy_possible = true;  // false once a step saw no heavy body (heavies never appear)
     bool merge_ran = false;      // the running bh_step call launched the merge rule
@@ -425,6 +427,8 @@ int merge_bufs(bh_engine *e) {
     if (e->dlog_cap < e->cap) {  // at most every body is removed within one call
         TRY(dev_alloc(e, e->dlog, (size_t)e->cap + 1));
         TRY(dev_alloc(e, e->dead_sorted, (size_t)e->cap + 1));
+        TRY(dev_alloc(e, e->mbits, ((size_t)e->cap >> 5) + 2));
+        TRY(dev_alloc(e, e->mslot, (size_t)e->cap + 1));
         e->dlog_cap = e->cap;
     }
     return BH_OK;
@@ -438,7 +442,7 @@ int merge(bh_engine *e) {
     merge_candidates(e->n, e->st.x, e->st.y, e->st.m, e->st.cidx, e->p.merge_max_mass, minD2,
                      e->heavy, e->box, e->box_cap, e->stream);
     merge_replay(e->box, e->box_cap, e->st.m, e->st.cidx, e->scalars, e->dlog, e->rkeys, e->ridx,
-                 e->stream);
+                 e->mbits, e->mslot, e->stream);
     HIPCHK(e, hipGetLastError());
     e->merge_ran = true;
     TRY(mark(e, 3));
@@ -668,7 +672,7 @@ void bh_destroy(bh_engine *e) {
     void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->keys32, e->keys32_s, e->idx, e->perm, e->cpl, e->cnt,
                     e->base, e->cell_start, e->nodes, e->span_list, e->super_list,
                     e->span_children, e->scalars, e->visits32, e->wave_iters, e->heavy, e->keep,
-                    e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->cub_tmp,
+                    e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->mbits, e->mslot, e->cub_tmp,
                     e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaves.xy, e->leaves.m,
                     e->leaves.slot, e->leaf_tmp};
     for (void *q : ptrs)

@@ -149,11 +149,153 @@ __device__ __forceinline__ uint64_t pair_key(const MergePair &p) {
     return ((uint64_t)p.h_cidx << 32) | p.v_cidx;
 }
 
+constexpr int LARGE_HMAX = 256;       // distinct heavy bodies the bitmap replay handles
+constexpr int LARGE_HTAB = 512;       // LDS hash table for them (power of two)
+constexpr uint32_t KILLED = 1u << 31;  // vslot flag: removed by the running heavy
+
+// Sequential rule (BHA:470-531) for long candidate lists, same semantics as replay_sorted:
+// heavy bodies in caller order (LDS hash set of the pairs' heavies, sorted by one thread);
+// for each live one, its victims in DESCENDING caller index come from a bitmap over caller
+// indices (set in parallel, enumerated by a block scan), their state is gathered into LDS in
+// chunks in parallel, and one thread adds the masses in order from LDS; tombstones are written
+// back in parallel.  Returns false, having done nothing, if the pairs name more than
+// LARGE_HMAX heavy bodies.
+__device__ bool replay_large(const MergePair *__restrict__ pairs, uint32_t count, double *m,
+                             uint32_t *cidx, uint32_t *dlog, uint32_t *scal, uint32_t *bits,
+                             uint32_t *slot_of, uint32_t *vlist, uint32_t *s_tab,
+                             uint32_t *s_hc, uint32_t *s_hs, uint32_t *s_scan, double *vm,
+                             uint32_t *vslot, uint32_t *vcid, int chunk) {
+    __shared__ uint32_t s_nh, s_maxc, s_total;
+    const uint32_t tid = threadIdx.x;
+    for (uint32_t i = tid; i < LARGE_HTAB; i += REPLAY_TB) s_tab[i] = 0xFFFFFFFFu;
+    if (tid == 0) {
+        s_nh = 0;
+        s_maxc = 0;
+    }
+    __syncthreads();
+    uint32_t maxc = 0;
+    for (uint32_t q = tid; q < count; q += REPLAY_TB) {  // distinct heavies (by slot)
+        const uint32_t hs = pairs[q].h_slot;
+        maxc = max(maxc, pairs[q].v_cidx);
+        uint32_t h = (hs * 2654435761u) & (LARGE_HTAB - 1);
+        for (uint32_t probe = 0; probe < LARGE_HTAB; ++probe) {
+            const uint32_t prev = atomicCAS(&s_tab[h], 0xFFFFFFFFu, hs);
+            if (prev == 0xFFFFFFFFu || prev == hs) break;
+            h = (h + 1) & (LARGE_HTAB - 1);
+        }
+    }
+    atomicMax(&s_maxc, maxc);
+    __syncthreads();
+    if (tid == 0) {  // compact, then order by caller index (insertion sort, <= LARGE_HMAX)
+        uint32_t nh = 0;
+        for (uint32_t i = 0; i < LARGE_HTAB; ++i) {
+            const uint32_t hs = s_tab[i];
+            if (hs == 0xFFFFFFFFu) continue;
+            if (nh == LARGE_HMAX) {
+                nh = LARGE_HMAX + 1;
+                break;
+            }
+            s_hs[nh] = hs;
+            s_hc[nh] = cidx[hs] & ~CIDX_DEAD;
+            ++nh;
+        }
+        if (nh <= LARGE_HMAX)
+            for (uint32_t i = 1; i < nh; ++i)
+                for (uint32_t j = i; j > 0 && s_hc[j - 1] > s_hc[j]; --j) {
+                    const uint32_t tc = s_hc[j], ts = s_hs[j];
+                    s_hc[j] = s_hc[j - 1];
+                    s_hs[j] = s_hs[j - 1];
+                    s_hc[j - 1] = tc;
+                    s_hs[j - 1] = ts;
+                }
+        s_nh = nh;
+    }
+    __syncthreads();
+    const uint32_t nh = s_nh;
+    if (nh > LARGE_HMAX) return false;
+    const uint32_t nwords = (s_maxc >> 5) + 1;
+    const uint32_t per = (nwords + REPLAY_TB - 1) / REPLAY_TB;
+    // thread t owns words [w0, w1), thread 0 the highest: enumeration order = descending index
+    const int64_t w1 = max((int64_t)nwords - (int64_t)tid * per, (int64_t)0);
+    const int64_t w0 = max(w1 - (int64_t)per, (int64_t)0);
+    uint32_t nd = scal[2];  // meaningful in thread 0
+    for (uint32_t hi = 0; hi < nh; ++hi) {
+        const uint32_t hs = s_hs[hi];
+        if (cidx[hs] & CIDX_DEAD) continue;  // absorbed earlier in this replay (uniform)
+        for (uint32_t w = tid; w < nwords; w += REPLAY_TB) bits[w] = 0u;
+        __syncthreads();
+        for (uint32_t q = tid; q < count; q += REPLAY_TB) {
+            const MergePair pr = pairs[q];
+            if (pr.h_slot != hs) continue;
+            atomicOr(&bits[pr.v_cidx >> 5], 1u << (pr.v_cidx & 31));
+            slot_of[pr.v_cidx] = pr.v_slot;
+        }
+        __syncthreads();
+        uint32_t c = 0;
+        for (int64_t w = w0; w < w1; ++w) c += __popc(bits[w]);
+        s_scan[tid] = c;
+        __syncthreads();
+        if (tid == 0) {
+            uint32_t acc = 0;
+            for (uint32_t t = 0; t < REPLAY_TB; ++t) {
+                const uint32_t v = s_scan[t];
+                s_scan[t] = acc;
+                acc += v;
+            }
+            s_total = acc;
+        }
+        __syncthreads();
+        uint32_t off = s_scan[tid];
+        for (int64_t w = w1 - 1; w >= w0; --w) {
+            uint32_t b = bits[w];
+            while (b) {
+                const int k = 31 - __clz(b);
+                vlist[off++] = ((uint32_t)w << 5) | (uint32_t)k;
+                b &= ~(1u << k);
+            }
+        }
+        __syncthreads();
+        const uint32_t nv = s_total;
+        double mi = tid == 0 ? m[hs] : 0.0;
+        bool any = false;
+        for (uint32_t c0 = 0; c0 < nv; c0 += (uint32_t)chunk) {
+            const uint32_t cn = min((uint32_t)chunk, nv - c0);
+            for (uint32_t k = tid; k < cn; k += REPLAY_TB) {
+                const uint32_t vs = slot_of[vlist[c0 + k]];
+                vslot[k] = vs;
+                vm[k] = m[vs];
+                vcid[k] = cidx[vs];
+            }
+            __syncthreads();
+            if (tid == 0) {
+                for (uint32_t k = 0; k < cn; ++k) {
+                    const uint32_t cv = vcid[k];
+                    if (cv & CIDX_DEAD) continue;
+                    mi += vm[k];  // BHA:518
+                    dlog[nd++] = cv;
+                    vcid[k] = cv | CIDX_DEAD;
+                    vslot[k] |= KILLED;
+                    any = true;
+                }
+            }
+            __syncthreads();
+            for (uint32_t k = tid; k < cn; k += REPLAY_TB)
+                if (vslot[k] & KILLED) cidx[vslot[k] & ~KILLED] = vcid[k];
+            __syncthreads();
+        }
+        if (tid == 0 && any) m[hs] = mi;
+        __syncthreads();
+    }
+    if (tid == 0) scal[2] = nd;
+    return true;
+}
+
 __global__ __launch_bounds__(REPLAY_TB) void k_merge_replay(const MergePair *__restrict__ box,
                                                             uint32_t cap, double *m,
                                                             uint32_t *cidx, uint32_t *scal,
                                                             uint32_t *dlog, uint64_t *skeys,
-                                                            uint32_t *sidx) {
+                                                            uint32_t *sidx, uint32_t *bits,
+                                                            uint32_t *slot_of) {
     __shared__ uint64_t lk[REPLAY_LDS];
     __shared__ uint32_t li[REPLAY_LDS];
     __shared__ uint32_t hkey[REPLAY_HASH], hcidx[REPLAY_HASH];
@@ -169,6 +311,13 @@ __global__ __launch_bounds__(REPLAY_TB) void k_merge_replay(const MergePair *__r
         return;
     }
     uint32_t nd = scal[2];
+    if (count > REPLAY_FAST) {  // long lists: bitmap-ordered replay (LDS reused as scratch)
+        static_assert(REPLAY_LDS >= REPLAY_TB && REPLAY_HASH >= 2 * LARGE_HTAB, "LDS reuse");
+        if (replay_large(pairs, count, m, cidx, dlog, scal, bits, slot_of, sidx, hkey,
+                         hcidx, hcidx + LARGE_HMAX, li, hmass, reinterpret_cast<uint32_t *>(lk),
+                         reinterpret_cast<uint32_t *>(lk) + REPLAY_LDS, REPLAY_LDS))
+            return;
+    }
     if (count <= REPLAY_LDS) {  // bitonic sort of (key, index) in LDS
         uint32_t P = 1;
         while (P < count) P <<= 1;
@@ -372,8 +521,10 @@ void merge_candidates(int64_t n, const double *x, const double *y, const double 
 }
 
 void merge_replay(const MergePair *box, uint32_t cap, double *m, uint32_t *cidx, uint32_t *scal,
-                  uint32_t *dlog, uint64_t *skeys, uint32_t *sidx, hipStream_t s) {
-    k_merge_replay<<<1, REPLAY_TB, 0, s>>>(box, cap, m, cidx, scal, dlog, skeys, sidx);
+                  uint32_t *dlog, uint64_t *skeys, uint32_t *sidx, uint32_t *bits,
+                  uint32_t *slot_of, hipStream_t s) {
+    k_merge_replay<<<1, REPLAY_TB, 0, s>>>(box, cap, m, cidx, scal, dlog, skeys, sidx, bits,
+                                           slot_of);
 }
 
 size_t compact_cub_bytes(int64_t n) {

@@ -153,6 +153,38 @@ def test_merge_rule():
     _assert_state_equal(eng2, ref2)
 
 
+@pytest.mark.parametrize("crowd", [400, 6000])
+def test_merge_rule_long_candidate_lists(crowd):
+    """More candidate pairs than the LDS replay holds (1024 / 2048): the bitmap-ordered replay
+    (integrate.hip replay_large).  Three heavy bodies inside one crowd -- the first absorbs the
+    second, whose grown mass it then carries -- plus a heavy in a second crowd; dt = 0 isolates
+    the rule, then full steps."""
+    rng = np.random.default_rng(crowd)
+    r = 7.9 * np.sqrt(rng.random(crowd))
+    phi = 2 * np.pi * rng.random(crowd)
+    cx = np.concatenate([1000.0 + r * np.cos(phi), 1600.0 + r[: crowd // 3] * np.sin(phi[: crowd // 3])])
+    cy = np.concatenate([400.0 + r * np.sin(phi), 300.0 + r[: crowd // 3] * np.cos(phi[: crowd // 3])])
+    cm = rng.uniform(0.1, 3.0, len(cx))
+    hx = [1000.0, 1003.0, 1001.0, 1600.0]
+    hy = [400.0, 401.0, 399.0, 300.0]
+    hm = [5000.0, 4500.0, 9000.0, 6000.0]
+    field = scenes.uniform(500, 0.5, seed=13)
+    x = np.concatenate([cx, hx, field[0]])
+    y = np.concatenate([cy, hy, field[1]])
+    m = np.concatenate([cm, hm, field[4]])
+    perm = rng.permutation(len(x))  # heavies and victims interleaved in list order
+    arrs = tuple(a[perm] for a in (x, y, np.zeros(len(x)), np.zeros(len(x)), m))
+    eng, ref = _pair(arrs, theta=0.5, dt=0.0)
+    eng.step(1)
+    ref.step(1)
+    _assert_state_equal(eng, ref)
+    assert eng.num_bodies() < len(x) - crowd
+    eng2, ref2 = _pair(arrs, theta=0.5)
+    eng2.step(3)
+    ref2.step(3)
+    _assert_state_equal(eng2, ref2)
+
+
 @pytest.mark.parametrize("n", [0, 1, 2])
 def test_tiny_and_empty(n):
     arrs = tuple(a[:n] for a in scenes.uniform(4, 2.0, seed=1))
@@ -286,8 +318,8 @@ def test_physics_engine_mirror_preserves_body_identity():
 
 def test_fast_math_sequences_exact():
     """The traversal's reduced sqrt / seeded-reciprocal sequences (traverse.hip) equal IEEE
-    sqrt, 1.0/sqrt and 1.0/x bit-for-bit on 2^26 operands across the fast-path range."""
-    assert bh_amd.selftest_fast_math(1 << 26, seed=20261015) == 0
+    sqrt, 1.0/sqrt and 1.0/x bit-for-bit on 2^30 operands across the fast-path range."""
+    assert bh_amd.selftest_fast_math(1 << 30, seed=20261015) == 0
 
 
 def _theta0_mixed_scene():
