@@ -87,10 +87,11 @@ __device__ __forceinline__ void sum_tile(const double4_t *s_rec, int cnt, double
         for (int u = 0; u < U; ++u) {
             const bool other = (uint32_t)__double_as_longlong(r[u].w) != self;  // BHA:219
             if (FAST) {
-                // self-skip without a branch: the own leaf enters with mass +0.0, so its term
-                // is an exact +-0.0 and fx, fy (never -0.0) are unchanged -- valid because the
-                // fast path guarantees finite Gm and r2 >= soft2 > 0
-                pair_force<true>(r[u].x, r[u].y, other ? r[u].z : 0.0, bx, by, Gm, soft2, fx, fy);
+                // no self-skip at all: the own leaf has dx = dy = +0.0, so its term is an exact
+                // +-0.0 and fx, fy (never -0.0) are unchanged -- valid because the fast path
+                // guarantees a finite f for it (fastmath.hpp, lane_self_ok) and r2 >= soft2 > 0
+                (void)other;
+                pair_force<true>(r[u].x, r[u].y, r[u].z, bx, by, Gm, soft2, fx, fy);
             } else if (other) {
                 pair_force<false>(r[u].x, r[u].y, r[u].z, bx, by, Gm, soft2, fx, fy);
             }
@@ -100,7 +101,7 @@ __device__ __forceinline__ void sum_tile(const double4_t *s_rec, int cnt, double
         const double4_t r = s_rec[j];
         const bool other = (uint32_t)__double_as_longlong(r.w) != self;
         if (FAST)
-            pair_force<true>(r.x, r.y, other ? r.z : 0.0, bx, by, Gm, soft2, fx, fy);
+            pair_force<true>(r.x, r.y, r.z, bx, by, Gm, soft2, fx, fy);
         else if (other)
             pair_force<false>(r.x, r.y, r.z, bx, by, Gm, soft2, fx, fy);
     }
@@ -121,7 +122,7 @@ __global__ __launch_bounds__(TB) void k_direct(LeafList L, const uint32_t *__res
     const double Gm = G * bm;  // (Config.G * b.m) first (BHA:256)
     const uint32_t self = valid ? (uint32_t)p : 0xFFFFFFFFu;
     const bool fast =
-        __ballot(valid && !(lane_fast_ok(bx, by, soft2) && __builtin_isfinite(Gm))) == 0ull;
+        __ballot(valid && !(lane_fast_ok(bx, by, soft2) && lane_self_ok(Gm, bm))) == 0ull;
     const uint32_t nl = *d_count;
     double fx = 0.0, fy = 0.0;
     for (uint32_t t0 = 0; t0 < nl; t0 += TILE) {

@@ -70,6 +70,15 @@ __device__ __forceinline__ double rcp_rn_inrange(double b) {
 // body is finite with |x|, |y| < 2^250 and soft2 is in [2^-600, 2^500], every dist2 of the
 // traversal is in [soft2, 2^503] and both sqrt and the reciprocals stay in the range where
 // sqrt_rn_inrange / rcp_rn_inrange equal the full IEEE sequences.
+// Self term.  In the fast path a body's own leaf is not excluded: its dx = dy = +0.0 exactly
+// (the leaf holds the body's own position), so the term is f * (+-0) * invR = +-0 with f and
+// invR finite, and adding +-0 leaves the running sum unchanged (the sum starts at +0.0 and can
+// never become -0.0) -- the reference's identity skip (BHA:219) without a compare or select.
+// lane_self_ok() bounds |G m_b * m_b / soft2| < 2^1000 so that f is finite for that term.
+__device__ __forceinline__ bool lane_self_ok(double Gm, double bm) {
+    return __builtin_fabs(Gm * bm) < 0x1p400;
+}
+
 __device__ __forceinline__ bool lane_fast_ok(double bx, double by, double soft2) {
     return __builtin_fabs(bx) < 0x1p250 && __builtin_fabs(by) < 0x1p250 && soft2 >= 0x1p-600 &&
            soft2 <= 0x1p500;

@@ -76,7 +76,9 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
         const double d2 = dx * dx + dy * dy + soft2;
         uint64_t contrib_m, open_m;  // lanes that take / open this node
         if (meta & NODE_LEAF) {  // BHA:217-221: skip self by identity
-            contrib_m = act_m & __builtin_amdgcn_ballot_w64((meta & NODE_BODY_MASK) != self);
+            // fast path: the own leaf's term is an exact +-0 (fastmath.hpp, lane_self_ok)
+            contrib_m = FAST ? act_m
+                             : act_m & __builtin_amdgcn_ballot_w64((meta & NODE_BODY_MASK) != self);
             open_m = 0;
         } else {
             // s2 = (h_d * 2.0)^2 with h_d = h_0 / 2^d exactly, so s2 = s2_0 * 4^-d exactly
@@ -135,7 +137,8 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     // lane is active for node `cur` iff cur >= resume; invalid lanes never are.
     const uint32_t resume = valid ? 0u : 0xFFFFFFFFu;
     const uint32_t T = __builtin_amdgcn_readfirstlane(*d_T);
-    const bool fast = __ballot(valid && !lane_fast_ok(bx, by, soft2)) == 0ull;
+    const bool fast =
+        __ballot(valid && !(lane_fast_ok(bx, by, soft2) && lane_self_ok(Gm, bm))) == 0ull;
     if (fast)
         walk<true, COUNT>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx, fy, nvis,
                           niters);
