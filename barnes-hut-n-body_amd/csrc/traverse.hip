@@ -49,9 +49,10 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
     double s2root_v;
     asm volatile("v_mov_b64 %0, %1" : "=v"(s2root_v) : "s"(s2root));
     uint32_t cur = 0;
-    u32x8 rec = nload(nodes);  // T >= 1 whenever the loop runs
-    nwait(rec);
-    while (cur < T) {
+    // one iteration on record `rec`; the next record is requested into `nrec`.  The loop body
+    // is unrolled twice with the two records swapping roles (no SGPR copies per iteration).
+    // Loading node T (past the last one) is harmless: the node array has slack beyond T.
+    auto iter = [&](const u32x8 &rec, u32x8 &nrec) __attribute__((always_inline)) {
         const double comX = as_f64(rec[0], rec[1]), comY = as_f64(rec[2], rec[3]);
         const double mass = as_f64(rec[4], rec[5]);
         uint32_t meta = rec[7];
@@ -60,10 +61,9 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
         next = next > cur ? next : cur + 1;  // structural guard: the cursor always advances
         if (meta & NODE_SKIP) {              // mass == 0.0 (BHA:216), uniform
             cur = next;
-            u32x8 nrec = nload(nodes + (cur < T ? cur : 0u));
+            nrec = nload(nodes + cur);
             nwait(nrec);
-            rec = nrec;
-            continue;
+            return;
         }
         // lane masks in SGPRs straight from the compares; per-lane booleans via inverse ballot
         const uint64_t act_m = __builtin_amdgcn_ballot_w64(cur >= resume);
@@ -90,7 +90,7 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
             open_m = act_m & ~acc_m;
         }
         const uint32_t ncur = open_m != 0ull ? cur + 1 : next;  // descend iff some lane opened
-        u32x8 nrec = nload(nodes + (ncur < T ? ncur : 0u));
+        nrec = nload(nodes + ncur);
         if (__builtin_amdgcn_inverse_ballot_w64(contrib_m)) {  // BHA:250-259, order as written
             double invR, invR2;
             if (FAST) {
@@ -108,8 +108,14 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
             resume = next;
         }
         nwait(nrec);
-        rec = nrec;
         cur = ncur;
+    };
+    u32x8 r0 = nload(nodes), r1;  // T >= 1 whenever the loop runs
+    nwait(r0);
+    while (cur < T) {
+        iter(r0, r1);
+        if (cur >= T) break;
+        iter(r1, r0);
     }
 }
 
