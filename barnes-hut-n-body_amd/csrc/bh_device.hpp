@@ -139,9 +139,11 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
 
 // ---- launchers (traverse.hip) ----------------------------------------------------
 // Accelerations F/m of slots [lo, hi), written interleaved to a2[2p], a2[2p+1].
-void traverse(const Node *nodes, const uint32_t *d_T, const double *x, const double *y,
-              const double *m, int64_t lo, int64_t hi, const Geometry &g, const ForceParams &fp,
-              double *a2, uint32_t *visits, uint32_t *wave_iters, hipStream_t s);
+// node_cap: allocated node records (reads may run up to one record past the tree's last one).
+void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, const double *x,
+              const double *y, const double *m, int64_t lo, int64_t hi, const Geometry &g,
+              const ForceParams &fp, double *a2, uint32_t *visits, uint32_t *wave_iters,
+              hipStream_t s);
 // ranks' Morton ranges are whole wavefronts (bh_shard_range)
 __host__ __device__ inline int64_t shard_chunk(int64_t n, int world) {
     const int64_t c = (n + world - 1) / world;

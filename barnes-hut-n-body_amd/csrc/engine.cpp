@@ -366,7 +366,7 @@ int evaluate(bh_engine *e, uint32_t *visits) {
         return BH_OK;
     }
     if (!e->comm || visits) {
-        traverse(e->nodes, d_T, e->st.x, e->st.y, e->st.m, 0, n, e->geo, fp, e->a2, visits,
+        traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, 0, n, e->geo, fp, e->a2, visits,
                  e->wave_iters, e->stream);
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
@@ -374,7 +374,7 @@ int evaluate(bh_engine *e, uint32_t *visits) {
         const int64_t chunk = shard_chunk(n, e->world);
         int64_t lo = 0, hi = 0;
         bh_shard_range(n, e->rank, e->world, &lo, &hi);
-        traverse(e->nodes, d_T, e->st.x, e->st.y, e->st.m, lo, hi, e->geo, fp, e->a2, nullptr,
+        traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, lo, hi, e->geo, fp, e->a2, nullptr,
                  nullptr, e->stream);
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));

@@ -35,12 +35,19 @@ __device__ __forceinline__ u32x8 nload(const Node *p) {
     asm volatile("s_load_dwordx8 %0, %1, 0x0" : "=s"(v) : "s"(p) : "memory");
     return v;
 }
+// Same, addressed as base + 32-bit byte offset (s_load's SGPR offset): one shift per
+// iteration instead of a 64-bit address computation.  Only for node arrays below 4 GiB.
+__device__ __forceinline__ u32x8 nload_off(const Node *base, uint32_t idx) {
+    u32x8 v;
+    asm volatile("s_load_dwordx8 %0, %1, %2" : "=s"(v) : "s"(base), "s"(idx << 5) : "memory");
+    return v;
+}
 __device__ __forceinline__ void nwait(u32x8 &v) { asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(v)); }
 __device__ __forceinline__ double as_f64(uint32_t lo, uint32_t hi) {
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
-template <bool FAST, bool COUNT>
+template <bool FAST, bool COUNT, bool OFF32>
 __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T, double bx,
                                      double by, double Gm, double soft2, double theta2,
                                      double s2root, uint32_t self, uint32_t resume, double &fx,
@@ -59,9 +66,12 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
         asm volatile("" : "+s"(meta));  // keep the flag tests scalar (s_bitcmp)
         uint32_t next = rec[6];
         next = next > cur ? next : cur + 1;  // structural guard: the cursor always advances
-        if (meta & NODE_SKIP) {              // mass == 0.0 (BHA:216), uniform
+        // mass == 0.0 (BHA:216): not visited.  The fast path needs no test: such a node's
+        // terms are exact +-0 (mass 0, finite f) and opening it only walks massless children,
+        // so the sums are unchanged -- only the visit-counting variant must skip it.
+        if ((!FAST || COUNT) && (meta & NODE_SKIP)) {
             cur = next;
-            nrec = nload(nodes + cur);
+            nrec = OFF32 ? nload_off(nodes, cur) : nload(nodes + cur);
             nwait(nrec);
             return;
         }
@@ -90,7 +100,7 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
             open_m = act_m & ~acc_m;
         }
         const uint32_t ncur = open_m != 0ull ? cur + 1 : next;  // descend iff some lane opened
-        nrec = nload(nodes + ncur);
+        nrec = OFF32 ? nload_off(nodes, ncur) : nload(nodes + ncur);
         if (__builtin_amdgcn_inverse_ballot_w64(contrib_m)) {  // BHA:250-259, order as written
             double invR, invR2;
             if (FAST) {
@@ -119,7 +129,7 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
     }
 }
 
-template <bool COUNT>
+template <bool COUNT, bool OFF32>
 __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
                                                  const uint32_t *__restrict__ d_T,
                                                  const double *__restrict__ x,
@@ -146,11 +156,11 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     const bool fast =
         __ballot(valid && !(lane_fast_ok(bx, by, soft2) && lane_self_ok(Gm, bm))) == 0ull;
     if (fast)
-        walk<true, COUNT>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx, fy, nvis,
-                          niters);
+        walk<true, COUNT, OFF32>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx,
+                                 fy, nvis, niters);
     else
-        walk<false, COUNT>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx, fy, nvis,
-                           niters);
+        walk<false, COUNT, OFF32>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx,
+                                  fy, nvis, niters);
     if (COUNT && (threadIdx.x & 63) == 0) wave_iters[(p - lo) >> 6] = niters;
     if (!valid) return;
     // BHA:390-391, interleaved (ax, ay): coalesced 16-byte stores in Morton order
@@ -213,17 +223,29 @@ hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_ba
     return hipGetLastError();
 }
 
-void traverse(const Node *nodes, const uint32_t *d_T, const double *x, const double *y,
-              const double *m, int64_t lo, int64_t hi, const Geometry &g, const ForceParams &fp,
-              double *a2, uint32_t *visits, uint32_t *wave_iters, hipStream_t s) {
+void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, const double *x,
+              const double *y, const double *m, int64_t lo, int64_t hi, const Geometry &g,
+              const ForceParams &fp, double *a2, uint32_t *visits, uint32_t *wave_iters,
+              hipStream_t s) {
     if (hi <= lo) return;
     unsigned grid = (unsigned)((hi - lo + TB - 1) / TB);
-    if (visits)
-        k_traverse<true><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2, visits,
-                                             wave_iters);
-    else
-        k_traverse<false><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2, visits,
-                                              wave_iters);
+    // node records addressed by a 32-bit byte offset while the array stays below 4 GiB
+    const bool off32 = node_cap * sizeof(Node) < (size_t(1) << 32);
+    if (visits) {
+        if (off32)
+            k_traverse<true, true><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2,
+                                                       visits, wave_iters);
+        else
+            k_traverse<true, false><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2,
+                                                        visits, wave_iters);
+    } else {
+        if (off32)
+            k_traverse<false, true><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2,
+                                                        visits, wave_iters);
+        else
+            k_traverse<false, false><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2,
+                                                         visits, wave_iters);
+    }
 }
 
 }  // namespace bh
