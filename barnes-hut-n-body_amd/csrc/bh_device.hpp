@@ -102,10 +102,11 @@ struct __attribute__((aligned(16))) SpanSlot {
 #define BH_XCD_RUN 16
 #endif
 #ifdef __HIP__  // HIP translation units only (engine.cpp is host C++)
+template <uint32_t RUN = BH_XCD_RUN>
 __device__ __forceinline__ uint32_t xcd_block() {
     uint32_t b = blockIdx.x;
-    if (BH_XCD_RUN > 0) {
-        constexpr uint32_t C = BH_XCD_RUN, G = 8 * C;
+    if (RUN > 0) {
+        constexpr uint32_t C = RUN, G = 8 * C;
         const uint32_t full = gridDim.x / G;
         if (b < full * G) b = (b / 8 / C) * G + (b % 8) * C + (b / 8) % C;
     }

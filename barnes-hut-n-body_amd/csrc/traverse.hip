@@ -129,6 +129,13 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
     }
 }
 
+// Workgroups in runs of BH_TRAV_XCD_RUN consecutive waves per XCD (bh_device.hpp): neighbouring
+// waves walk nearly the same nodes, so a run shares its XCD's L2 (C3 -1.5 % at runs of 32..512
+// against the round-robin default).
+#ifndef BH_TRAV_XCD_RUN
+#define BH_TRAV_XCD_RUN 64
+#endif
+
 template <bool COUNT, bool OFF32>
 __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
                                                  const uint32_t *__restrict__ d_T,
@@ -139,7 +146,7 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
                                                  double *__restrict__ a2,
                                                  uint32_t *__restrict__ visits,
                                                  uint32_t *__restrict__ wave_iters) {
-    const int64_t p = lo + (int64_t)blockIdx.x * TB + threadIdx.x;
+    const int64_t p = lo + (int64_t)xcd_block<BH_TRAV_XCD_RUN>() * TB + threadIdx.x;
     const bool valid = p < hi;
     const double bx = valid ? x[p] : 0.0;
     const double by = valid ? y[p] : 0.0;

@@ -704,9 +704,10 @@ __global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__r
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < span_stride; i += gridDim.x * TB) {
         const size_t slot = (size_t)L * span_stride + i;
         const uint32_t e = span_list[slot];
+        if (e == NO_SPAN) continue;  // empty slot: never read
         const uint32_t ni = e & ~SPAN_SUPER;
         SpanSlot out;
-        const uint32_t end = e != NO_SPAN ? nodes[ni].next : 0u;  // empty slot: no children
+        const uint32_t end = nodes[ni].next;
         uint32_t c = ni + 1;
         for (int k = 0; k < 4; ++k) {
             out.ch[k] = 0xFFFFFFFFu;
@@ -734,9 +735,10 @@ __global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__r
 // Chunk-spanning nodes, levels J..0: workgroup g owns the chunk boundaries
 // [g*SPAN_GROUP, (g+1)*SPAN_GROUP), thread = boundary, and finishes the span nodes that do
 // not cross a group boundary (their span children are then in the same group).  The previous
-// level's results live in LDS (a span child is referenced by its owner slot); each level's
-// records are loaded one level ahead; stores to global stay in flight across the LDS-only
-// barriers.
+// level's results live in LDS (a span child is referenced by its owner slot).  A thread first
+// reads its whole span_list column (one latency) into a bit mask of the levels it owns a node
+// at -- deep levels are mostly empty -- and then loads only those records, two levels ahead;
+// stores to global stay in flight across the LDS-only barriers.
 constexpr int SPAN_TB = SPAN_GROUP;
 
 struct SpanRegs {
@@ -766,14 +768,23 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span(int J, const uint32_t *__r
     const uint32_t g0 = blockIdx.x * SPAN_GROUP;
     const uint32_t kl = threadIdx.x, k = g0 + kl;
     const bool valid = k < span_stride;
-    const uint32_t kk = valid ? k : g0;  // threads past the table mirror the group's first slot
-    SpanRegs A;
-    load_span(A, span_list, span_children, (size_t)J * span_stride + kk);
-    for (int L = J; L >= 0; --L) {
+    // levels (bit L) at which this boundary owns a node finished here (not group-crossing)
+    uint64_t own = 0;
+    if (valid) {
+#pragma unroll 8
+        for (int L = 0; L <= J; ++L) {
+            const uint32_t e = span_list[(size_t)L * span_stride + k];
+            if (e != NO_SPAN && !(e & SPAN_SUPER)) own |= 1ull << L;
+        }
+    }
+    auto fetch = [&](SpanRegs &r, int L) __attribute__((always_inline)) {
+        r.ni = NO_SPAN;
+        if (L >= 0 && ((own >> L) & 1ull))
+            load_span(r, span_list, span_children, (size_t)L * span_stride + k);
+    };
+    auto level = [&](const SpanRegs &C, int L) __attribute__((always_inline)) {
         const int cur = L & 1, prev = cur ^ 1;
-        const SpanRegs C = A;
-        if (L > 0) load_span(A, span_list, span_children, (size_t)(L - 1) * span_stride + kk);
-        if (valid && C.ni != NO_SPAN && !(C.ni & SPAN_SUPER)) {
+        if (C.ni != NO_SPAN) {
             double mSum = 0.0, cx = 0.0, cy = 0.0;  // children 0..3 in order (BHA:189-192)
 #pragma unroll
             for (int c = 0; c < 4; ++c) {
@@ -807,6 +818,18 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span(int J, const uint32_t *__r
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): LDS results visible; stores fly on
         __builtin_amdgcn_s_barrier();
+    };
+    // a span child always sits one level below its parent and is owned by a boundary of the
+    // same group, so the level pass needs no other synchronisation
+    SpanRegs P, Q;
+    fetch(P, J);
+    fetch(Q, J - 1);
+    for (int L = J; L >= 0; L -= 2) {
+        level(P, L);
+        fetch(P, L - 2);
+        if (L == 0) break;
+        level(Q, L - 1);
+        fetch(Q, L - 3);
     }
 }
 
