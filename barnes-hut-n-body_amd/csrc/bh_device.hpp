@@ -52,6 +52,13 @@ __host__ __device__ inline uint32_t span_groups(uint32_t span_stride) {
     return (span_stride + 1023) / 1024;
 }
 
+// Adaptive bucket sort (tree_build.hip): splitter spacing of the previous build's sorted
+// order = the expected bucket size.
+constexpr int SORT_B = 1024;
+__host__ __device__ inline uint32_t sort_buckets(int64_t n) {
+    return (uint32_t)((n + SORT_B - 1) / SORT_B);
+}
+
 // Cell-start table: first sorted body of every depth-D0 cell, so the end of any node at
 // depth <= D0 is one load, and deeper searches stay inside one depth-D0 cell.
 constexpr int CELL_TABLE_MAX_DEPTH = 8;
@@ -132,6 +139,11 @@ struct TreeBuffers {
     uint32_t *super_list;  // [(J + 1) * span_groups]: group-crossing span node per (level, group)
     void *cub_tmp;
     size_t cub_bytes;
+    // adaptive bucket sort: splitters of the previous build (spl_nb of them, 0 = none: rocprim
+    // sort), bucket counts (kept zeroed between builds) and starts, sort_buckets(cap) + 2 each
+    uint64_t *spl;
+    uint32_t spl_nb;
+    uint32_t *bcount, *bstart;
 };
 
 int cell_table_depth(int J, int64_t n);

@@ -86,6 +86,11 @@ struct bh_engine {
     void *cub_tmp = nullptr;
     size_t cub_bytes = 0;
 
+    // adaptive bucket sort (tree_build.hip): splitters written by every build
+    uint64_t *spl = nullptr;
+    uint32_t *bcount = nullptr, *bstart = nullptr;
+    uint32_t spl_nb = 0;  // splitters of the last build; 0 = none (next build sorts with rocprim)
+
     // theta = 0 all-pairs path (direct.hip), allocated on first use
     uint8_t *leaf_flags = nullptr;
     uint32_t *leaf_sel = nullptr, *leaf_count = nullptr;
@@ -220,6 +225,11 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(dev_alloc(e, e->heavy, cap));
         TRY(dev_alloc(e, e->keep, cap));
         TRY(dev_alloc(e, e->pos, cap));
+        TRY(dev_alloc(e, e->spl, (size_t)sort_buckets(cap) + 2));
+        TRY(dev_alloc(e, e->bcount, (size_t)sort_buckets(cap) + 2));
+        TRY(dev_alloc(e, e->bstart, (size_t)sort_buckets(cap) + 2));
+        HIPCHK(e, hipMemset(e->bcount, 0, sizeof(uint32_t) * ((size_t)sort_buckets(cap) + 2)));
+        e->spl_nb = 0;
         e->cap = cap;
     }
     size_t ncap = node_capacity(e->cap, J);
@@ -266,6 +276,10 @@ TreeBuffers tree_buffers(bh_engine *e) {
     b.super_list = e->super_list;
     b.cub_tmp = e->cub_tmp;
     b.cub_bytes = e->cub_bytes;
+    b.spl = e->spl;
+    b.spl_nb = e->spl_nb;
+    b.bcount = e->bcount;
+    b.bstart = e->bstart;
     return b;
 }
 
@@ -310,6 +324,7 @@ int collect_timings(bh_engine *e) {
 int build(bh_engine *e) {
     const int64_t n = e->n;
     HIPCHK(e, tree_build(tree_buffers(e), n, e->geo, e->stream));
+    e->spl_nb = sort_buckets(n);  // k_prep wrote this build's splitters
     if (n > 0) std::swap(e->st, e->alt);
     e->tree_valid = true;
     return BH_OK;
@@ -674,7 +689,7 @@ void bh_destroy(bh_engine *e) {
                     e->span_children, e->scalars, e->visits32, e->wave_iters, e->heavy, e->keep,
                     e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->mbits, e->mslot, e->cub_tmp,
                     e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaves.xy, e->leaves.m,
-                    e->leaves.slot, e->leaf_tmp};
+                    e->leaves.slot, e->leaf_tmp, e->spl, e->bcount, e->bstart};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     for (hipEvent_t ev : e->ev) (void)hipEventDestroy(ev);
@@ -697,6 +712,7 @@ int bh_set_params(bh_engine *e, const bh_params *p) {
     if (geo_changed) {
         e->geo = g;
         e->tree_valid = false;
+        e->spl_nb = 0;  // keys change meaning
         if (g.J != e->J_alloc) {  // tree workspace sized for another depth; the state stays
             HIPCHK(e, hipStreamSynchronize(e->stream));
             TRY(ensure_capacity(e, e->n));
@@ -735,6 +751,7 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     e->heavy_possible = true;
     e->removed.clear();
     e->tree_valid = false;  // BHA:348
+    e->spl_nb = 0;          // other bodies: the first build sorts from scratch
     return BH_OK;
 }
 

@@ -82,7 +82,184 @@ __global__ __launch_bounds__(TB) void k_morton(int64_t n, const double *__restri
     }
     keys[i] = key;
     keys32[i] = (uint32_t)(key >> key32_shift(g.J));  // the sort key: top 32 of 2J+1 bits
-    idx[i] = (uint32_t)i;
+    if (idx) idx[i] = (uint32_t)i;  // rocprim path only (the bucket sort uses the slot itself)
+}
+
+// ---- adaptive bucket sort of the 32-bit key prefixes -----------------------------------
+// The state is kept in the Morton order of the previous build, so this build's keys arrive
+// nearly sorted: bodies drift a few depth-16 cells per step, a few cross a high-level cell
+// boundary and jump far in the order.  The previous build's sorted order supplies splitters:
+// spl[t] = (key32 << 32 | slot) of its sorted position t * SORT_B, a sorted sequence of
+// composites.  Sorting by the composite (key32, slot) IS the stable sort of key32 (ties in
+// slot order), so buckets [spl[t], spl[t+1]) partition it exactly whatever the bucket sizes
+// are, and each bucket is sorted on its own:
+//   k_bucket_count    bucket of every element (galloping from its old position's bucket),
+//                     wave-aggregated atomic count -> offset inside the bucket
+//   exclusive scan    bucket starts
+//   k_bucket_scatter  composites to their bucket's range (any order inside it)
+//   k_bucket_sort     one workgroup per bucket: bitonic sort in LDS (global memory for a
+//                     bucket above SORT_CAP -- correct, slow, never seen in smooth evolution),
+//                     then keys32_s, perm and the full keys keys_s = keys[perm]
+// Splitters are (re)written by k_prep of every build; the first build after a reset uses
+// rocprim (the splitters would describe other bodies).
+constexpr int SORT_TB = 256;
+constexpr int SORT_CAP = 4096;  // LDS bucket capacity (32 KB of composites)
+
+__device__ __forceinline__ bool spl_le(const uint64_t *__restrict__ spl, uint32_t t, uint64_t v) {
+    return t == 0 || spl[t] <= v;  // spl[0] acts as -infinity: bucket 0 takes everything below
+}
+
+// largest t in [0, nb) with spl[t] <= v, galloping from `guess`
+__device__ uint32_t find_bucket(const uint64_t *__restrict__ spl, uint32_t nb, uint64_t v,
+                                uint32_t guess) {
+    uint32_t t = min(guess, nb - 1);
+    uint32_t lo, hi;  // spl_le(lo) holds; hi == nb or !spl_le(hi)
+    if (spl_le(spl, t, v)) {
+        lo = t;
+        uint32_t step = 1;
+        for (;;) {
+            const uint32_t j = lo + step;
+            if (j >= nb) {
+                hi = nb;
+                break;
+            }
+            if (!spl_le(spl, j, v)) {
+                hi = j;
+                break;
+            }
+            lo = j;
+            step <<= 1;
+        }
+    } else {  // t > 0
+        hi = t;
+        uint32_t step = 1;
+        for (;;) {
+            if (step >= hi) {
+                lo = 0;
+                break;
+            }
+            const uint32_t j = hi - step;
+            if (spl_le(spl, j, v)) {
+                lo = j;
+                break;
+            }
+            hi = j;
+            step <<= 1;
+        }
+    }
+    while (hi - lo > 1) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        if (spl_le(spl, mid, v)) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+__global__ __launch_bounds__(SORT_TB) void k_bucket_count(int64_t n,
+                                                          const uint32_t *__restrict__ keys32,
+                                                          const uint64_t *__restrict__ spl,
+                                                          uint32_t nb, uint32_t *__restrict__ bkt,
+                                                          uint32_t *__restrict__ off,
+                                                          uint32_t *__restrict__ counts) {
+    const int64_t i = (int64_t)blockIdx.x * SORT_TB + threadIdx.x;
+    const bool valid = i < n;
+    uint32_t b = 0;
+    if (valid) {
+        const uint64_t v = ((uint64_t)keys32[i] << 32) | (uint64_t)i;
+        b = find_bucket(spl, nb, v, (uint32_t)(i / SORT_B));
+    }
+    // one atomic per distinct bucket of the wave (usually one): offsets in lane order
+    uint64_t todo = __ballot(valid);
+    uint32_t myoff = 0;
+    while (todo) {
+        const int leader = __builtin_ctzll(todo);
+        const uint32_t bl = __builtin_amdgcn_readlane(b, leader);
+        const uint64_t same = __ballot(valid && b == bl);
+        uint32_t o = 0;
+        if ((int)__lane_id() == leader) o = atomicAdd(&counts[bl], (uint32_t)__popcll(same));
+        o = __builtin_amdgcn_readlane(o, leader);
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(same >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)same, 0u));
+        if (valid && b == bl) myoff = o + below;
+        todo &= ~same;
+    }
+    if (valid) {
+        bkt[i] = b;
+        off[i] = myoff;
+    }
+}
+
+__global__ __launch_bounds__(SORT_TB) void k_bucket_scatter(int64_t n,
+                                                            const uint32_t *__restrict__ keys32,
+                                                            const uint32_t *__restrict__ bkt,
+                                                            const uint32_t *__restrict__ off,
+                                                            const uint32_t *__restrict__ starts,
+                                                            uint64_t *__restrict__ comp) {
+    const int64_t i = (int64_t)blockIdx.x * SORT_TB + threadIdx.x;
+    if (i >= n) return;
+    comp[starts[bkt[i]] + off[i]] = ((uint64_t)keys32[i] << 32) | (uint64_t)i;
+}
+
+// Bitonic network in its all-ascending form (the first step of every merge compares mirrored
+// pairs): a comparator never moves the larger value down, so the elements past `s` can stay
+// virtual +infinity -- sizes need no padding.  `A` is LDS or global memory of this workgroup.
+template <typename Sync>
+__device__ __forceinline__ void bitonic_sort(uint64_t *A, uint32_t s, Sync sync) {
+    uint32_t P = 1;
+    while (P < s) P <<= 1;
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t q = threadIdx.x; q < (P >> 1); q += SORT_TB) {
+                const uint32_t lo = (q / j) * 2 * j + (q % j);
+                const uint32_t hi = (j == (k >> 1)) ? (lo ^ (k - 1)) : lo + j;
+                if (hi < s) {
+                    const uint64_t a = A[lo], c = A[hi];
+                    if (c < a) {
+                        A[lo] = c;
+                        A[hi] = a;
+                    }
+                }
+            }
+            sync();
+        }
+    }
+}
+
+__global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restrict__ starts,
+                                                         uint32_t *__restrict__ counts,
+                                                         uint64_t *comp,
+                                                         const uint64_t *__restrict__ keys,
+                                                         uint32_t *__restrict__ keys32_s,
+                                                         uint32_t *__restrict__ perm,
+                                                         uint64_t *keys_s) {
+    __shared__ uint64_t L[SORT_CAP];
+    const uint32_t t = blockIdx.x;
+    const uint32_t b0 = starts[t], s = starts[t + 1] - b0;
+    if (threadIdx.x == 0) counts[t] = 0;  // ready for the next build (counts were scanned)
+    if (s <= (uint32_t)SORT_CAP) {
+        for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) L[j] = comp[b0 + j];
+        __syncthreads();
+        bitonic_sort(L, s, [] { __syncthreads(); });
+        for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) {
+            const uint64_t v = L[j];
+            const uint32_t src = (uint32_t)v;
+            keys32_s[b0 + j] = (uint32_t)(v >> 32);
+            perm[b0 + j] = src;
+            keys_s[b0 + j] = keys[src];  // comp and keys_s share storage: L holds the bucket
+        }
+    } else {  // oversized bucket: the same network on global memory, in place
+        uint64_t *A = comp + b0;
+        bitonic_sort(A, s, [] {
+            __threadfence_block();
+            __syncthreads();
+        });
+        for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) {  // each thread its own j: in place
+            const uint64_t v = A[j];
+            const uint32_t src = (uint32_t)v;
+            keys32_s[b0 + j] = (uint32_t)(v >> 32);
+            perm[b0 + j] = src;
+            keys_s[b0 + j] = keys[src];
+        }
+    }
 }
 
 // After the 32-bit-prefix sort: keys_s = keys[perm] (k_key_gather), then every run of equal
@@ -125,7 +302,8 @@ __global__ __launch_bounds__(TB) void k_key_fixup(int64_t n, int J,
 __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *__restrict__ keys_s,
                                              const uint32_t *__restrict__ perm, BodyState src,
                                              BodyState dst, int8_t *__restrict__ cpl,
-                                             uint32_t *__restrict__ cnt) {
+                                             uint32_t *__restrict__ cnt,
+                                             uint64_t *__restrict__ spl) {
     int64_t a = (int64_t)xcd_block() * TB + threadIdx.x;
     if (a > n) return;
     if (a == n) {
@@ -135,6 +313,8 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
     const uint64_t SENT = sentinel_key(J);
     uint64_t k = keys_s[a];
     uint32_t i = perm[a];  // nearly the identity: the state is kept in the last Morton order
+    if ((a & (SORT_B - 1)) == 0)  // splitters of the next build's bucket sort
+        spl[a / SORT_B] = ((k >> key32_shift(J)) << 32) | (uint64_t)a;
     dst.x[a] = src.x[i];
     dst.y[a] = src.y[i];
     dst.vx[a] = src.vx[i];
@@ -910,15 +1090,29 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     if (n <= 0) return hipMemsetAsync(b.base, 0, sizeof(uint32_t), s);
     hipError_t st;
     const int D0 = cell_table_depth(g.J, n);
+    const bool bucket = b.spl_nb > 0;
     k_morton<<<grid_for(n), TB, 0, s>>>(n, b.src.x, b.src.y, b.src.cidx, g, b.keys, b.keys32,
-                                        b.idx);
+                                        bucket ? nullptr : b.idx);
     size_t bytes = b.cub_bytes;
-    st = rocprim::radix_sort_pairs<SortConfig>(b.cub_tmp, bytes, b.keys32, b.keys32_s, b.idx,
-                                               b.perm, (size_t)n, 0u, 32u, s);
-    if (st != hipSuccess) return st;
-    k_key_gather<<<grid_for(n), TB, 0, s>>>(n, b.keys, b.perm, b.keys_s);
+    if (bucket) {  // bucket ids / offsets live in cnt / base until k_prep needs them
+        const unsigned sg = (unsigned)((n + SORT_TB - 1) / SORT_TB);
+        k_bucket_count<<<sg, SORT_TB, 0, s>>>(n, b.keys32, b.spl, b.spl_nb, b.cnt, b.base,
+                                              b.bcount);
+        st = hipcub::DeviceScan::ExclusiveSum(b.cub_tmp, bytes, b.bcount, b.bstart,
+                                              (int)b.spl_nb + 1, s);
+        if (st != hipSuccess) return st;
+        k_bucket_scatter<<<sg, SORT_TB, 0, s>>>(n, b.keys32, b.cnt, b.base, b.bstart, b.keys_s);
+        k_bucket_sort<<<b.spl_nb, SORT_TB, 0, s>>>(b.bstart, b.bcount, b.keys_s, b.keys,
+                                                   b.keys32_s, b.perm, b.keys_s);
+    } else {
+        st = rocprim::radix_sort_pairs<SortConfig>(b.cub_tmp, bytes, b.keys32, b.keys32_s, b.idx,
+                                                   b.perm, (size_t)n, 0u, 32u, s);
+        if (st != hipSuccess) return st;
+        k_key_gather<<<grid_for(n), TB, 0, s>>>(n, b.keys, b.perm, b.keys_s);
+    }
     k_key_fixup<<<grid_for(n), TB, 0, s>>>(n, g.J, b.keys32_s, b.keys_s, b.perm);
-    k_prep<<<grid_for(n + 1), TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.src, b.dst, b.cpl, b.cnt);
+    k_prep<<<grid_for(n + 1), TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.src, b.dst, b.cpl, b.cnt,
+                                          b.spl);
     bytes = b.cub_bytes;
     st = hipcub::DeviceScan::ExclusiveSum(b.cub_tmp, bytes, b.cnt, b.base, (int)(n + 1), s);
     if (st != hipSuccess) return st;
