@@ -53,8 +53,12 @@ __host__ __device__ inline uint32_t span_groups(uint32_t span_stride) {
 }
 
 // Adaptive bucket sort (tree_build.hip): splitter spacing of the previous build's sorted
-// order = the expected bucket size.
-constexpr int SORT_B = 1024;
+// order = the expected bucket size (896, so that drift rarely pushes a bucket past the
+// 1024-element network, measured within noise at C3 and C4).
+#ifndef BH_SORT_B
+#define BH_SORT_B 1024
+#endif
+constexpr int SORT_B = BH_SORT_B;
 __host__ __device__ inline uint32_t sort_buckets(int64_t n) {
     return (uint32_t)((n + SORT_B - 1) / SORT_B);
 }

@@ -163,9 +163,16 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_count(int64_t n,
     const int64_t i = (int64_t)blockIdx.x * SORT_TB + threadIdx.x;
     const bool valid = i < n;
     uint32_t b = 0;
+    // the wave's old bucket t (its first lane's) and its bounds through scalar loads: most
+    // elements are still inside it; the others gallop
+    const int64_t i0 = (int64_t)blockIdx.x * SORT_TB + (threadIdx.x & ~63u);
+    const uint32_t t = __builtin_amdgcn_readfirstlane(min((uint32_t)(i0 / SORT_B), nb - 1));
+    const uint64_t lo_s = t == 0 ? 0ull : spl[t];
+    const uint64_t hi_s = t + 1 < nb ? spl[t + 1] : ~0ull;
     if (valid) {
         const uint64_t v = ((uint64_t)keys32[i] << 32) | (uint64_t)i;
-        b = find_bucket(spl, nb, v, (uint32_t)(i / SORT_B));
+        if (lo_s <= v && (v < hi_s || t + 1 == nb)) b = t;
+        else b = find_bucket(spl, nb, v, (uint32_t)(i / SORT_B));
     }
     // one atomic per distinct bucket of the wave (usually one): offsets in lane order
     uint64_t todo = __ballot(valid);
@@ -202,15 +209,20 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_scatter(int64_t n,
 // Bitonic network in its all-ascending form (the first step of every merge compares mirrored
 // pairs): a comparator never moves the larger value down, so the elements past `s` can stay
 // virtual +infinity -- sizes need no padding.  `A` is LDS or global memory of this workgroup.
-template <typename Sync>
-__device__ __forceinline__ void bitonic_sort(uint64_t *A, uint32_t s, Sync sync) {
-    uint32_t P = 1;
-    while (P < s) P <<= 1;
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t q = threadIdx.x; q < (P >> 1); q += SORT_TB) {
-                const uint32_t lo = (q / j) * 2 * j + (q % j);
-                const uint32_t hi = (j == (k >> 1)) ? (lo ^ (k - 1)) : lo + j;
+// (Measured at C4: batching a stage's loads, and skipping the barrier between stages whose
+// pairs stay inside one wave's 128-element block, were both slower than this plain form.)
+template <bool LDS>
+__device__ __forceinline__ void bitonic_sort(uint64_t *A, uint32_t s) {
+    int lP = 0;
+    while ((1u << lP) < s) ++lP;
+    const uint32_t half = (1u << lP) >> 1;
+    for (int lk = 1; lk <= lP; ++lk) {
+        for (int lj = lk - 1; lj >= 0; --lj) {
+            const uint32_t j = 1u << lj;
+            const uint32_t flip = lj == lk - 1 ? (1u << lk) - 1 : 0u;  // mirrored partner
+            for (uint32_t q = threadIdx.x; q < half; q += SORT_TB) {
+                const uint32_t lo = ((q >> lj) << (lj + 1)) | (q & (j - 1));  // bit lj clear
+                const uint32_t hi = flip ? (lo ^ flip) : (lo | j);
                 if (hi < s) {
                     const uint64_t a = A[lo], c = A[hi];
                     if (c < a) {
@@ -219,7 +231,8 @@ __device__ __forceinline__ void bitonic_sort(uint64_t *A, uint32_t s, Sync sync)
                     }
                 }
             }
-            sync();
+            if (!LDS) __threadfence_block();
+            __syncthreads();
         }
     }
 }
@@ -238,7 +251,8 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
     if (s <= (uint32_t)SORT_CAP) {
         for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) L[j] = comp[b0 + j];
         __syncthreads();
-        bitonic_sort(L, s, [] { __syncthreads(); });
+        bitonic_sort<true>(L, s);
+        __syncthreads();
         for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) {
             const uint64_t v = L[j];
             const uint32_t src = (uint32_t)v;
@@ -248,10 +262,7 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
         }
     } else {  // oversized bucket: the same network on global memory, in place
         uint64_t *A = comp + b0;
-        bitonic_sort(A, s, [] {
-            __threadfence_block();
-            __syncthreads();
-        });
+        bitonic_sort<false>(A, s);
         for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) {  // each thread its own j: in place
             const uint64_t v = A[j];
             const uint32_t src = (uint32_t)v;
@@ -313,7 +324,7 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
     const uint64_t SENT = sentinel_key(J);
     uint64_t k = keys_s[a];
     uint32_t i = perm[a];  // nearly the identity: the state is kept in the last Morton order
-    if ((a & (SORT_B - 1)) == 0)  // splitters of the next build's bucket sort
+    if (a % SORT_B == 0)  // splitters of the next build's bucket sort
         spl[a / SORT_B] = ((k >> key32_shift(J)) << 32) | (uint64_t)a;
     dst.x[a] = src.x[i];
     dst.y[a] = src.y[i];
