@@ -268,6 +268,41 @@ def test_c3_1e6_full_size_sampled():
     _assert_state_equal(eng, ref)
 
 
+def _assert_sampled_evaluation(arrs, theta, stride):
+    """Engine: every body's acceleration (and visit count unless theta = 0); oracle: its own
+    serial tree, then the walk of every `stride`-th body; the sampled bodies bit-identical."""
+    eng, ref = _pair(arrs, theta=theta)
+    sample = np.arange(0, len(arrs[0]), stride, dtype=np.int64)
+    if theta == 0.0:  # the all-pairs kernel (no visit counts on that path)
+        ax, ay = eng.compute_accelerations()
+        rax, ray = ref.accelerations(subset=sample)
+    else:
+        ax, ay, vis = eng.compute_accelerations(visits=True)
+        rax, ray, rvis = ref.accelerations(subset=sample, visits=True)
+        assert np.array_equal(vis[sample], rvis), "node-visit counts differ"
+    bad = np.flatnonzero(ax[sample].view(np.int64) != rax.view(np.int64))
+    assert bad.size == 0, f"ax: {bad.size} of {len(sample)} sampled bodies differ"
+    assert bits_equal(ay[sample], ray)
+    eng.close()
+    ref.close()
+
+
+def test_c4_1e7_full_size_sampled():
+    """C4 at its full size (uniform cloud, N = 1e7, theta 0.5): 4097 sampled bodies."""
+    _assert_sampled_evaluation(scenes.config_scene("c4"), 0.5, 2441)
+
+
+def test_c3x8_8e6_weak_scaling_scene_sampled():
+    """The 8-GPU weak-scaling scene (two disks, 8e6 bodies) on one GPU: 4000 sampled bodies."""
+    _assert_sampled_evaluation(scenes.config_scene("c3x8"), 0.5, 2000)
+
+
+def test_c5_full_size_theta0_sampled():
+    """C5 at its full size (N = 262 144, theta = 0, all-pairs kernel): 1024 sampled bodies,
+    each the exact direct sum over every leaf in pre-order."""
+    _assert_sampled_evaluation(scenes.config_scene("c5"), 0.0, 256)
+
+
 def test_bucket_sort_collapse_oversized_buckets():
     """A cloud whose velocities aim every body at the centre: the first drift shrinks it 50x,
     the next one flings it out again, so the previous build's splitters (the adaptive bucket
