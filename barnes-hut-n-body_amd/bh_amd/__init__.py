@@ -107,7 +107,8 @@ def load_library(path: str | None = None):
     lib.bh_synchronize.argtypes = [_VP]
     lib.bh_traversal_stats.argtypes = [_VP, _I64P, _I64P, _I64P]
     lib.bh_last_removed.argtypes = [_VP, _I64P, ctypes.c_int64, _I64P]
-    lib.bh_shard_range.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, _I64P, _I64P]
+    lib.bh_shard_range.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   _I64P, _I64P]
     lib.bh_selftest_fast_math.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, _I64P]
     _F = ctypes.POINTER(ctypes.c_float)
     lib.bh_nbody3d_create.argtypes = [ctypes.c_int, ctypes.POINTER(_VP)]
@@ -147,12 +148,17 @@ def default_params(**over) -> BhParams:
     return p
 
 
-def shard_range(n: int, rank: int, world: int):
-    """Morton-order range [lo, hi) of bodies whose forces `rank` evaluates (bh_shard_range)."""
+SHARD_ROUNDS = 4  # BH_SHARD_ROUNDS (include/bh_engine.h)
+
+
+def shard_range(n: int, rank: int, world: int, round: int = 0):
+    """Morton-order piece [lo, hi) of bodies whose forces `rank` evaluates in round `round`
+    of a multi-GPU evaluation (bh_shard_range); pieces of round k sit at
+    [(k * world + r) * sub, + sub), so round k's all-gather is in place."""
     lo = ctypes.c_int64(0)
     hi = ctypes.c_int64(0)
-    rc = load_library().bh_shard_range(int(n), int(rank), int(world), ctypes.byref(lo),
-                                       ctypes.byref(hi))
+    rc = load_library().bh_shard_range(int(n), int(rank), int(world), int(round),
+                                       ctypes.byref(lo), ctypes.byref(hi))
     if rc != BH_OK:
         raise BhError(rc, "bh_shard_range: invalid arguments")
     return lo.value, hi.value

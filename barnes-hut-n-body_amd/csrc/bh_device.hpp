@@ -161,9 +161,10 @@ void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, const dou
               const double *y, const double *m, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, uint32_t *visits, uint32_t *wave_iters,
               hipStream_t s);
-// ranks' Morton ranges are whole wavefronts (bh_shard_range)
-__host__ __device__ inline int64_t shard_chunk(int64_t n, int world) {
-    const int64_t c = (n + world - 1) / world;
+// multi-GPU shard pieces (bh_shard_range): `rounds` x `world` pieces of whole wavefronts
+__host__ __device__ inline int64_t shard_sub(int64_t n, int world, int rounds) {
+    const int64_t parts = (int64_t)world * rounds;
+    const int64_t c = (n + parts - 1) / parts;
     return (c + 63) / 64 * 64;
 }
 

@@ -40,6 +40,9 @@ struct bh_engine {
     hipStream_t stream = nullptr;
     int rank = 0, world = 1;
     ncclComm_t comm = nullptr;
+    hipStream_t comm_stream = nullptr;            // all-gathers, overlapping the next round
+    hipEvent_t round_ev[BH_SHARD_ROUNDS] = {};   // round k's forces written (compute stream)
+    hipEvent_t gathered_ev = nullptr;            // every round gathered (comm stream)
 
     int64_t n = 0;     // live bodies
     int64_t cap = 0;   // allocated bodies
@@ -207,8 +210,11 @@ int ensure_capacity(bh_engine *e, int64_t n) {
     if (n > e->cap || !e->st.x) {
         TRY(alloc_state(e, e->st, cap));
         TRY(alloc_state(e, e->alt, cap));
-        const int64_t chunk = shard_chunk(cap, e->world);
-        TRY(dev_alloc(e, e->a2, 2 * chunk * e->world));
+        // multi-GPU: rounds x world pieces of whole wavefronts (bh_shard_range)
+        const int64_t padded = e->comm ? shard_sub(cap, e->world, BH_SHARD_ROUNDS) *
+                                             e->world * BH_SHARD_ROUNDS
+                                       : cap;
+        TRY(dev_alloc(e, e->a2, 2 * padded));
         TRY(dev_alloc(e, e->ax, cap));
         TRY(dev_alloc(e, e->ay, cap));
         TRY(dev_alloc(e, e->keys, cap));
@@ -354,6 +360,12 @@ int ensure_direct(bh_engine *e) {
 // direct sum over the tree's non-empty leaves in pre-order -- run by the all-pairs kernel
 // (direct.hip) on the leaf list instead of the tree walk; bit-identical either way.  The
 // visit-counting diagnostic keeps the walk (it counts internal nodes too).
+//
+// Multi-GPU (e->comm): BH_SHARD_ROUNDS rounds; round k evaluates this rank's piece of the
+// Morton order (bh_shard_range) on the compute stream, then the pieces of round k are
+// all-gathered in place on the comm stream while round k + 1 is evaluated; the compute
+// stream waits for the last gather before the kick.  Pieces of different rounds and ranks
+// are disjoint, so the concurrent writes never overlap.
 int evaluate(bh_engine *e, uint32_t *visits) {
     const int64_t n = e->n;
     TRY(mark(e, -1));
@@ -361,43 +373,43 @@ int evaluate(bh_engine *e, uint32_t *visits) {
     TRY(mark(e, 0));
     ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};  // BHA:378
     const uint32_t *d_T = e->base + n;
-    if (fp.theta2 == 0.0 && !visits) {
+    const bool direct = fp.theta2 == 0.0 && !visits;
+    if (direct) {
         TRY(ensure_direct(e));
         HIPCHK(e, leaf_list_build(e->nodes, d_T, (int64_t)e->node_cap, e->leaf_flags, e->leaf_sel,
                                   e->leaf_count, e->leaves, n, e->leaf_tmp, e->leaf_tmp_bytes,
                                   e->stream));
-        int64_t lo = 0, hi = n;
-        if (e->comm) bh_shard_range(n, e->rank, e->world, &lo, &hi);
-        direct_forces(e->leaves, e->leaf_count, e->st.x, e->st.y, e->st.m, lo, hi, fp.G,
-                      fp.soft2, e->a2, e->stream);
+    }
+    auto forces = [&](int64_t lo, int64_t hi, uint32_t *vis) {
+        if (direct)
+            direct_forces(e->leaves, e->leaf_count, e->st.x, e->st.y, e->st.m, lo, hi, fp.G,
+                          fp.soft2, e->a2, e->stream);
+        else
+            traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, lo, hi, e->geo, fp,
+                     e->a2, vis, vis ? e->wave_iters : nullptr, e->stream);
+    };
+    if (!e->comm || visits) {
+        forces(0, n, visits);
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
-        if (e->comm) {
-            const int64_t chunk = shard_chunk(n, e->world);
-            NCCLCHK(e, ncclAllGather(e->a2 + 2 * e->rank * chunk, e->a2, (size_t)(2 * chunk),
-                                     ncclDouble, e->comm, e->stream));
-            TRY(mark(e, 4));
-        }
         return BH_OK;
     }
-    if (!e->comm || visits) {
-        traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, 0, n, e->geo, fp, e->a2, visits,
-                 e->wave_iters, e->stream);
-        HIPCHK(e, hipGetLastError());
-        TRY(mark(e, 1));
-    } else {
-        const int64_t chunk = shard_chunk(n, e->world);
+    const int64_t sub = shard_sub(n, e->world, BH_SHARD_ROUNDS);
+    for (int k = 0; k < BH_SHARD_ROUNDS; ++k) {
         int64_t lo = 0, hi = 0;
-        bh_shard_range(n, e->rank, e->world, &lo, &hi);
-        traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, lo, hi, e->geo, fp, e->a2, nullptr,
-                 nullptr, e->stream);
+        bh_shard_range(n, e->rank, e->world, k, &lo, &hi);
+        forces(lo, hi, nullptr);
         HIPCHK(e, hipGetLastError());
-        TRY(mark(e, 1));
-        // in place: rank r's chunk already sits at a2 + 2 * r * chunk
-        NCCLCHK(e, ncclAllGather(e->a2 + 2 * e->rank * chunk, e->a2, (size_t)(2 * chunk),
-                                 ncclDouble, e->comm, e->stream));
-        TRY(mark(e, 4));
+        HIPCHK(e, hipEventRecord(e->round_ev[k], e->stream));
+        HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
+        double *piece = e->a2 + 2 * ((int64_t)k * e->world) * sub;  // round k, rank 0
+        NCCLCHK(e, ncclAllGather(piece + 2 * e->rank * sub, piece, (size_t)(2 * sub), ncclDouble,
+                                 e->comm, e->comm_stream));
     }
+    TRY(mark(e, 1));
+    HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
+    HIPCHK(e, hipStreamWaitEvent(e->stream, e->gathered_ev, 0));
+    TRY(mark(e, 4));
     return BH_OK;
 }
 
@@ -667,6 +679,20 @@ int bh_create_dist(const bh_params *p, int device, int rank, int world, const vo
             e->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(nr);
             rc = BH_E_COMM;
         }
+        hipError_t hr = hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking);
+        for (int k = 0; k < BH_SHARD_ROUNDS && hr == hipSuccess; ++k)
+            hr = hipEventCreateWithFlags(&e->round_ev[k], hipEventDisableTiming);
+        if (hr == hipSuccess) hr = hipEventCreateWithFlags(&e->gathered_ev, hipEventDisableTiming);
+        if (rc == BH_OK && hr != hipSuccess) {
+            e->err = std::string("comm stream/events: ") + hipGetErrorString(hr);
+            rc = BH_E_DEVICE;
+        }
+        // the accelerations buffer is laid out in rounds x world pieces from now on
+        if (rc == BH_OK) {
+            const int64_t cap = e->cap;
+            e->cap = 0;
+            rc = ensure_capacity(e, cap);
+        }
     }
     if (rc != BH_OK) {
         std::fprintf(stderr, "bh_create_dist: %s\n", e->err.c_str());
@@ -681,7 +707,12 @@ void bh_destroy(bh_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
+    if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
     if (e->comm) (void)ncclCommDestroy(e->comm);
+    for (hipEvent_t ev : e->round_ev)
+        if (ev) (void)hipEventDestroy(ev);
+    if (e->gathered_ev) (void)hipEventDestroy(e->gathered_ev);
+    if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
     free_state(e->st);
     free_state(e->alt);
     void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->keys32, e->keys32_s, e->idx, e->perm, e->cpl, e->cnt,
@@ -908,11 +939,13 @@ int bh_set_profiling(bh_engine *e, int enabled) {
     return BH_OK;
 }
 
-int bh_shard_range(int64_t n, int rank, int world, int64_t *lo, int64_t *hi) {
-    if (n < 0 || world < 1 || rank < 0 || rank >= world || !lo || !hi) return BH_E_INVALID;
-    const int64_t chunk = shard_chunk(n, world);  // whole wavefronts
-    *lo = std::min<int64_t>(n, (int64_t)rank * chunk);
-    *hi = std::min<int64_t>(n, *lo + chunk);
+int bh_shard_range(int64_t n, int rank, int world, int round, int64_t *lo, int64_t *hi) {
+    if (n < 0 || world < 1 || rank < 0 || rank >= world || round < 0 ||
+        round >= BH_SHARD_ROUNDS || !lo || !hi)
+        return BH_E_INVALID;
+    const int64_t sub = shard_sub(n, world, BH_SHARD_ROUNDS);  // whole wavefronts
+    *lo = std::min<int64_t>(n, ((int64_t)round * world + rank) * sub);
+    *hi = std::min<int64_t>(n, *lo + sub);
     return BH_OK;
 }
 

@@ -185,8 +185,10 @@ def main():
             "traffic": measured_traffic(scene_name, "k_traverse")[0],
             "traffic_source": measured_traffic(scene_name, "k_traverse")[1],
             "kernel": "k_traverse",
+            # N > 1: per evaluation (BH_SHARD_ROUNDS launches overlapped with the all-gathers)
             "kernel_avg_ms": round(trav_ms, 4),
             "launches": trav_launches,
+            "rounds_per_eval": bh_amd.SHARD_ROUNDS if world > 1 else 1,
             "vbar_nodes_per_body_eval": round(vbar, 2),
             "wave_lane_efficiency": round(lane_eff, 4),
             "bytes_per_launch": round(bytes_per_launch),

@@ -126,10 +126,13 @@ int bh_traversal_stats(const bh_engine *e, int64_t *lane_visits, int64_t *wave_i
 /* Enable/disable per-phase event timing (default off: no events in the hot loop). */
 int bh_set_profiling(bh_engine *e, int enabled);
 
-/* Morton-order body range [lo, hi) whose forces rank `rank` of `world` evaluates for n
- * bodies (equal-count contiguous chunks of ceil(n / world); the all-gather exchanges
- * 2 * ceil(n / world) doubles per rank).  Host-only; used by the engine itself. */
-int bh_shard_range(int64_t n, int rank, int world, int64_t *lo, int64_t *hi);
+/* Multi-GPU force evaluation runs in BH_SHARD_ROUNDS rounds.  Round k of rank r evaluates
+ * the Morton-order bodies [lo, hi) = [(k * world + r) * sub, + sub) clipped to n, with
+ * sub = ceil(n / (world * rounds)) rounded up to whole wavefronts; the (ax, ay) of round k
+ * are all-gathered in place (one ncclAllGather of 2 * sub doubles per rank) on a second
+ * stream while round k + 1 is evaluated.  Host-only; used by the engine itself. */
+#define BH_SHARD_ROUNDS 4
+int bh_shard_range(int64_t n, int rank, int world, int round, int64_t *lo, int64_t *hi);
 
 /* Diagnostic: checks, on HIP device `device`, the traversal's reduced-range exact sequences
  * for sqrt(d2), 1/sqrt(d2) and 1/d2 (traverse.hip) bit-for-bit against the IEEE operations on

@@ -45,21 +45,27 @@ def test_default_params_match_config_kt():
 
 @pytest.mark.parametrize("n,world", [(0, 1), (1, 2), (7, 2), (1000, 3), (1_000_003, 8), (5, 8)])
 def test_shard_ranges_partition_the_bodies(n, world):
-    covered = []
-    for r in range(world):
-        lo, hi = bh_amd.shard_range(n, r, world)
-        assert 0 <= lo <= hi <= n
-        covered.extend(range(lo, hi)) if n < 10_000 else covered.append((lo, hi))
-    if n < 10_000:
-        assert covered == list(range(n))
-    else:
-        assert covered[0][0] == 0 and covered[-1][1] == n
-        assert all(covered[i][1] == covered[i + 1][0] for i in range(world - 1))
+    """Pieces (round k, rank r) tile [0, n) in the order k-major, r-minor, each a whole
+    number of wavefronts except the last non-empty one: round k's in-place all-gather
+    (ranks' pieces of one round are adjacent) covers exactly that round."""
+    pieces = []
+    for k in range(bh_amd.SHARD_ROUNDS):
+        for r in range(world):
+            lo, hi = bh_amd.shard_range(n, r, world, k)
+            assert 0 <= lo <= hi <= n
+            pieces.append((lo, hi))
+    assert pieces[0][0] == 0 and pieces[-1][1] == n
+    assert all(pieces[i][1] == pieces[i + 1][0] for i in range(len(pieces) - 1))
+    sub = pieces[0][1] - pieces[0][0]
+    assert sub % 64 == 0 or n <= 64
+    assert all(hi - lo in (sub, 0) or hi == n for lo, hi in pieces)
 
 
 def test_shard_range_rejects_bad_arguments():
     with pytest.raises(bh_amd.BhError):
         bh_amd.shard_range(10, 3, 2)
+    with pytest.raises(bh_amd.BhError):
+        bh_amd.shard_range(10, 0, 2, bh_amd.SHARD_ROUNDS)
 
 
 def _gpu_visible():

@@ -1,11 +1,13 @@
 """Multi-rank decomposition on CPU (torch.distributed / gloo, world_size 2).
 
 The engine's multi-GPU step (engine.cpp `evaluate`, bh_create_dist) keeps the state replicated,
-builds the same tree on every rank, evaluates forces only for the Morton-sorted range
-bh_shard_range(n, rank, world), all-gathers the interleaved (ax, ay) chunks (RCCL on the GPU
-box) and scatters them back through the sort permutation.  This test runs exactly that
-decomposition with gloo in place of RCCL and the oracle in place of the HIP traversal, and
-requires the gathered result to be bit-identical to a single-process evaluation.
+builds the same tree on every rank and evaluates forces in BH_SHARD_ROUNDS rounds: in round k
+a rank evaluates its Morton-sorted piece bh_shard_range(n, rank, world, k), and the round's
+interleaved (ax, ay) pieces are all-gathered in place (RCCL on the GPU box, overlapping the
+next round) into the slot-indexed buffer, which is scattered back through the sort
+permutation.  This test runs exactly that decomposition with gloo in place of RCCL and the
+oracle in place of the HIP traversal, and requires the gathered result to be bit-identical to
+a single-process evaluation.
 """
 import os
 import socket
@@ -61,15 +63,20 @@ def _worker(rank, world, port, out_dir):
     x, y = arrs[0], arrs[1]
     perm = morton_order(x, y)
     n = len(x)
-    lo, hi = bh_amd.shard_range(n, rank, world)
-    chunk = bh_amd.shard_range(n, 0, world)[1]  # whole wavefronts per rank (engine.cpp)
-    ax, ay = ref.accelerations(subset=perm[lo:hi])  # this rank's Morton range
-    send = np.zeros(2 * chunk)
-    send[0:2 * (hi - lo):2] = ax
-    send[1:2 * (hi - lo):2] = ay
-    gathered = [torch.zeros(2 * chunk, dtype=torch.float64) for _ in range(world)]
-    dist.all_gather(gathered, torch.from_numpy(send))
-    a_sorted = torch.cat(gathered).numpy()
+    sub = bh_amd.shard_range(n, 0, world, 0)[1]  # whole wavefronts per piece (engine.cpp)
+    a2 = np.zeros(2 * sub * world * bh_amd.SHARD_ROUNDS)  # slot-indexed, interleaved
+    for k in range(bh_amd.SHARD_ROUNDS):
+        lo, hi = bh_amd.shard_range(n, rank, world, k)
+        if hi > lo:
+            ax, ay = ref.accelerations(subset=perm[lo:hi])  # this rank's piece of round k
+            a2[2 * lo:2 * hi:2] = ax
+            a2[2 * lo + 1:2 * hi:2] = ay
+        base = 2 * k * world * sub  # in place: rank r's piece sits at base + 2 * r * sub
+        send = torch.from_numpy(a2[base + 2 * rank * sub:base + 2 * (rank + 1) * sub].copy())
+        gathered = [torch.zeros(2 * sub, dtype=torch.float64) for _ in range(world)]
+        dist.all_gather(gathered, send)
+        a2[base:base + 2 * world * sub] = torch.cat(gathered).numpy()
+    a_sorted = a2
     full_ax = np.empty(n)
     full_ay = np.empty(n)
     full_ax[perm] = a_sorted[0:2 * n:2]
@@ -80,7 +87,7 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2])
+@pytest.mark.parametrize("world", [2, 3])
 def test_sharded_evaluation_matches_single_process(tmp_path, world):
     import bh_amd  # noqa: F401  (library must load before spawning)
     import oracle
