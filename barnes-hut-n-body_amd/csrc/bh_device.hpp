@@ -34,7 +34,7 @@ static_assert(sizeof(Node) == 32, "node record must be 32 bytes");
 constexpr uint32_t NODE_LEAF = 1u << 31;             // leaf holding one body (BHA:97)
 constexpr uint32_t NODE_SKIP = 1u << 30;             // mass == 0.0: never visited (BHA:216)
 constexpr uint32_t NODE_BODY_MASK = (1u << 30) - 1;  // leaf: body slot (Morton position)
-constexpr uint32_t NODE_DEPTH_MASK = 0xFFu;          // internal: depth (root = 0)
+constexpr uint32_t NODE_DEPTH2_MASK = 0xFFu;         // internal: 2 x depth (root = 0)
 constexpr int NODE_JMASK_SHIFT = 8;                  // jitter cell: children that got subdivided
 constexpr uint32_t NODE_SPAN = 1u << 12;             // internal: body range crosses a COM chunk
 

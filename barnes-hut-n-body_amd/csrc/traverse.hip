@@ -52,9 +52,6 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
                                      double by, double Gm, double soft2, double theta2,
                                      double s2root, uint32_t self, uint32_t resume, double &fx,
                                      double &fy, uint32_t &nvis, uint32_t &niters) {
-    // s2root in a VGPR: v_ldexp_f64 then takes the uniform exponent straight from an SGPR
-    double s2root_v;
-    asm volatile("v_mov_b64 %0, %1" : "=v"(s2root_v) : "s"(s2root));
     uint32_t cur = 0;
     // one iteration on record `rec`; the next record is requested into `nrec`.  The loop body
     // is unrolled twice with the two records swapping roles (no SGPR copies per iteration).
@@ -92,10 +89,11 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
             open_m = 0;
         } else {
             // s2 = (h_d * 2.0)^2 with h_d = h_0 / 2^d exactly, so s2 = s2_0 * 4^-d exactly
-            // (a power-of-two scaling commutes with rounding): one v_ldexp, no table load.
-            const double s2 = __builtin_ldexp(s2root_v, -2 * (int)(meta & NODE_DEPTH_MASK));
-            const double t2 = theta2 * d2;
-            const uint64_t acc_m = __builtin_amdgcn_ballot_w64(s2 < t2);  // BHA:226-228
+            // (a power-of-two scaling commutes with rounding), and s2 < t2 <=> s2_0 < t2 * 4^d:
+            // the scaling of t2 is exact too (up from a subnormal included) or overflows to
+            // +inf where s2 < t2 holds anyway.  The record carries 2d: one scalar mask.
+            const double t2 = __builtin_ldexp(theta2 * d2, (int)(meta & NODE_DEPTH2_MASK));
+            const uint64_t acc_m = __builtin_amdgcn_ballot_w64(s2root < t2);  // BHA:226-228
             contrib_m = act_m & acc_m;
             open_m = act_m & ~acc_m;
         }

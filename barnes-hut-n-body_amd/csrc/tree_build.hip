@@ -449,7 +449,7 @@ __global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, int D0,
         nd.comY = 0.0;
         nd.mass = 0.0;
         nd.next = base[end + 1];
-        nd.meta = (uint32_t)L | (span ? NODE_SPAN : 0u);
+        nd.meta = (uint32_t)(2 * L) | (span ? NODE_SPAN : 0u);  // 2 x depth: traversal's exponent
         nodes[ni] = nd;
     }
     const uint32_t li = b0 + (uint32_t)max(0, cc - cp);
