@@ -518,19 +518,17 @@ __device__ void sort_by_cidx(uint32_t *ord, int64_t k, const uint32_t *__restric
     }
 }
 
-__global__ __launch_bounds__(TB) void k_jitter(int64_t n, Geometry g,
-                                               const uint64_t *__restrict__ keys_s,
-                                               const int8_t *__restrict__ cpl,
-                                               const uint32_t *__restrict__ base, double *x,
-                                               double *y, const double *__restrict__ m,
-                                               const uint32_t *__restrict__ cidx,
-                                               uint32_t *scratch, Node *nodes, uint32_t *err) {
-    int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (a >= n) return;
+// Replay of BHA:125-156 inside the jitter cell whose run of sorted bodies starts at `a`
+// (c(a) == J, c(a-1) != J): the run's positions are mutated in place and the cell's k child
+// slots s0.. are produced through put(slot, record) -- leaves in child order 0..3, then
+// massless dead slots.  Returns the mask of subdivided children (for visitQuads).
+template <typename Put>
+__device__ uint32_t jitter_run(int64_t n, const Geometry &g, int64_t a, int cp,
+                               const uint64_t *__restrict__ keys_s, const int8_t *__restrict__ cpl,
+                               const uint32_t *__restrict__ base, double *x, double *y,
+                               const double *__restrict__ m, const uint32_t *__restrict__ cidx,
+                               uint32_t *scratch, uint32_t *err, Put put) {
     const int J = g.J;
-    if ((int)cpl[a] != J) return;
-    int cp = a > 0 ? (int)cpl[a - 1] : -1;
-    if (cp == J) return;  // not the first body of its jitter cell
     int64_t b = a;
     while (b < n && (int)cpl[b] == J) ++b;  // run = sorted bodies a..b
     const int64_t k = b - a + 1;
@@ -586,8 +584,8 @@ __global__ __launch_bounds__(TB) void k_jitter(int64_t n, Geometry g,
         into_child(j);
     }
 
-    // Write the cell's children into its k contiguous slots, child order 0..3.
-    uint32_t s0 = base[a] + (uint32_t)(J - cp);
+    // The cell's children into its k contiguous slots, child order 0..3.
+    const uint32_t s0 = base[a] + (uint32_t)(J - cp);
     uint32_t w = 0;
     uint32_t jmask = 0;
     for (int q = 0; q < 4; ++q) {
@@ -601,7 +599,7 @@ __global__ __launch_bounds__(TB) void k_jitter(int64_t n, Geometry g,
         leaf.mass = mm;
         leaf.next = s0 + w + 1;
         leaf.meta = NODE_LEAF | (uint32_t)j | (mm == 0.0 ? NODE_SKIP : 0u);
-        nodes[s0 + w] = leaf;
+        put(s0 + w, leaf);
         ++w;
     }
     for (; w < (uint32_t)k; ++w) {
@@ -611,8 +609,26 @@ __global__ __launch_bounds__(TB) void k_jitter(int64_t n, Geometry g,
         dead.mass = 0.0;
         dead.next = s0 + w + 1;
         dead.meta = NODE_SKIP;
-        nodes[s0 + w] = dead;
+        put(s0 + w, dead);
     }
+    return jmask;
+}
+
+__global__ __launch_bounds__(TB) void k_jitter(int64_t n, Geometry g,
+                                               const uint64_t *__restrict__ keys_s,
+                                               const int8_t *__restrict__ cpl,
+                                               const uint32_t *__restrict__ base, double *x,
+                                               double *y, const double *__restrict__ m,
+                                               const uint32_t *__restrict__ cidx,
+                                               uint32_t *scratch, Node *nodes, uint32_t *err) {
+    int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (a >= n) return;
+    const int J = g.J;
+    if ((int)cpl[a] != J) return;
+    int cp = a > 0 ? (int)cpl[a - 1] : -1;
+    if (cp == J) return;  // not the first body of its jitter cell
+    const uint32_t jmask = jitter_run(n, g, a, cp, keys_s, cpl, base, x, y, m, cidx, scratch, err,
+                                      [&](uint32_t slot, const Node &nd) { nodes[slot] = nd; });
     // remember which children were subdivided (for getTreeForDebug/visitQuads)
     uint32_t ni = base[a] + (uint32_t)(J - cp - 1);
     nodes[ni].meta |= jmask << NODE_JMASK_SHIFT;

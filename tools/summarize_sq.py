@@ -1,0 +1,57 @@
+#!/usr/bin/env python3
+"""Condense the SQ counter passes of tools/profile_sq.sh (gpurun_out/prof_sq/p*/) for the
+traversal kernel into profiles/<prefix>_sq_summary.md.
+
+Usage: python tools/summarize_sq.py gpurun_out/prof_sq profiles/r01_c3
+VALU busy per SIMD = SQ_ACTIVE_INST_VALU x 4 (quad-cycles) / (256 CUs x 4 SIMDs), against the
+kernel length GRBM_GUI_ACTIVE / 8 XCDs (counters summed over the shader engines).
+"""
+import collections
+import csv
+import glob
+import os
+import sys
+
+KERNEL = "k_traverse<false, true>"
+
+
+def main():
+    src, prefix = sys.argv[1], sys.argv[2]
+    acc = collections.defaultdict(list)  # counter -> per-dispatch totals
+    for f in sorted(glob.glob(os.path.join(src, "p*", "*counter_collection.csv"))):
+        per = collections.defaultdict(float)
+        for r in csv.DictReader(open(f)):
+            if KERNEL not in r["Kernel_Name"]:
+                continue
+            per[(r["Dispatch_Id"], r["Counter_Name"])] += float(r["Counter_Value"])
+        for (_, c), v in per.items():
+            acc[c].append(v)
+    avg = {c: sum(v) / len(v) for c, v in acc.items()}
+    waves = avg.get("SQ_WAVES", 0.0)
+    out = [f"## {KERNEL} SQ counters (C3, average per dispatch; rocprofv3 --pmc, "
+           f"{len(glob.glob(os.path.join(src, 'p*')))} passes)", "",
+           "| counter | per dispatch | per wave |", "|---|---|---|"]
+    for c in sorted(avg):
+        pw = avg[c] / waves if waves else 0.0
+        out.append(f"| {c} | {avg[c]:.4g} | {pw:.4g} |")
+    if "GRBM_GUI_ACTIVE" in avg and "SQ_ACTIVE_INST_VALU" in avg:
+        klen = avg["GRBM_GUI_ACTIVE"] / 8
+        busy = avg["SQ_ACTIVE_INST_VALU"] * 4 / 1024
+        out += ["", f"- kernel length: GRBM_GUI_ACTIVE / 8 XCDs = {klen:.4g} cycles",
+                f"- VALU busy per SIMD: SQ_ACTIVE_INST_VALU x 4 / 1024 SIMDs = {busy:.4g} cycles "
+                f"= {100 * busy / klen:.1f} % of the kernel"]
+    if waves and "SQ_INSTS_VALU" in avg:
+        out.append(f"- per wave: VALU {avg['SQ_INSTS_VALU'] / waves:.0f}, SALU "
+                   f"{avg.get('SQ_INSTS_SALU', 0) / waves:.0f}, SMEM "
+                   f"{avg.get('SQ_INSTS_SMEM', 0) / waves:.0f} instructions")
+    if "SQ_WAVE_CYCLES" in avg:
+        wc = avg["SQ_WAVE_CYCLES"]
+        out.append(f"- wave time split: active {100 * avg.get('SQ_ACTIVE_INST_ANY', 0) / wc:.0f} %, "
+                   f"waiting on memory (WAIT_ANY) {100 * avg.get('SQ_WAIT_ANY', 0) / wc:.0f} %, "
+                   f"waiting for issue (WAIT_INST_ANY) {100 * avg.get('SQ_WAIT_INST_ANY', 0) / wc:.0f} %")
+    open(prefix + "_sq_summary.md", "w").write("\n".join(out) + "\n")
+    print("\n".join(out))
+
+
+if __name__ == "__main__":
+    main()
