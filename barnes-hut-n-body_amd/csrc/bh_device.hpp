@@ -108,7 +108,7 @@ struct __attribute__((aligned(16))) SpanSlot {
 // Workgroup i of a launch runs on XCD i % 8 (8 XCDs, each with its own 4 MB L2).  For gathers
 // whose neighbouring blocks read overlapping lines, xcd_block() remaps the hardware block index
 // so that every XCD takes runs of BH_XCD_RUN consecutive logical blocks (0: identity; 16 is
-// ~1% faster for k_prep/k_key_gather/k_emit at C3 and C4 than the identity, A/B on one box).
+// ~1% faster for k_prep/k_key_gather and the old per-body emit kernel at C3 and C4 than the identity, A/B on one box).
 #ifndef BH_XCD_RUN
 #define BH_XCD_RUN 16
 #endif

@@ -9,20 +9,19 @@
 // the reference — the deterministic jitter applied when a cell with h < 1e-3 is subdivided
 // (BHA:146-151), which mutates positions and can drop bodies — is confined to the cells at
 // the first depth J with h < 1e-3 that hold >= 2 bodies.  Those "jitter cells" are replayed
-// exactly, in caller-list order, by one thread each (k_jitter).
+// exactly, in caller-list order, by one thread each (jitter_run).
 //
 // Pipeline (all on one stream, no host synchronisation):
 //   k_morton     keys (2 bits per level, J levels) + slot payload
-//   radix sort   (stable)                    -> keys_s, perm
+//   sort         (stable; bucket sort from the previous order) -> keys_s, perm
 //   k_prep       state permuted into the new Morton order; c(a) = common digit count of
 //                neighbours; node slot counts
 //   exclusive scan                            -> base (pre-order slot of each body's nodes)
 //   k_cells      first sorted body of every depth-D0 cell
-//   k_emit       internal node skeletons (depth, next) + leaf records
-//   k_jitter     replay of BHA:125-156 inside each jitter cell
-//   k_com_local  centre of mass bottom-up (children 0..3 in order, BHA:184-200) for every
-//                node inside a 1024-body chunk, all levels in one launch
-//   k_com_span   the few chunk-spanning nodes, levels J..0, one workgroup
+//   k_emit_com   per 1024-body chunk, in LDS: internal node skeletons (depth, next) + leaf
+//                records, replay of BHA:125-156 inside each jitter cell, centre of mass
+//                bottom-up (children 0..3 in order, BHA:184-200) of the chunk-local nodes
+//   k_span_*     the chunk-spanning nodes, levels J..0
 #include <hipcub/hipcub.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 
@@ -378,12 +377,11 @@ __device__ __forceinline__ int64_t run_end(const uint64_t *__restrict__ keys_s, 
     return lo;
 }
 
-// c(j) + 1 of a window of EMIT_WIN sorted positions starting at the block's first body, in
-// LDS: a node's end is found by a word-wise SWAR scan of the window (most nodes end inside
-// it); only nodes that outrun the window gallop over the keys in global memory.
-constexpr int EMIT_WIN = 2048;
-
-// first j in [from, c0 + EMIT_WIN) with c(j) < L, or -1; w[i] = c(c0 + i) + 1 in [0, 42]
+// c(j) + 1 of a window of WIN sorted positions starting at the chunk's first body, in LDS:
+// a node's end is found by a word-wise SWAR scan of the window (most nodes end inside it);
+// only nodes that outrun the window gallop over the keys in global memory.
+// first j in [from, c0 + WIN) with c(j) < L, or -1; w[i] = c(c0 + i) + 1 in [0, 42]
+template <int WIN>
 __device__ __forceinline__ int64_t lds_scan(const uint64_t *w, int64_t c0, int64_t from, int L) {
     const uint64_t ones = 0x0101010101010101ull, highs = 0x8080808080808080ull;
     const uint64_t sub = ones * (uint64_t)(L + 1);
@@ -391,76 +389,13 @@ __device__ __forceinline__ int64_t lds_scan(const uint64_t *w, int64_t c0, int64
     int wi = (int)(o >> 3);
     // bytes before `from` are raised to 0x7F (>= L + 1): they neither match nor borrow
     uint64_t pad = ~(~0ull << (8 * (o & 7))) & 0x7F7F7F7F7F7F7F7Full;
-    for (; wi < EMIT_WIN / 8; ++wi) {
+    for (; wi < WIN / 8; ++wi) {
         const uint64_t x = w[wi] | pad;
         const uint64_t t = (x - sub) & ~x & highs;  // lowest flag = first byte with c + 1 < L + 1
         if (t) return c0 + 8 * (int64_t)wi + (__builtin_ctzll(t) >> 3);
         pad = 0;
     }
     return -1;
-}
-
-__global__ __launch_bounds__(TB) void k_emit(int64_t n, int J, int D0,
-                                             const uint64_t *__restrict__ keys_s,
-                                             const int8_t *__restrict__ cpl,
-                                             const uint32_t *__restrict__ base,
-                                             const uint32_t *__restrict__ cell_start,
-                                             const double *__restrict__ x,
-                                             const double *__restrict__ y,
-                                             const double *__restrict__ m,
-                                             Node *__restrict__ nodes) {
-    __shared__ uint64_t win[EMIT_WIN / 8];
-    const int64_t c0 = (int64_t)xcd_block() * TB;
-    {
-        uint8_t *wb = reinterpret_cast<uint8_t *>(win);
-        for (int i = threadIdx.x; i < EMIT_WIN; i += TB) {
-            const int64_t j = c0 + i;
-            wb[i] = (uint8_t)(j < n ? (int)cpl[j] + 1 : 0);  // past the end: c = -1
-        }
-    }
-    __syncthreads();
-    const int64_t a = c0 + threadIdx.x;
-    if (a >= n) return;
-    const uint64_t k = keys_s[a];
-    if (k == sentinel_key(J)) return;
-    const int cp = a > 0 ? (int)cpl[a - 1] : -1;
-    const int cc = (int)cpl[a];
-    const uint32_t b0 = base[a];
-    const int shift0 = 2 * (J - D0);
-    int64_t end = a;
-    for (int L = cc; L > cp; --L) {  // deepest first: ends are nested
-        int64_t b;
-        if (L <= D0) {  // one load: the next depth-L cell starts at a depth-D0 cell start
-            const uint64_t nextcell = ((k >> (2 * (J - L))) + 1) << (2 * (D0 - L));
-            b = (int64_t)cell_start[nextcell] - 1;
-        } else {  // inside a's depth-D0 cell: scan the LDS window, then bounded galloping
-            b = lds_scan(win, c0, end, L);
-            if (b < 0) {  // c >= L up to the window's end: the cell continues past it
-                const int64_t limit = (int64_t)cell_start[(k >> shift0) + 1] - 1;
-                const int shift = 2 * (J - L);
-                b = run_end(keys_s, limit, c0 + EMIT_WIN - 1, shift, k >> shift);
-            }
-        }
-        end = b;
-        const bool span = (a >> COM_CHUNK_SHIFT) != (end >> COM_CHUNK_SHIFT);
-        const uint32_t ni = b0 + (uint32_t)(L - cp - 1);
-        Node nd;
-        nd.comX = 0.0;
-        nd.comY = 0.0;
-        nd.mass = 0.0;
-        nd.next = base[end + 1];
-        nd.meta = (uint32_t)(2 * L) | (span ? NODE_SPAN : 0u);  // 2 x depth: traversal's exponent
-        nodes[ni] = nd;
-    }
-    const uint32_t li = b0 + (uint32_t)max(0, cc - cp);
-    const double mm = m[a];
-    Node leaf;
-    leaf.comX = x[a];  // BHA:176-178
-    leaf.comY = y[a];
-    leaf.mass = mm;
-    leaf.next = li + 1;
-    leaf.meta = NODE_LEAF | (uint32_t)a | (mm == 0.0 ? NODE_SKIP : 0u);
-    nodes[li] = leaf;
 }
 
 // ---- exact replay of BHA:125-156 inside one jitter cell (depth J, h_J < 1e-3) ---------
@@ -614,26 +549,6 @@ __device__ uint32_t jitter_run(int64_t n, const Geometry &g, int64_t a, int cp,
     return jmask;
 }
 
-__global__ __launch_bounds__(TB) void k_jitter(int64_t n, Geometry g,
-                                               const uint64_t *__restrict__ keys_s,
-                                               const int8_t *__restrict__ cpl,
-                                               const uint32_t *__restrict__ base, double *x,
-                                               double *y, const double *__restrict__ m,
-                                               const uint32_t *__restrict__ cidx,
-                                               uint32_t *scratch, Node *nodes, uint32_t *err) {
-    int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (a >= n) return;
-    const int J = g.J;
-    if ((int)cpl[a] != J) return;
-    int cp = a > 0 ? (int)cpl[a - 1] : -1;
-    if (cp == J) return;  // not the first body of its jitter cell
-    const uint32_t jmask = jitter_run(n, g, a, cp, keys_s, cpl, base, x, y, m, cidx, scratch, err,
-                                      [&](uint32_t slot, const Node &nd) { nodes[slot] = nd; });
-    // remember which children were subdivided (for getTreeForDebug/visitQuads)
-    uint32_t ni = base[a] + (uint32_t)(J - cp - 1);
-    nodes[ni].meta |= jmask << NODE_JMASK_SHIFT;
-}
-
 // BHA:173-202 for one internal node: children 0..3 in pre-order, skipping mass <= 0.
 __device__ __forceinline__ void node_com(Node *nodes, uint32_t ni, const Geometry &g,
                                          uint64_t key, int L) {
@@ -660,41 +575,68 @@ __device__ __forceinline__ void node_com(Node *nodes, uint32_t ni, const Geometr
     nodes[ni] = nd;
 }
 
-// Every internal node whose body range lies inside one COM chunk (2^COM_CHUNK_SHIFT bodies
-// of the Morton order) is finished here, all levels bottom-up in ONE launch: a workgroup owns
-// a chunk, stages the chunk's pre-order slot range [base[c0], base[c1]) in LDS (a local
-// node's whole subtree lives in that range), walks children at LDS latency, and separates
-// levels with barriers.  Chunks whose range exceeds the LDS capacity use global memory.
-constexpr int COM_TB = 256;
-constexpr int COM_PER_THREAD = (1 << COM_CHUNK_SHIFT) / COM_TB;
+// Chunk-local centre of mass (k_emit_com below): LDS capacity per chunk and its encoding.
 #ifndef BH_COM_CAP
 #define BH_COM_CAP 2048
 #endif
 constexpr int COM_CAP = BH_COM_CAP;  // nodes staged per chunk (C3 at 1e6, 1024-body chunks: max 1814)
-constexpr int COM_LOAD_BATCH = 4;
-constexpr uint32_t LDS_SPAN = 1u << 31;
-constexpr uint32_t LDS_LEAF = 1u << 30;
-constexpr uint32_t LDS_NEXT_MASK = LDS_LEAF - 1;
 constexpr uint16_t NO_CHILD = (uint16_t)COM_CAP;  // the massless pad entry
 constexpr uint16_t SPAN_CHILD = 0xFFFFu;         // s_ch.x of a chunk-spanning node
 
-__global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
-                                                      const uint64_t *__restrict__ keys_s,
-                                                      const int8_t *__restrict__ cpl,
-                                                      const uint32_t *__restrict__ base,
-                                                      Node *nodes) {
+// ---- node emission, jitter replay and chunk-local centre of mass in one pass -----------
+// One workgroup per 2^COM_CHUNK_SHIFT-body chunk of the Morton order.  Its bodies' node
+// skeletons and leaves are produced straight into LDS (the chunk's pre-order slot range
+// [base[c0], base[c1])), the jitter cells whose run starts in the chunk are replayed by one
+// thread each (BHA:125-156, jitter_run), and the chunk-local internal nodes get their centre
+// of mass level by level; every record is written to HBM once: leaves and
+// jitter slots when produced, local internal nodes complete at the end, chunk-spanning nodes
+// as skeletons for the span passes.  A chunk whose slot range exceeds the LDS capacity runs
+// the same steps on global memory.  Jitter slots of a run that started in an earlier chunk are
+// written by that chunk's workgroup; here they are inert leaves (no local node owns them).
+constexpr int EC_WIN = (1 << COM_CHUNK_SHIFT) + 2048;  // c(j) + 1 of the chunk + look-ahead
+#ifndef BH_EC_TB
+#define BH_EC_TB 512
+#endif
+constexpr int EC_TB = BH_EC_TB;  // 2 bodies per thread (measured: 256 and 1024 threads slower)
+constexpr int EC_PER = (1 << COM_CHUNK_SHIFT) / EC_TB;
+constexpr uint32_t EC_SPAN = 1u << 31;
+constexpr uint32_t EC_LEAF = 1u << 30;
+constexpr uint32_t EC_NEXT_MASK = 0xFFFFu;  // next - S0 (<= COM_CAP)
+constexpr int EC_JMASK_SHIFT = 16;          // jitter cell: subdivided children
+constexpr int EC_D2_SHIFT = 20;             // 2 x depth
+static_assert(COM_CAP <= (int)EC_NEXT_MASK, "LDS next offsets must fit 16 bits");
+
+__global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D0,
+                                                     const uint64_t *__restrict__ keys_s,
+                                                     const int8_t *__restrict__ cpl,
+                                                     const uint32_t *__restrict__ base,
+                                                     const uint32_t *__restrict__ cell_start,
+                                                     double *x, double *y,
+                                                     const double *__restrict__ m,
+                                                     const uint32_t *__restrict__ cidx,
+                                                     uint32_t *scratch, Node *nodes,
+                                                     uint32_t *err) {
     __shared__ double s_m[COM_CAP + 1], s_x[COM_CAP + 1], s_y[COM_CAP + 1];  // [COM_CAP]: pad
     __shared__ uint32_t s_next[COM_CAP];
-    __shared__ ushort4 s_ch[COM_CAP];  // child offsets of internal nodes (NO_CHILD-padded)
+    __shared__ ushort4 s_ch[COM_CAP];
+    __shared__ uint64_t win[EC_WIN / 8];
     __shared__ int s_lmax;
+    const int J = g.J;
     const int64_t c0 = (int64_t)blockIdx.x << COM_CHUNK_SHIFT;
     const int64_t c1 = min(c0 + (1 << COM_CHUNK_SHIFT), n);
-    const int64_t a0 = c0 + (int64_t)threadIdx.x * COM_PER_THREAD;
-    int cps[COM_PER_THREAD], ccs[COM_PER_THREAD];
-    uint32_t bases[COM_PER_THREAD];
+    const int64_t a0 = c0 + (int64_t)threadIdx.x * EC_PER;
+    {
+        uint8_t *wb = reinterpret_cast<uint8_t *>(win);
+        for (int i = threadIdx.x; i < EC_WIN; i += EC_TB) {
+            const int64_t j = c0 + i;
+            wb[i] = (uint8_t)(j < n ? (int)cpl[j] + 1 : 0);  // past the end: c = -1
+        }
+    }
+    int cps[EC_PER], ccs[EC_PER];
+    uint32_t bases[EC_PER];
     int lmax = -1;
 #pragma unroll
-    for (int i = 0; i < COM_PER_THREAD; ++i) {
+    for (int i = 0; i < EC_PER; ++i) {
         const int64_t a = a0 + i;
         int cp = -1, cc = -1;
         uint32_t ba = 0;
@@ -714,92 +656,161 @@ __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
     const bool lds = cnt <= (uint32_t)COM_CAP;
     __syncthreads();
     atomicMax(&s_lmax, lmax);
-    if (lds) {
-        // stage the chunk's pre-order range; loads issued in batches (independent)
-        for (uint32_t i0 = threadIdx.x; i0 < cnt; i0 += COM_TB * COM_LOAD_BATCH) {
-            Node nd[COM_LOAD_BATCH];
+
+    // ---- skeletons and leaves (BHA:125-137, 159-166, 176-178) ----
+    const uint64_t SENT = sentinel_key(J);
+    const int shift0 = 2 * (J - D0);
 #pragma unroll
-            for (int k = 0; k < COM_LOAD_BATCH; ++k) {
-                const uint32_t i = i0 + k * COM_TB;
-                if (i < cnt) nd[k] = nodes[S0 + i];
-            }
-#pragma unroll
-            for (int k = 0; k < COM_LOAD_BATCH; ++k) {
-                const uint32_t i = i0 + k * COM_TB;
-                if (i < cnt) {
-                    s_m[i] = nd[k].mass;
-                    s_x[i] = nd[k].comX;
-                    s_y[i] = nd[k].comY;
-                    // leaves and dead jitter slots (SKIP before COM) have no children
-                    const bool leaf = nd[k].meta & (NODE_LEAF | NODE_SKIP);
-                    s_next[i] = (nd[k].next - S0) | (leaf ? LDS_LEAF : 0u) |
-                                ((!leaf && (nd[k].meta & NODE_SPAN)) ? LDS_SPAN : 0u);
+    for (int i = 0; i < EC_PER; ++i) {
+        const int64_t a = a0 + i;
+        if (a >= n) continue;
+        const uint64_t k = keys_s[a];
+        if (k == SENT) continue;  // not in the tree: no slots
+        const int cp = cps[i], cc = ccs[i];
+        const uint32_t b0 = bases[i];
+        int64_t end = a;
+        for (int L = cc; L > cp; --L) {  // deepest first: ends are nested
+            int64_t b;
+            if (L <= D0) {  // one load: the next depth-L cell starts at a depth-D0 cell start
+                const uint64_t nextcell = ((k >> (2 * (J - L))) + 1) << (2 * (D0 - L));
+                b = (int64_t)cell_start[nextcell] - 1;
+            } else {  // inside a's depth-D0 cell: scan the LDS window, then bounded galloping
+                b = lds_scan<EC_WIN>(win, c0, end, L);
+                if (b < 0) {
+                    const int64_t limit = (int64_t)cell_start[(k >> shift0) + 1] - 1;
+                    const int shift = 2 * (J - L);
+                    b = run_end(keys_s, limit, c0 + EC_WIN - 1, shift, k >> shift);
                 }
             }
+            end = b;
+            const bool span = (a >> COM_CHUNK_SHIFT) != (end >> COM_CHUNK_SHIFT);
+            const uint32_t ni = b0 + (uint32_t)(L - cp - 1);
+            const uint32_t nx = base[end + 1];
+            if (span || !lds) {
+                Node nd;
+                nd.comX = 0.0;
+                nd.comY = 0.0;
+                nd.mass = 0.0;
+                nd.next = nx;
+                nd.meta = (uint32_t)(2 * L) | (span ? NODE_SPAN : 0u);  // 2 x depth
+                nodes[ni] = nd;
+            }
+            if (lds)
+                s_next[ni - S0] = span ? EC_SPAN : ((nx - S0) | ((uint32_t)(2 * L) << EC_D2_SHIFT));
         }
-        __syncthreads();
+        const uint32_t li = b0 + (uint32_t)max(0, cc - cp);
+        if (cc == J || cp == J) {  // a jitter run's slot: written by the run's replay below
+            if (lds) {
+                s_m[li - S0] = 0.0;
+                s_x[li - S0] = 0.0;
+                s_y[li - S0] = 0.0;
+                s_next[li - S0] = (li + 1 - S0) | EC_LEAF;
+            }
+            continue;
+        }
+        const double mm = m[a];
+        Node leaf;
+        leaf.comX = x[a];  // BHA:176-178
+        leaf.comY = y[a];
+        leaf.mass = mm;
+        leaf.next = li + 1;
+        leaf.meta = NODE_LEAF | (uint32_t)a | (mm == 0.0 ? NODE_SKIP : 0u);
+        nodes[li] = leaf;
+        if (lds) {
+            s_m[li - S0] = mm;
+            s_x[li - S0] = leaf.comX;
+            s_y[li - S0] = leaf.comY;
+            s_next[li - S0] = (li + 1 - S0) | EC_LEAF;
+        }
+    }
+    __syncthreads();
+
+    // ---- jitter cells whose run starts in this chunk (BHA:145-156) ----
+#pragma unroll
+    for (int i = 0; i < EC_PER; ++i) {
+        const int64_t a = a0 + i;
+        if (a >= n || ccs[i] != J || cps[i] == J) continue;
+        const uint32_t jm = jitter_run(
+            n, g, a, cps[i], keys_s, cpl, base, x, y, m, cidx, scratch, err,
+            [&](uint32_t slot, const Node &nd) {
+                nodes[slot] = nd;
+                if (lds && slot >= S0 && slot < S1) {
+                    s_m[slot - S0] = nd.mass;
+                    s_x[slot - S0] = nd.comX;
+                    s_y[slot - S0] = nd.comY;
+                    s_next[slot - S0] = (slot + 1 - S0) | EC_LEAF;
+                }
+            });
+        const uint32_t ni = bases[i] + (uint32_t)(J - cps[i] - 1);  // the jitter cell
+        if (lds && !(s_next[ni - S0] & EC_SPAN))
+            s_next[ni - S0] |= jm << EC_JMASK_SHIFT;
+        else
+            nodes[ni].meta |= jm << NODE_JMASK_SHIFT;  // skeleton written above by this thread
+    }
+    if (!lds) __threadfence_block();
+    __syncthreads();
+
+    // ---- centre of mass of the chunk-local internal nodes (BHA:173-202) ----
+    if (lds) {
         if (threadIdx.x == 0) {
             s_m[COM_CAP] = 0.0;
             s_x[COM_CAP] = 0.0;
             s_y[COM_CAP] = 0.0;
         }
-        // child offsets of every staged local internal node, found once, in parallel
-        for (uint32_t i = threadIdx.x; i < cnt; i += COM_TB) {
+        for (uint32_t i = threadIdx.x; i < cnt; i += EC_TB) {
             const uint32_t nx = s_next[i];
-            if (nx & LDS_LEAF) continue;
-            if (nx & LDS_SPAN) {
+            if (nx & EC_LEAF) continue;
+            if (nx & EC_SPAN) {
                 s_ch[i] = make_ushort4(SPAN_CHILD, SPAN_CHILD, SPAN_CHILD, SPAN_CHILD);
                 continue;
             }
-            const uint32_t end = nx & LDS_NEXT_MASK;
+            const uint32_t e2 = nx & EC_NEXT_MASK;
             uint16_t ch[4] = {NO_CHILD, NO_CHILD, NO_CHILD, NO_CHILD};
             uint32_t c = i + 1;
-            for (int k = 0; k < 4 && c < end; ++k) {
-                ch[k] = (uint16_t)c;
-                c = max(s_next[c] & LDS_NEXT_MASK, c + 1);
+            for (int q = 0; q < 4 && c < e2; ++q) {
+                ch[q] = (uint16_t)c;
+                c = max(s_next[c] & EC_NEXT_MASK, c + 1);
             }
             s_ch[i] = make_ushort4(ch[0], ch[1], ch[2], ch[3]);
         }
     }
     __syncthreads();
     const int top = s_lmax;
-    // level masks: bit i set when body a0+i owns a depth-L node (cp < L <= cc)
     for (int L = top; L >= 0; --L) {
         uint32_t mask = 0;
 #pragma unroll
-        for (int i = 0; i < COM_PER_THREAD; ++i)
+        for (int i = 0; i < EC_PER; ++i)
             if (ccs[i] >= L && cps[i] < L) mask |= 1u << i;
         if (lds) {
-            while (mask) {  // usually one node per lane and level
+            while (mask) {
                 const int i = __builtin_ctz(mask);
                 mask &= mask - 1;
                 int cpi = cps[0];
                 uint32_t bi = bases[0];
 #pragma unroll
-                for (int q = 1; q < COM_PER_THREAD; ++q)
+                for (int q = 1; q < EC_PER; ++q)
                     if (i == q) {
                         cpi = cps[q];
                         bi = bases[q];
                     }
                 const uint32_t li = bi + (uint32_t)(L - cpi - 1) - S0;
                 const ushort4 chv = s_ch[li];
-                if (chv.x == SPAN_CHILD) continue;  // finished by k_com_span
-                // all four children fetched at once (absent ones read the massless pad)
+                if (chv.x == SPAN_CHILD) continue;  // finished by the span passes
                 const uint16_t cs[4] = {chv.x, chv.y, chv.z, chv.w};
                 double cm[4], ccx[4], ccy[4];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    cm[k] = s_m[cs[k]];
-                    ccx[k] = s_x[cs[k]];
-                    ccy[k] = s_y[cs[k]];
+                for (int q = 0; q < 4; ++q) {
+                    cm[q] = s_m[cs[q]];
+                    ccx[q] = s_x[cs[q]];
+                    ccy[q] = s_y[cs[q]];
                 }
                 double mSum = 0.0, cx = 0.0, cy = 0.0;
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {  // children 0..3 in pre-order (BHA:189-192)
-                    if (cm[k] > 0.0) {
-                        mSum += cm[k];
-                        cx += ccx[k] * cm[k];
-                        cy += ccy[k] * cm[k];
+                for (int q = 0; q < 4; ++q) {  // children 0..3 in pre-order (BHA:189-192)
+                    if (cm[q] > 0.0) {
+                        mSum += cm[q];
+                        cx += ccx[q] * cm[q];
+                        cy += ccy[q] * cm[q];
                     }
                 }
                 double ox, oy;
@@ -813,8 +824,7 @@ __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
                 s_x[li] = ox;
                 s_y[li] = oy;
             }
-            // only LDS traffic inside the level loop: wait on LDS, not on stores
-            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): LDS only inside the level loop
             __builtin_amdgcn_s_barrier();
         } else {
             while (mask) {
@@ -823,20 +833,25 @@ __global__ __launch_bounds__(COM_TB) void k_com_local(int64_t n, Geometry g,
                 const uint32_t ni = bases[i] + (uint32_t)(L - cps[i] - 1);
                 if (!(nodes[ni].meta & NODE_SPAN)) node_com(nodes, ni, g, keys_s[a0 + i], L);
             }
+            __threadfence_block();
             __syncthreads();
         }
     }
-    if (lds) {  // write the chunk's local internal nodes back once
+    if (lds) {  // the chunk's local internal nodes, complete, once
         __syncthreads();
-        for (uint32_t i = threadIdx.x; i < cnt; i += COM_TB) {
+        for (uint32_t i = threadIdx.x; i < cnt; i += EC_TB) {
             const uint32_t nx = s_next[i];
-            if (nx & (LDS_LEAF | LDS_SPAN)) continue;
-            Node *dst = nodes + S0 + i;
+            if (nx & (EC_LEAF | EC_SPAN)) continue;
             const double mSum = s_m[i];
-            dst->comX = s_x[i];
-            dst->comY = s_y[i];
-            dst->mass = mSum;
-            if (!(mSum > 0.0)) dst->meta |= NODE_SKIP;
+            Node nd;
+            nd.comX = s_x[i];
+            nd.comY = s_y[i];
+            nd.mass = mSum;
+            nd.next = (nx & EC_NEXT_MASK) + S0;
+            nd.meta = ((nx >> EC_D2_SHIFT) & 0xFFu) |
+                      (((nx >> EC_JMASK_SHIFT) & 0xFu) << NODE_JMASK_SHIFT) |
+                      (mSum > 0.0 ? 0u : NODE_SKIP);
+            nodes[S0 + i] = nd;
         }
     }
 }
@@ -901,7 +916,7 @@ __global__ __launch_bounds__(TB) void k_span_find(int64_t n, int J, int D0,
 }
 
 // Children of every chunk-spanning node with the values of the local ones (final after
-// k_com_local), gathered in parallel so the level-by-level pass below reads one
+// k_emit_com), gathered in parallel so the level-by-level pass below reads one
 // independent record per level.
 __global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__restrict__ span_list,
                                                       uint32_t span_stride,
@@ -1145,12 +1160,9 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     if (st != hipSuccess) return st;
     k_cells<<<grid_for(((int64_t)1 << (2 * D0)) + 1), TB, 0, s>>>(n, g.J, D0, b.keys_s,
                                                                   b.cell_start);
-    k_emit<<<grid_for(n), TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cpl, b.base, b.cell_start, b.dst.x,
-                                      b.dst.y, b.dst.m, b.nodes);
-    k_jitter<<<grid_for(n), TB, 0, s>>>(n, g, b.keys_s, b.cpl, b.base, b.dst.x, b.dst.y, b.dst.m,
-                                        b.dst.cidx, b.idx, b.nodes, b.scalars + 1);
-    k_com_local<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), COM_TB, 0, s>>>(
-        n, g, b.keys_s, b.cpl, b.base, b.nodes);
+    k_emit_com<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), EC_TB, 0, s>>>(
+        n, g, D0, b.keys_s, b.cpl, b.base, b.cell_start, b.dst.x, b.dst.y, b.dst.m, b.dst.cidx,
+        b.idx, b.nodes, b.scalars + 1);
     const dim3 span_grid((b.span_stride + TB - 1) / TB, g.J + 1);
     const uint32_t n_groups = span_groups(b.span_stride);
     if (n_groups > 1) {
