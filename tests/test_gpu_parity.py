@@ -303,6 +303,28 @@ def test_c5_full_size_theta0_sampled():
     _assert_sampled_evaluation(scenes.config_scene("c5"), 0.0, 256)
 
 
+def test_deep_pairs_chunks_beyond_lds_capacity():
+    """Close pairs (1e-2 apart: ~17 nested cells each) and jitter pairs (4e-4 apart) make the
+    1024-body chunks need far more node slots than the LDS holds, so the fused emit/COM kernel
+    (tree_build.hip k_emit_com) takes its global-memory path; 3 steps bit-identical."""
+    rng = np.random.default_rng(31)
+    npair = 3000
+    cx = rng.uniform(100.0, 2300.0, npair)
+    cy = rng.uniform(50.0, 750.0, npair)
+    sep = np.where(rng.random(npair) < 0.1, 4e-4, 1e-2)
+    ang = rng.uniform(0.0, 2 * np.pi, npair)
+    x = np.concatenate([cx, cx + sep * np.cos(ang)])
+    y = np.concatenate([cy, cy + sep * np.sin(ang)])
+    m = rng.uniform(0.5, 2.0, 2 * npair)
+    perm = rng.permutation(2 * npair)
+    arrs = (x[perm], y[perm], np.zeros(2 * npair), np.zeros(2 * npair), m[perm])
+    eng, ref = _pair(arrs, theta=0.5, merge_min_dist=0.0)
+    _assert_acc_equal(eng, ref)
+    eng.step(3)
+    ref.step(3)
+    _assert_state_equal(eng, ref)
+
+
 def test_bucket_sort_collapse_oversized_buckets():
     """A cloud whose velocities aim every body at the centre: the first drift shrinks it 50x,
     the next one flings it out again, so the previous build's splitters (the adaptive bucket
