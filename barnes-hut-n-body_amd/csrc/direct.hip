@@ -18,7 +18,10 @@ namespace bh {
 namespace {
 
 constexpr int TB = 256;
-constexpr int TILE = 1024;
+#ifndef BH_DIRECT_TILE
+#define BH_DIRECT_TILE 1024
+#endif
+constexpr int TILE = BH_DIRECT_TILE;
 
 __global__ __launch_bounds__(TB) void k_leaf_flags(const Node *__restrict__ nodes,
                                                    const uint32_t *__restrict__ d_T,
@@ -77,7 +80,10 @@ template <bool FAST>
 __device__ __forceinline__ void sum_tile(const double4_t *s_rec, int cnt, double bx, double by,
                                          double Gm, double soft2, uint32_t self, double &fx,
                                          double &fy) {
-    constexpr int U = 4;
+#ifndef BH_DIRECT_U
+#define BH_DIRECT_U 4
+#endif
+    constexpr int U = BH_DIRECT_U;
     int j = 0;
     for (; j + U <= cnt; j += U) {
         double4_t r[U];
