@@ -60,6 +60,18 @@ def measured_traffic(config, kernel):
     return ent.get("hbm_bytes_per_launch"), ent.get("source")
 
 
+def measured_valu_busy(config, kernel):
+    """VALU-busy fraction of `kernel` on this workload from the committed SQ counter summary
+    (profiles/valu_busy.json, written by tools/summarize_sq.py), or None: the traversal is
+    fp64-VALU bound, so this is its efficiency figure next to the HBM roofline."""
+    try:
+        with open(os.path.join(ROOT, "profiles", "valu_busy.json")) as fh:
+            ent = json.load(fh).get(config, {}).get(kernel)
+    except (OSError, ValueError):
+        return None
+    return ent
+
+
 def scene_for(config, world):
     from bh_amd import scenes
     if config == "c3" and world > 1:
@@ -190,6 +202,7 @@ def main():
             "launches": trav_launches,
             "rounds_per_eval": bh_amd.SHARD_ROUNDS if world > 1 else 1,
             "vbar_nodes_per_body_eval": round(vbar, 2),
+            "valu_busy": (measured_valu_busy(scene_name, "k_traverse") or {}).get("valu_busy"),
             "wave_lane_efficiency": round(lane_eff, 4),
             "bytes_per_launch": round(bytes_per_launch),
         }

@@ -9,6 +9,7 @@ kernel length GRBM_GUI_ACTIVE / 8 XCDs (counters summed over the shader engines)
 import collections
 import csv
 import glob
+import json
 import os
 import sys
 
@@ -50,6 +51,19 @@ def main():
                    f"waiting on memory (WAIT_ANY) {100 * avg.get('SQ_WAIT_ANY', 0) / wc:.0f} %, "
                    f"waiting for issue (WAIT_INST_ANY) {100 * avg.get('SQ_WAIT_INST_ANY', 0) / wc:.0f} %")
     open(prefix + "_sq_summary.md", "w").write("\n".join(out) + "\n")
+    if "GRBM_GUI_ACTIVE" in avg and "SQ_ACTIVE_INST_VALU" in avg:  # for bench.py's roofline
+        path = os.path.join(os.path.dirname(prefix) or ".", "valu_busy.json")
+        try:
+            doc = json.load(open(path))
+        except (OSError, ValueError):
+            doc = {}
+        doc.setdefault("c3", {})["k_traverse"] = {
+            "valu_busy": round(busy / klen, 4),
+            "valu_insts_per_wave": round(avg.get("SQ_INSTS_VALU", 0) / waves) if waves else None,
+            "method": "SQ_ACTIVE_INST_VALU x 4 / 1024 SIMDs over GRBM_GUI_ACTIVE / 8 XCDs",
+            "source": prefix + "_sq_summary.md",
+        }
+        json.dump(doc, open(path, "w"), indent=1)
     print("\n".join(out))
 
 
