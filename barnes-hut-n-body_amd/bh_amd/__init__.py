@@ -41,6 +41,7 @@ EXPORTED_SYMBOLS = (
     "bh_selftest_fast_math", "bh_scene_galaxy_disk", "bh_scene_kepler_disk", "bh_scene_uniform",
     "bh_nbody3d_create", "bh_nbody3d_destroy", "bh_nbody3d_last_error", "bh_nbody3d_set",
     "bh_nbody3d_step", "bh_nbody3d_accelerations", "bh_nbody3d_get", "bh_nbody3d_last_ms",
+    "bh_local_group_create", "bh_local_group_destroy", "bh_create_local",
 )
 
 
@@ -86,6 +87,11 @@ def load_library(path: str | None = None):
     lib.bh_create_dist.argtypes = [ctypes.POINTER(BhParams), ctypes.c_int, ctypes.c_int,
                                    ctypes.c_int, ctypes.c_char_p, ctypes.POINTER(_VP)]
     lib.bh_comm_unique_id.argtypes = [ctypes.c_char_p]
+    lib.bh_local_group_create.argtypes = [ctypes.c_int, ctypes.POINTER(_VP)]
+    lib.bh_local_group_destroy.argtypes = [_VP]
+    lib.bh_local_group_destroy.restype = None
+    lib.bh_create_local.argtypes = [ctypes.POINTER(BhParams), ctypes.c_int, ctypes.c_int, _VP,
+                                    ctypes.POINTER(_VP)]
     lib.bh_destroy.argtypes = [_VP]
     lib.bh_destroy.restype = None
     lib.bh_last_error.argtypes = [_VP]
@@ -242,15 +248,38 @@ def comm_unique_id() -> bytes:
     return buf.raw
 
 
+class LocalGroup:
+    """In-process rank group (bh_local_group_*): the multi-GPU decomposition with device-to-
+    device copies in place of RCCL, for `world` engines driven by one thread each."""
+
+    def __init__(self, world: int):
+        self._lib = load_library()
+        self._h = _VP()
+        rc = self._lib.bh_local_group_create(int(world), ctypes.byref(self._h))
+        if rc != BH_OK:
+            raise BhError(rc, "bh_local_group_create failed")
+        self.world = world
+
+    def close(self):  # after every member engine is closed
+        if self._h:
+            self._lib.bh_local_group_destroy(self._h)
+            self._h = _VP()
+
+
 class Engine:
     """The C-ABI, one call per method.  State lives in HBM; arrays are copied in/out."""
 
     def __init__(self, params: BhParams | None = None, device: int = 0, rank: int = 0,
-                 world: int = 1, unique_id: bytes | None = None):
+                 world: int = 1, unique_id: bytes | None = None,
+                 local_group: "LocalGroup | None" = None):
         self._lib = load_library()
         self._h = _VP()
         self.params = params if params is not None else default_params()
-        if world > 1 or unique_id is not None:
+        if local_group is not None:
+            world = local_group.world
+            rc = self._lib.bh_create_local(ctypes.byref(self.params), device, rank,
+                                           local_group._h, ctypes.byref(self._h))
+        elif world > 1 or unique_id is not None:
             rc = self._lib.bh_create_dist(ctypes.byref(self.params), device, rank, world,
                                           unique_id, ctypes.byref(self._h))
         else:

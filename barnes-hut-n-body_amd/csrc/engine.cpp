@@ -16,6 +16,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <iterator>
@@ -33,6 +35,30 @@ namespace {
 constexpr int kPhases = 5;  // build, traverse, integrate, merge, allgather
 }  // namespace
 
+// In-process rank group (bh_local_group_*): `world` engines of one process, one host thread
+// each, that exchange the force pieces through device-to-device copies instead of RCCL -- the
+// same pieces, rounds and in-place layout as the ncclAllGather path, so the multi-rank
+// decomposition runs on one GPU (RCCL refuses several ranks per device).
+struct bh_local_group {
+    int world = 0;
+    std::vector<bh_engine *> members;
+    std::mutex mu;
+    std::condition_variable cv;
+    int arrived = 0;
+    uint64_t generation = 0;
+    void barrier() {
+        std::unique_lock<std::mutex> lk(mu);
+        const uint64_t gen = generation;
+        if (++arrived == world) {
+            arrived = 0;
+            ++generation;
+            cv.notify_all();
+        } else {
+            cv.wait(lk, [&] { return generation != gen; });
+        }
+    }
+};
+
 struct bh_engine {
     bh_params p{};
     Geometry geo{};
@@ -40,6 +66,7 @@ struct bh_engine {
     hipStream_t stream = nullptr;
     int rank = 0, world = 1;
     ncclComm_t comm = nullptr;
+    bh_local_group *group = nullptr;             // in-process ranks (test path), or RCCL:
     hipStream_t comm_stream = nullptr;            // all-gathers, overlapping the next round
     hipEvent_t round_ev[BH_SHARD_ROUNDS] = {};   // round k's forces written (compute stream)
     hipEvent_t gathered_ev = nullptr;            // every round gathered (comm stream)
@@ -211,7 +238,7 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(alloc_state(e, e->st, cap));
         TRY(alloc_state(e, e->alt, cap));
         // multi-GPU: rounds x world pieces of whole wavefronts (bh_shard_range)
-        const int64_t padded = e->comm ? shard_sub(cap, e->world, BH_SHARD_ROUNDS) *
+        const int64_t padded = (e->comm || e->group) ? shard_sub(cap, e->world, BH_SHARD_ROUNDS) *
                                              e->world * BH_SHARD_ROUNDS
                                        : cap;
         TRY(dev_alloc(e, e->a2, 2 * padded));
@@ -388,13 +415,18 @@ int evaluate(bh_engine *e, uint32_t *visits) {
             traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, lo, hi, e->geo, fp,
                      e->a2, vis, vis ? e->wave_iters : nullptr, e->stream);
     };
-    if (!e->comm || visits) {
+    if ((!e->comm && !e->group) || visits) {
         forces(0, n, visits);
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
         return BH_OK;
     }
     const int64_t sub = shard_sub(n, e->world, BH_SHARD_ROUNDS);
+    if (e->group) {  // a collective's implicit ordering: peers' copies of our last pieces done
+        e->group->barrier();
+        for (bh_engine *peer : e->group->members)
+            if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->gathered_ev, 0));
+    }
     for (int k = 0; k < BH_SHARD_ROUNDS; ++k) {
         int64_t lo = 0, hi = 0;
         bh_shard_range(n, e->rank, e->world, k, &lo, &hi);
@@ -403,8 +435,20 @@ int evaluate(bh_engine *e, uint32_t *visits) {
         HIPCHK(e, hipEventRecord(e->round_ev[k], e->stream));
         HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
         double *piece = e->a2 + 2 * ((int64_t)k * e->world) * sub;  // round k, rank 0
-        NCCLCHK(e, ncclAllGather(piece + 2 * e->rank * sub, piece, (size_t)(2 * sub), ncclDouble,
-                                 e->comm, e->comm_stream));
+        if (e->comm) {
+            NCCLCHK(e, ncclAllGather(piece + 2 * e->rank * sub, piece, (size_t)(2 * sub),
+                                     ncclDouble, e->comm, e->comm_stream));
+        } else {  // in-process: every member recorded round k, then copy the peers' pieces
+            e->group->barrier();
+            for (int q = 0; q < e->world; ++q) {
+                if (q == e->rank) continue;
+                bh_engine *peer = e->group->members[q];
+                HIPCHK(e, hipStreamWaitEvent(e->comm_stream, peer->round_ev[k], 0));
+                const int64_t off = 2 * ((int64_t)k * e->world + q) * sub;
+                HIPCHK(e, hipMemcpyAsync(e->a2 + off, peer->a2 + off, sizeof(double) * 2 * sub,
+                                         hipMemcpyDeviceToDevice, e->comm_stream));
+            }
+        }
     }
     TRY(mark(e, 1));
     HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
@@ -703,12 +747,61 @@ int bh_create_dist(const bh_params *p, int device, int rank, int world, const vo
     return BH_OK;
 }
 
+int bh_local_group_create(int world, bh_local_group **out) {
+    if (!out || world < 1) return BH_E_INVALID;
+    bh_local_group *g = new bh_local_group();
+    g->world = world;
+    g->members.assign((size_t)world, nullptr);
+    *out = g;
+    return BH_OK;
+}
+
+void bh_local_group_destroy(bh_local_group *g) { delete g; }
+
+int bh_create_local(const bh_params *p, int device, int rank, bh_local_group *group,
+                    bh_engine **out) {
+    if (!out || !group || rank < 0 || rank >= group->world || group->members[rank])
+        return BH_E_INVALID;
+    *out = nullptr;
+    bh_engine *e = new bh_engine();
+    e->rank = rank;
+    e->world = group->world;
+    int rc = engine_init(e, p, device);
+    if (rc == BH_OK) {
+        hipError_t hr = hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking);
+        for (int k = 0; k < BH_SHARD_ROUNDS && hr == hipSuccess; ++k)
+            hr = hipEventCreateWithFlags(&e->round_ev[k], hipEventDisableTiming);
+        if (hr == hipSuccess) hr = hipEventCreateWithFlags(&e->gathered_ev, hipEventDisableTiming);
+        if (hr != hipSuccess) {
+            e->err = std::string("comm stream/events: ") + hipGetErrorString(hr);
+            rc = BH_E_DEVICE;
+        }
+    }
+    if (rc == BH_OK) {
+        e->group = group;
+        const int64_t cap = e->cap;  // the accelerations buffer in rounds x world pieces
+        e->cap = 0;
+        rc = ensure_capacity(e, cap);
+    }
+    if (rc != BH_OK) {
+        std::fprintf(stderr, "bh_create_local: %s\n", e->err.c_str());
+        e->group = nullptr;
+        bh_destroy(e);
+        return rc;
+    }
+    group->members[rank] = e;
+    *out = e;
+    return BH_OK;
+}
+
 void bh_destroy(bh_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
     if (e->comm) (void)ncclCommDestroy(e->comm);
+    if (e->group && e->rank < (int)e->group->members.size() && e->group->members[e->rank] == e)
+        e->group->members[e->rank] = nullptr;
     for (hipEvent_t ev : e->round_ev)
         if (ev) (void)hipEventDestroy(ev);
     if (e->gathered_ev) (void)hipEventDestroy(e->gathered_ev);

@@ -66,6 +66,16 @@ int bh_create_dist(const bh_params *p, int device, int rank, int world, const vo
                    bh_engine **out);
 int bh_comm_unique_id(void *out128);
 
+/* In-process rank group (testing the multi-GPU decomposition on one device, where RCCL refuses
+ * several ranks): `world` engines of one process, each driven by its own host thread with
+ * identical calls, exchange the force pieces with device-to-device copies on the same pieces,
+ * rounds and in-place layout as bh_create_dist's ncclAllGather. */
+typedef struct bh_local_group bh_local_group;
+int bh_local_group_create(int world, bh_local_group **out);
+void bh_local_group_destroy(bh_local_group *g);  /* after its members' bh_destroy */
+int bh_create_local(const bh_params *p, int device, int rank, bh_local_group *group,
+                    bh_engine **out);
+
 void bh_destroy(bh_engine *e);
 const char *bh_last_error(const bh_engine *e);
 

@@ -529,3 +529,44 @@ def test_c5_fp32_vs_fp64_tolerance_study():
     assert np.all(fz == 0.0)
     assert np.percentile(err, 99.9) < 1e-3, np.percentile(err, [50, 99, 99.9, 100])
     eng.close()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_multi_rank_decomposition_in_process(world):
+    """The multi-GPU step with `world` ranks on one GPU (bh_create_local: one host thread per
+    rank, the in-place all-gather of every round emulated with device-to-device copies, RCCL
+    being unable to host several ranks per device): every rank's state after 3 steps of a
+    merge-active scene, and one theta = 0 evaluation, bit-identical to the oracle."""
+    import threading
+    for theta in (0.5, 0.0):
+        arrs = scenes.config_scene("c1_code")
+        group = bh_amd.LocalGroup(world)
+        engines = [bh_amd.Engine(bh_amd.default_params(theta=theta), device=0, rank=r,
+                                 local_group=group) for r in range(world)]
+        results, errors = [None] * world, []
+
+        def run(r):
+            try:
+                engines[r].reset_bodies(*arrs)
+                engines[r].step(3)
+                results[r] = engines[r].get_bodies()
+            except Exception as exc:  # surfaced below
+                errors.append(exc)
+
+        threads = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=120)
+        assert not errors, errors
+        assert not any(t.is_alive() for t in threads), "rank thread hung"
+        ref = oracle.Oracle(*arrs, theta=theta)
+        ref.step(3)
+        want = ref.get_bodies()
+        for r in range(world):
+            for k, name in enumerate(FIELDS):
+                assert bits_equal(results[r][k], want[k]), f"rank {r} theta {theta}: {name}"
+        for e in engines:
+            e.close()
+        group.close()
+        ref.close()
