@@ -236,6 +236,15 @@ __device__ __forceinline__ void bitonic_sort(uint64_t *A, uint32_t s) {
     }
 }
 
+// Buckets of up to RADIX_CAP elements: one counting pass on the top 8 bits of the key
+// prefix's span inside the bucket (bins are key ranges, so bins in order are sorted relative
+// to each other), then every element's rank inside its bin -- bins hold a few elements, ties
+// of equal prefixes included, ordered by the whole composite.  A bin above RADIX_MAXBIN
+// (clustered keys) sends the bucket to the bitonic network instead.
+constexpr int RADIX_CAP = SORT_CAP / 2;  // the bin-grouped copy lives in the upper half of L
+constexpr int RADIX_BINS = 256;
+constexpr uint32_t RADIX_MAXBIN = 48;
+
 __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restrict__ starts,
                                                          uint32_t *__restrict__ counts,
                                                          uint64_t *comp,
@@ -244,31 +253,100 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
                                                          uint32_t *__restrict__ perm,
                                                          uint64_t *keys_s) {
     __shared__ uint64_t L[SORT_CAP];
+    __shared__ uint32_t s_cnt[RADIX_BINS], s_start[RADIX_BINS];
+    __shared__ uint32_t s_min, s_max, s_maxbin;
     const uint32_t t = blockIdx.x;
     const uint32_t b0 = starts[t], s = starts[t + 1] - b0;
     if (threadIdx.x == 0) counts[t] = 0;  // ready for the next build (counts were scanned)
+    auto emit = [&](uint32_t j, uint64_t v) __attribute__((always_inline)) {
+        const uint32_t src = (uint32_t)v;
+        keys32_s[b0 + j] = (uint32_t)(v >> 32);
+        perm[b0 + j] = src;
+        keys_s[b0 + j] = keys[src];  // comp and keys_s share storage: L holds the bucket
+    };
     if (s <= (uint32_t)SORT_CAP) {
-        for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) L[j] = comp[b0 + j];
+        if (threadIdx.x == 0) {
+            s_min = 0xFFFFFFFFu;
+            s_max = 0;
+            s_maxbin = 0;
+        }
+        if (threadIdx.x < RADIX_BINS) s_cnt[threadIdx.x] = 0;
         __syncthreads();
+        uint32_t kmin = 0xFFFFFFFFu, kmax = 0;
+        for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) {
+            const uint64_t v = comp[b0 + j];
+            L[j] = v;
+            kmin = min(kmin, (uint32_t)(v >> 32));
+            kmax = max(kmax, (uint32_t)(v >> 32));
+        }
+        bool radix = s <= (uint32_t)RADIX_CAP;
+        if (radix) {
+            atomicMin(&s_min, kmin);
+            atomicMax(&s_max, kmax);
+        }
+        __syncthreads();
+        if (radix) {
+            const uint32_t lo = s_min, span = s_max - s_min;
+            const int shift = span >= RADIX_BINS ? (32 - __clz(span)) - 8 : 0;  // span >> shift < 256
+            uint32_t bin[RADIX_CAP / SORT_TB], off[RADIX_CAP / SORT_TB];
+#pragma unroll
+            for (int r = 0; r < RADIX_CAP / SORT_TB; ++r) {
+                const uint32_t j = threadIdx.x + r * SORT_TB;
+                if (j < s) {
+                    bin[r] = ((uint32_t)(L[j] >> 32) - lo) >> shift;
+                    off[r] = atomicAdd(&s_cnt[bin[r]], 1u);
+                }
+            }
+            __syncthreads();
+            static_assert(RADIX_BINS == SORT_TB, "one bin per thread");
+            {  // inclusive scan of the bin counts: within each wave by shuffles, then wave sums
+                const uint32_t c = s_cnt[threadIdx.x];
+                atomicMax(&s_maxbin, c);
+                const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+                uint32_t v = c;
+#pragma unroll
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t u = __shfl_up(v, d, 64);
+                    if (lane >= d) v += u;
+                }
+                if (lane == 63) s_start[w] = v;  // wave totals (slots 0..3, rewritten below)
+                __syncthreads();
+                uint32_t add = 0;
+                for (int q = 0; q < w; ++q) add += s_start[q];
+                __syncthreads();
+                s_start[threadIdx.x] = v + add;
+            }
+            __syncthreads();
+            radix = s_maxbin <= RADIX_MAXBIN;  // uniform
+            if (radix) {
+                uint64_t *G = L + RADIX_CAP;  // bin-grouped copy
+#pragma unroll
+                for (int r = 0; r < RADIX_CAP / SORT_TB; ++r) {
+                    const uint32_t j = threadIdx.x + r * SORT_TB;
+                    if (j < s) G[s_start[bin[r]] - s_cnt[bin[r]] + off[r]] = L[j];
+                }
+                __syncthreads();
+#pragma unroll
+                for (int r = 0; r < RADIX_CAP / SORT_TB; ++r) {
+                    const uint32_t j = threadIdx.x + r * SORT_TB;
+                    if (j < s) {
+                        const uint32_t be = s_start[bin[r]], bs = be - s_cnt[bin[r]];
+                        const uint64_t v = L[j];
+                        uint32_t rank = 0;
+                        for (uint32_t q = bs; q < be; ++q) rank += G[q] < v ? 1u : 0u;
+                        emit(bs + rank, v);
+                    }
+                }
+                return;
+            }
+        }
         bitonic_sort<true>(L, s);
         __syncthreads();
-        for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) {
-            const uint64_t v = L[j];
-            const uint32_t src = (uint32_t)v;
-            keys32_s[b0 + j] = (uint32_t)(v >> 32);
-            perm[b0 + j] = src;
-            keys_s[b0 + j] = keys[src];  // comp and keys_s share storage: L holds the bucket
-        }
+        for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) emit(j, L[j]);
     } else {  // oversized bucket: the same network on global memory, in place
         uint64_t *A = comp + b0;
         bitonic_sort<false>(A, s);
-        for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) {  // each thread its own j: in place
-            const uint64_t v = A[j];
-            const uint32_t src = (uint32_t)v;
-            keys32_s[b0 + j] = (uint32_t)(v >> 32);
-            perm[b0 + j] = src;
-            keys_s[b0 + j] = keys[src];
-        }
+        for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) emit(j, A[j]);  // own j: in place
     }
 }
 
