@@ -1,0 +1,15 @@
+set -u
+cd "${GRAFT_REPO_ROOT}"
+export TMPDIR=/tmp
+OUT=gpurun_out/prof_sq2
+mkdir -p $OUT
+ARGS="--steps 2 --warmup 1 --no-cpu-baseline"
+i=0
+for SET in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_ANY SQ_WAIT_INST_ANY SQ_WAIT_ANY GRBM_GUI_ACTIVE" \
+           "SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_SMEM SQ_INSTS_VMEM_RD SQ_INSTS_LDS SQ_WAVES SQ_INSTS_VMEM_WR" \
+           "SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_INSTS_BRANCH" ; do
+  i=$((i+1))
+  timeout -k 10 300 rocprofv3 --pmc $SET --kernel-trace -d $OUT/p$i -o run --output-format csv \
+    -- python3 bench.py $ARGS > $OUT/p$i.log 2>&1 || { echo "pass $i rc=$?"; tail -5 $OUT/p$i.log; exit 1; }
+  echo "pass $i ok"
+done

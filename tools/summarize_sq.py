@@ -17,7 +17,11 @@ KERNEL = "k_traverse<false, true>"
 
 
 def main():
+    global KERNEL
     src, prefix = sys.argv[1], sys.argv[2]
+    if len(sys.argv) > 3:  # another kernel: print only, the committed files stay the traversal's
+        KERNEL = sys.argv[3]
+        prefix = "/tmp/sq_other"
     acc = collections.defaultdict(list)  # counter -> per-dispatch totals
     for f in sorted(glob.glob(os.path.join(src, "p*", "*counter_collection.csv"))):
         per = collections.defaultdict(float)
@@ -51,7 +55,7 @@ def main():
                    f"waiting on memory (WAIT_ANY) {100 * avg.get('SQ_WAIT_ANY', 0) / wc:.0f} %, "
                    f"waiting for issue (WAIT_INST_ANY) {100 * avg.get('SQ_WAIT_INST_ANY', 0) / wc:.0f} %")
     open(prefix + "_sq_summary.md", "w").write("\n".join(out) + "\n")
-    if "GRBM_GUI_ACTIVE" in avg and "SQ_ACTIVE_INST_VALU" in avg:  # for bench.py's roofline
+    if KERNEL.startswith("k_traverse") and "GRBM_GUI_ACTIVE" in avg and "SQ_ACTIVE_INST_VALU" in avg:
         path = os.path.join(os.path.dirname(prefix) or ".", "valu_busy.json")
         try:
             doc = json.load(open(path))
