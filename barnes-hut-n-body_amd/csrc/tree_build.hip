@@ -734,6 +734,17 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
     const bool lds = cnt <= (uint32_t)COM_CAP;
     __syncthreads();
     atomicMax(&s_lmax, lmax);
+    // Phases exchange data through LDS only (in the LDS mode): the barriers wait for LDS, not
+    // for the global stores of leaves and skeletons, which nothing in this kernel reads back.
+    auto phase_barrier = [&]() __attribute__((always_inline)) {
+        if (lds) {
+            __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0)
+            __builtin_amdgcn_s_barrier();
+        } else {
+            __threadfence_block();
+            __syncthreads();
+        }
+    };
 
     // ---- skeletons and leaves (BHA:125-137, 159-166, 176-178) ----
     const uint64_t SENT = sentinel_key(J);
@@ -801,7 +812,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
             s_next[li - S0] = (li + 1 - S0) | EC_LEAF;
         }
     }
-    __syncthreads();
+    phase_barrier();
 
     // ---- jitter cells whose run starts in this chunk (BHA:145-156) ----
 #pragma unroll
@@ -825,8 +836,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
         else
             nodes[ni].meta |= jm << NODE_JMASK_SHIFT;  // skeleton written above by this thread
     }
-    if (!lds) __threadfence_block();
-    __syncthreads();
+    phase_barrier();
 
     // ---- centre of mass of the chunk-local internal nodes (BHA:173-202) ----
     if (lds) {
@@ -852,7 +862,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
             s_ch[i] = make_ushort4(ch[0], ch[1], ch[2], ch[3]);
         }
     }
-    __syncthreads();
+    phase_barrier();
     const int top = s_lmax;
     for (int L = top; L >= 0; --L) {
         uint32_t mask = 0;
@@ -916,7 +926,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
         }
     }
     if (lds) {  // the chunk's local internal nodes, complete, once
-        __syncthreads();
+        phase_barrier();
         for (uint32_t i = threadIdx.x; i < cnt; i += EC_TB) {
             const uint32_t nx = s_next[i];
             if (nx & (EC_LEAF | EC_SPAN)) continue;
