@@ -248,11 +248,23 @@ def test_deterministic_rerun():
         assert bits_equal(u, v)
 
 
-def test_c2_kepler_1e5_steps():
+def test_c2_kepler_1e5_100_steps():
+    """C2 (Kepler disk, 1e5 bodies, theta 0.5) over the north star's 100 steps (SURVEY §8d
+    parity runs: K = 100 for C1/C2): positions, velocities and masses bit-identical, i.e.
+    zero drift against the <= 1e-6 bound."""
     arrs = scenes.config_scene("c2")
     eng, ref = _pair(arrs, theta=0.5)
-    eng.step(3)
-    ref.step(3)
+    eng.step(100)
+    ref.step(100)
+    _assert_state_equal(eng, ref)
+
+
+def test_c3_1e6_10_steps():
+    """C3 (two colliding disks, 1e6 bodies, merge rule active) over K = 10 steps."""
+    arrs = scenes.config_scene("c3")
+    eng, ref = _pair(arrs, theta=0.5)
+    eng.step(10)
+    ref.step(10)
     _assert_state_equal(eng, ref)
 
 
