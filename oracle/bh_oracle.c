@@ -487,7 +487,37 @@ static int g_sim_q, g_sim_t;
 static int g_sim_cnt[64];
 static int64_t g_sim_flushes;
 
+/* Pair-merge model (analysis helper): a wave defers its point-force block by one iteration
+ * and runs the next iteration's block together with it when the two lane sets are
+ * disjoint (each lane still adds its terms in order).  Counts blocks under that rule. */
+static uint64_t g_pm_pend;
+static int64_t g_pm_blocks, g_pm_merges;
+
+static void pm_push(uint64_t contrib) {
+    if (g_pm_pend) {
+        ++g_pm_blocks;
+        if (contrib && !(contrib & g_pm_pend)) {
+            ++g_pm_merges;
+            g_pm_pend = 0;
+            return;
+        }
+        g_pm_pend = 0;
+    }
+    g_pm_pend = contrib;
+}
+
+static void pm_drain(void) {
+    if (g_pm_pend) ++g_pm_blocks;
+    g_pm_pend = 0;
+}
+
+void oracle_pairmerge_stats(int64_t *blocks, int64_t *merges) {
+    *blocks = g_pm_blocks;
+    *merges = g_pm_merges;
+}
+
 static void sim_push(uint64_t contrib) {
+    pm_push(contrib);
     if (!g_sim_q) return;
     int full = 0, nonempty = 0;
     for (int l = 0; l < 64; ++l) {
@@ -571,10 +601,13 @@ int64_t oracle_group_union(oracle_engine *e, const int64_t *order, int64_t count
     ForceCtx c = {e->p.G, e->p.soft2, e->p.theta * e->p.theta};
     int64_t iters = 0, lv = 0;
     g_force_iters = g_contribs = 0;
+    g_pm_blocks = g_pm_merges = 0;
+    g_pm_pend = 0;
     for (int64_t g0 = 0; g0 < count; g0 += group) {
         const int nb = (int)((count - g0) < group ? (count - g0) : group);
         const uint64_t mask = nb == 64 ? ~0ull : ((1ull << nb) - 1);
         const int64_t it = union_walk(&e->tree, &c, 0, order + g0, mask, &lv);
+        pm_drain();
         if (g_sim_q) sim_drain();
         if (per_group) per_group[g0 / group] = it;
         iters += it;

@@ -24,8 +24,19 @@ def _pair(arrs, **kw):
     p = bh_amd.default_params(theta=theta, **kw)
     eng = bh_amd.Engine(p, device=0)
     eng.reset_bodies(*arrs)
+    eng.initial = arrs  # for a second engine on the same start (a build may jitter positions)
     ref = oracle.Oracle(*arrs, theta=theta, **kw)
     return eng, ref
+
+
+def _production_walk(eng):
+    """Accelerations of the production walk (paired force blocks, no counters) on a fresh
+    engine from the same start: a second build on `eng` would see jittered positions."""
+    e2 = bh_amd.Engine(eng.params, device=0)
+    e2.reset_bodies(*eng.initial)
+    fx, fy = e2.compute_accelerations()
+    e2.close()
+    return fx, fy
 
 
 def _assert_state_equal(eng, ref, nan_ok=False):
@@ -40,8 +51,15 @@ def _assert_state_equal(eng, ref, nan_ok=False):
 
 
 def _assert_acc_equal(eng, ref, nan_ok=False):
+    """Accelerations and visit counts vs the oracle.  The engine evaluates twice on the same
+    tree: the production walk (no counters: paired force blocks) and the counting walk."""
+    fx, fy = _production_walk(eng)
     ax, ay, vis = eng.compute_accelerations(visits=True)
     rax, ray, rvis = ref.accelerations(visits=True)
+    if nan_ok:
+        assert np.array_equal(fx, rax, equal_nan=True) and np.array_equal(fy, ray, equal_nan=True)
+    else:
+        assert bits_equal(fx, rax) and bits_equal(fy, ray), "production walk differs"
     if nan_ok:
         assert np.array_equal(ax, rax, equal_nan=True)
         assert np.array_equal(ay, ray, equal_nan=True)
@@ -289,9 +307,11 @@ def _assert_sampled_evaluation(arrs, theta, stride):
         ax, ay = eng.compute_accelerations()
         rax, ray = ref.accelerations(subset=sample)
     else:
+        fx, fy = _production_walk(eng)  # paired force blocks
         ax, ay, vis = eng.compute_accelerations(visits=True)
         rax, ray, rvis = ref.accelerations(subset=sample, visits=True)
         assert np.array_equal(vis[sample], rvis), "node-visit counts differ"
+        assert bits_equal(fx[sample], rax) and bits_equal(fy[sample], ray), "production walk"
     bad = np.flatnonzero(ax[sample].view(np.int64) != rax.view(np.int64))
     assert bad.size == 0, f"ax: {bad.size} of {len(sample)} sampled bodies differ"
     assert bits_equal(ay[sample], ray)
