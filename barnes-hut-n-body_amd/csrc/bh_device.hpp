@@ -157,10 +157,19 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
 // ---- launchers (traverse.hip) ----------------------------------------------------
 // Accelerations F/m of slots [lo, hi), written interleaved to a2[2p], a2[2p+1].
 // node_cap: allocated node records (reads may run up to one record past the tree's last one).
-void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, const double *x,
-              const double *y, const double *m, int64_t lo, int64_t hi, const Geometry &g,
+// kick (optional, one GPU, no visit counting): the KDK update of the evaluated slots is applied
+// in the kernel's epilogue instead of writing a2 -- KICK_DRIFT = k_kick_drift (BHA:414-422),
+// KICK_ONLY = k_kick (BHA:429-432), same operations in the same order.
+enum KickMode { KICK_NONE = 0, KICK_DRIFT = 1, KICK_ONLY = 2 };
+struct KickArgs {
+    KickMode mode;
+    double *vx, *vy;  // x, y are the traversal's own position arrays
+    double dtHalf, dt;
+};
+void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
+              const double *m, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, uint32_t *visits, uint32_t *wave_iters,
-              hipStream_t s);
+              hipStream_t s, const KickArgs *kick = nullptr);
 // multi-GPU shard pieces (bh_shard_range): `rounds` x `world` pieces of whole wavefronts
 __host__ __device__ inline int64_t shard_sub(int64_t n, int world, int rounds) {
     const int64_t parts = (int64_t)world * rounds;

@@ -393,7 +393,13 @@ int ensure_direct(bh_engine *e) {
 // all-gathered in place on the comm stream while round k + 1 is evaluated; the compute
 // stream waits for the last gather before the kick.  Pieces of different rounds and ranks
 // are disjoint, so the concurrent writes never overlap.
-int evaluate(bh_engine *e, uint32_t *visits) {
+// kick (one GPU, tree walk): the following KDK update is fused into the traversal's epilogue
+// and *fused is set; otherwise the caller runs the integration kernel on a2.
+#ifndef BH_FUSE_KICK
+#define BH_FUSE_KICK 1
+#endif
+int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fused = nullptr) {
+    if (fused) *fused = false;
     const int64_t n = e->n;
     TRY(mark(e, -1));
     TRY(build(e));
@@ -416,7 +422,14 @@ int evaluate(bh_engine *e, uint32_t *visits) {
                      e->a2, vis, vis ? e->wave_iters : nullptr, e->stream);
     };
     if ((!e->comm && !e->group) || visits) {
-        forces(0, n, visits);
+        if (BH_FUSE_KICK && kick != KICK_NONE && !direct && !visits && fused) {
+            const KickArgs ka{kick, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
+            traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, 0, n, e->geo, fp,
+                     e->a2, nullptr, nullptr, e->stream, &ka);
+            *fused = true;
+        } else {
+            forces(0, n, visits);
+        }
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
         return BH_OK;
@@ -560,16 +573,22 @@ int step_once(bh_engine *e) {
     const int64_t n = e->n;
     const double dtHalf = e->p.dt * 0.5;  // BHA:412
     if (n > 0) {
-        TRY(evaluate(e, nullptr));  // a(t)
-        TRY(mark(e, -1));
-        kick_drift(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->p.dt, e->stream);
-        HIPCHK(e, hipGetLastError());
-        TRY(mark(e, 2));
-        TRY(evaluate(e, nullptr));  // a(t+dt)
-        TRY(mark(e, -1));
-        kick(n, e->a2, e->st.vx, e->st.vy, dtHalf, e->stream);
-        HIPCHK(e, hipGetLastError());
-        TRY(mark(e, 2));
+        bool fused = false;  // one GPU: the kicks ride in the traversal's epilogue
+        TRY(evaluate(e, nullptr, KICK_DRIFT, &fused));  // a(t)
+        if (!fused) {
+            TRY(mark(e, -1));
+            kick_drift(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->p.dt,
+                       e->stream);
+            HIPCHK(e, hipGetLastError());
+            TRY(mark(e, 2));
+        }
+        TRY(evaluate(e, nullptr, KICK_ONLY, &fused));  // a(t+dt)
+        if (!fused) {
+            TRY(mark(e, -1));
+            kick(n, e->a2, e->st.vx, e->st.vy, dtHalf, e->stream);
+            HIPCHK(e, hipGetLastError());
+            TRY(mark(e, 2));
+        }
         e->tree_valid = true;  // lastTree = root (BHA:435)
     }
     return merge(e);  // BHA:438

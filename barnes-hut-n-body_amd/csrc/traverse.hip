@@ -134,16 +134,18 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
 #define BH_TRAV_XCD_RUN 64
 #endif
 
-template <bool COUNT, bool OFF32>
+// KICK (KickMode): the integration step that follows the evaluation is applied by the lane
+// itself after its walk -- the body's x, y are only ever read by its own lane (other lanes see
+// it through the leaf records), so the update in place is race-free and a2 is not written.
+template <bool COUNT, bool OFF32, int KICK>
 __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
-                                                 const uint32_t *__restrict__ d_T,
-                                                 const double *__restrict__ x,
-                                                 const double *__restrict__ y,
-                                                 const double *__restrict__ m, int64_t lo,
-                                                 int64_t hi, ForceParams fp, Geometry g,
-                                                 double *__restrict__ a2,
+                                                 const uint32_t *__restrict__ d_T, double *x,
+                                                 double *y, const double *__restrict__ m,
+                                                 int64_t lo, int64_t hi, ForceParams fp,
+                                                 Geometry g, double *__restrict__ a2,
                                                  uint32_t *__restrict__ visits,
-                                                 uint32_t *__restrict__ wave_iters) {
+                                                 uint32_t *__restrict__ wave_iters,
+                                                 KickArgs kick) {
     const int64_t p = lo + (int64_t)xcd_block<BH_TRAV_XCD_RUN>() * TB + threadIdx.x;
     const bool valid = p < hi;
     const double bx = valid ? x[p] : 0.0;
@@ -173,7 +175,18 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     double2_t acc;
     acc.x = fx / bm;
     acc.y = fy / bm;
-    *reinterpret_cast<double2_t *>(a2 + 2 * p) = acc;
+    if (KICK == KICK_NONE) {
+        *reinterpret_cast<double2_t *>(a2 + 2 * p) = acc;
+    } else {  // k_kick_drift / k_kick (integrate.hip), operation for operation
+        const double vxi = kick.vx[p] + acc.x * kick.dtHalf;
+        const double vyi = kick.vy[p] + acc.y * kick.dtHalf;
+        kick.vx[p] = vxi;
+        kick.vy[p] = vyi;
+        if (KICK == KICK_DRIFT) {
+            x[p] = bx + vxi * kick.dt;
+            y[p] = by + vyi * kick.dt;
+        }
+    }
     if (COUNT) visits[p] = nvis;
 }
 
@@ -228,29 +241,31 @@ hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_ba
     return hipGetLastError();
 }
 
-void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, const double *x,
-              const double *y, const double *m, int64_t lo, int64_t hi, const Geometry &g,
+void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
+              const double *m, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, uint32_t *visits, uint32_t *wave_iters,
-              hipStream_t s) {
+              hipStream_t s, const KickArgs *kick) {
     if (hi <= lo) return;
     unsigned grid = (unsigned)((hi - lo + TB - 1) / TB);
     // node records addressed by a 32-bit byte offset while the array stays below 4 GiB
     const bool off32 = node_cap * sizeof(Node) < (size_t(1) << 32);
-    if (visits) {
-        if (off32)
-            k_traverse<true, true><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2,
-                                                       visits, wave_iters);
-        else
-            k_traverse<true, false><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2,
-                                                        visits, wave_iters);
+    const KickArgs ka = kick ? *kick : KickArgs{KICK_NONE, nullptr, nullptr, 0.0, 0.0};
+#define BH_TRAV(C, O, K)                                                                    \
+    k_traverse<C, O, K><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2, visits, \
+                                            wave_iters, ka)
+    if (visits) {  // diagnostic counting walk: accelerations out, never fused
+        if (off32) BH_TRAV(true, true, KICK_NONE);
+        else BH_TRAV(true, false, KICK_NONE);
+    } else if (off32) {
+        if (ka.mode == KICK_DRIFT) BH_TRAV(false, true, KICK_DRIFT);
+        else if (ka.mode == KICK_ONLY) BH_TRAV(false, true, KICK_ONLY);
+        else BH_TRAV(false, true, KICK_NONE);
     } else {
-        if (off32)
-            k_traverse<false, true><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2,
-                                                        visits, wave_iters);
-        else
-            k_traverse<false, false><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2,
-                                                         visits, wave_iters);
+        if (ka.mode == KICK_DRIFT) BH_TRAV(false, false, KICK_DRIFT);
+        else if (ka.mode == KICK_ONLY) BH_TRAV(false, false, KICK_ONLY);
+        else BH_TRAV(false, false, KICK_NONE);
     }
+#undef BH_TRAV
 }
 
 }  // namespace bh
