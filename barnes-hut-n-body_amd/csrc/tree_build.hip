@@ -458,20 +458,45 @@ __device__ __forceinline__ int64_t run_end(const uint64_t *__restrict__ keys_s, 
 // c(j) + 1 of a window of WIN sorted positions starting at the chunk's first body, in LDS:
 // a node's end is found by a word-wise SWAR scan of the window (most nodes end inside it);
 // only nodes that outrun the window gallop over the keys in global memory.
-// first j in [from, c0 + WIN) with c(j) < L, or -1; w[i] = c(c0 + i) + 1 in [0, 42]
+// first j in [from, c0 + WIN) with c(j) < L, or -1; w[i] = c(c0 + i) + 1 in [0, 42];
+// bm[b] = min of w over the 64-byte block b.  The SWAR scan covers the rest of from's block,
+// then the block minima locate the first block holding a match, which is scanned last: at most
+// 8 + WIN / 512 + 8 LDS words per search instead of up to WIN / 8 (a node near the top of a
+// dense region ends thousands of bodies later; one such lane used to hold its wave and, at
+// the phase barrier, its workgroup).
 template <int WIN>
-__device__ __forceinline__ int64_t lds_scan(const uint64_t *w, int64_t c0, int64_t from, int L) {
+__device__ __forceinline__ int64_t lds_scan(const uint64_t *w, const uint64_t *bm, int64_t c0,
+                                            int64_t from, int L) {
+    static_assert(WIN % 512 == 0, "whole words of block minima");
     const uint64_t ones = 0x0101010101010101ull, highs = 0x8080808080808080ull;
     const uint64_t sub = ones * (uint64_t)(L + 1);
-    int64_t o = from - c0;
-    int wi = (int)(o >> 3);
+    const int64_t o = from - c0;
+    if (o >= WIN) return -1;
     // bytes before `from` are raised to 0x7F (>= L + 1): they neither match nor borrow
     uint64_t pad = ~(~0ull << (8 * (o & 7))) & 0x7F7F7F7F7F7F7F7Full;
-    for (; wi < WIN / 8; ++wi) {
+    int wi = (int)(o >> 3);
+    const int wend = (wi | 7) + 1;  // end of from's 64-byte block
+    for (; wi < wend; ++wi) {
         const uint64_t x = w[wi] | pad;
         const uint64_t t = (x - sub) & ~x & highs;  // lowest flag = first byte with c + 1 < L + 1
         if (t) return c0 + 8 * (int64_t)wi + (__builtin_ctzll(t) >> 3);
         pad = 0;
+    }
+    const int b = (int)(o >> 6) + 1;  // first later block
+    if (b >= WIN / 64) return -1;
+    uint64_t bpad = ~(~0ull << (8 * (b & 7))) & 0x7F7F7F7F7F7F7F7Full;
+    for (int bw = b >> 3; bw < WIN / 512; ++bw) {
+        const uint64_t x = bm[bw] | bpad;
+        const uint64_t t = (x - sub) & ~x & highs;
+        if (t) {
+            const int blk = 8 * bw + (__builtin_ctzll(t) >> 3);
+            for (int q = 8 * blk;; ++q) {  // the block holds a match
+                const uint64_t y = w[q];
+                const uint64_t u = (y - sub) & ~y & highs;
+                if (u) return c0 + 8 * (int64_t)q + (__builtin_ctzll(u) >> 3);
+            }
+        }
+        bpad = 0;
     }
     return -1;
 }
@@ -671,6 +696,10 @@ constexpr uint16_t SPAN_CHILD = 0xFFFFu;         // s_ch.x of a chunk-spanning n
 // as skeletons for the span passes.  A chunk whose slot range exceeds the LDS capacity runs
 // the same steps on global memory.  Jitter slots of a run that started in an earlier chunk are
 // written by that chunk's workgroup; here they are inert leaves (no local node owns them).
+#ifdef BH_EC_TIMING  // diagnostic build only: per-workgroup phase stamps (wall clock), slots, levels
+constexpr int EC_TIMING_MAX = 1 << 16, EC_TIMING_W = 8;
+__device__ uint64_t g_ec_times[EC_TIMING_W * EC_TIMING_MAX];
+#endif
 constexpr int EC_WIN = (1 << COM_CHUNK_SHIFT) + 2048;  // c(j) + 1 of the chunk + look-ahead
 #ifndef BH_EC_TB
 #define BH_EC_TB 512
@@ -698,16 +727,31 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
     __shared__ uint32_t s_next[COM_CAP];
     __shared__ ushort4 s_ch[COM_CAP];
     __shared__ uint64_t win[EC_WIN / 8];
+    __shared__ uint64_t win_min[EC_WIN / 512];  // per 64-byte block of win: its minimum byte
     __shared__ int s_lmax;
+#ifdef BH_EC_TIMING
+    uint64_t t_ph[6];
+    t_ph[0] = wall_clock64();
+#define EC_STAMP(q) t_ph[q] = wall_clock64()
+#else
+#define EC_STAMP(q) (void)0
+#endif
     const int J = g.J;
     const int64_t c0 = (int64_t)blockIdx.x << COM_CHUNK_SHIFT;
     const int64_t c1 = min(c0 + (1 << COM_CHUNK_SHIFT), n);
     const int64_t a0 = c0 + (int64_t)threadIdx.x * EC_PER;
     {
         uint8_t *wb = reinterpret_cast<uint8_t *>(win);
-        for (int i = threadIdx.x; i < EC_WIN; i += EC_TB) {
+        uint8_t *mb = reinterpret_cast<uint8_t *>(win_min);
+        static_assert(EC_WIN % EC_TB == 0 && EC_TB % 64 == 0, "a wave fills whole blocks");
+        for (int i = threadIdx.x; i < EC_WIN; i += EC_TB) {  // a wave writes block i / 64
             const int64_t j = c0 + i;
-            wb[i] = (uint8_t)(j < n ? (int)cpl[j] + 1 : 0);  // past the end: c = -1
+            const int v = j < n ? (int)cpl[j] + 1 : 0;  // past the end: c = -1
+            wb[i] = (uint8_t)v;
+            int mv = v;
+#pragma unroll
+            for (int off = 32; off > 0; off >>= 1) mv = min(mv, __shfl_xor(mv, off));
+            if ((threadIdx.x & 63) == 0) mb[i >> 6] = (uint8_t)mv;
         }
     }
     int cps[EC_PER], ccs[EC_PER];
@@ -764,7 +808,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
                 const uint64_t nextcell = ((k >> (2 * (J - L))) + 1) << (2 * (D0 - L));
                 b = (int64_t)cell_start[nextcell] - 1;
             } else {  // inside a's depth-D0 cell: scan the LDS window, then bounded galloping
-                b = lds_scan<EC_WIN>(win, c0, end, L);
+                b = lds_scan<EC_WIN>(win, win_min, c0, end, L);
                 if (b < 0) {
                     const int64_t limit = (int64_t)cell_start[(k >> shift0) + 1] - 1;
                     const int shift = 2 * (J - L);
@@ -813,6 +857,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
         }
     }
     phase_barrier();
+    EC_STAMP(1);
 
     // ---- jitter cells whose run starts in this chunk (BHA:145-156) ----
 #pragma unroll
@@ -837,6 +882,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
             nodes[ni].meta |= jm << NODE_JMASK_SHIFT;  // skeleton written above by this thread
     }
     phase_barrier();
+    EC_STAMP(2);
 
     // ---- centre of mass of the chunk-local internal nodes (BHA:173-202) ----
     if (lds) {
@@ -863,6 +909,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
         }
     }
     phase_barrier();
+    EC_STAMP(3);
     const int top = s_lmax;
     for (int L = top; L >= 0; --L) {
         uint32_t mask = 0;
@@ -925,6 +972,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
             __syncthreads();
         }
     }
+    EC_STAMP(4);
     if (lds) {  // the chunk's local internal nodes, complete, once
         phase_barrier();
         for (uint32_t i = threadIdx.x; i < cnt; i += EC_TB) {
@@ -942,6 +990,16 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
             nodes[S0 + i] = nd;
         }
     }
+#ifdef BH_EC_TIMING
+    EC_STAMP(5);
+    if (threadIdx.x == 0 && blockIdx.x < EC_TIMING_MAX) {
+        uint64_t *o = g_ec_times + EC_TIMING_W * blockIdx.x;
+        for (int q = 0; q < 6; ++q) o[q] = t_ph[q];
+        o[6] = cnt;
+        o[7] = (uint64_t)(s_lmax + 1) | ((uint64_t)__smid() << 32);
+    }
+#endif
+#undef EC_STAMP
 }
 
 // The nodes crossing the boundary between chunk k and k+1 (bodies b = end of chunk k and
@@ -1269,5 +1327,13 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
                                              b.super_list, n_groups, b.nodes);
     return hipGetLastError();
 }
+
+#ifdef BH_EC_TIMING
+extern "C" int bh_debug_ec_times(uint64_t *out, int n) {
+    if (n > EC_TIMING_MAX) n = EC_TIMING_MAX;
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_ec_times),
+                                    sizeof(uint64_t) * EC_TIMING_W * (size_t)n);
+}
+#endif
 
 }  // namespace bh
