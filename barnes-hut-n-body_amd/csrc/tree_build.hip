@@ -697,7 +697,7 @@ constexpr uint16_t SPAN_CHILD = 0xFFFFu;         // s_ch.x of a chunk-spanning n
 // the same steps on global memory.  Jitter slots of a run that started in an earlier chunk are
 // written by that chunk's workgroup; here they are inert leaves (no local node owns them).
 #ifdef BH_EC_TIMING  // diagnostic build only: per-workgroup phase stamps (wall clock), slots, levels
-constexpr int EC_TIMING_MAX = 1 << 16, EC_TIMING_W = 8;
+constexpr int EC_TIMING_MAX = 1 << 16, EC_TIMING_W = 8;  // 7 stamps, slots | levels | CU
 __device__ uint64_t g_ec_times[EC_TIMING_W * EC_TIMING_MAX];
 #endif
 constexpr int EC_WIN = (1 << COM_CHUNK_SHIFT) + 2048;  // c(j) + 1 of the chunk + look-ahead
@@ -730,7 +730,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
     __shared__ uint64_t win_min[EC_WIN / 512];  // per 64-byte block of win: its minimum byte
     __shared__ int s_lmax;
 #ifdef BH_EC_TIMING
-    uint64_t t_ph[6];
+    uint64_t t_ph[7];
     t_ph[0] = wall_clock64();
 #define EC_STAMP(q) t_ph[q] = wall_clock64()
 #else
@@ -744,11 +744,18 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
         uint8_t *wb = reinterpret_cast<uint8_t *>(win);
         uint8_t *mb = reinterpret_cast<uint8_t *>(win_min);
         static_assert(EC_WIN % EC_TB == 0 && EC_TB % 64 == 0, "a wave fills whole blocks");
-        for (int i = threadIdx.x; i < EC_WIN; i += EC_TB) {  // a wave writes block i / 64
-            const int64_t j = c0 + i;
-            const int v = j < n ? (int)cpl[j] + 1 : 0;  // past the end: c = -1
-            wb[i] = (uint8_t)v;
-            int mv = v;
+        constexpr int R = EC_WIN / EC_TB;
+        int v[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {  // every load in flight before the first use
+            const int64_t j = c0 + threadIdx.x + r * EC_TB;
+            v[r] = j < n ? (int)cpl[j] + 1 : 0;  // past the end: c = -1
+        }
+#pragma unroll
+        for (int r = 0; r < R; ++r) {  // a wave writes block i / 64
+            const int i = threadIdx.x + r * EC_TB;
+            wb[i] = (uint8_t)v[r];
+            int mv = v[r];
 #pragma unroll
             for (int off = 32; off > 0; off >>= 1) mv = min(mv, __shfl_xor(mv, off));
             if ((threadIdx.x & 63) == 0) mb[i >> 6] = (uint8_t)mv;
@@ -777,6 +784,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
     const uint32_t cnt = S1 - S0;
     const bool lds = cnt <= (uint32_t)COM_CAP;
     __syncthreads();
+    EC_STAMP(1);
     atomicMax(&s_lmax, lmax);
     // Phases exchange data through LDS only (in the LDS mode): the barriers wait for LDS, not
     // for the global stores of leaves and skeletons, which nothing in this kernel reads back.
@@ -857,7 +865,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
         }
     }
     phase_barrier();
-    EC_STAMP(1);
+    EC_STAMP(2);
 
     // ---- jitter cells whose run starts in this chunk (BHA:145-156) ----
 #pragma unroll
@@ -882,7 +890,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
             nodes[ni].meta |= jm << NODE_JMASK_SHIFT;  // skeleton written above by this thread
     }
     phase_barrier();
-    EC_STAMP(2);
+    EC_STAMP(3);
 
     // ---- centre of mass of the chunk-local internal nodes (BHA:173-202) ----
     if (lds) {
@@ -909,7 +917,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
         }
     }
     phase_barrier();
-    EC_STAMP(3);
+    EC_STAMP(4);
     const int top = s_lmax;
     for (int L = top; L >= 0; --L) {
         uint32_t mask = 0;
@@ -972,7 +980,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
             __syncthreads();
         }
     }
-    EC_STAMP(4);
+    EC_STAMP(5);
     if (lds) {  // the chunk's local internal nodes, complete, once
         phase_barrier();
         for (uint32_t i = threadIdx.x; i < cnt; i += EC_TB) {
@@ -991,12 +999,11 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
         }
     }
 #ifdef BH_EC_TIMING
-    EC_STAMP(5);
+    EC_STAMP(6);
     if (threadIdx.x == 0 && blockIdx.x < EC_TIMING_MAX) {
         uint64_t *o = g_ec_times + EC_TIMING_W * blockIdx.x;
-        for (int q = 0; q < 6; ++q) o[q] = t_ph[q];
-        o[6] = cnt;
-        o[7] = (uint64_t)(s_lmax + 1) | ((uint64_t)__smid() << 32);
+        for (int q = 0; q < 7; ++q) o[q] = t_ph[q];
+        o[7] = (uint64_t)(cnt & 0xFFFFu) | ((uint64_t)(s_lmax + 1) << 16) | ((uint64_t)__smid() << 32);
     }
 #endif
 #undef EC_STAMP

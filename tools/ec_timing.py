@@ -32,9 +32,9 @@ def main():
     rc = lib.bh_debug_ec_times(buf, nwg)
     assert rc == 0, rc
     a = np.frombuffer(buf, dtype=np.uint64).reshape(nwg, 8).astype(np.int64)
-    ph, cnt, lv = a[:, 0:6], a[:, 6], a[:, 7]
-    t0, t1 = ph[:, 0], ph[:, 5]
-    levels, cu = lv & 0xFFFFFFFF, lv >> 32
+    ph, lv = a[:, 0:7], a[:, 7]
+    t0, t1 = ph[:, 0], ph[:, 6]
+    cnt, levels, cu = lv & 0xFFFF, (lv >> 16) & 0xFFFF, lv >> 32
     dur = (t1 - t0) * 10.0  # 100 MHz wall clock -> ns
     span = (t1.max() - t0.min()) * 10.0
     print(f"{cfg}: n={n} workgroups={nwg} kernel span {span / 1e3:.1f} us")
@@ -44,7 +44,7 @@ def main():
     start_rel = (t0 - t0.min()) * 10.0 / 1e3
     print("WG start offsets us p50/p90/max:",
           " ".join(f"{x:.1f}" for x in np.percentile(start_rel, [50, 90, 100])))
-    names = ["skeleton+leaves", "jitter", "child lists", "COM levels", "final write"]
+    names = ["init loads", "skeleton+leaves", "jitter", "child lists", "COM levels", "final write"]
     for q_, nm in enumerate(names):
         d = (ph[:, q_ + 1] - ph[:, q_]) * 10.0 / 1e3
         print(f"  phase {nm:16s} us mean {d.mean():6.2f} p50 {np.median(d):6.2f} "
@@ -54,8 +54,8 @@ def main():
           f"levels mean {levels[slow].mean():.1f} vs {levels[~slow].mean():.1f}")
     for lvl in sorted(set(levels.tolist())):
         sel = levels == lvl
-        d_sk = (ph[sel, 1] - ph[sel, 0]) * 10.0 / 1e3
-        d_com = (ph[sel, 4] - ph[sel, 3]) * 10.0 / 1e3
+        d_sk = (ph[sel, 2] - ph[sel, 1]) * 10.0 / 1e3
+        d_com = (ph[sel, 5] - ph[sel, 4]) * 10.0 / 1e3
         print(f"  levels {lvl:2d}: {sel.sum():5d} WGs, mean {dur[sel].mean() / 1e3:.1f} us "
               f"(skeleton {d_sk.mean():.1f}, COM levels {d_com.mean():.1f})")
     print("distinct hw ids:", len(set(cu.tolist())))
