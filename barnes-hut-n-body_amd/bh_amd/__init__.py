@@ -36,8 +36,9 @@ EXPORTED_SYMBOLS = (
     "bh_default_params", "bh_create", "bh_create_dist", "bh_comm_unique_id", "bh_destroy",
     "bh_last_error", "bh_set_params", "bh_get_params", "bh_reset_bodies", "bh_step",
     "bh_num_bodies", "bh_get_bodies", "bh_compute_accelerations", "bh_get_quads",
-    "bh_last_timings", "bh_last_tree_nodes", "bh_traverse_kernel_ms", "bh_set_profiling",
-    "bh_synchronize", "bh_shard_range", "bh_traversal_stats", "bh_last_removed",
+    "bh_last_timings", "bh_last_tree_nodes", "bh_traverse_kernel_ms",
+    "bh_traverse_kernel_samples", "bh_set_profiling",
+    "bh_synchronize", "bh_shard_range", "bh_traversal_stats", "bh_traversal_counters", "bh_last_removed",
     "bh_selftest_fast_math", "bh_scene_galaxy_disk", "bh_scene_kepler_disk", "bh_scene_uniform",
     "bh_nbody3d_create", "bh_nbody3d_destroy", "bh_nbody3d_last_error", "bh_nbody3d_set",
     "bh_nbody3d_step", "bh_nbody3d_accelerations", "bh_nbody3d_get", "bh_nbody3d_last_ms",
@@ -109,9 +110,11 @@ def load_library(path: str | None = None):
     lib.bh_last_tree_nodes.argtypes = [_VP]
     lib.bh_last_tree_nodes.restype = ctypes.c_int64
     lib.bh_traverse_kernel_ms.argtypes = [_VP, _D, _I64P]
+    lib.bh_traverse_kernel_samples.argtypes = [_VP, _D, ctypes.c_int64, _I64P]
     lib.bh_set_profiling.argtypes = [_VP, ctypes.c_int]
     lib.bh_synchronize.argtypes = [_VP]
     lib.bh_traversal_stats.argtypes = [_VP, _I64P, _I64P, _I64P]
+    lib.bh_traversal_counters.argtypes = [_VP, _I64P]
     lib.bh_last_removed.argtypes = [_VP, _I64P, ctypes.c_int64, _I64P]
     lib.bh_shard_range.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    _I64P, _I64P]
@@ -371,6 +374,17 @@ class Engine:
         self._check(self._lib.bh_traverse_kernel_ms(self._h, ctypes.byref(avg), ctypes.byref(cnt)))
         return avg.value, cnt.value
 
+    def traverse_kernel_samples(self):
+        """Per-launch traversal kernel times (ms) of the last step() call, in launch order."""
+        need = ctypes.c_int64(0)
+        rc = self._lib.bh_traverse_kernel_samples(self._h, None, 0, ctypes.byref(need))
+        if rc not in (BH_OK, BH_E_CAPACITY):
+            self._check(rc)
+        out = np.empty(need.value, dtype=np.float64)
+        self._check(self._lib.bh_traverse_kernel_samples(self._h, _dp(out), need.value,
+                                                         ctypes.byref(need)))
+        return out
+
     def traversal_stats(self):
         """(lane visits, wave iterations, waves) of the last compute_accelerations(visits=True);
         lane efficiency = lane_visits / (64 * wave_iters)."""
@@ -378,6 +392,14 @@ class Engine:
         self._check(self._lib.bh_traversal_stats(self._h, ctypes.byref(a), ctypes.byref(b),
                                                  ctypes.byref(c)))
         return a.value, b.value, c.value
+
+    def traversal_counters(self):
+        """Counters of the last compute_accelerations(visits=True) (bh_traversal_counters):
+        dict of lane_visits, lane_contrib, wave_iters, wave_blocks, waves."""
+        out = np.zeros(5, dtype=np.int64)
+        self._check(self._lib.bh_traversal_counters(self._h, out.ctypes.data_as(_I64P)))
+        return dict(zip(("lane_visits", "lane_contrib", "wave_iters", "wave_blocks", "waves"),
+                        (int(v) for v in out)))
 
     def last_tree_nodes(self) -> int:
         return int(self._lib.bh_last_tree_nodes(self._h))

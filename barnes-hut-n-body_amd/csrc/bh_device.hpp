@@ -166,9 +166,17 @@ struct KickArgs {
     double *vx, *vy;  // x, y are the traversal's own position arrays
     double dtHalf, dt;
 };
+// Diagnostic counters of the counting walk (all per evaluation): per body, the non-empty
+// nodes visited (BHA:216 passed) and the point-force contributions (accepted internal nodes
+// + other bodies' leaves, BHA:219-221,228-230); per wavefront, the nodes the shared cursor
+// stopped at and the point-force blocks it executed.
+struct TraverseCounters {
+    uint32_t *visits, *contrib;
+    uint32_t *wave_iters, *wave_blocks;
+};
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
-              const double *m, int64_t lo, int64_t hi, const Geometry &g,
-              const ForceParams &fp, double *a2, uint32_t *visits, uint32_t *wave_iters,
+              const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,
+              const ForceParams &fp, double *a2, const TraverseCounters *cnt,
               hipStream_t s, const KickArgs *kick = nullptr);
 // multi-GPU shard pieces (bh_shard_range): `rounds` x `world` pieces of whole wavefronts
 __host__ __device__ inline int64_t shard_sub(int64_t n, int world, int rounds) {

@@ -92,8 +92,11 @@ struct bh_engine {
     bh::SpanSlot *span_children = nullptr;
     uint32_t *scalars = nullptr;  // [1] tree error flags
     uint32_t *visits32 = nullptr;
+    uint32_t *contrib32 = nullptr;     // per-body point-force contributions (diagnostics)
     uint32_t *wave_iters = nullptr;  // per-wave union of visited nodes (diagnostics)
+    uint32_t *wave_blocks = nullptr; // per-wave point-force blocks executed (diagnostics)
     int64_t stat_lane_visits = 0, stat_wave_iters = 0, stat_waves = 0;
+    int64_t stat_lane_contrib = 0, stat_wave_blocks = 0;
 
     // merge
     uint32_t *heavy = nullptr;
@@ -140,6 +143,7 @@ struct bh_engine {
     double phase_ms[kPhases] = {0, 0, 0, 0, 0};
     double trav_ms_sum = 0.0;
     int64_t trav_launches = 0;
+    std::vector<double> trav_samples;  // per-launch traversal times of the last call (ms)
     bool timings_pending = false;
 
     std::string err;
@@ -254,7 +258,9 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(dev_alloc(e, e->cnt, cap + 1));
         TRY(dev_alloc(e, e->base, cap + 1));
         TRY(dev_alloc(e, e->visits32, cap));
+        TRY(dev_alloc(e, e->contrib32, cap));
         TRY(dev_alloc(e, e->wave_iters, cap / 64 + 2));
+        TRY(dev_alloc(e, e->wave_blocks, cap / 64 + 2));
         TRY(dev_alloc(e, e->heavy, cap));
         TRY(dev_alloc(e, e->keep, cap));
         TRY(dev_alloc(e, e->pos, cap));
@@ -338,6 +344,7 @@ int collect_timings(bh_engine *e) {
     for (int k = 0; k < kPhases; ++k) e->phase_ms[k] = 0.0;
     e->trav_ms_sum = 0.0;
     e->trav_launches = 0;
+    e->trav_samples.clear();
     for (size_t i = 1; i < e->ev_used; ++i) {
         int ph = e->ev_phase[i];
         if (ph < 0) continue;
@@ -347,6 +354,7 @@ int collect_timings(bh_engine *e) {
         if (ph == 1) {
             e->trav_ms_sum += ms;
             e->trav_launches += 1;
+            e->trav_samples.push_back(ms);
         }
     }
     e->timings_pending = false;
@@ -413,19 +421,20 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
                                   e->leaf_count, e->leaves, n, e->leaf_tmp, e->leaf_tmp_bytes,
                                   e->stream));
     }
+    const TraverseCounters counters{visits, e->contrib32, e->wave_iters, e->wave_blocks};
     auto forces = [&](int64_t lo, int64_t hi, uint32_t *vis) {
         if (direct)
             direct_forces(e->leaves, e->leaf_count, e->st.x, e->st.y, e->st.m, lo, hi, fp.G,
                           fp.soft2, e->a2, e->stream);
         else
-            traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, lo, hi, e->geo, fp,
-                     e->a2, vis, vis ? e->wave_iters : nullptr, e->stream);
+            traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, e->st.cidx, lo, hi, e->geo, fp,
+                     e->a2, vis ? &counters : nullptr, e->stream);
     };
     if ((!e->comm && !e->group) || visits) {
         if (BH_FUSE_KICK && kick != KICK_NONE && !direct && !visits && fused) {
             const KickArgs ka{kick, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
-            traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, 0, n, e->geo, fp,
-                     e->a2, nullptr, nullptr, e->stream, &ka);
+            traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, e->st.cidx, 0, n, e->geo, fp,
+                     e->a2, nullptr, e->stream, &ka);
             *fused = true;
         } else {
             forces(0, n, visits);
@@ -829,7 +838,7 @@ void bh_destroy(bh_engine *e) {
     free_state(e->alt);
     void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->keys32, e->keys32_s, e->idx, e->perm, e->cpl, e->cnt,
                     e->base, e->cell_start, e->nodes, e->span_list, e->super_list,
-                    e->span_children, e->scalars, e->visits32, e->wave_iters, e->heavy, e->keep,
+                    e->span_children, e->scalars, e->visits32, e->contrib32, e->wave_iters, e->wave_blocks, e->heavy, e->keep,
                     e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->mbits, e->mslot, e->cub_tmp,
                     e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaves.xy, e->leaves.m,
                     e->leaves.slot, e->leaf_tmp, e->spl, e->bcount, e->bstart};
@@ -962,14 +971,22 @@ int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visi
                 visits[c[(size_t)i]] = v[(size_t)i];
                 lane_sum += v[(size_t)i];
             }
+            HIPCHK(e, hipMemcpy(v.data(), e->contrib32, sizeof(uint32_t) * n, hipMemcpyDeviceToHost));
+            int64_t contrib_sum = 0;
+            for (int64_t i = 0; i < n; ++i) contrib_sum += v[(size_t)i];
             const int64_t waves = (n + 63) / 64;
-            std::vector<uint32_t> wi((size_t)waves);
+            std::vector<uint32_t> wi((size_t)waves), wb((size_t)waves);
             HIPCHK(e, hipMemcpy(wi.data(), e->wave_iters, sizeof(uint32_t) * waves,
                                 hipMemcpyDeviceToHost));
-            int64_t wsum = 0;
+            HIPCHK(e, hipMemcpy(wb.data(), e->wave_blocks, sizeof(uint32_t) * waves,
+                                hipMemcpyDeviceToHost));
+            int64_t wsum = 0, bsum = 0;
             for (uint32_t w : wi) wsum += w;
+            for (uint32_t w : wb) bsum += w;
             e->stat_lane_visits = lane_sum;
+            e->stat_lane_contrib = contrib_sum;
             e->stat_wave_iters = wsum;
+            e->stat_wave_blocks = bsum;
             e->stat_waves = waves;
         }
     }
@@ -1036,12 +1053,31 @@ int bh_traverse_kernel_ms(const bh_engine *e, double *avg_ms, int64_t *launches)
     return BH_OK;
 }
 
+int bh_traverse_kernel_samples(const bh_engine *e, double *ms, int64_t cap, int64_t *n_out) {
+    if (!e || cap < 0 || (cap > 0 && !ms)) return BH_E_INVALID;
+    const int64_t n = (int64_t)e->trav_samples.size();
+    if (n_out) *n_out = n;
+    if (n > cap) return BH_E_CAPACITY;
+    for (int64_t i = 0; i < n; ++i) ms[i] = e->trav_samples[(size_t)i];
+    return BH_OK;
+}
+
 int bh_traversal_stats(const bh_engine *e, int64_t *lane_visits, int64_t *wave_iters,
                        int64_t *waves) {
     if (!e || !lane_visits || !wave_iters || !waves) return BH_E_INVALID;
     *lane_visits = e->stat_lane_visits;
     *wave_iters = e->stat_wave_iters;
     *waves = e->stat_waves;
+    return BH_OK;
+}
+
+int bh_traversal_counters(const bh_engine *e, int64_t *out5) {
+    if (!e || !out5) return BH_E_INVALID;
+    out5[0] = e->stat_lane_visits;
+    out5[1] = e->stat_lane_contrib;
+    out5[2] = e->stat_wave_iters;
+    out5[3] = e->stat_wave_blocks;
+    out5[4] = e->stat_waves;
     return BH_OK;
 }
 

@@ -51,7 +51,8 @@ template <bool FAST, bool COUNT, bool OFF32>
 __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T, double bx,
                                      double by, double Gm, double soft2, double theta2,
                                      double s2root, uint32_t self, uint32_t resume, double &fx,
-                                     double &fy, uint32_t &nvis, uint32_t &niters) {
+                                     double &fy, uint32_t &nvis, uint32_t &niters,
+                                     uint32_t &ncontrib, uint32_t &nblocks) {
     uint32_t cur = 0;
     // one iteration on record `rec`; the next record is requested into `nrec`.  The loop body
     // is unrolled twice with the two records swapping roles (no SGPR copies per iteration).
@@ -99,6 +100,11 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
         }
         const uint32_t ncur = open_m != 0ull ? cur + 1 : next;  // descend iff some lane opened
         nrec = OFF32 ? nload_off(nodes, ncur) : nload(nodes + ncur);
+        if (COUNT) {  // contributions in the reference's sense: the own leaf is not one
+            const bool own = (meta & NODE_LEAF) && (meta & NODE_BODY_MASK) == self;
+            ncontrib += (__builtin_amdgcn_inverse_ballot_w64(contrib_m) && !own) ? 1u : 0u;
+            nblocks += contrib_m != 0ull ? 1u : 0u;
+        }
         if (__builtin_amdgcn_inverse_ballot_w64(contrib_m)) {  // BHA:250-259, order as written
             double invR, invR2;
             if (FAST) {
@@ -141,13 +147,18 @@ template <bool COUNT, bool OFF32, int KICK>
 __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
                                                  const uint32_t *__restrict__ d_T, double *x,
                                                  double *y, const double *__restrict__ m,
+                                                 const uint32_t *__restrict__ cidx,
                                                  int64_t lo, int64_t hi, ForceParams fp,
                                                  Geometry g, double *__restrict__ a2,
-                                                 uint32_t *__restrict__ visits,
-                                                 uint32_t *__restrict__ wave_iters,
-                                                 KickArgs kick) {
+                                                 TraverseCounters cnt, KickArgs kick) {
     const int64_t p = lo + (int64_t)xcd_block<BH_TRAV_XCD_RUN>() * TB + threadIdx.x;
     const bool valid = p < hi;
+    // A body merged away earlier in this bh_step call (a tombstone until the call's compaction)
+    // needs no force: it does not walk.  Tombstones sort to the tail with the out-of-root
+    // bodies and are flung across the domain by the heavy body that absorbed them, so a tail
+    // wave of walking tombstones visits the union of 64 unrelated interaction lists -- it set
+    // the kernel's duration (0.8 -> 2 ms over 20 steps at C3) before this test.
+    const bool walks = valid && !(cidx[p] & CIDX_DEAD);
     const double bx = valid ? x[p] : 0.0;
     const double by = valid ? y[p] : 0.0;
     const double bm = valid ? m[p] : 1.0;
@@ -156,19 +167,22 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     const double s2root = g.s2[0];
     const uint32_t self = (uint32_t)p;
     double fx = 0.0, fy = 0.0;
-    uint32_t nvis = 0, niters = 0;
-    // lane is active for node `cur` iff cur >= resume; invalid lanes never are.
-    const uint32_t resume = valid ? 0u : 0xFFFFFFFFu;
+    uint32_t nvis = 0, niters = 0, ncontrib = 0, nblocks = 0;
+    // lane is active for node `cur` iff cur >= resume; invalid lanes and tombstones never are.
+    const uint32_t resume = walks ? 0u : 0xFFFFFFFFu;
     const uint32_t T = __builtin_amdgcn_readfirstlane(*d_T);
     const bool fast =
-        __ballot(valid && !(lane_fast_ok(bx, by, soft2) && lane_self_ok(Gm, bm))) == 0ull;
+        __ballot(walks && !(lane_fast_ok(bx, by, soft2) && lane_self_ok(Gm, bm))) == 0ull;
     if (fast)
         walk<true, COUNT, OFF32>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx,
-                                 fy, nvis, niters);
+                                 fy, nvis, niters, ncontrib, nblocks);
     else
         walk<false, COUNT, OFF32>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx,
-                                  fy, nvis, niters);
-    if (COUNT && (threadIdx.x & 63) == 0) wave_iters[(p - lo) >> 6] = niters;
+                                  fy, nvis, niters, ncontrib, nblocks);
+    if (COUNT && (threadIdx.x & 63) == 0) {
+        cnt.wave_iters[(p - lo) >> 6] = niters;
+        cnt.wave_blocks[(p - lo) >> 6] = nblocks;
+    }
     if (!valid) return;
     // BHA:390-391, interleaved (ax, ay): coalesced 16-byte stores in Morton order
     typedef double double2_t __attribute__((ext_vector_type(2)));
@@ -187,7 +201,10 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
             y[p] = by + vyi * kick.dt;
         }
     }
-    if (COUNT) visits[p] = nvis;
+    if (COUNT) {
+        cnt.visits[p] = nvis;
+        cnt.contrib[p] = ncontrib;
+    }
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
@@ -242,18 +259,18 @@ hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_ba
 }
 
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
-              const double *m, int64_t lo, int64_t hi, const Geometry &g,
-              const ForceParams &fp, double *a2, uint32_t *visits, uint32_t *wave_iters,
+              const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,
+              const ForceParams &fp, double *a2, const TraverseCounters *cnt,
               hipStream_t s, const KickArgs *kick) {
     if (hi <= lo) return;
     unsigned grid = (unsigned)((hi - lo + TB - 1) / TB);
     // node records addressed by a 32-bit byte offset while the array stays below 4 GiB
     const bool off32 = node_cap * sizeof(Node) < (size_t(1) << 32);
     const KickArgs ka = kick ? *kick : KickArgs{KICK_NONE, nullptr, nullptr, 0.0, 0.0};
-#define BH_TRAV(C, O, K)                                                                    \
-    k_traverse<C, O, K><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, lo, hi, fp, g, a2, visits, \
-                                            wave_iters, ka)
-    if (visits) {  // diagnostic counting walk: accelerations out, never fused
+    const TraverseCounters tc = cnt ? *cnt : TraverseCounters{nullptr, nullptr, nullptr, nullptr};
+#define BH_TRAV(C, O, K) \
+    k_traverse<C, O, K><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, tc, ka)
+    if (cnt) {  // diagnostic counting walk: accelerations out, never fused
         if (off32) BH_TRAV(true, true, KICK_NONE);
         else BH_TRAV(true, false, KICK_NONE);
     } else if (off32) {

@@ -25,9 +25,10 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "barnes-hut-n-body_amd"))
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
-FP64_VEC_PEAK_TF = 78.6  # MI355X FP64 vector peak, AMD spec sheet (not in the local guide)
-FLOP_PER_INTERACTION = 20  # SURVEY §8d C5 convention (sqrt and divisions counted as 1)
-NODE_BYTES = 32        # one fp64 node record (comX, comY, mass, s2/next) — SURVEY §8d
+FP64_VEC_PEAK_TF = 78.6  # MI355X FP64 vector peak (FMA = 2 flop), AMD spec sheet (not in the guide)
+FP64_NOFMA_PEAK_TF = 39.3  # the same issue rate without FMA: -ffp-contract=off (bit-exactness)
+FLOP_PER_INTERACTION = 20  # SURVEY §8d convention: one point force (BHA:250-259), sqrt/div = 1
+NODE_BYTES = 32        # one fp64 node record (comX, comY, mass, next/meta) — SURVEY §8d
 BODY_EVAL_BYTES = 40   # body read (x, y, m) + acceleration write (ax, ay) per evaluation
 
 
@@ -36,53 +37,126 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", default="c3",
-                    help="c3 (default), c2, c4, c5 (theta=0 all-pairs), c1_code, c1_baseline")
+    ap.add_argument("--config", default=None,
+                    help="c3 (default on one GPU), c4 (default on N>1 GPUs: strong scaling of "
+                         "the north-star 1e7 cloud), c3x (weak scaling: 1e6 bodies per GPU), "
+                         "c2, c5 (theta=0 all-pairs), c1_code, c1_baseline")
     ap.add_argument("--theta", type=float, default=None, help="default 0.5 (c5: 0.0)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-counters", action="store_true",
+                    help="skip the V-bar / lane-efficiency counting walks on the timed state")
     ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
     return ap.parse_args()
 
 
-def measured_traffic(config, kernel):
-    """HBM bytes per launch of `kernel` from the committed PMC summary of this workload
-    (profiles/hbm_traffic.json, written from rocprofv3 FETCH_SIZE/WRITE_SIZE passes by
+def committed_traffic(config, kernel):
+    """HBM bytes per launch of `kernel` on this workload from the committed PMC summary
+    (profiles/hbm_traffic.json, rocprofv3 FETCH_SIZE / WRITE_SIZE passes summarised by
     tools/summarize_profile.py), or None."""
     path = os.path.join(ROOT, "profiles", "hbm_traffic.json")
     try:
         with open(path) as fh:
-            ent = json.load(fh).get(config, {}).get(kernel)
-    except (OSError, ValueError):
-        return None, None
-    if not ent:
-        return None, None
-    return ent.get("hbm_bytes_per_launch"), ent.get("source")
-
-
-def measured_valu_busy(config, kernel):
-    """VALU-busy fraction of `kernel` on this workload from the committed SQ counter summary
-    (profiles/valu_busy.json, written by tools/summarize_sq.py), or None: the traversal is
-    fp64-VALU bound, so this is its efficiency figure next to the HBM roofline."""
-    try:
-        with open(os.path.join(ROOT, "profiles", "valu_busy.json")) as fh:
-            ent = json.load(fh).get(config, {}).get(kernel)
+            return json.load(fh).get(config, {}).get(kernel)
     except (OSError, ValueError):
         return None
-    return ent
+
+
+class ClockSampler:
+    """GPU clock / activity during the timed region, sampled by amdsmi from a host thread
+    (the GPU is matched by PCI bus id).  Silent no-op where amdsmi is unavailable."""
+
+    def __init__(self, device):
+        self.samples = []
+        self._stop = None
+        self._h = None
+        try:
+            import amdsmi
+            import torch
+            amdsmi.amdsmi_init()
+            props = torch.cuda.get_device_properties(device)
+            want = getattr(props, "pci_bus_id", None)
+            handles = amdsmi.amdsmi_get_processor_handles()
+            for h in handles:
+                bdf = amdsmi.amdsmi_get_gpu_device_bdf(h)
+                if want is None or int(bdf.split(":")[1], 16) == int(want):
+                    self._h = h
+                    break
+            self._amdsmi = amdsmi
+        except Exception as exc:  # noqa: BLE001 - diagnostics only
+            self.error = repr(exc)[:200]
+
+    def _read(self):
+        a = self._amdsmi
+        c = a.amdsmi_get_clock_info(self._h, a.AmdSmiClkType.SYS)
+        return c.get("clk"), c.get("max_clk")
+
+    def start(self):
+        if self._h is None:
+            return
+        import threading
+        self._stop = threading.Event()
+
+        def run():
+            while not self._stop.is_set():
+                try:
+                    self.samples.append(self._read())
+                except Exception:  # noqa: BLE001
+                    return
+                self._stop.wait(0.002)
+        self._t = threading.Thread(target=run, daemon=True)
+        self._t.start()
+
+    def stop(self):
+        if self._stop is None:
+            return None
+        self._stop.set()
+        self._t.join()
+        clk = [c for c, _ in self.samples if isinstance(c, (int, float))]
+        if not clk:
+            return None
+        clk.sort()
+        return {"samples": len(clk), "min_mhz": clk[0], "median_mhz": clk[len(clk) // 2],
+                "max_mhz": clk[-1], "max_clk_mhz": self.samples[-1][1]}
+
+
+def traversal_counters(bh_amd, params, device, arrs):
+    """Counting walk (bh_compute_accelerations with visits) on a copy of `arrs` in a separate
+    engine: V-bar, point-force contributions, lane efficiency, force-block lane use."""
+    import numpy as np
+    probe = bh_amd.Engine(params, device=device)
+    probe.reset_bodies(*arrs)
+    _, _, vis = probe.compute_accelerations(visits=True)
+    c = probe.traversal_counters()
+    probe.close()
+    n = len(vis)
+    return {
+        "bodies": n,
+        "vbar": float(np.mean(vis)) if n else 0.0,
+        "contrib_per_body": c["lane_contrib"] / n if n else 0.0,
+        "lane_efficiency": c["lane_visits"] / (64.0 * c["wave_iters"]) if c["wave_iters"] else 0.0,
+        "force_block_lane_use": (c["lane_contrib"] + n) / (64.0 * c["wave_blocks"])
+        if c["wave_blocks"] else 0.0,
+        "wave_iters_per_wave": c["wave_iters"] / c["waves"] if c["waves"] else 0.0,
+        "blocks_per_wave": c["wave_blocks"] / c["waves"] if c["waves"] else 0.0,
+        "lane_contrib": c["lane_contrib"],
+    }
 
 
 def scene_for(config, world):
+    """(arrays, scene name, scaling): c3x = weak scaling (1e6 bodies per GPU of the two-disk
+    geometry), every other config is a fixed total (strong scaling over GPUs)."""
     from bh_amd import scenes
-    if config == "c3" and world > 1:
-        return scenes.config_scene(f"c3x{world}"), f"c3x{world}"
-    return scenes.config_scene(config), config
+    if config == "c3x":
+        name = f"c3x{world}" if world > 1 else "c3"
+        return scenes.config_scene(name), name, "weak"
+    return scenes.config_scene(config), config, "strong"
 
 
 WORKLOAD_DESC = {
     "c3": "two colliding galaxy disks (8e5 r=300 + 2e5 r=100 y=160 vx=-50), N=1e6",
     "c2": "Kepler disk N=1e5 (BodyFactory.makeKeplerDisk, seed 3)",
-    "c4": "uniform cloud N=1e7 over 2400x800, m=0.5",
+    "c4": "uniform cloud N=1e7 over 2400x800, m=0.5 (the north-star configuration)",
     "c1_code": "defaultBodies(): two galaxy disks 10000 + 2500",
     "c1_baseline": "BASELINE 'R' scene: two galaxy disks 2 x 1000",
     "c5": "uniform cloud N=262144, theta=0: direct all-pairs sum in tree leaf order",
@@ -91,12 +165,14 @@ WORKLOAD_DESC = {
 
 def main():
     args = parse()
-    if args.theta is None:
-        args.theta = 0.0 if args.config == "c5" else 0.5
-    direct = args.theta == 0.0
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.config is None:  # BASELINE's metric on one GPU; the north-star cloud on N > 1
+        args.config = "c3" if world == 1 else "c4"
+    if args.theta is None:
+        args.theta = 0.0 if args.config == "c5" else 0.5
+    direct = args.theta == 0.0
     if args.gpus != world and world > 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
 
@@ -118,32 +194,27 @@ def main():
     else:
         eng = bh_amd.Engine(params, device=local_rank)
 
-    arrs, scene_name = scene_for(args.config, world)
+    arrs, scene_name, scaling = scene_for(args.config, world)
     n0 = len(arrs[0])
-
-    # V-bar: mean non-empty nodes visited per body per evaluation on this scene,
-    # counted by the engine on a separate instance so the timed state is untouched.
-    vbar = lane_eff = 0.0
-    if not direct:
-        probe = bh_amd.Engine(params, device=local_rank)
-        probe.reset_bodies(*arrs)
-        _, _, vis = probe.compute_accelerations(visits=True)
-        vbar = float(np.mean(vis)) if len(vis) else 0.0
-        lane_visits, wave_iters, waves = probe.traversal_stats()
-        lane_eff = lane_visits / (64.0 * wave_iters) if wave_iters else 0.0
-        probe.close()
-        del probe
 
     eng.reset_bodies(*arrs)
     if args.warmup > 0:
         eng.step(args.warmup)
     n_start = eng.num_bodies()
+    # V-bar and the lane counters on the state the timed region starts from (a copy in a
+    # separate engine: the timed state is untouched)
+    cnt_start = None
+    if not direct and not args.no_counters and rank == 0:
+        cnt_start = traversal_counters(bh_amd, params, local_rank, eng.get_bodies())
 
+    clocks = ClockSampler(local_rank) if rank == 0 else None
     eng.set_profiling(True)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     eng.synchronize()
+    if clocks:
+        clocks.start()
     t0 = time.perf_counter()
     eng.step(args.steps)  # blocks until the device work is complete
     eng.synchronize()
@@ -151,6 +222,7 @@ def main():
     if world > 1:
         dist.barrier()
     t1 = time.perf_counter()
+    clock_stats = clocks.stop() if clocks else None
     elapsed = t1 - t0
     if world > 1:
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -158,54 +230,82 @@ def main():
         elapsed = float(t.item())
     n_end = eng.num_bodies()
     trav_ms, trav_launches = eng.traverse_kernel_ms()
+    samples = eng.traverse_kernel_samples()
     phases = eng.last_timings()
     eng.set_profiling(False)
+    per_rank = None
+    if world > 1:
+        mine = {k: round(v / max(args.steps, 1), 3) for k, v in phases.items()}
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+        per_rank = gathered
+    cnt_end = None
+    if not direct and not args.no_counters and rank == 0:
+        cnt_end = traversal_counters(bh_amd, params, local_rank, eng.get_bodies())
 
     bodies = 0.5 * (n_start + n_end)  # the merge rule can remove a handful of bodies
     value = bodies * args.steps / elapsed
     ms_per_step = 1e3 * elapsed / max(args.steps, 1)
+    kstats = {}
+    if len(samples):
+        ss = np.sort(samples)
+        kstats = {"min": round(float(ss[0]), 4), "median": round(float(np.median(ss)), 4),
+                  "max": round(float(ss[-1]), 4)}
 
-    # Roofline of the dominant kernel: algorithmic bytes (traversal) or flops (theta = 0
-    # all-pairs) per launch / its average duration on the engine's stream.
-    bodies_per_launch = bodies / world
+    # Roofline of the dominant kernel.  Both paths are bound by fp64 VALU issue: the flop
+    # figure is SURVEY §8d's 20 flop per point-force interaction (BHA:250-259, the IEEE sqrt
+    # and each division counted as one flop; the criterion's compare work is not counted).
     if direct:
+        bodies_per_launch = bodies / world
         flops_per_launch = FLOP_PER_INTERACTION * bodies_per_launch * (bodies - 1)
-        achieved = flops_per_launch / (trav_ms * 1e-3) / 1e12 if trav_ms > 0 else 0.0
-        roofline = {
-            "bound": "valu",
-            "achieved": round(achieved, 2),
-            "peak": FP64_VEC_PEAK_TF,
-            "unit": "TFLOP/s",
-            "frac": round(achieved / FP64_VEC_PEAK_TF, 4),
-            "traffic": measured_traffic(scene_name, "k_direct")[0],
-            "kernel": "k_direct",
-            "kernel_avg_ms": round(trav_ms, 4),
-            "launches": trav_launches,
-            "flops_per_launch": round(flops_per_launch),
-            "interactions_per_s": round(flops_per_launch / FLOP_PER_INTERACTION / (trav_ms * 1e-3))
-            if trav_ms > 0 else 0,
-        }
+        kernel = "k_direct"
+        extra = {"interactions_per_s": round(flops_per_launch / FLOP_PER_INTERACTION /
+                                             (trav_ms * 1e-3)) if trav_ms > 0 else 0}
     else:
-        bytes_per_launch = (NODE_BYTES * vbar + BODY_EVAL_BYTES) * bodies_per_launch
-        achieved = bytes_per_launch / (trav_ms * 1e-3) / 1e9 if trav_ms > 0 else 0.0
-        roofline = {
-            "bound": "hbm",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBS,
-            "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBS, 4),
-            "traffic": measured_traffic(scene_name, "k_traverse")[0],
-            "traffic_source": measured_traffic(scene_name, "k_traverse")[1],
-            "kernel": "k_traverse",
-            # N > 1: per evaluation (BH_SHARD_ROUNDS launches overlapped with the all-gathers)
-            "kernel_avg_ms": round(trav_ms, 4),
-            "launches": trav_launches,
-            "rounds_per_eval": bh_amd.SHARD_ROUNDS if world > 1 else 1,
+        kernel = "k_traverse"
+        cs = [c for c in (cnt_start, cnt_end) if c]
+        contrib = float(np.mean([c["contrib_per_body"] for c in cs])) if cs else 0.0
+        vbar = float(np.mean([c["vbar"] for c in cs])) if cs else 0.0
+        # world > 1: one launch per round evaluates 1 / (world * rounds) of the bodies
+        bodies_per_launch = bodies / (world * (bh_amd.SHARD_ROUNDS if world > 1 else 1))
+        flops_per_launch = FLOP_PER_INTERACTION * contrib * bodies_per_launch
+        node_bytes = (NODE_BYTES * vbar + BODY_EVAL_BYTES) * bodies_per_launch
+        extra = {
+            "contrib_per_body_eval": round(contrib, 2),
             "vbar_nodes_per_body_eval": round(vbar, 2),
-            "valu_busy": (measured_valu_busy(scene_name, "k_traverse") or {}).get("valu_busy"),
-            "wave_lane_efficiency": round(lane_eff, 4),
-            "bytes_per_launch": round(bytes_per_launch),
+            "counted_on": "copies of the state at the start and the end of the timed region",
+            "lane_efficiency": round(float(np.mean([c["lane_efficiency"] for c in cs])), 4)
+            if cs else None,
+            "force_block_lane_use": round(float(np.mean([c["force_block_lane_use"] for c in cs])), 4)
+            if cs else None,
+            "node_stream_gbs": round(node_bytes / (trav_ms * 1e-3) / 1e9, 1) if trav_ms > 0 else 0,
+            "node_stream_note": "(32 V-bar + 40) B per body: served by the scalar cache / L2, "
+                                "not HBM (one record feeds 64 lanes)",
         }
+    achieved = flops_per_launch / (trav_ms * 1e-3) / 1e12 if trav_ms > 0 else 0.0
+    tr = committed_traffic(scene_name, kernel)
+    traffic = tr.get("hbm_bytes_per_launch") if tr else None
+    roofline = {
+        "bound": "fp64_valu",
+        "achieved": round(achieved, 3),
+        "peak": FP64_VEC_PEAK_TF,
+        "unit": "TFLOP/s",
+        "frac": round(achieved / FP64_VEC_PEAK_TF, 4),
+        "frac_of_nofma_ceiling": round(achieved / FP64_NOFMA_PEAK_TF, 4),
+        "flop_convention": "20 flop per point-force contribution (SURVEY 8d); peak 78.6 TF "
+                           "counts FMA as 2, the FMA-free ceiling (-ffp-contract=off, needed "
+                           "for bit-exactness) is 39.3 TF",
+        "traffic": traffic,
+        "traffic_source": tr.get("source") if tr else None,
+        "hbm_measured_gbs": round(traffic / (trav_ms * 1e-3) / 1e9, 1)
+        if traffic and trav_ms > 0 else None,
+        "kernel": kernel,
+        "kernel_ms": dict(avg=round(trav_ms, 4), **kstats),
+        "launches": trav_launches,
+        "flops_per_launch": round(flops_per_launch),
+        "gpu_clock": clock_stats,
+    }
+    roofline.update(extra)
 
     cpu_baseline = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline and direct:
@@ -252,7 +352,7 @@ def main():
     if rank == 0:
         line = {
             "metric": "body-steps/sec at N=1e6, theta=0.5; achieved HBM GB/s vs roofline"
-            if args.config == "c3" else f"body-steps/sec ({args.config}, theta={args.theta})",
+            if args.config == "c3" else f"body-steps/sec ({scene_name}, theta={args.theta})",
             "value": round(value, 1),
             "unit": "body-steps/s",
             "n_gpus": world,
@@ -260,7 +360,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": scaling,
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (seeded BodyFactory scenes generated in-process)",
@@ -280,6 +380,8 @@ def main():
             "roofline": roofline,
             "cpu_baseline": cpu_baseline,
         }
+        if per_rank is not None:
+            line["per_rank_phase_ms_per_step"] = per_rank
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:

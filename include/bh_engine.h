@@ -127,11 +127,22 @@ int64_t bh_last_tree_nodes(const bh_engine *e);
  * engine's own stream; *launches receives the count. */
 int bh_traverse_kernel_ms(const bh_engine *e, double *avg_ms, int64_t *launches);
 
+/* The same measurement per launch, in launch order (ms): min / median / max of the traversal
+ * over a timed region.  BH_E_CAPACITY + *n_out if cap is too small. */
+int bh_traverse_kernel_samples(const bh_engine *e, double *ms, int64_t cap, int64_t *n_out);
+
 /* Lane efficiency of the last bh_compute_accelerations(..., visits != NULL): the sum over
  * bodies of visited nodes, the sum over wavefronts of nodes the wave's shared cursor stopped
  * at (union of its 64 bodies' traversals), and the number of wavefronts. */
 int bh_traversal_stats(const bh_engine *e, int64_t *lane_visits, int64_t *wave_iters,
                        int64_t *waves);
+
+/* All counters of the last bh_compute_accelerations(..., visits != NULL), summed over bodies /
+ * wavefronts: [0] nodes visited, [1] point-force contributions (accepted internal nodes and
+ * other bodies' leaves: the 20-flop work units of the FP64 roofline), [2] nodes the wavefronts'
+ * shared cursors stopped at, [3] point-force blocks the wavefronts executed, [4] wavefronts.
+ * Lane efficiency = [0] / (64 [2]); force-block lane use = ([1] + bodies) / (64 [3]). */
+int bh_traversal_counters(const bh_engine *e, int64_t *out5);
 
 /* Enable/disable per-phase event timing (default off: no events in the hot loop). */
 int bh_set_profiling(bh_engine *e, int enabled);
