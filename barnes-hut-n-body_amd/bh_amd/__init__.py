@@ -480,10 +480,21 @@ class PhysicsEngine:
                               merge_max_mass=self.merge_max_mass,
                               merge_min_dist=self.merge_min_dist)
 
-    def _push(self):
+    def _soa(self):
         bs = self._bodies
-        self._eng.reset_bodies(*(np.array([getattr(b, f) for b in bs], dtype=np.float64)
-                                 for f in ("x", "y", "vx", "vy", "m")))
+        return np.array([[b.x, b.y, b.vx, b.vy, b.m] for b in bs], dtype=np.float64).reshape(-1, 5)
+
+    def _push(self):
+        soa = self._soa()
+        self._eng.reset_bodies(*soa.T)
+        self._shadow = soa
+
+    def _changed(self) -> bool:
+        """Whether the caller's bodies differ (bitwise) from what the engine holds; step()
+        re-uploads only then, so the engine keeps its Morton-ordered state across frames."""
+        soa = self._soa()
+        return soa.shape != self._shadow.shape or not np.array_equal(
+            soa.view(np.int64), self._shadow.view(np.int64))
 
     def _pull(self, after_step=False):
         x, y, vx, vy, m = self._eng.get_bodies()
@@ -497,10 +508,12 @@ class PhysicsEngine:
         for i in range(n):
             b = bs[i]
             b.x, b.y, b.vx, b.vy, b.m = float(x[i]), float(y[i]), float(vx[i]), float(vy[i]), float(m[i])
+        self._shadow = np.stack([x, y, vx, vy, m], axis=1) if n else np.zeros((0, 5))
 
     def step(self):  # BHA:405-439
         self._eng.set_params(self._params())
-        self._push()
+        if self._changed():  # the caller edited bodies between frames
+            self._push()
         self._eng.step(1)
         self._pull(after_step=True)
 

@@ -232,11 +232,12 @@ void merge_candidates(int64_t n, const double *x, const double *y, const double 
                       MergePair *box, uint32_t cap, hipStream_t s);
 // Sequential merge rule on the device (one workgroup): removals become tombstones
 // (cidx |= CIDX_DEAD) logged in dlog[scal[2]++]; scal[3] = pair count if the mailbox overflowed.
-// skeys/sidx: scratch of cap entries (long lists); bits: (n_cap >> 5) + 1 words and slot_of:
-// n_cap entries, n_cap > every caller index (the bitmap replay of long lists).
+// skeys/sidx: scratch of 2 x cap entries (long lists); bits: (n_cap >> 5) + 1 words and
+// slot_of: n_cap entries, n_cap > every caller index (the bitmap replay of long lists); n bounds
+// the caller indices (radix sort width).
 void merge_replay(const MergePair *box, uint32_t cap, double *m, uint32_t *cidx, uint32_t *scal,
                   uint32_t *dlog, uint64_t *skeys, uint32_t *sidx, uint32_t *bits,
-                  uint32_t *slot_of, hipStream_t s);
+                  uint32_t *slot_of, int64_t n, hipStream_t s);
 size_t compact_cub_bytes(int64_t n);
 // Remove tombstoned slots preserving order; caller indices are renumbered past the removed
 // ones (dead_cidx sorted ascending, n_dead entries).  keep, pos: n-entry scratch.

@@ -103,6 +103,9 @@ struct bh_engine {
     uint32_t *keep = nullptr, *pos = nullptr;
     MergePair *box = nullptr;  // candidate pairs: header + pairs
     uint32_t box_cap = 0;
+    uint32_t box_need = 0;     // pairs a step needed beyond the capacity (grown on retry)
+    BodyState snap{};          // state at the start of a bh_step call (exact merge retry)
+    int64_t snap_cap = 0, snap_n = 0;
     uint32_t *dlog = nullptr;        // removal log of the running bh_step call (caller indices)
     uint32_t *dead_sorted = nullptr; // the log sorted, for the compaction's renumbering
     uint64_t *rkeys = nullptr;       // replay sort scratch (long candidate lists)
@@ -510,12 +513,14 @@ int pinned_reserve(bh_engine *e, size_t bytes) {
 }
 
 int merge_bufs(bh_engine *e) {
-    const uint32_t cap = (uint32_t)std::max<int64_t>(1 << 16, e->cap);
+    // two candidate pairs per body, or what an overflowing step needed (bh_step's retry)
+    const uint32_t cap = (uint32_t)std::min<int64_t>(
+        0xFFFFFFF0ll, std::max<int64_t>({1 << 16, 2 * e->cap, (int64_t)e->box_need}));
     if (!e->box || e->box_cap < cap) {
         e->box_cap = cap;
         TRY(dev_alloc(e, e->box, (size_t)cap + 1));
-        TRY(dev_alloc(e, e->rkeys, cap));
-        TRY(dev_alloc(e, e->ridx, cap));
+        TRY(dev_alloc(e, e->rkeys, 2 * (size_t)cap));
+        TRY(dev_alloc(e, e->ridx, 2 * (size_t)cap));
     }
     if (e->dlog_cap < e->cap) {  // at most every body is removed within one call
         TRY(dev_alloc(e, e->dlog, (size_t)e->cap + 1));
@@ -535,7 +540,7 @@ int merge(bh_engine *e) {
     merge_candidates(e->n, e->st.x, e->st.y, e->st.m, e->st.cidx, e->p.merge_max_mass, minD2,
                      e->heavy, e->box, e->box_cap, e->stream);
     merge_replay(e->box, e->box_cap, e->st.m, e->st.cidx, e->scalars, e->dlog, e->rkeys, e->ridx,
-                 e->mbits, e->mslot, e->stream);
+                 e->mbits, e->mslot, e->n, e->stream);
     HIPCHK(e, hipGetLastError());
     e->merge_ran = true;
     TRY(mark(e, 3));
@@ -543,8 +548,11 @@ int merge(bh_engine *e) {
 }
 
 // End of a bh_step call (the stream is idle): read the removal count, compact the state and
-// renumber caller indices; record the removals for bh_last_removed.
-int finish_merges(bh_engine *e) {
+// renumber caller indices; record the removals for bh_last_removed.  *overflow receives the
+// candidate count of a step whose pairs did not fit the mailbox (nothing is compacted then:
+// the call is replayed from its snapshot with a larger mailbox, see bh_step).
+int finish_merges(bh_engine *e, uint32_t *overflow) {
+    *overflow = 0;
     e->removed.clear();
     if (!e->merge_ran) return BH_OK;
     e->merge_ran = false;
@@ -553,12 +561,11 @@ int finish_merges(bh_engine *e) {
     HIPCHK(e, hipMemcpyAsync(h, e->scalars, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipMemcpyAsync(h + 4, e->box, sizeof(MergeHeader), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
-    const uint32_t nd = h[2], overflow = h[3];
+    const uint32_t nd = h[2];
     const MergeHeader hdr = *reinterpret_cast<const MergeHeader *>(h + 4);
-    if (overflow) {
-        e->err = "merge rule: " + std::to_string(overflow) + " candidate pairs in one step exceed "
-                 "the mailbox capacity " + std::to_string(e->box_cap);
-        return BH_E_CAPACITY;
+    if (h[3]) {
+        *overflow = h[3];
+        return BH_OK;
     }
     if (hdr.heavies == 0) e->heavy_possible = false;
     if (nd == 0) return BH_OK;
@@ -574,6 +581,40 @@ int finish_merges(bh_engine *e) {
     e->removed.assign(dead.begin(), dead.end());
     e->tree_valid = false;  // BHA:526
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    return BH_OK;
+}
+
+// Copy of the state at the start of a bh_step call that may merge: if a step's candidate
+// pairs overflow the mailbox, the call is replayed from here with a larger one, so the rule
+// (BHA:478-520) holds for any number of pairs.
+int copy_state(bh_engine *e, const BodyState &src, const BodyState &dst, int64_t n) {
+    if (n <= 0) return BH_OK;
+    const size_t d = sizeof(double) * (size_t)n;
+    HIPCHK(e, hipMemcpyAsync(dst.x, src.x, d, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(dst.y, src.y, d, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(dst.vx, src.vx, d, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(dst.vy, src.vy, d, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(dst.m, src.m, d, hipMemcpyDeviceToDevice, e->stream));
+    HIPCHK(e, hipMemcpyAsync(dst.cidx, src.cidx, sizeof(uint32_t) * (size_t)n,
+                             hipMemcpyDeviceToDevice, e->stream));
+    return BH_OK;
+}
+
+int snapshot(bh_engine *e) {
+    if (e->snap_cap < e->cap) {
+        TRY(alloc_state(e, e->snap, (size_t)e->cap));
+        e->snap_cap = e->cap;
+    }
+    e->snap_n = e->n;
+    return copy_state(e, e->st, e->snap, e->n);
+}
+
+int restore(bh_engine *e) {
+    TRY(copy_state(e, e->snap, e->st, e->snap_n));
+    e->n = e->snap_n;
+    e->spl_nb = 0;  // the splitters describe the discarded builds' order
+    e->heavy_possible = true;
+    e->tree_valid = false;
     return BH_OK;
 }
 
@@ -836,6 +877,7 @@ void bh_destroy(bh_engine *e) {
     if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
     free_state(e->st);
     free_state(e->alt);
+    free_state(e->snap);
     void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->keys32, e->keys32_s, e->idx, e->perm, e->cpl, e->cnt,
                     e->base, e->cell_start, e->nodes, e->span_list, e->super_list,
                     e->span_children, e->scalars, e->visits32, e->contrib32, e->wave_iters, e->wave_blocks, e->heavy, e->keep,
@@ -910,15 +952,33 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
 int bh_step(bh_engine *e, int32_t k) {
     if (!e || k < 0) return BH_E_INVALID;
     HIPCHK(e, hipSetDevice(e->device));
-    e->ev_used = 0;
-    e->timings_pending = false;
-    HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, 3 * sizeof(uint32_t), e->stream));
-    e->removed.clear();
-    e->merge_ran = false;
-    for (int32_t s = 0; s < k; ++s) TRY(step_once(e));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    if (e->n > 0 && k > 0) TRY(check_tree_flags(e));
-    TRY(finish_merges(e));
+    const bool may_merge = k > 0 && e->n > 1 && e->p.merge_min_dist > 0.0 && e->heavy_possible;
+    if (may_merge) TRY(snapshot(e));
+    for (;;) {
+        e->ev_used = 0;
+        e->timings_pending = false;
+        HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, 3 * sizeof(uint32_t), e->stream));
+        e->removed.clear();
+        e->merge_ran = false;
+        for (int32_t s = 0; s < k; ++s) TRY(step_once(e));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        // the merge bookkeeping first, so that an error below leaves a compacted state
+        const int tree_rc = (e->n > 0 && k > 0) ? check_tree_flags(e) : BH_OK;
+        uint32_t overflow = 0;
+        TRY(finish_merges(e, &overflow));
+        if (overflow) {  // a step's candidate pairs exceeded the mailbox: replay the call
+            if (!may_merge) {
+                e->err = "merge rule: candidate mailbox overflow without a snapshot";
+                return BH_E_STATE;
+            }
+            e->box_need = (uint32_t)std::min<uint64_t>(0xFFFFFFF0ull, 2ull * overflow);
+            TRY(merge_bufs(e));
+            TRY(restore(e));
+            continue;
+        }
+        if (tree_rc != BH_OK) return tree_rc;
+        break;
+    }
     if (e->profiling) TRY(collect_timings(e));
     return BH_OK;
 }

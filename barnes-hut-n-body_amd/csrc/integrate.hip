@@ -56,6 +56,7 @@ __global__ __launch_bounds__(TB) void k_scatter_caller(int64_t n, const uint32_t
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
     const uint32_t o = cidx[i];
+    if (o & CIDX_DEAD) return;  // a tombstone has no caller slot
     for (int j = 0; j < k; ++j) p.dst[j][o] = p.src[j][i];
 }
 
@@ -66,6 +67,7 @@ __global__ __launch_bounds__(TB) void k_scatter_acc(int64_t n, const uint32_t *_
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
     const uint32_t o = cidx[i];
+    if (o & CIDX_DEAD) return;  // a tombstone has no caller slot
     ax[o] = a2[2 * i];
     ay[o] = a2[2 * i + 1];
 }
@@ -295,7 +297,7 @@ __global__ __launch_bounds__(REPLAY_TB) void k_merge_replay(const MergePair *__r
                                                             uint32_t *cidx, uint32_t *scal,
                                                             uint32_t *dlog, uint64_t *skeys,
                                                             uint32_t *sidx, uint32_t *bits,
-                                                            uint32_t *slot_of) {
+                                                            uint32_t *slot_of, int key_bits) {
     __shared__ uint64_t lk[REPLAY_LDS];
     __shared__ uint32_t li[REPLAY_LDS];
     __shared__ uint32_t hkey[REPLAY_HASH], hcidx[REPLAY_HASH];
@@ -415,38 +417,56 @@ __global__ __launch_bounds__(REPLAY_TB) void k_merge_replay(const MergePair *__r
         }
         return;
     }
-    if (threadIdx.x != 0) return;  // large lists (rare): one-thread heapsort in global scratch
-    for (uint32_t i = 0; i < count; ++i) {
-        skeys[i] = pair_key(pairs[i]);
-        sidx[i] = i;
+    // Long lists naming more heavies than the bitmap replay takes (rare): stable LSD radix sort
+    // of (key, index) by the whole workgroup in global scratch (skeys / sidx hold 2 x cap),
+    // 4-bit digits over the caller-index bits of the victim, then of the heavy.
+    uint64_t *ka = skeys, *kb = skeys + cap;
+    uint32_t *ia = sidx, *ib = sidx + cap;
+    for (uint32_t i = threadIdx.x; i < count; i += REPLAY_TB) {
+        ka[i] = pair_key(pairs[i]);
+        ia[i] = i;
     }
-    auto sift = [&](uint32_t root, uint32_t end) {
-        for (;;) {
-            uint32_t c = 2 * root + 1;
-            if (c >= end) return;
-            if (c + 1 < end && skeys[c] < skeys[c + 1]) ++c;
-            if (skeys[root] >= skeys[c]) return;
-            const uint64_t tk = skeys[root];
-            skeys[root] = skeys[c];
-            skeys[c] = tk;
-            const uint32_t ti = sidx[root];
-            sidx[root] = sidx[c];
-            sidx[c] = ti;
-            root = c;
+    uint32_t *cnt = reinterpret_cast<uint32_t *>(lk);  // 16 digits x REPLAY_TB threads
+    static_assert(sizeof(lk) >= 16 * REPLAY_TB * sizeof(uint32_t), "radix counters in LDS");
+    const uint32_t per = (count + REPLAY_TB - 1) / REPLAY_TB;
+    const uint32_t b0 = min(threadIdx.x * per, count), b1 = min(b0 + per, count);
+    for (int pass = 0; pass < 2 * ((key_bits + 3) / 4); ++pass) {
+        const int half = pass / ((key_bits + 3) / 4);  // 0: victim bits, 1: heavy bits
+        const int shift = 32 * half + 4 * (pass % ((key_bits + 3) / 4));
+        __syncthreads();
+        uint32_t c[16];
+        for (int d = 0; d < 16; ++d) c[d] = 0;
+        for (uint32_t i = b0; i < b1; ++i) ++c[(ka[i] >> shift) & 15u];
+        for (int d = 0; d < 16; ++d) cnt[d * REPLAY_TB + threadIdx.x] = c[d];
+        __syncthreads();
+        if (threadIdx.x == 0) {  // exclusive scan, digit-major: stable across threads
+            uint32_t acc = 0;
+            for (int i = 0; i < 16 * REPLAY_TB; ++i) {
+                const uint32_t v = cnt[i];
+                cnt[i] = acc;
+                acc += v;
+            }
         }
-    };
-    for (uint32_t r = count / 2; r-- > 0;) sift(r, count);
-    for (uint32_t end = count; end-- > 1;) {
-        const uint64_t tk = skeys[0];
-        skeys[0] = skeys[end];
-        skeys[end] = tk;
-        const uint32_t ti = sidx[0];
-        sidx[0] = sidx[end];
-        sidx[end] = ti;
-        sift(0, end);
+        __syncthreads();
+        for (int d = 0; d < 16; ++d) c[d] = cnt[d * REPLAY_TB + threadIdx.x];
+        for (uint32_t i = b0; i < b1; ++i) {
+            const uint64_t k = ka[i];
+            const uint32_t o = c[(k >> shift) & 15u]++;
+            kb[o] = k;
+            ib[o] = ia[i];
+        }
+        __threadfence_block();
+        uint64_t *tk = ka;
+        ka = kb;
+        kb = tk;
+        uint32_t *ti = ia;
+        ia = ib;
+        ib = ti;
     }
+    __syncthreads();
+    if (threadIdx.x != 0) return;
     replay_sorted(
-        pairs, count, [&](uint32_t q) { return skeys[q]; }, [&](uint32_t q) { return sidx[q]; },
+        pairs, count, [&](uint32_t q) { return ka[q]; }, [&](uint32_t q) { return ia[q]; },
         m, cidx, dlog, nd);
     scal[2] = nd;
 }
@@ -522,9 +542,11 @@ void merge_candidates(int64_t n, const double *x, const double *y, const double 
 
 void merge_replay(const MergePair *box, uint32_t cap, double *m, uint32_t *cidx, uint32_t *scal,
                   uint32_t *dlog, uint64_t *skeys, uint32_t *sidx, uint32_t *bits,
-                  uint32_t *slot_of, hipStream_t s) {
+                  uint32_t *slot_of, int64_t n, hipStream_t s) {
+    int key_bits = 1;  // caller indices are < n
+    while (key_bits < 32 && (int64_t(1) << key_bits) < n) ++key_bits;
     k_merge_replay<<<1, REPLAY_TB, 0, s>>>(box, cap, m, cidx, scal, dlog, skeys, sidx, bits,
-                                           slot_of);
+                                           slot_of, key_bits);
 }
 
 size_t compact_cub_bytes(int64_t n) {

@@ -1,6 +1,7 @@
 // C++ PhysicsEngine mirror over the C-ABI (see physics_engine.hpp).
 #include "physics_engine.hpp"
 
+#include <cstring>
 #include <string>
 
 namespace bh {
@@ -55,6 +56,13 @@ void PhysicsEngine::pushBodies() {
         x[i] = b.x; y[i] = b.y; vx[i] = b.vx; vy[i] = b.vy; m[i] = b.m;
     }
     check(bh_reset_bodies(eng_, (int64_t)n, x.data(), y.data(), vx.data(), vy.data(), m.data()));
+    shadow_ = *bodies_;
+}
+
+// Bitwise: a caller that wrote the same value back (or a NaN) does not force an upload.
+bool PhysicsEngine::bodiesChanged() const {
+    return bodies_->size() != shadow_.size() ||
+           std::memcmp(bodies_->data(), shadow_.data(), sizeof(Body) * shadow_.size()) != 0;
 }
 
 // Write results back into the SAME Body objects (the reference mutates in place,
@@ -74,11 +82,12 @@ void PhysicsEngine::pullBodies(bool afterStep) {
     check(bh_get_bodies(eng_, x.data(), y.data(), vx.data(), vy.data(), m.data(), n, &got));
     if ((int64_t)bodies_->size() != got) throw std::runtime_error("engine and caller lists diverged");
     for (int64_t i = 0; i < got; ++i) (*bodies_)[(size_t)i] = Body{x[i], y[i], vx[i], vy[i], m[i]};
+    shadow_ = *bodies_;
 }
 
 void PhysicsEngine::step() {
     pushParams();
-    pushBodies();  // the caller may have edited bodies between frames
+    if (bodiesChanged()) pushBodies();  // the caller edited bodies between frames
     check(bh_step(eng_, 1));
     pullBodies(true);
 }

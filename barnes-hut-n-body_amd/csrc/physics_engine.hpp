@@ -79,11 +79,15 @@ public:
 private:
     void pushParams();
     void pushBodies();
+    bool bodiesChanged() const;
     void pullBodies(bool afterStep);
     void check(int rc) const;
 
     std::vector<Body> *bodies_;
     bh_engine *eng_ = nullptr;
+    // What the engine holds, in the caller's order (as last pushed or pulled): step() re-uploads
+    // only when the caller's list differs, so the engine keeps its Morton-ordered state.
+    std::vector<Body> shadow_;
 };
 
 }  // namespace bh

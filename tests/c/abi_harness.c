@@ -1,0 +1,303 @@
+/*
+ * C-side replay of the Kotlin drop-in through include/bh_engine.h --
+ * TEST INFRASTRUCTURE (links the oracle as the checker).
+ *
+ * The Kotlin shim cannot be compiled here (no JDK), so this harness performs exactly the
+ * calls its JNI glue makes, with the shim's own logic (shadow copy, upload only when the
+ * caller's list changed, pull(afterStep) applying bh_last_removed once), driven by the frame
+ * sequence of NBodyPanel (PNL:103 ctor, :291 step, :333-340 getTreeForDebug().visitQuads,
+ * :247-260 live Config edits, :262/:285 resetBodies, :228-234 getBodies() + new disk).  After
+ * every frame the caller's list must equal the reference restatement's list word for word,
+ * and every surviving light body must still be the same Body object (its unique start mass).
+ *
+ * Exit status 0 = pass; the last line says what was checked.
+ */
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "bh_engine.h"
+#include "bh_oracle.h"
+
+/* ---- Config (CFG:5-23), read live ---------------------------------------------------- */
+static double cfg_G = 80.0, cfg_DT = 0.005, cfg_theta = 0.5, cfg_SOFT2 = 1.0;
+static int cfg_W = 2400, cfg_H = 800;
+
+/* ---- the caller's MutableList<Body> (BHA:21-25); `id` stands for object identity ------- */
+typedef struct {
+    double x, y, vx, vy, m;
+    long id;
+} Body;
+typedef struct {
+    Body *b;
+    long n;
+} List;
+
+static double *start_mass; /* by id */
+static long next_id;
+
+static void fail(const char *what, long frame) {
+    fprintf(stderr, "abi_harness: FAIL at frame %ld: %s\n", frame, what);
+    exit(1);
+}
+
+/* ---- the Kotlin shim, over the C-ABI ------------------------------- */
+typedef struct {
+    bh_engine *h;
+    List *bodies;
+    double *shadow; /* 5 * n SoA of what the engine holds */
+    long shadow_n;
+    double mergeMaxMass, mergeMinDist; /* BHA:315,321 */
+} Shim;
+
+static void shim_check(Shim *s, int rc, const char *call) {
+    if (rc != BH_OK) {
+        fprintf(stderr, "abi_harness: %s rc=%d: %s\n", call, rc, bh_last_error(s->h));
+        exit(1);
+    }
+}
+
+static void shim_params(Shim *s) {
+    bh_params p = {cfg_G, cfg_DT, cfg_theta, cfg_SOFT2, cfg_W, cfg_H, s->mergeMaxMass,
+                   s->mergeMinDist};
+    shim_check(s, bh_set_params(s->h, &p), "bh_set_params");
+}
+
+static void soa_of(const List *l, double *a) {
+    long n = l->n;
+    for (long i = 0; i < n; ++i) {
+        a[i] = l->b[i].x;
+        a[n + i] = l->b[i].y;
+        a[2 * n + i] = l->b[i].vx;
+        a[3 * n + i] = l->b[i].vy;
+        a[4 * n + i] = l->b[i].m;
+    }
+}
+
+static void shim_push(Shim *s) {
+    long n = s->bodies->n;
+    free(s->shadow);
+    s->shadow = malloc(sizeof(double) * (5 * n + 1));
+    soa_of(s->bodies, s->shadow);
+    s->shadow_n = n;
+    double *a = s->shadow;
+    shim_check(s, bh_reset_bodies(s->h, n, a, a + n, a + 2 * n, a + 3 * n, a + 4 * n),
+               "bh_reset_bodies");
+}
+
+static int shim_changed(Shim *s) {
+    long n = s->bodies->n;
+    if (n != s->shadow_n) return 1;
+    double *a = malloc(sizeof(double) * (5 * n + 1));
+    soa_of(s->bodies, a);
+    int diff = memcmp(a, s->shadow, sizeof(double) * 5 * n) != 0;
+    free(a);
+    return diff;
+}
+
+/* pull(afterStep): removals are applied once, right after the step that made them */
+static void shim_pull(Shim *s, int after_step) {
+    bh_engine *e = s->h;
+    if (after_step) {
+        int64_t nr = 0;
+        int rc = bh_last_removed(e, NULL, 0, &nr);
+        if (rc != BH_OK && rc != BH_E_CAPACITY) shim_check(s, rc, "bh_last_removed");
+        int64_t *rem = malloc(sizeof(int64_t) * (nr + 1));
+        shim_check(s, bh_last_removed(e, rem, nr, &nr), "bh_last_removed");
+        for (int64_t k = nr; k-- > 0;) { /* removeAt in descending index (BHA:519) */
+            long j = (long)rem[k];
+            memmove(&s->bodies->b[j], &s->bodies->b[j + 1], sizeof(Body) * (s->bodies->n - j - 1));
+            s->bodies->n -= 1;
+        }
+        free(rem);
+    }
+    int64_t n = bh_num_bodies(e), got = 0;
+    double *a = malloc(sizeof(double) * (5 * n + 1));
+    shim_check(s, bh_get_bodies(e, a, a + n, a + 2 * n, a + 3 * n, a + 4 * n, n, &got),
+               "bh_get_bodies");
+    if (got != s->bodies->n) {
+        fprintf(stderr, "abi_harness: engine N %ld vs caller list %ld\n", (long)got, s->bodies->n);
+        exit(1);
+    }
+    for (long i = 0; i < n; ++i) { /* into the SAME Body objects (BHA:414-432) */
+        Body *b = &s->bodies->b[i];
+        b->x = a[i];
+        b->y = a[n + i];
+        b->vx = a[2 * n + i];
+        b->vy = a[3 * n + i];
+        b->m = a[4 * n + i];
+    }
+    free(s->shadow);
+    s->shadow = a;
+    s->shadow_n = n;
+}
+
+static void shim_create(Shim *s, List *initial) {
+    memset(s, 0, sizeof(*s));
+    bh_params p;
+    bh_default_params(&p);
+    s->mergeMaxMass = 4000.0;
+    s->mergeMinDist = 8.0;
+    if (bh_create(&p, 0, &s->h) != BH_OK) {
+        fprintf(stderr, "abi_harness: bh_create failed (no GPU?)\n");
+        exit(1);
+    }
+    s->bodies = initial;
+    shim_params(s);
+    shim_push(s);
+}
+
+static void shim_reset(Shim *s, List *l) {
+    s->bodies = l;
+    shim_push(s);
+}
+
+static long shim_steps_uploaded;
+static void shim_step(Shim *s) {
+    shim_params(s);
+    if (shim_changed(s)) {
+        shim_push(s);
+        ++shim_steps_uploaded;
+    }
+    shim_check(s, bh_step(s->h, 1), "bh_step");
+    shim_pull(s, 1);
+}
+
+/* getTreeForDebug(): the quads (BHTree.fromQuads), then pull(false) */
+static double *shim_tree(Shim *s, int64_t *nq) {
+    shim_params(s);
+    int rc = bh_get_quads(s->h, NULL, NULL, NULL, 0, nq);
+    if (rc != BH_OK && rc != BH_E_CAPACITY) shim_check(s, rc, "bh_get_quads");
+    double *q = malloc(sizeof(double) * (3 * *nq + 1));
+    shim_check(s, bh_get_quads(s->h, q, q + *nq, q + 2 * *nq, *nq, nq), "bh_get_quads");
+    shim_pull(s, 0);
+    return q;
+}
+
+/* ---- scenes --------------------------------------------------------------------------- */
+static void list_append_soa(List *l, long n, const double *x, const double *y, const double *vx,
+                            const double *vy, const double *m) {
+    l->b = realloc(l->b, sizeof(Body) * (l->n + n + 1));
+    start_mass = realloc(start_mass, sizeof(double) * (next_id + n + 1));
+    for (long i = 0; i < n; ++i) {
+        /* a unique start mass per body (light bodies keep theirs: only heavies absorb) */
+        double mi = m[i] <= 4000.0 ? m[i] * (1.0 + (double)(next_id + 1) * 0x1p-40) : m[i];
+        Body b = {x[i], y[i], vx[i], vy[i], mi, next_id};
+        start_mass[next_id++] = mi;
+        l->b[l->n++] = b;
+    }
+}
+
+static void add_galaxy(List *l, long n, double x, double y, double vx, double r, double mc,
+                       double msat, long seed) {
+    double *a = malloc(sizeof(double) * 5 * n);
+    if (bh_scene_galaxy_disk((int32_t)n, 0.03, 0.0, -1.0, -1.0, 0.01, 0.0, 1, seed, vx, 0.0, x, y,
+                             r, 8.0, mc, msat, 80.0, a, a + n, a + 2 * n, a + 3 * n, a + 4 * n) != 0)
+        fail("bh_scene_galaxy_disk", -1);
+    list_append_soa(l, n, a, a + n, a + 2 * n, a + 3 * n, a + 4 * n);
+    free(a);
+}
+
+static void add_uniform(List *l, long n, double m, long seed) {
+    double *a = malloc(sizeof(double) * 5 * n);
+    if (bh_scene_uniform((int32_t)n, m, seed, cfg_W, cfg_H, a, a + n, a + 2 * n, a + 3 * n,
+                         a + 4 * n) != 0)
+        fail("bh_scene_uniform", -1);
+    list_append_soa(l, n, a, a + n, a + 2 * n, a + 3 * n, a + 4 * n);
+    free(a);
+}
+
+/* ---- the checker ---------------------------------------------------------------------- */
+static oracle_params oparams(const Shim *s) {
+    oracle_params p = {cfg_G, cfg_DT, cfg_theta, cfg_SOFT2, cfg_W, cfg_H, s->mergeMaxMass,
+                       s->mergeMinDist, 0, 0};
+    return p;
+}
+
+static oracle_engine *oracle_of(const List *l, const Shim *s) {
+    long n = l->n;
+    double *a = malloc(sizeof(double) * (5 * n + 1));
+    soa_of(l, a);
+    oracle_params p = oparams(s);
+    oracle_engine *o = oracle_create(&p, n, a, a + n, a + 2 * n, a + 3 * n, a + 4 * n);
+    free(a);
+    return o;
+}
+
+static void compare(const List *l, oracle_engine *o, long frame) {
+    long n = oracle_num_bodies(o);
+    if (n != l->n) fail("N differs from the oracle", frame);
+    double *a = malloc(sizeof(double) * (5 * n + 1)), *b = malloc(sizeof(double) * (5 * n + 1));
+    oracle_get_bodies(o, a, a + n, a + 2 * n, a + 3 * n, a + 4 * n);
+    soa_of(l, b);
+    if (memcmp(a, b, sizeof(double) * 5 * n) != 0) fail("state differs from the oracle", frame);
+    free(a);
+    free(b);
+    for (long i = 0; i < n; ++i) { /* identity: light bodies keep their unique start mass */
+        const Body *bd = &l->b[i];
+        if (start_mass[bd->id] <= 4000.0 && bd->m != start_mass[bd->id])
+            fail("a surviving Body is not the object the reference keeps", frame);
+    }
+}
+
+int main(void) {
+    List list = {NULL, 0};
+    /* defaultBodies() (PNL:83-100), scaled down */
+    add_galaxy(&list, 3000, 1200.0, 400.0, 0.0, 300.0, 50000.0, 5000.0, 1);
+    add_galaxy(&list, 800, 1200.0, 160.0, -50.0, 100.0, 5000.0, 500.0, 2);
+    Shim s;
+    shim_create(&s, &list); /* PNL:103 */
+    oracle_engine *o = oracle_of(&list, &s);
+    List list2 = {NULL, 0}, list3 = {NULL, 0};
+    long removed_total = 0, quads_checked = 0;
+    for (long frame = 0; frame < 40; ++frame) {
+        if (frame == 10) cfg_theta = 0.7; /* Z/X keys (PNL:247-248), read live */
+        if (frame == 14) cfg_DT = 0.008;  /* O/P keys (PNL:255-257) */
+        if (frame == 16) s.mergeMaxMass = 3000.0;
+        if (frame == 20) { /* 'C' key: resetBodies(makeUniformRandom(...)) (PNL:282-286) */
+            add_uniform(&list2, 2500, 0.5, 5);
+            add_galaxy(&list2, 400, 600.0, 300.0, 20.0, 60.0, 8000.0, 400.0, 7);
+            shim_reset(&s, &list2);
+            oracle_destroy(o);
+            o = oracle_of(&list2, &s);
+        }
+        if (frame == 30) { /* mouse release: getBodies() + new disk -> resetBodies (PNL:228-234) */
+            for (long i = 0; i < s.bodies->n; ++i) {
+                list3.b = realloc(list3.b, sizeof(Body) * (list3.n + 1));
+                list3.b[list3.n++] = s.bodies->b[i]; /* the same objects, re-listed */
+            }
+            add_galaxy(&list3, 500, 1700.0, 500.0, 0.0, 80.0, 6000.0, 300.0, 9);
+            shim_reset(&s, &list3);
+            oracle_destroy(o);
+            o = oracle_of(&list3, &s);
+        }
+        oracle_params op = oparams(&s);
+        oracle_set_params(o, &op);
+        long before = s.bodies->n;
+        shim_step(&s); /* PNL:291 */
+        oracle_step(o, 1);
+        removed_total += before - s.bodies->n;
+        compare(s.bodies, o, frame);
+        if (frame % 4 == 3) { /* showTree: getTreeForDebug().visitQuads (PNL:333-340) */
+            int64_t nq = 0;
+            double *q = shim_tree(&s, &nq);
+            int64_t mq = oracle_quads(o, NULL, NULL, NULL, 0);
+            double *w = malloc(sizeof(double) * (3 * mq + 1));
+            oracle_quads(o, w, w + mq, w + 2 * mq, mq);
+            if (mq != nq || memcmp(q, w, sizeof(double) * 3 * nq) != 0)
+                fail("quads differ from the reference's visitQuads", frame);
+            quads_checked += nq;
+            free(q);
+            free(w);
+            compare(s.bodies, o, frame); /* a fresh debug build may jitter (BHA:146-151) */
+        }
+    }
+    if (removed_total == 0) fail("the scene never merged: identity bookkeeping untested", 40);
+    printf("abi_harness: 40 frames bit-identical to the oracle; %ld bodies merged away, "
+           "%ld quads checked, %ld uploads after the constructor/resets\n",
+           removed_total, quads_checked, shim_steps_uploaded);
+    oracle_destroy(o);
+    bh_destroy(s.h);
+    return 0;
+}
