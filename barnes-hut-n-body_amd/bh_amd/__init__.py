@@ -43,6 +43,7 @@ EXPORTED_SYMBOLS = (
     "bh_nbody3d_create", "bh_nbody3d_destroy", "bh_nbody3d_last_error", "bh_nbody3d_set",
     "bh_nbody3d_step", "bh_nbody3d_accelerations", "bh_nbody3d_get", "bh_nbody3d_last_ms",
     "bh_local_group_create", "bh_local_group_destroy", "bh_create_local",
+    "bh_save_state", "bh_load_state",
 )
 
 
@@ -101,6 +102,8 @@ def load_library(path: str | None = None):
     lib.bh_get_params.argtypes = [_VP, ctypes.POINTER(BhParams)]
     lib.bh_reset_bodies.argtypes = [_VP, ctypes.c_int64, _D, _D, _D, _D, _D]
     lib.bh_step.argtypes = [_VP, ctypes.c_int32]
+    lib.bh_save_state.argtypes = [_VP, ctypes.c_char_p]
+    lib.bh_load_state.argtypes = [_VP, ctypes.c_char_p]
     lib.bh_num_bodies.argtypes = [_VP]
     lib.bh_num_bodies.restype = ctypes.c_int64
     lib.bh_get_bodies.argtypes = [_VP, _D, _D, _D, _D, _D, ctypes.c_int64, _I64P]
@@ -319,6 +322,16 @@ class Engine:
 
     def step(self, k: int = 1):
         self._check(self._lib.bh_step(self._h, int(k)))
+
+    def save_state(self, path: str):
+        """Checkpoint: Config fields + bodies in caller order (bh_save_state)."""
+        self._check(self._lib.bh_save_state(self._h, os.fsencode(path)))
+
+    def load_state(self, path: str):
+        """Resume from a bh_save_state file (params and bodies replaced)."""
+        self._check(self._lib.bh_load_state(self._h, os.fsencode(path)))
+        self.params = BhParams()
+        self._check(self._lib.bh_get_params(self._h, ctypes.byref(self.params)))
 
     def num_bodies(self) -> int:
         return int(self._lib.bh_num_bodies(self._h))

@@ -141,8 +141,8 @@ struct TreeBuffers {
     uint32_t span_stride;
     struct SpanSlot *span_children;  // [(J + 1) * span_stride]
     uint32_t *super_list;  // [(J + 1) * span_groups]: group-crossing span node per (level, group)
-    void *cub_tmp;
-    size_t cub_bytes;
+    void *scratch;
+    size_t scratch_bytes;
     // adaptive bucket sort: splitters of the previous build (spl_nb of them, 0 = none: rocprim
     // sort), bucket counts (kept zeroed between builds) and starts, sort_buckets(cap) + 2 each
     uint64_t *spl;
@@ -151,7 +151,7 @@ struct TreeBuffers {
 };
 
 int cell_table_depth(int J, int64_t n);
-size_t tree_cub_bytes(int64_t n, int J);
+size_t tree_scratch_bytes(int64_t n, int J);
 hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStream_t s);
 
 // ---- launchers (traverse.hip) ----------------------------------------------------
@@ -238,7 +238,7 @@ void merge_candidates(int64_t n, const double *x, const double *y, const double 
 void merge_replay(const MergePair *box, uint32_t cap, double *m, uint32_t *cidx, uint32_t *scal,
                   uint32_t *dlog, uint64_t *skeys, uint32_t *sidx, uint32_t *bits,
                   uint32_t *slot_of, int64_t n, hipStream_t s);
-size_t compact_cub_bytes(int64_t n);
+size_t compact_scratch_bytes(int64_t n);
 // Remove tombstoned slots preserving order; caller indices are renumbered past the removed
 // ones (dead_cidx sorted ascending, n_dead entries).  keep, pos: n-entry scratch.
 hipError_t compact_state(int64_t n, uint32_t *keep, const BodyState &src, const BodyState &dst,

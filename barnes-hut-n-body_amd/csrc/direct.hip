@@ -9,7 +9,8 @@
 // body) reads them as broadcasts in sequence order — the reference's order, so the result is
 // bit-identical to the tree walk — with no criterion, cursor or ballot in the loop.  Bound by
 // fp64 VALU issue (one v_rsq_f64 and ~35 fp64 ops per interaction).
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_select.hpp>
+#include <rocprim/iterator/counting_iterator.hpp>
 
 #include "bh_device.hpp"
 #include "fastmath.hpp"
@@ -160,9 +161,9 @@ __global__ __launch_bounds__(TB) void k_direct(LeafList L, const uint32_t *__res
 
 size_t leaf_select_bytes(int64_t node_cap) {
     size_t b = 0;
-    (void)hipcub::DeviceSelect::Flagged(nullptr, b, hipcub::CountingInputIterator<uint32_t>(0),
-                                        (const uint8_t *)nullptr, (uint32_t *)nullptr,
-                                        (uint32_t *)nullptr, (int)node_cap);
+    (void)rocprim::select(nullptr, b, rocprim::counting_iterator<uint32_t>(0),
+                          (const uint8_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
+                          (size_t)node_cap);
     return b;
 }
 
@@ -171,9 +172,8 @@ hipError_t leaf_list_build(const Node *nodes, const uint32_t *d_T, int64_t node_
                            int64_t n, void *tmp, size_t tmp_bytes, hipStream_t s) {
     if (node_cap <= 0) return hipSuccess;
     k_leaf_flags<<<(unsigned)((node_cap + TB - 1) / TB), TB, 0, s>>>(nodes, d_T, flags, node_cap);
-    hipError_t st = hipcub::DeviceSelect::Flagged(tmp, tmp_bytes,
-                                                  hipcub::CountingInputIterator<uint32_t>(0), flags,
-                                                  sel, d_count, (int)node_cap, s);
+    hipError_t st = rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<uint32_t>(0),
+                                    flags, sel, d_count, (size_t)node_cap, s);
     if (st != hipSuccess) return st;
     if (n > 0) k_leaf_gather<<<(unsigned)((n + TB - 1) / TB), TB, 0, s>>>(nodes, sel, d_count, L);
     return hipGetLastError();

@@ -35,6 +35,10 @@ namespace {
 constexpr int kPhases = 5;  // build, traverse, integrate, merge, allgather
 }  // namespace
 
+namespace bh {
+void set_error(bh_engine *e, const std::string &msg);  // for the C-ABI's other translation units
+}
+
 // In-process rank group (bh_local_group_*): `world` engines of one process, one host thread
 // each, that exchange the force pieces through device-to-device copies instead of RCCL -- the
 // same pieces, rounds and in-place layout as the ncclAllGather path, so the multi-rank
@@ -119,8 +123,8 @@ struct bh_engine {
     void *pin = nullptr;  // pinned staging for small read-backs
     size_t pin_bytes = 0;
 
-    void *cub_tmp = nullptr;
-    size_t cub_bytes = 0;
+    void *scratch = nullptr;
+    size_t scratch_bytes = 0;
 
     // adaptive bucket sort (tree_build.hip): splitters written by every build
     uint64_t *spl = nullptr;
@@ -286,12 +290,12 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         e->node_cap = ncap;
         e->J_alloc = J;
     }
-    size_t cb = std::max(tree_cub_bytes(e->cap, J), compact_cub_bytes(e->cap));
-    if (cb > e->cub_bytes) {
-        if (e->cub_tmp) (void)hipFree(e->cub_tmp);
-        e->cub_tmp = nullptr;
-        HIPCHK(e, hipMalloc(&e->cub_tmp, cb));
-        e->cub_bytes = cb;
+    size_t cb = std::max(tree_scratch_bytes(e->cap, J), compact_scratch_bytes(e->cap));
+    if (cb > e->scratch_bytes) {
+        if (e->scratch) (void)hipFree(e->scratch);
+        e->scratch = nullptr;
+        HIPCHK(e, hipMalloc(&e->scratch, cb));
+        e->scratch_bytes = cb;
     }
     return BH_OK;
 }
@@ -316,8 +320,8 @@ TreeBuffers tree_buffers(bh_engine *e) {
     b.span_stride = span_stride_for(e->cap);
     b.span_children = e->span_children;
     b.super_list = e->super_list;
-    b.cub_tmp = e->cub_tmp;
-    b.cub_bytes = e->cub_bytes;
+    b.scratch = e->scratch;
+    b.scratch_bytes = e->scratch_bytes;
     b.spl = e->spl;
     b.spl_nb = e->spl_nb;
     b.bcount = e->bcount;
@@ -574,8 +578,8 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
     std::sort(dead.begin(), dead.end());
     HIPCHK(e, hipMemcpy(e->dead_sorted, dead.data(), 4 * (size_t)nd, hipMemcpyHostToDevice));
     const int64_t n = e->n;
-    HIPCHK(e, compact_state(n, e->keep, e->st, e->alt, e->dead_sorted, nd, e->pos, e->cub_tmp,
-                            e->cub_bytes, e->stream));
+    HIPCHK(e, compact_state(n, e->keep, e->st, e->alt, e->dead_sorted, nd, e->pos, e->scratch,
+                            e->scratch_bytes, e->stream));
     std::swap(e->st, e->alt);
     e->n = n - (int64_t)nd;
     e->removed.assign(dead.begin(), dead.end());
@@ -745,6 +749,10 @@ void free_state(BodyState &s) {
 
 }  // namespace
 
+void bh::set_error(bh_engine *e, const std::string &msg) {
+    if (e) e->err = msg;
+}
+
 // =========================================================================================
 extern "C" {
 
@@ -881,7 +889,7 @@ void bh_destroy(bh_engine *e) {
     void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->keys32, e->keys32_s, e->idx, e->perm, e->cpl, e->cnt,
                     e->base, e->cell_start, e->nodes, e->span_list, e->super_list,
                     e->span_children, e->scalars, e->visits32, e->contrib32, e->wave_iters, e->wave_blocks, e->heavy, e->keep,
-                    e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->mbits, e->mslot, e->cub_tmp,
+                    e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->mbits, e->mslot, e->scratch,
                     e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaves.xy, e->leaves.m,
                     e->leaves.slot, e->leaf_tmp, e->spl, e->bcount, e->bstart};
     for (void *q : ptrs)

@@ -1,6 +1,6 @@
 // Kick-drift-kick integration (BHA:410-432), caller-order copies, and the device side of the
 // merge rule (BHA:463-532).  All elementwise and coalesced over the slot (Morton) order.
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_scan.hpp>
 
 #include "bh_device.hpp"
 
@@ -549,10 +549,10 @@ void merge_replay(const MergePair *box, uint32_t cap, double *m, uint32_t *cidx,
                                            slot_of, key_bits);
 }
 
-size_t compact_cub_bytes(int64_t n) {
+size_t compact_scratch_bytes(int64_t n) {
     size_t b = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, b, (uint32_t *)nullptr, (uint32_t *)nullptr,
-                                           (int)n);
+    (void)rocprim::exclusive_scan(nullptr, b, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u,
+                                  (size_t)n, rocprim::plus<uint32_t>());
     return b;
 }
 
@@ -560,7 +560,8 @@ hipError_t compact_state(int64_t n, uint32_t *keep, const BodyState &src, const 
                          const uint32_t *dead_cidx, uint32_t n_dead, uint32_t *pos, void *tmp,
                          size_t tmp_bytes, hipStream_t s) {
     k_keep<<<grid_for(n), TB, 0, s>>>(n, src.cidx, keep);
-    hipError_t st = hipcub::DeviceScan::ExclusiveSum(tmp, tmp_bytes, keep, pos, (int)n, s);
+    hipError_t st = rocprim::exclusive_scan(tmp, tmp_bytes, keep, pos, 0u, (size_t)n,
+                                            rocprim::plus<uint32_t>(), s);
     if (st != hipSuccess) return st;
     k_compact<<<grid_for(n), TB, 0, s>>>(n, keep, pos, src, dst, dead_cidx, n_dead);
     return hipGetLastError();

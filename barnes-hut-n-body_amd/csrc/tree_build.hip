@@ -22,7 +22,7 @@
 //                records, replay of BHA:125-156 inside each jitter cell, centre of mass
 //                bottom-up (children 0..3 in order, BHA:184-200) of the chunk-local nodes
 //   k_span_*     the chunk-spanning nodes, levels J..0
-#include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 
 #include "bh_device.hpp"
@@ -1270,14 +1270,15 @@ int cell_table_depth(int J, int64_t n) {
     return d < J ? d : J;
 }
 
-size_t tree_cub_bytes(int64_t n, int J) {
+size_t tree_scratch_bytes(int64_t n, int J) {
     size_t sort_bytes = 0, scan_bytes = 0;
     (void)J;
     (void)rocprim::radix_sort_pairs<SortConfig>(nullptr, sort_bytes, (uint32_t *)nullptr,
                                                 (uint32_t *)nullptr, (uint32_t *)nullptr,
                                                 (uint32_t *)nullptr, (size_t)n, 0u, 32u);
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, scan_bytes, (uint32_t *)nullptr,
-                                           (uint32_t *)nullptr, (int)(n + 1));
+    (void)rocprim::exclusive_scan(nullptr, scan_bytes, (const uint32_t *)nullptr,
+                                  (uint32_t *)nullptr, 0u, (size_t)(n + 1),
+                                  rocprim::plus<uint32_t>());
     return sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
 }
 
@@ -1288,19 +1289,19 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     const bool bucket = b.spl_nb > 0;
     k_morton<<<grid_for(n), TB, 0, s>>>(n, b.src.x, b.src.y, b.src.cidx, g, b.keys, b.keys32,
                                         bucket ? nullptr : b.idx);
-    size_t bytes = b.cub_bytes;
+    size_t bytes = b.scratch_bytes;
     if (bucket) {  // bucket ids / offsets live in cnt / base until k_prep needs them
         const unsigned sg = (unsigned)((n + SORT_TB - 1) / SORT_TB);
         k_bucket_count<<<sg, SORT_TB, 0, s>>>(n, b.keys32, b.spl, b.spl_nb, b.cnt, b.base,
                                               b.bcount);
-        st = hipcub::DeviceScan::ExclusiveSum(b.cub_tmp, bytes, b.bcount, b.bstart,
-                                              (int)b.spl_nb + 1, s);
+        st = rocprim::exclusive_scan(b.scratch, bytes, b.bcount, b.bstart, 0u,
+                                     (size_t)b.spl_nb + 1, rocprim::plus<uint32_t>(), s);
         if (st != hipSuccess) return st;
         k_bucket_scatter<<<sg, SORT_TB, 0, s>>>(n, b.keys32, b.cnt, b.base, b.bstart, b.keys_s);
         k_bucket_sort<<<b.spl_nb, SORT_TB, 0, s>>>(b.bstart, b.bcount, b.keys_s, b.keys,
                                                    b.keys32_s, b.perm, b.keys_s);
     } else {
-        st = rocprim::radix_sort_pairs<SortConfig>(b.cub_tmp, bytes, b.keys32, b.keys32_s, b.idx,
+        st = rocprim::radix_sort_pairs<SortConfig>(b.scratch, bytes, b.keys32, b.keys32_s, b.idx,
                                                    b.perm, (size_t)n, 0u, 32u, s);
         if (st != hipSuccess) return st;
         k_key_gather<<<grid_for(n), TB, 0, s>>>(n, b.keys, b.perm, b.keys_s);
@@ -1308,8 +1309,9 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     k_key_fixup<<<grid_for(n), TB, 0, s>>>(n, g.J, b.keys32_s, b.keys_s, b.perm);
     k_prep<<<grid_for(n + 1), TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.src, b.dst, b.cpl, b.cnt,
                                           b.spl);
-    bytes = b.cub_bytes;
-    st = hipcub::DeviceScan::ExclusiveSum(b.cub_tmp, bytes, b.cnt, b.base, (int)(n + 1), s);
+    bytes = b.scratch_bytes;
+    st = rocprim::exclusive_scan(b.scratch, bytes, b.cnt, b.base, 0u, (size_t)(n + 1),
+                                 rocprim::plus<uint32_t>(), s);
     if (st != hipSuccess) return st;
     k_cells<<<grid_for(((int64_t)1 << (2 * D0)) + 1), TB, 0, s>>>(n, g.J, D0, b.keys_s,
                                                                   b.cell_start);

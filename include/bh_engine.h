@@ -87,6 +87,14 @@ int bh_get_params(const bh_engine *e, bh_params *p);
 int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, const double *vx,
                     const double *vy, const double *m);
 
+/* On-disk state (checkpoint / resume): the Config fields and the body list in the caller's
+ * order as one little-endian file ("BHSTATE1" magic, 64-byte header of bh_params + N, then
+ * x[N], y[N], vx[N], vy[N], m[N] fp64; layout in csrc/state_io.cpp).  Loading = bh_set_params
+ * + bh_reset_bodies (resetBodies, BHA:342-349) of the saved list, so a resumed run is
+ * bit-identical to an uninterrupted one.  The file is written to path.tmp, then renamed. */
+int bh_save_state(bh_engine *e, const char *path);
+int bh_load_state(bh_engine *e, const char *path);
+
 /* k x PhysicsEngine.step() (BHA:405-439). */
 int bh_step(bh_engine *e, int32_t k);
 

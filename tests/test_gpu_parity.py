@@ -650,3 +650,37 @@ def test_multi_rank_decomposition_in_process(world):
             e.close()
         group.close()
         ref.close()
+
+
+def test_checkpoint_resume_bit_identical(tmp_path):
+    """bh_save_state after 6 steps of a merge-active two-disk scene, bh_load_state into a fresh
+    engine, 6 more steps: bit-identical to 12 uninterrupted steps and to the oracle; the file
+    is readable by the host-side reader and holds the caller-order state and the params."""
+    from bh_amd import state_file
+    arrs = scenes.two_disks(3000, 800)
+    p = bh_amd.default_params(theta=0.6, dt=0.004)
+    straight = bh_amd.Engine(p, device=0)
+    straight.reset_bodies(*arrs)
+    straight.step(12)
+    first = bh_amd.Engine(p, device=0)
+    first.reset_bodies(*arrs)
+    first.step(6)
+    path = str(tmp_path / "mid.bhstate")
+    first.save_state(path)
+    params, saved = state_file.read(path)
+    assert params["theta"] == 0.6 and params["dt"] == 0.004 and params["width_px"] == 2400
+    for a, b in zip(saved, first.get_bodies()):
+        assert bits_equal(a, b)
+    first.close()
+    resumed = bh_amd.Engine(bh_amd.default_params(), device=0)  # other params until loaded
+    resumed.load_state(path)
+    assert resumed.params.theta == 0.6
+    resumed.step(6)
+    for a, b in zip(resumed.get_bodies(), straight.get_bodies()):
+        assert bits_equal(a, b)
+    ref = oracle.Oracle(*arrs, theta=0.6, dt=0.004)
+    ref.step(12)
+    _assert_state_equal(resumed, ref)
+    assert resumed.num_bodies() < len(arrs[0])  # the merge rule ran on both sides of the save
+    with pytest.raises(bh_amd.BhError):
+        resumed.load_state(str(tmp_path / "missing.bhstate"))

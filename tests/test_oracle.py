@@ -208,3 +208,26 @@ def test_scene_generators_are_deterministic_and_shaped():
     assert u[0].min() >= 0.0 and u[0].max() < 2400.0 and u[1].max() < 800.0
     k = scenes.kepler_disk(300, seed=3)
     assert k[4][0] == 50_000.0
+
+
+def test_state_file_round_trip(tmp_path):
+    """The checkpoint format (csrc/state_io.cpp) written and read back by the host-side
+    reader / writer: header fields and every fp64 word survive, N = 0 included."""
+    from bh_amd import state_file
+    rng = np.random.default_rng(3)
+    params = dict(G=80.0, dt=0.005, theta=0.5, soft2=1.0, width_px=1920, height_px=1080,
+                  merge_max_mass=4000.0, merge_min_dist=8.0)
+    for n in (0, 1, 777):
+        arrs = [rng.standard_normal(n) for _ in range(5)]
+        p = tmp_path / f"s{n}.bhstate"
+        state_file.write(p, params, *arrs)
+        assert p.stat().st_size == 80 + 40 * n
+        got_p, got = state_file.read(p)
+        assert got_p == params
+        for a, b in zip(arrs, got):
+            assert np.array_equal(a.view(np.int64), b.view(np.int64))
+    raw = bytearray((tmp_path / "s1.bhstate").read_bytes())
+    raw[0] = ord("X")
+    (tmp_path / "bad.bhstate").write_bytes(bytes(raw))
+    with pytest.raises(ValueError):
+        state_file.read(tmp_path / "bad.bhstate")
