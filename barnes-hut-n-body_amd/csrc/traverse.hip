@@ -140,6 +140,11 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
 #define BH_TRAV_XCD_RUN 64
 #endif
 
+#ifdef BH_TRAV_TIMING  // diagnostic build only: per-wave wall-clock start / end, hardware ids
+constexpr int TRAV_TIMING_MAX = 1 << 18;
+__device__ uint64_t g_trav_times[4 * TRAV_TIMING_MAX];
+#endif
+
 // KICK (KickMode): the integration step that follows the evaluation is applied by the lane
 // itself after its walk -- the body's x, y are only ever read by its own lane (other lanes see
 // it through the leaf records), so the update in place is race-free and a2 is not written.
@@ -151,6 +156,9 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
                                                  int64_t lo, int64_t hi, ForceParams fp,
                                                  Geometry g, double *__restrict__ a2,
                                                  TraverseCounters cnt, KickArgs kick) {
+#ifdef BH_TRAV_TIMING
+    const uint64_t t_start = wall_clock64();
+#endif
     const int64_t p = lo + (int64_t)xcd_block<BH_TRAV_XCD_RUN>() * TB + threadIdx.x;
     const bool valid = p < hi;
     // A body merged away earlier in this bh_step call (a tombstone until the call's compaction)
@@ -183,6 +191,15 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
         cnt.wave_iters[(p - lo) >> 6] = niters;
         cnt.wave_blocks[(p - lo) >> 6] = nblocks;
     }
+#ifdef BH_TRAV_TIMING
+    if (threadIdx.x == 0 && ((p - lo) >> 6) < TRAV_TIMING_MAX) {
+        uint64_t *t = g_trav_times + 4 * ((p - lo) >> 6);
+        t[0] = t_start;
+        t[1] = wall_clock64();
+        t[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID: wave, SIMD, CU, SE
+        t[3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
+    }
+#endif
     if (!valid) return;
     // BHA:390-391, interleaved (ax, ay): coalesced 16-byte stores in Morton order
     typedef double double2_t __attribute__((ext_vector_type(2)));
@@ -284,5 +301,12 @@ void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x
     }
 #undef BH_TRAV
 }
+
+#ifdef BH_TRAV_TIMING
+extern "C" int bh_debug_trav_times(uint64_t *out, int waves) {
+    if (waves > TRAV_TIMING_MAX) waves = TRAV_TIMING_MAX;
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_trav_times), sizeof(uint64_t) * 4 * (size_t)waves);
+}
+#endif
 
 }  // namespace bh

@@ -16,7 +16,7 @@ for r in $(seq 1 $ROUNDS); do
 import json, sys
 line = [l for l in open(sys.argv[2]) if l.startswith("{")][-1]
 d = json.loads(line)
-print(sys.argv[1], d["ms_per_step"], d["roofline"]["kernel_avg_ms"], d["phase_ms"])
+r = d["roofline"]; print(sys.argv[1], d["ms_per_step"], r.get("kernel_ms", {}).get("avg"), r.get("kernel_ms", {}).get("max"), d["phase_ms"])
 PY
   done
 done

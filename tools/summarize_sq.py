@@ -13,7 +13,7 @@ import json
 import os
 import sys
 
-KERNEL = "k_traverse<false, true>"
+KERNEL = "k_traverse<false, true, "  # both fused-kick variants (1: kick+drift, 2: kick)
 
 
 def main():
@@ -33,7 +33,7 @@ def main():
             acc[c].append(v)
     avg = {c: sum(v) / len(v) for c, v in acc.items()}
     waves = avg.get("SQ_WAVES", 0.0)
-    out = [f"## {KERNEL} SQ counters (C3, average per dispatch; rocprofv3 --pmc, "
+    out = [f"## {KERNEL.strip(', ')}...> SQ counters (C3, average per dispatch; rocprofv3 --pmc, "
            f"{len(glob.glob(os.path.join(src, 'p*')))} passes)", "",
            "| counter | per dispatch | per wave |", "|---|---|---|"]
     for c in sorted(avg):
