@@ -153,6 +153,11 @@ struct TreeBuffers {
 int cell_table_depth(int J, int64_t n);
 size_t tree_scratch_bytes(int64_t n, int J);
 hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStream_t s);
+// After a tree_build: lanes = the bodies in Hilbert order of their cells (refresh), or the
+// previous lane map carried through this build's permutation (k_prep leaves old slot -> new
+// slot in keys32).  Uses keys32 / keys32_s / idx.
+hipError_t lane_order(const TreeBuffers &b, int64_t n, int J, bool refresh, uint32_t *lanes,
+                      hipStream_t s);
 
 // ---- launchers (traverse.hip) ----------------------------------------------------
 // Accelerations F/m of slots [lo, hi), written interleaved to a2[2p], a2[2p+1].
@@ -174,10 +179,12 @@ struct TraverseCounters {
     uint32_t *visits, *contrib;
     uint32_t *wave_iters, *wave_blocks;
 };
+// lanes (nullable): lane -> body slot map of a full single-GPU launch (lo = 0, hi = n; the
+// Hilbert grouping made by lane_order in tree_build.hip); null = lane q walks slot q.
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
               const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, const TraverseCounters *cnt,
-              hipStream_t s, const KickArgs *kick = nullptr);
+              hipStream_t s, const KickArgs *kick = nullptr, const uint32_t *lanes = nullptr);
 // multi-GPU shard pieces (bh_shard_range): `rounds` x `world` pieces of whole wavefronts
 __host__ __device__ inline int64_t shard_sub(int64_t n, int world, int rounds) {
     const int64_t parts = (int64_t)world * rounds;

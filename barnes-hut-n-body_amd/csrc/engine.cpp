@@ -142,6 +142,11 @@ struct bh_engine {
 
     bool tree_valid = false;  // lastTree (BHA:304): keys_s / cpl / base / nodes are current
 
+    // Hilbert lane map of the single-GPU traversal (tree_build.hip lane_order): lane -> slot
+    uint32_t *lanes = nullptr;
+    bool lanes_valid = false;  // the map is a permutation of the current slots
+    int lanes_age = 0;         // builds since the last Hilbert sort
+
     // profiling
     bool profiling = false;
     std::vector<hipEvent_t> ev;
@@ -266,6 +271,8 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(dev_alloc(e, e->base, cap + 1));
         TRY(dev_alloc(e, e->visits32, cap));
         TRY(dev_alloc(e, e->contrib32, cap));
+        TRY(dev_alloc(e, e->lanes, cap));
+        e->lanes_valid = false;
         TRY(dev_alloc(e, e->wave_iters, cap / 64 + 2));
         TRY(dev_alloc(e, e->wave_blocks, cap / 64 + 2));
         TRY(dev_alloc(e, e->heavy, cap));
@@ -369,9 +376,19 @@ int collect_timings(bh_engine *e) {
 }
 
 // ---- buildTree() (BHA:359-366): sort + build; the state moves to the new Morton order ----
+#ifndef BH_LANE_REFRESH
+#define BH_LANE_REFRESH 16  // builds between Hilbert re-sorts of the lane map (0: Morton lanes)
+#endif
 int build(bh_engine *e) {
     const int64_t n = e->n;
-    HIPCHK(e, tree_build(tree_buffers(e), n, e->geo, e->stream));
+    const TreeBuffers tb = tree_buffers(e);
+    HIPCHK(e, tree_build(tb, n, e->geo, e->stream));
+    if (BH_LANE_REFRESH > 0 && !e->comm && !e->group && n > 0 && e->p.theta != 0.0) {  // Hilbert waves
+        const bool refresh = !e->lanes_valid || e->lanes_age >= BH_LANE_REFRESH;
+        HIPCHK(e, lane_order(tb, n, e->geo.J, refresh, e->lanes, e->stream));
+        e->lanes_valid = true;
+        e->lanes_age = refresh ? 1 : e->lanes_age + 1;
+    }
     e->spl_nb = sort_buckets(n);  // k_prep wrote this build's splitters
     if (n > 0) std::swap(e->st, e->alt);
     e->tree_valid = true;
@@ -429,19 +446,21 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
                                   e->stream));
     }
     const TraverseCounters counters{visits, e->contrib32, e->wave_iters, e->wave_blocks};
+    const bool single = !e->comm && !e->group;  // lo = 0, hi = n: the lane map applies
     auto forces = [&](int64_t lo, int64_t hi, uint32_t *vis) {
         if (direct)
             direct_forces(e->leaves, e->leaf_count, e->st.x, e->st.y, e->st.m, lo, hi, fp.G,
                           fp.soft2, e->a2, e->stream);
         else
             traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, e->st.cidx, lo, hi, e->geo, fp,
-                     e->a2, vis ? &counters : nullptr, e->stream);
+                     e->a2, vis ? &counters : nullptr, e->stream, nullptr,
+                     single && e->lanes_valid ? e->lanes : nullptr);
     };
     if ((!e->comm && !e->group) || visits) {
         if (BH_FUSE_KICK && kick != KICK_NONE && !direct && !visits && fused) {
             const KickArgs ka{kick, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
             traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, e->st.cidx, 0, n, e->geo, fp,
-                     e->a2, nullptr, e->stream, &ka);
+                     e->a2, nullptr, e->stream, &ka, e->lanes_valid ? e->lanes : nullptr);
             *fused = true;
         } else {
             forces(0, n, visits);
@@ -584,6 +603,7 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
     e->n = n - (int64_t)nd;
     e->removed.assign(dead.begin(), dead.end());
     e->tree_valid = false;  // BHA:526
+    e->lanes_valid = false;  // slots renumbered
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return BH_OK;
 }
@@ -617,6 +637,7 @@ int restore(bh_engine *e) {
     TRY(copy_state(e, e->snap, e->st, e->snap_n));
     e->n = e->snap_n;
     e->spl_nb = 0;  // the splitters describe the discarded builds' order
+    e->lanes_valid = false;
     e->heavy_possible = true;
     e->tree_valid = false;
     return BH_OK;
@@ -888,7 +909,7 @@ void bh_destroy(bh_engine *e) {
     free_state(e->snap);
     void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->keys32, e->keys32_s, e->idx, e->perm, e->cpl, e->cnt,
                     e->base, e->cell_start, e->nodes, e->span_list, e->super_list,
-                    e->span_children, e->scalars, e->visits32, e->contrib32, e->wave_iters, e->wave_blocks, e->heavy, e->keep,
+                    e->span_children, e->scalars, e->visits32, e->contrib32, e->lanes, e->wave_iters, e->wave_blocks, e->heavy, e->keep,
                     e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->mbits, e->mslot, e->scratch,
                     e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaves.xy, e->leaves.m,
                     e->leaves.slot, e->leaf_tmp, e->spl, e->bcount, e->bstart};
@@ -915,6 +936,7 @@ int bh_set_params(bh_engine *e, const bh_params *p) {
         e->geo = g;
         e->tree_valid = false;
         e->spl_nb = 0;  // keys change meaning
+        e->lanes_valid = false;
         if (g.J != e->J_alloc) {  // tree workspace sized for another depth; the state stays
             HIPCHK(e, hipStreamSynchronize(e->stream));
             TRY(ensure_capacity(e, e->n));
@@ -954,6 +976,7 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     e->removed.clear();
     e->tree_valid = false;  // BHA:348
     e->spl_nb = 0;          // other bodies: the first build sorts from scratch
+    e->lanes_valid = false;
     return BH_OK;
 }
 

@@ -155,12 +155,14 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
                                                  const uint32_t *__restrict__ cidx,
                                                  int64_t lo, int64_t hi, ForceParams fp,
                                                  Geometry g, double *__restrict__ a2,
-                                                 TraverseCounters cnt, KickArgs kick) {
+                                                 TraverseCounters cnt, KickArgs kick,
+                                                 const uint32_t *__restrict__ lanes) {
 #ifdef BH_TRAV_TIMING
     const uint64_t t_start = wall_clock64();
 #endif
-    const int64_t p = lo + (int64_t)xcd_block<BH_TRAV_XCD_RUN>() * TB + threadIdx.x;
-    const bool valid = p < hi;
+    const int64_t q = lo + (int64_t)xcd_block<BH_TRAV_XCD_RUN>() * TB + threadIdx.x;  // lane
+    const bool valid = q < hi;
+    const int64_t p = lanes && valid ? (int64_t)lanes[q] : q;  // its body's slot
     // A body merged away earlier in this bh_step call (a tombstone until the call's compaction)
     // needs no force: it does not walk.  Tombstones sort to the tail with the out-of-root
     // bodies and are flung across the domain by the heavy body that absorbed them, so a tail
@@ -188,12 +190,12 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
         walk<false, COUNT, OFF32>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx,
                                   fy, nvis, niters, ncontrib, nblocks);
     if (COUNT && (threadIdx.x & 63) == 0) {
-        cnt.wave_iters[(p - lo) >> 6] = niters;
-        cnt.wave_blocks[(p - lo) >> 6] = nblocks;
+        cnt.wave_iters[(q - lo) >> 6] = niters;
+        cnt.wave_blocks[(q - lo) >> 6] = nblocks;
     }
 #ifdef BH_TRAV_TIMING
-    if (threadIdx.x == 0 && ((p - lo) >> 6) < TRAV_TIMING_MAX) {
-        uint64_t *t = g_trav_times + 4 * ((p - lo) >> 6);
+    if (threadIdx.x == 0 && ((q - lo) >> 6) < TRAV_TIMING_MAX) {
+        uint64_t *t = g_trav_times + 4 * ((q - lo) >> 6);
         t[0] = t_start;
         t[1] = wall_clock64();
         t[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID: wave, SIMD, CU, SE
@@ -278,7 +280,7 @@ hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_ba
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
               const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, const TraverseCounters *cnt,
-              hipStream_t s, const KickArgs *kick) {
+              hipStream_t s, const KickArgs *kick, const uint32_t *lanes) {
     if (hi <= lo) return;
     unsigned grid = (unsigned)((hi - lo + TB - 1) / TB);
     // node records addressed by a 32-bit byte offset while the array stays below 4 GiB
@@ -286,7 +288,8 @@ void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x
     const KickArgs ka = kick ? *kick : KickArgs{KICK_NONE, nullptr, nullptr, 0.0, 0.0};
     const TraverseCounters tc = cnt ? *cnt : TraverseCounters{nullptr, nullptr, nullptr, nullptr};
 #define BH_TRAV(C, O, K) \
-    k_traverse<C, O, K><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, tc, ka)
+    k_traverse<C, O, K><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, tc, ka, \
+                                            lanes)
     if (cnt) {  // diagnostic counting walk: accelerations out, never fused
         if (off32) BH_TRAV(true, true, KICK_NONE);
         else BH_TRAV(true, false, KICK_NONE);

@@ -391,7 +391,8 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
                                              const uint32_t *__restrict__ perm, BodyState src,
                                              BodyState dst, int8_t *__restrict__ cpl,
                                              uint32_t *__restrict__ cnt,
-                                             uint64_t *__restrict__ spl) {
+                                             uint64_t *__restrict__ spl,
+                                             uint32_t *__restrict__ inv) {
     int64_t a = (int64_t)xcd_block() * TB + threadIdx.x;
     if (a > n) return;
     if (a == n) {
@@ -401,6 +402,7 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
     const uint64_t SENT = sentinel_key(J);
     uint64_t k = keys_s[a];
     uint32_t i = perm[a];  // nearly the identity: the state is kept in the last Morton order
+    inv[i] = (uint32_t)a;  // old slot -> new slot (carries the traversal's lane map, lane_order)
     if (a % SORT_B == 0)  // splitters of the next build's bucket sort
         spl[a / SORT_B] = ((k >> key32_shift(J)) << 32) | (uint64_t)a;
     dst.x[a] = src.x[i];
@@ -1270,12 +1272,91 @@ int cell_table_depth(int J, int64_t n) {
     return d < J ? d : J;
 }
 
+// ---- Hilbert lane order for the traversal (traverse.hip) ---------------------------------
+// The traversal's wave walks the union of its 64 lanes' interaction lists, so how bodies are
+// grouped into waves sets its work.  64 Hilbert-consecutive bodies form more compact groups than
+// 64 Morton-consecutive ones (no Z jumps): 6.5 % fewer cursor stops and 7.7 % fewer point-force
+// blocks at C3 and C4 (oracle union-walk model).  The lane map lane -> slot is made by sorting
+// the bodies by the Hilbert index of their depth-16 cell (from the Morton key of the build) and
+// carried through later builds by the builds' permutations, re-sorted every LANE_REFRESH builds.
+// It only groups bodies into waves: every body's sum is unchanged.
+__device__ __forceinline__ uint32_t hilbert16(uint64_t key, int J) {
+    // de-interleave the top 16 Morton digits (digit = ix | iy << 1, root first)
+    uint32_t ix = 0, iy = 0;
+    const int lv = J < 16 ? J : 16;
+    for (int d = 0; d < lv; ++d) {
+        const uint32_t dig = (uint32_t)(key >> (2 * (J - 1 - d))) & 3u;
+        ix = (ix << 1) | (dig & 1u);
+        iy = (iy << 1) | (dig >> 1);
+    }
+    uint32_t h = 0;  // classic xy -> d over lv levels
+    for (uint32_t sbit = 1u << (lv - 1); sbit > 0; sbit >>= 1) {
+        const uint32_t rx = (ix & sbit) ? 1u : 0u, ry = (iy & sbit) ? 1u : 0u;
+        h += sbit * sbit * ((3u * rx) ^ ry);
+        if (ry == 0) {
+            if (rx == 1) {
+                ix = sbit - 1 - (ix & (sbit - 1)) + (ix & ~(sbit - 1));
+                iy = sbit - 1 - (iy & (sbit - 1)) + (iy & ~(sbit - 1));
+            }
+            const uint32_t t = ix;
+            ix = iy;
+            iy = t;
+        }
+    }
+    return h;
+}
+
+__global__ __launch_bounds__(TB) void k_hilbert_keys(int64_t n, int J, const uint64_t *__restrict__ keys_s,
+                                                     uint32_t *__restrict__ hkey,
+                                                     uint32_t *__restrict__ slot) {
+    const int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (a >= n) return;
+    const uint64_t k = keys_s[a];
+    hkey[a] = k == sentinel_key(J) ? 0xFFFFFFFFu : hilbert16(k, J);  // not in the tree: last
+    slot[a] = (uint32_t)a;
+}
+
+__global__ __launch_bounds__(TB) void k_lane_remap(int64_t n, const uint32_t *__restrict__ inv,
+                                                   uint32_t *__restrict__ lanes) {
+    const int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (q < n) lanes[q] = inv[lanes[q]];
+}
+
+// The refresh sorts 24 bits (the depth-12 Hilbert cell: ~0.6 px at the 2400x800 root) with
+// rocprim's onesweep radix sort (3 passes) -- its merge sort, the default below 2^20 keys, took
+// ~150 us at C3.
+using LaneSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                                  rocprim::default_config, 1024>;
+constexpr unsigned LANE_SORT_LO_BIT = 8;
+
+hipError_t lane_order(const TreeBuffers &b, int64_t n, int J, bool refresh, uint32_t *lanes,
+                      hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    if (!refresh) {  // carry the grouping through this build's permutation (k_prep: keys32 =
+                     // old slot -> new slot)
+        k_lane_remap<<<grid_for(n), TB, 0, s>>>(n, b.keys32, lanes);
+        return hipGetLastError();
+    }
+    // keys32 / keys32_s / idx are free once the build has run
+    k_hilbert_keys<<<grid_for(n), TB, 0, s>>>(n, J, b.keys_s, b.keys32, b.idx);
+    size_t bytes = b.scratch_bytes;
+    return rocprim::radix_sort_pairs<LaneSortConfig>(b.scratch, bytes, b.keys32, b.keys32_s,
+                                                     b.idx, lanes, (size_t)n, LANE_SORT_LO_BIT,
+                                                     32u, s);
+}
+
 size_t tree_scratch_bytes(int64_t n, int J) {
     size_t sort_bytes = 0, scan_bytes = 0;
     (void)J;
     (void)rocprim::radix_sort_pairs<SortConfig>(nullptr, sort_bytes, (uint32_t *)nullptr,
                                                 (uint32_t *)nullptr, (uint32_t *)nullptr,
                                                 (uint32_t *)nullptr, (size_t)n, 0u, 32u);
+    size_t lane_bytes = 0;
+    (void)rocprim::radix_sort_pairs<LaneSortConfig>(nullptr, lane_bytes, (uint32_t *)nullptr,
+                                                    (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                    (uint32_t *)nullptr, (size_t)n,
+                                                    LANE_SORT_LO_BIT, 32u);
+    sort_bytes = sort_bytes > lane_bytes ? sort_bytes : lane_bytes;
     (void)rocprim::exclusive_scan(nullptr, scan_bytes, (const uint32_t *)nullptr,
                                   (uint32_t *)nullptr, 0u, (size_t)(n + 1),
                                   rocprim::plus<uint32_t>());
@@ -1308,7 +1389,7 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     }
     k_key_fixup<<<grid_for(n), TB, 0, s>>>(n, g.J, b.keys32_s, b.keys_s, b.perm);
     k_prep<<<grid_for(n + 1), TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.src, b.dst, b.cpl, b.cnt,
-                                          b.spl);
+                                          b.spl, b.keys32);
     bytes = b.scratch_bytes;
     st = rocprim::exclusive_scan(b.scratch, bytes, b.cnt, b.base, 0u, (size_t)(n + 1),
                                  rocprim::plus<uint32_t>(), s);
