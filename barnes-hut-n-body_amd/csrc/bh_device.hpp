@@ -179,8 +179,9 @@ struct TraverseCounters {
     uint32_t *visits, *contrib;
     uint32_t *wave_iters, *wave_blocks;
 };
-// lanes (nullable): lane -> body slot map of a full single-GPU launch (lo = 0, hi = n; the
-// Hilbert grouping made by lane_order in tree_build.hip); null = lane q walks slot q.
+// lanes (nullable): lane -> body slot map (the Hilbert grouping made by lane_order in
+// tree_build.hip); [lo, hi) is then a range of lanes and a2 is written by lane; null = lane q
+// walks slot q and a2 is written by slot.
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
               const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, const TraverseCounters *cnt,
@@ -212,15 +213,17 @@ void direct_forces(const LeafList &L, const uint32_t *d_count, const double *x, 
                    hipStream_t s);
 
 // ---- launchers (integrate.hip) ---------------------------------------------------
+// a2 indexed by traversal lane when lanes != null (lane i holds body slot lanes[i])
 void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
-                double dtHalf, double dt, hipStream_t s);
-void kick(int64_t n, const double *a2, double *vx, double *vy, double dtHalf, hipStream_t s);
+                double dtHalf, double dt, hipStream_t s, const uint32_t *lanes = nullptr);
+void kick(int64_t n, const double *a2, double *vx, double *vy, double dtHalf, hipStream_t s,
+          const uint32_t *lanes = nullptr);
 void iota_u32(uint32_t *p, int64_t n, hipStream_t s);
 // caller-order copies: dst_k[cidx[s]] = src_k[s]
 void scatter_to_caller(int64_t n, const uint32_t *cidx, int k, const double *const *src,
                        double *const *dst, hipStream_t s);
 void scatter_acc_to_caller(int64_t n, const uint32_t *cidx, const double *a2, double *ax,
-                           double *ay, hipStream_t s);
+                           double *ay, hipStream_t s, const uint32_t *lanes = nullptr);
 
 struct MergePair {
     uint32_t h_cidx, v_cidx;  // heavy body and candidate victim, caller indices

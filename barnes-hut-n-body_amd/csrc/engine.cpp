@@ -146,6 +146,7 @@ struct bh_engine {
     uint32_t *lanes = nullptr;
     bool lanes_valid = false;  // the map is a permutation of the current slots
     int lanes_age = 0;         // builds since the last Hilbert sort
+    const uint32_t *a2_lanes = nullptr;  // the last evaluation wrote a2 by lane of this map
 
     // profiling
     bool profiling = false;
@@ -383,11 +384,13 @@ int build(bh_engine *e) {
     const int64_t n = e->n;
     const TreeBuffers tb = tree_buffers(e);
     HIPCHK(e, tree_build(tb, n, e->geo, e->stream));
-    if (BH_LANE_REFRESH > 0 && !e->comm && !e->group && n > 0 && e->p.theta != 0.0) {  // Hilbert waves
+    if (BH_LANE_REFRESH > 0 && n > 0 && e->p.theta != 0.0) {  // Hilbert waves (every rank alike)
         const bool refresh = !e->lanes_valid || e->lanes_age >= BH_LANE_REFRESH;
         HIPCHK(e, lane_order(tb, n, e->geo.J, refresh, e->lanes, e->stream));
         e->lanes_valid = true;
         e->lanes_age = refresh ? 1 : e->lanes_age + 1;
+    } else {
+        e->lanes_valid = false;  // this build's permutation was not applied to the map
     }
     e->spl_nb = sort_buckets(n);  // k_prep wrote this build's splitters
     if (n > 0) std::swap(e->st, e->alt);
@@ -446,21 +449,21 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
                                   e->stream));
     }
     const TraverseCounters counters{visits, e->contrib32, e->wave_iters, e->wave_blocks};
-    const bool single = !e->comm && !e->group;  // lo = 0, hi = n: the lane map applies
+    const uint32_t *lanes = e->lanes_valid ? e->lanes : nullptr;  // [lo, hi): lane ranges
+    e->a2_lanes = direct ? nullptr : lanes;
     auto forces = [&](int64_t lo, int64_t hi, uint32_t *vis) {
         if (direct)
             direct_forces(e->leaves, e->leaf_count, e->st.x, e->st.y, e->st.m, lo, hi, fp.G,
                           fp.soft2, e->a2, e->stream);
         else
             traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, e->st.cidx, lo, hi, e->geo, fp,
-                     e->a2, vis ? &counters : nullptr, e->stream, nullptr,
-                     single && e->lanes_valid ? e->lanes : nullptr);
+                     e->a2, vis ? &counters : nullptr, e->stream, nullptr, lanes);
     };
     if ((!e->comm && !e->group) || visits) {
         if (BH_FUSE_KICK && kick != KICK_NONE && !direct && !visits && fused) {
             const KickArgs ka{kick, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
             traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, e->st.cidx, 0, n, e->geo, fp,
-                     e->a2, nullptr, e->stream, &ka, e->lanes_valid ? e->lanes : nullptr);
+                     e->a2, nullptr, e->stream, &ka, lanes);
             *fused = true;
         } else {
             forces(0, n, visits);
@@ -653,14 +656,14 @@ int step_once(bh_engine *e) {
         if (!fused) {
             TRY(mark(e, -1));
             kick_drift(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->p.dt,
-                       e->stream);
+                       e->stream, e->a2_lanes);
             HIPCHK(e, hipGetLastError());
             TRY(mark(e, 2));
         }
         TRY(evaluate(e, nullptr, KICK_ONLY, &fused));  // a(t+dt)
         if (!fused) {
             TRY(mark(e, -1));
-            kick(n, e->a2, e->st.vx, e->st.vy, dtHalf, e->stream);
+            kick(n, e->a2, e->st.vx, e->st.vy, dtHalf, e->stream, e->a2_lanes);
             HIPCHK(e, hipGetLastError());
             TRY(mark(e, 2));
         }
@@ -1047,7 +1050,7 @@ int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visi
     HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
     if (n > 0) {
         TRY(evaluate(e, visits ? e->visits32 : nullptr));
-        scatter_acc_to_caller(n, e->st.cidx, e->a2, e->ax, e->ay, e->stream);
+        scatter_acc_to_caller(n, e->st.cidx, e->a2, e->ax, e->ay, e->stream, e->a2_lanes);
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipStreamSynchronize(e->stream));
         TRY(check_tree_flags(e));

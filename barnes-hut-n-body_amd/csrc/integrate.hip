@@ -14,31 +14,34 @@ typedef double double2_t __attribute__((ext_vector_type(2)));
 
 // BHA:412-422 fused: v += a * dtHalf; x += v * DT.  The reference runs the kick loop over
 // all bodies and then the drift loop; per body the operations are identical.
+// a2 is indexed by the traversal's lane when `lanes` is given (lane i holds body lanes[i]).
 __global__ __launch_bounds__(TB) void k_kick_drift(int64_t n, const double *__restrict__ a2,
                                                    double *__restrict__ x, double *__restrict__ y,
                                                    double *__restrict__ vx,
                                                    double *__restrict__ vy, double dtHalf,
-                                                   double dt) {
+                                                   double dt, const uint32_t *__restrict__ lanes) {
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
     const double2_t a = *reinterpret_cast<const double2_t *>(a2 + 2 * i);
-    double vxi = vx[i] + a.x * dtHalf;
-    double vyi = vy[i] + a.y * dtHalf;
-    vx[i] = vxi;
-    vy[i] = vyi;
-    x[i] = x[i] + vxi * dt;
-    y[i] = y[i] + vyi * dt;
+    const int64_t p = lanes ? (int64_t)lanes[i] : i;
+    double vxi = vx[p] + a.x * dtHalf;
+    double vyi = vy[p] + a.y * dtHalf;
+    vx[p] = vxi;
+    vy[p] = vyi;
+    x[p] = x[p] + vxi * dt;
+    y[p] = y[p] + vyi * dt;
 }
 
 // BHA:429-432
 __global__ __launch_bounds__(TB) void k_kick(int64_t n, const double *__restrict__ a2,
                                              double *__restrict__ vx, double *__restrict__ vy,
-                                             double dtHalf) {
+                                             double dtHalf, const uint32_t *__restrict__ lanes) {
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
     const double2_t a = *reinterpret_cast<const double2_t *>(a2 + 2 * i);
-    vx[i] = vx[i] + a.x * dtHalf;
-    vy[i] = vy[i] + a.y * dtHalf;
+    const int64_t p = lanes ? (int64_t)lanes[i] : i;
+    vx[p] = vx[p] + a.x * dtHalf;
+    vy[p] = vy[p] + a.y * dtHalf;
 }
 
 __global__ __launch_bounds__(TB) void k_iota(uint32_t *__restrict__ p, int64_t n) {
@@ -63,10 +66,11 @@ __global__ __launch_bounds__(TB) void k_scatter_caller(int64_t n, const uint32_t
 __global__ __launch_bounds__(TB) void k_scatter_acc(int64_t n, const uint32_t *__restrict__ cidx,
                                                     const double *__restrict__ a2,
                                                     double *__restrict__ ax,
-                                                    double *__restrict__ ay) {
+                                                    double *__restrict__ ay,
+                                                    const uint32_t *__restrict__ lanes) {
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
-    const uint32_t o = cidx[i];
+    const uint32_t o = cidx[lanes ? (int64_t)lanes[i] : i];
     if (o & CIDX_DEAD) return;  // a tombstone has no caller slot
     ax[o] = a2[2 * i];
     ay[o] = a2[2 * i + 1];
@@ -502,12 +506,13 @@ __global__ __launch_bounds__(TB) void k_compact(int64_t n, const uint32_t *__res
 }  // namespace
 
 void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
-                double dtHalf, double dt, hipStream_t s) {
-    if (n > 0) k_kick_drift<<<grid_for(n), TB, 0, s>>>(n, a2, x, y, vx, vy, dtHalf, dt);
+                double dtHalf, double dt, hipStream_t s, const uint32_t *lanes) {
+    if (n > 0) k_kick_drift<<<grid_for(n), TB, 0, s>>>(n, a2, x, y, vx, vy, dtHalf, dt, lanes);
 }
 
-void kick(int64_t n, const double *a2, double *vx, double *vy, double dtHalf, hipStream_t s) {
-    if (n > 0) k_kick<<<grid_for(n), TB, 0, s>>>(n, a2, vx, vy, dtHalf);
+void kick(int64_t n, const double *a2, double *vx, double *vy, double dtHalf, hipStream_t s,
+          const uint32_t *lanes) {
+    if (n > 0) k_kick<<<grid_for(n), TB, 0, s>>>(n, a2, vx, vy, dtHalf, lanes);
 }
 
 void iota_u32(uint32_t *p, int64_t n, hipStream_t s) {
@@ -526,8 +531,8 @@ void scatter_to_caller(int64_t n, const uint32_t *cidx, int k, const double *con
 }
 
 void scatter_acc_to_caller(int64_t n, const uint32_t *cidx, const double *a2, double *ax,
-                           double *ay, hipStream_t s) {
-    if (n > 0) k_scatter_acc<<<grid_for(n), TB, 0, s>>>(n, cidx, a2, ax, ay);
+                           double *ay, hipStream_t s, const uint32_t *lanes) {
+    if (n > 0) k_scatter_acc<<<grid_for(n), TB, 0, s>>>(n, cidx, a2, ax, ay, lanes);
 }
 
 void merge_candidates(int64_t n, const double *x, const double *y, const double *m,

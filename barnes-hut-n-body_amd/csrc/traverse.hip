@@ -208,8 +208,8 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     double2_t acc;
     acc.x = fx / bm;
     acc.y = fy / bm;
-    if (KICK == KICK_NONE) {
-        *reinterpret_cast<double2_t *>(a2 + 2 * p) = acc;
+    if (KICK == KICK_NONE) {  // by lane with a lane map (the multi-GPU pieces stay contiguous)
+        *reinterpret_cast<double2_t *>(a2 + 2 * q) = acc;
     } else {  // k_kick_drift / k_kick (integrate.hip), operation for operation
         const double vxi = kick.vx[p] + acc.x * kick.dtHalf;
         const double vyi = kick.vy[p] + acc.y * kick.dtHalf;

@@ -289,10 +289,12 @@ def test_other_screen_geometry():
 
 
 def test_live_config_changes_between_steps():
-    """theta / DT / G are read live at every step (PNL:247-260)."""
+    """theta / DT / G are read live at every step (PNL:247-260); theta 0 in between switches to
+    the all-pairs kernel and back (the Hilbert lane map is rebuilt after it)."""
     arrs = scenes.two_disks(1500, 400)
     eng, ref = _pair(arrs, theta=0.5)
-    for theta, dt, G in ((0.5, 0.005, 80.0), (0.9, 0.01, 60.0), (0.3, -0.005, 80.0)):
+    for theta, dt, G in ((0.5, 0.005, 80.0), (0.9, 0.01, 60.0), (0.0, 0.005, 80.0),
+                         (0.3, -0.005, 80.0)):
         eng.set_params(bh_amd.default_params(theta=theta, dt=dt, G=G))
         ref.set_params(oracle.params(theta=theta, dt=dt, G=G))
         eng.step(2)
