@@ -251,6 +251,11 @@ void merge_replay(const MergePair *box, uint32_t cap, double *m, uint32_t *cidx,
 size_t compact_scratch_bytes(int64_t n);
 // Remove tombstoned slots preserving order; caller indices are renumbered past the removed
 // ones (dead_cidx sorted ascending, n_dead entries).  keep, pos: n-entry scratch.
+// The traversal's lane map through compact_state (keep / pos of that call): surviving lanes in
+// order, renumbered to the new slots, into out.  flag, qpos: n-entry scratch.
+hipError_t compact_lanes(int64_t n, const uint32_t *lanes, const uint32_t *keep,
+                         const uint32_t *pos, uint32_t *flag, uint32_t *qpos, uint32_t *out,
+                         void *tmp, size_t tmp_bytes, hipStream_t s);
 hipError_t compact_state(int64_t n, uint32_t *keep, const BodyState &src, const BodyState &dst,
                          const uint32_t *dead_cidx, uint32_t n_dead, uint32_t *pos, void *tmp,
                          size_t tmp_bytes, hipStream_t s);

@@ -603,10 +603,14 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
     HIPCHK(e, compact_state(n, e->keep, e->st, e->alt, e->dead_sorted, nd, e->pos, e->scratch,
                             e->scratch_bytes, e->stream));
     std::swap(e->st, e->alt);
+    if (e->lanes_valid) {  // carry the wave grouping over the removals (no re-sort)
+        HIPCHK(e, compact_lanes(n, e->lanes, e->keep, e->pos, e->idx, e->keys32, e->keys32_s,
+                                e->scratch, e->scratch_bytes, e->stream));
+        std::swap(e->lanes, e->keys32_s);
+    }
     e->n = n - (int64_t)nd;
     e->removed.assign(dead.begin(), dead.end());
     e->tree_valid = false;  // BHA:526
-    e->lanes_valid = false;  // slots renumbered
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return BH_OK;
 }

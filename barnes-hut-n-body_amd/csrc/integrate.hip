@@ -503,7 +503,37 @@ __global__ __launch_bounds__(TB) void k_compact(int64_t n, const uint32_t *__res
     dst.cidx[o] = c - lo;
 }
 
+// Lane map through a compaction: keep the lanes whose body survives (lane order preserved),
+// renumbered to the bodies' new slots.
+__global__ __launch_bounds__(TB) void k_lane_keep(int64_t n, const uint32_t *__restrict__ lanes,
+                                                  const uint32_t *__restrict__ keep,
+                                                  uint32_t *__restrict__ flag) {
+    int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (q < n) flag[q] = keep[lanes[q]];
+}
+
+__global__ __launch_bounds__(TB) void k_lane_compact(int64_t n, const uint32_t *__restrict__ lanes,
+                                                     const uint32_t *__restrict__ flag,
+                                                     const uint32_t *__restrict__ qpos,
+                                                     const uint32_t *__restrict__ pos,
+                                                     uint32_t *__restrict__ out) {
+    int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (q < n && flag[q]) out[qpos[q]] = pos[lanes[q]];
+}
+
 }  // namespace
+
+hipError_t compact_lanes(int64_t n, const uint32_t *lanes, const uint32_t *keep,
+                         const uint32_t *pos, uint32_t *flag, uint32_t *qpos, uint32_t *out,
+                         void *tmp, size_t tmp_bytes, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    k_lane_keep<<<grid_for(n), TB, 0, s>>>(n, lanes, keep, flag);
+    hipError_t st = rocprim::exclusive_scan(tmp, tmp_bytes, flag, qpos, 0u, (size_t)n,
+                                            rocprim::plus<uint32_t>(), s);
+    if (st != hipSuccess) return st;
+    k_lane_compact<<<grid_for(n), TB, 0, s>>>(n, lanes, flag, qpos, pos, out);
+    return hipGetLastError();
+}
 
 void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
                 double dtHalf, double dt, hipStream_t s, const uint32_t *lanes) {

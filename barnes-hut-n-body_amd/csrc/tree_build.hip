@@ -1327,7 +1327,10 @@ __global__ __launch_bounds__(TB) void k_lane_remap(int64_t n, const uint32_t *__
 // ~150 us at C3.
 using LaneSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
                                                   rocprim::default_config, 1024>;
-constexpr unsigned LANE_SORT_LO_BIT = 8;
+#ifndef BH_LANE_LO_BIT
+#define BH_LANE_LO_BIT 8
+#endif
+constexpr unsigned LANE_SORT_LO_BIT = BH_LANE_LO_BIT;
 
 hipError_t lane_order(const TreeBuffers &b, int64_t n, int J, bool refresh, uint32_t *lanes,
                       hipStream_t s) {
