@@ -135,6 +135,7 @@ struct TreeBuffers {
     int8_t *cpl;           // c(a): common digit count between sorted keys a, a+1; -1 at ends
     uint32_t *cnt, *base;  // node slots per sorted body; exclusive scan (n + 1 entries)
     uint32_t *cell_start;  // [4^D0 + 1] first sorted body of each depth-D0 cell
+    uint32_t *lanes_remap = nullptr;  // traversal lane map to carry through this build (or null)
     Node *nodes;
     uint32_t *scalars;     // [1] = error flags
     uint32_t *span_list;   // [(J + 1) * span_stride]: chunk-spanning node per (level, boundary)

@@ -340,9 +340,16 @@ TreeBuffers tree_buffers(bh_engine *e) {
 // ---- profiling events ----------------------------------------------------------------
 int mark(bh_engine *e, int phase) {  // close the interval of `phase` that began at the last mark
     if (!e->profiling) return BH_OK;
+    // phases are contiguous on the stream: the previous phase's end mark starts the next one
+    if (phase < 0 && e->ev_used > 0) return BH_OK;
     if (e->ev_used + 1 > e->ev.size()) {
+        // timing-only events: a device-scope release, no system-scope fence (the default one
+        // writes back and invalidates the caches: ~10 us of idle GPU per event in the step)
         hipEvent_t ev;
-        HIPCHK(e, hipEventCreate(&ev));
+        if (hipEventCreateWithFlags(&ev, hipEventDisableSystemFence) != hipSuccess) {
+            (void)hipGetLastError();
+            HIPCHK(e, hipEventCreate(&ev));
+        }
         e->ev.push_back(ev);
         e->ev_phase.push_back(-1);
     }
@@ -382,11 +389,15 @@ int collect_timings(bh_engine *e) {
 #endif
 int build(bh_engine *e) {
     const int64_t n = e->n;
-    const TreeBuffers tb = tree_buffers(e);
+    TreeBuffers tb = tree_buffers(e);
+    // Hilbert waves (every rank alike): re-sorted every BH_LANE_REFRESH builds, carried through
+    // the build's permutation by k_emit_com in between
+    const bool use_lanes = BH_LANE_REFRESH > 0 && n > 0 && e->p.theta != 0.0;
+    const bool refresh = use_lanes && (!e->lanes_valid || e->lanes_age >= BH_LANE_REFRESH);
+    tb.lanes_remap = use_lanes && !refresh ? e->lanes : nullptr;
     HIPCHK(e, tree_build(tb, n, e->geo, e->stream));
-    if (BH_LANE_REFRESH > 0 && n > 0 && e->p.theta != 0.0) {  // Hilbert waves (every rank alike)
-        const bool refresh = !e->lanes_valid || e->lanes_age >= BH_LANE_REFRESH;
-        HIPCHK(e, lane_order(tb, n, e->geo.J, refresh, e->lanes, e->stream));
+    if (use_lanes) {
+        if (refresh) HIPCHK(e, lane_order(tb, n, e->geo.J, true, e->lanes, e->stream));
         e->lanes_valid = true;
         e->lanes_age = refresh ? 1 : e->lanes_age + 1;
     } else {

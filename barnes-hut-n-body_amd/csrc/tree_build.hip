@@ -724,7 +724,9 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
                                                      const double *__restrict__ m,
                                                      const uint32_t *__restrict__ cidx,
                                                      uint32_t *scratch, Node *nodes,
-                                                     uint32_t *err) {
+                                                     uint32_t *err,
+                                                     const uint32_t *__restrict__ inv,
+                                                     uint32_t *__restrict__ lanes) {
     __shared__ double s_m[COM_CAP + 1], s_x[COM_CAP + 1], s_y[COM_CAP + 1];  // [COM_CAP]: pad
     __shared__ uint32_t s_next[COM_CAP];
     __shared__ ushort4 s_ch[COM_CAP];
@@ -782,6 +784,11 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
         lmax = max(lmax, cc);
     }
     if (threadIdx.x == 0) s_lmax = -1;
+    if (lanes) {  // the traversal's lane map through this build's permutation (lane_order)
+#pragma unroll
+        for (int i = 0; i < EC_PER; ++i)
+            if (a0 + i < n) lanes[a0 + i] = inv[lanes[a0 + i]];
+    }
     const uint32_t S0 = base[c0], S1 = base[c1];
     const uint32_t cnt = S1 - S0;
     const bool lds = cnt <= (uint32_t)COM_CAP;
@@ -1336,8 +1343,9 @@ hipError_t lane_order(const TreeBuffers &b, int64_t n, int J, bool refresh, uint
                       hipStream_t s) {
     if (n <= 0) return hipSuccess;
     if (!refresh) {  // carry the grouping through this build's permutation (k_prep: keys32 =
-                     // old slot -> new slot)
-        k_lane_remap<<<grid_for(n), TB, 0, s>>>(n, b.keys32, lanes);
+                     // old slot -> new slot); tree_build does it inside k_emit_com when
+                     // b.lanes_remap is set
+        if (b.lanes_remap != lanes) k_lane_remap<<<grid_for(n), TB, 0, s>>>(n, b.keys32, lanes);
         return hipGetLastError();
     }
     // keys32 / keys32_s / idx are free once the build has run
@@ -1401,7 +1409,7 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
                                                                   b.cell_start);
     k_emit_com<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), EC_TB, 0, s>>>(
         n, g, D0, b.keys_s, b.cpl, b.base, b.cell_start, b.dst.x, b.dst.y, b.dst.m, b.dst.cidx,
-        b.idx, b.nodes, b.scalars + 1);
+        b.idx, b.nodes, b.scalars + 1, b.keys32, b.lanes_remap);
     const dim3 span_grid((b.span_stride + TB - 1) / TB, g.J + 1);
     const uint32_t n_groups = span_groups(b.span_stride);
     if (n_groups > 1) {

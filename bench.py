@@ -45,6 +45,8 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-counters", action="store_true",
                     help="skip the V-bar / lane-efficiency counting walks on the timed state")
+    ap.add_argument("--no-events", action="store_true",
+                    help="diagnostic: no HIP events in the timed region (no kernel times)")
     ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
     return ap.parse_args()
@@ -208,7 +210,7 @@ def main():
         cnt_start = traversal_counters(bh_amd, params, local_rank, eng.get_bodies())
 
     clocks = ClockSampler(local_rank) if rank == 0 else None
-    eng.set_profiling(True)
+    eng.set_profiling(not args.no_events)
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()

@@ -686,3 +686,24 @@ def test_checkpoint_resume_bit_identical(tmp_path):
     assert resumed.num_bodies() < len(arrs[0])  # the merge rule ran on both sides of the save
     with pytest.raises(bh_amd.BhError):
         resumed.load_state(str(tmp_path / "missing.bhstate"))
+
+
+def test_profiling_timings_do_not_change_results():
+    """bench.py's timed region: per-phase HIP events and per-launch traversal samples on, the
+    same state as with them off, and every timing positive."""
+    arrs = scenes.two_disks(4000, 1000)
+    a = bh_amd.Engine(bh_amd.default_params(theta=0.5))
+    a.reset_bodies(*arrs)
+    a.set_profiling(True)
+    a.step(4)
+    t = a.last_timings()
+    samples = a.traverse_kernel_samples()
+    avg, launches = a.traverse_kernel_ms()
+    assert t["build"] > 0 and t["traverse"] > 0
+    assert launches == 8 and len(samples) == 8 and np.all(samples > 0)
+    assert abs(avg - samples.mean()) < 1e-9
+    b = bh_amd.Engine(bh_amd.default_params(theta=0.5))
+    b.reset_bodies(*arrs)
+    b.step(4)
+    for u, v in zip(a.get_bodies(), b.get_bodies()):
+        assert bits_equal(u, v)
