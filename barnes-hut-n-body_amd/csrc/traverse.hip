@@ -126,10 +126,13 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
     };
     u32x8 r0 = nload(nodes), r1;  // T >= 1 whenever the loop runs
     nwait(r0);
-    while (cur < T) {
+    // (a `while (cur < T)` head with one exit test in the middle made the compiler keep a dead
+    // v_readfirstlane per two stops)
+    while (true) {
         iter(r0, r1);
         if (cur >= T) break;
         iter(r1, r0);
+        if (cur >= T) break;
     }
 }
 
