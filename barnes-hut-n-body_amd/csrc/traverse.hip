@@ -124,7 +124,8 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
         nwait(nrec);
         cur = ncur;
     };
-    u32x8 r0 = nload(nodes), r1;  // T >= 1 whenever the loop runs
+    if (T == 0) return;  // no body inside the root cell: an empty tree
+    u32x8 r0 = nload(nodes), r1;
     nwait(r0);
     // (a `while (cur < T)` head with one exit test in the middle made the compiler keep a dead
     // v_readfirstlane per two stops)

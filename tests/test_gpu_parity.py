@@ -150,6 +150,23 @@ def test_bodies_outside_root_cell():
     _assert_state_equal(eng, ref)
 
 
+def test_every_body_outside_the_root_cell():
+    """No body inside the root cell: the tree is empty, every body feels no force and just
+    drifts (BHA:126, 216); also after a live geometry change that puts them all outside."""
+    n = 300
+    rng = np.random.default_rng(8)
+    x = rng.uniform(2500.0, 2600.0, n)  # x >= cx + h = 2402
+    y = rng.uniform(0.0, 800.0, n)
+    arrs = (x, y, rng.uniform(-5, 5, n), rng.uniform(-5, 5, n), np.full(n, 2.0))
+    eng, ref = _pair(arrs, theta=0.5)
+    ax, ay = eng.compute_accelerations()
+    rax, ray = ref.accelerations()
+    assert bits_equal(ax, rax) and bits_equal(ay, ray) and not np.any(ax)
+    eng.step(3)
+    ref.step(3)
+    _assert_state_equal(eng, ref)
+
+
 def test_merge_rule():
     """Heavy bodies (m > 4000) absorb bodies with d^2 < 64 (BHA:463-532): 7.9 eaten, 8.1 not;
     a heavy absorbed by a later heavy carries its grown mass; N shrinks."""
