@@ -461,46 +461,47 @@ __device__ __forceinline__ int64_t run_end(const uint64_t *__restrict__ keys_s, 
 // a node's end is found by a word-wise SWAR scan of the window (most nodes end inside it);
 // only nodes that outrun the window gallop over the keys in global memory.
 // first j in [from, c0 + WIN) with c(j) < L, or -1; w[i] = c(c0 + i) + 1 in [0, 42];
-// bm[b] = min of w over the 64-byte block b.  The SWAR scan covers the rest of from's block,
-// then the block minima locate the first block holding a match, which is scanned last: at most
-// 8 + WIN / 512 + 8 LDS words per search instead of up to WIN / 8 (a node near the top of a
-// dense region ends thousands of bodies later; one such lane used to hold its wave and, at
-// the phase barrier, its workgroup).
+// wm[k] = min of w over the 8-byte word k, bm[b] = min over the 64-byte block b.  SWAR tests
+// on from's word, then on the word minima of the rest of its block, then on the block minima
+// locate the first word holding a match: 3 LDS reads per search, at most 5 + WIN / 512 (a node
+// near the top of a dense region ends thousands of bodies later; one such lane used to hold
+// its wave and, at the phase barrier, its workgroup).
 template <int WIN>
-__device__ __forceinline__ int64_t lds_scan(const uint64_t *w, const uint64_t *bm, int64_t c0,
-                                            int64_t from, int L) {
+__device__ __forceinline__ int64_t lds_scan(const uint64_t *w, const uint64_t *wm,
+                                            const uint64_t *bm, int64_t c0, int64_t from, int L) {
     static_assert(WIN % 512 == 0, "whole words of block minima");
     const uint64_t ones = 0x0101010101010101ull, highs = 0x8080808080808080ull;
     const uint64_t sub = ones * (uint64_t)(L + 1);
+    auto first = [&](uint64_t x) { return (x - sub) & ~x & highs; };  // bytes with c + 1 < L + 1
     const int64_t o = from - c0;
     if (o >= WIN) return -1;
-    // bytes before `from` are raised to 0x7F (>= L + 1): they neither match nor borrow
-    uint64_t pad = ~(~0ull << (8 * (o & 7))) & 0x7F7F7F7F7F7F7F7Full;
-    int wi = (int)(o >> 3);
-    const int wend = (wi | 7) + 1;  // end of from's 64-byte block
-    for (; wi < wend; ++wi) {
-        const uint64_t x = w[wi] | pad;
-        const uint64_t t = (x - sub) & ~x & highs;  // lowest flag = first byte with c + 1 < L + 1
-        if (t) return c0 + 8 * (int64_t)wi + (__builtin_ctzll(t) >> 3);
-        pad = 0;
-    }
-    const int b = (int)(o >> 6) + 1;  // first later block
-    if (b >= WIN / 64) return -1;
-    uint64_t bpad = ~(~0ull << (8 * (b & 7))) & 0x7F7F7F7F7F7F7F7Full;
-    for (int bw = b >> 3; bw < WIN / 512; ++bw) {
-        const uint64_t x = bm[bw] | bpad;
-        const uint64_t t = (x - sub) & ~x & highs;
-        if (t) {
-            const int blk = 8 * bw + (__builtin_ctzll(t) >> 3);
-            for (int q = 8 * blk;; ++q) {  // the block holds a match
-                const uint64_t y = w[q];
-                const uint64_t u = (y - sub) & ~y & highs;
-                if (u) return c0 + 8 * (int64_t)q + (__builtin_ctzll(u) >> 3);
+    // from's word, bytes before `from` raised to 0x7F (>= L + 1): they neither match nor borrow
+    const int wi = (int)(o >> 3);
+    const uint64_t t0 = first(w[wi] | (~(~0ull << (8 * (o & 7))) & 0x7F7F7F7F7F7F7F7Full));
+    if (t0) return c0 + 8 * (int64_t)wi + (__builtin_ctzll(t0) >> 3);
+    // the later words of from's block, by their minima; then the matching word itself
+    const int blk = wi >> 3;
+    const uint64_t lo1 = (wi & 7) == 7 ? ~0ull : ~(~0ull << (8 * ((wi & 7) + 1)));
+    const uint64_t t1 = first(wm[blk] | (lo1 & 0x7F7F7F7F7F7F7F7Full));
+    int q = -1;
+    if (t1) {
+        q = 8 * blk + (__builtin_ctzll(t1) >> 3);
+    } else {  // later blocks, by their minima
+        const int b = blk + 1;
+        if (b >= WIN / 64) return -1;
+        uint64_t bpad = ~(~0ull << (8 * (b & 7))) & 0x7F7F7F7F7F7F7F7Full;
+        for (int bw = b >> 3; bw < WIN / 512; ++bw) {
+            const uint64_t t = first(bm[bw] | bpad);
+            if (t) {
+                const int b2 = 8 * bw + (__builtin_ctzll(t) >> 3);  // the block holds a match
+                q = 8 * b2 + (__builtin_ctzll(first(wm[b2])) >> 3);
+                break;
             }
+            bpad = 0;
         }
-        bpad = 0;
+        if (q < 0) return -1;
     }
-    return -1;
+    return c0 + 8 * (int64_t)q + (__builtin_ctzll(first(w[q])) >> 3);
 }
 
 // ---- exact replay of BHA:125-156 inside one jitter cell (depth J, h_J < 1e-3) ---------
@@ -708,11 +709,19 @@ constexpr int EC_WIN = (1 << COM_CHUNK_SHIFT) + 2048;  // c(j) + 1 of the chunk 
 #endif
 constexpr int EC_TB = BH_EC_TB;  // 2 bodies per thread (measured: 256 and 1024 threads slower)
 constexpr int EC_PER = (1 << COM_CHUNK_SHIFT) / EC_TB;
+#ifndef BH_EC_LVL
+#define BH_EC_LVL 4
+#endif
+constexpr int EC_LVL = BH_EC_LVL;  // skeleton levels whose loads are batched
 constexpr uint32_t EC_SPAN = 1u << 31;
 constexpr uint32_t EC_LEAF = 1u << 30;
 constexpr uint32_t EC_NEXT_MASK = 0xFFFFu;  // next - S0 (<= COM_CAP)
 constexpr int EC_JMASK_SHIFT = 16;          // jitter cell: subdivided children
 constexpr int EC_D2_SHIFT = 20;             // 2 x depth
+constexpr uint16_t EC_OWN_DONE = 0xFFFFu;   // s_own: a leaf, or a node finished body-wise
+constexpr uint32_t EC_OWN_BODY_MASK = (1u << COM_CHUNK_SHIFT) - 1;  // s_own: body - c0
+constexpr int EC_OWN_L_SHIFT = COM_CHUNK_SHIFT;                      // s_own: depth
+static_assert(COM_CHUNK_SHIFT + 5 <= 16, "s_own packs body and depth (depth <= J <= 30)");
 static_assert(COM_CAP <= (int)EC_NEXT_MASK, "LDS next offsets must fit 16 bits");
 
 __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D0,
@@ -732,6 +741,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
     __shared__ ushort4 s_ch[COM_CAP];
     __shared__ uint64_t win[EC_WIN / 8];
     __shared__ uint64_t win_min[EC_WIN / 512];  // per 64-byte block of win: its minimum byte
+    __shared__ uint64_t win_wmin[EC_WIN / 64];  // per 8-byte word of win: its minimum byte
     __shared__ int s_lmax;
 #ifdef BH_EC_TIMING
     uint64_t t_ph[7];
@@ -744,16 +754,46 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
     const int64_t c0 = (int64_t)blockIdx.x << COM_CHUNK_SHIFT;
     const int64_t c1 = min(c0 + (1 << COM_CHUNK_SHIFT), n);
     const int64_t a0 = c0 + (int64_t)threadIdx.x * EC_PER;
+    uint32_t lv[EC_PER];  // lane map entries, loaded first: the remap's second load waits on them
+    if (lanes) {
+#pragma unroll
+        for (int i = 0; i < EC_PER; ++i) lv[i] = lanes[min(a0 + i, n - 1)];
+    }
+    int cps[EC_PER], ccs[EC_PER];
+    uint32_t bases[EC_PER];
+    // the bodies' keys and leaf data too: every independent load of the thread is in flight
+    // before the first barrier (unconditional, clamped: a branch per load serialises them),
+    // none waits behind the window or the skeleton's dependent chains
+    uint64_t ks[EC_PER];
+    double xs[EC_PER], ys[EC_PER], ms[EC_PER];
+    int lmax = -1;
+#pragma unroll
+    for (int i = 0; i < EC_PER; ++i) {
+        const int64_t a = a0 + i;
+        const int64_t ac = min(a, n - 1);
+        const int cp = (int)cpl[max(ac - 1, (int64_t)0)], cc = (int)cpl[ac];
+        const uint32_t ba = base[ac];
+        ks[i] = keys_s[ac];
+        xs[i] = x[ac];
+        ys[i] = y[ac];
+        ms[i] = m[ac];
+        cps[i] = a < n ? (a > 0 ? cp : -1) : -1;
+        ccs[i] = a < n ? cc : -1;
+        bases[i] = a < n ? ba : 0u;
+        lmax = max(lmax, ccs[i]);
+    }
     {
         uint8_t *wb = reinterpret_cast<uint8_t *>(win);
         uint8_t *mb = reinterpret_cast<uint8_t *>(win_min);
+        uint8_t *wm = reinterpret_cast<uint8_t *>(win_wmin);
         static_assert(EC_WIN % EC_TB == 0 && EC_TB % 64 == 0, "a wave fills whole blocks");
         constexpr int R = EC_WIN / EC_TB;
         int v[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {  // every load in flight before the first use
-            const int64_t j = c0 + threadIdx.x + r * EC_TB;
-            v[r] = j < n ? (int)cpl[j] + 1 : 0;  // past the end: c = -1
+            const int64_t j = c0 + threadIdx.x + r * EC_TB;  // unconditional loads (a branch
+            const int c = (int)cpl[min(j, n - 1)] + 1;        // per load serialises them)
+            v[r] = j < n ? c : 0;  // past the end: c = -1
         }
 #pragma unroll
         for (int r = 0; r < R; ++r) {  // a wave writes block i / 64
@@ -761,33 +801,21 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
             wb[i] = (uint8_t)v[r];
             int mv = v[r];
 #pragma unroll
-            for (int off = 32; off > 0; off >>= 1) mv = min(mv, __shfl_xor(mv, off));
+            for (int off = 1; off < 8; off <<= 1) mv = min(mv, __shfl_xor(mv, off));
+            if ((threadIdx.x & 7) == 0) wm[i >> 3] = (uint8_t)mv;
+#pragma unroll
+            for (int off = 8; off < 64; off <<= 1) mv = min(mv, __shfl_xor(mv, off));
             if ((threadIdx.x & 63) == 0) mb[i >> 6] = (uint8_t)mv;
         }
     }
-    int cps[EC_PER], ccs[EC_PER];
-    uint32_t bases[EC_PER];
-    int lmax = -1;
-#pragma unroll
-    for (int i = 0; i < EC_PER; ++i) {
-        const int64_t a = a0 + i;
-        int cp = -1, cc = -1;
-        uint32_t ba = 0;
-        if (a < n) {
-            cp = a > 0 ? (int)cpl[a - 1] : -1;
-            cc = (int)cpl[a];
-            ba = base[a];
-        }
-        cps[i] = cp;
-        ccs[i] = cc;
-        bases[i] = ba;
-        lmax = max(lmax, cc);
-    }
     if (threadIdx.x == 0) s_lmax = -1;
     if (lanes) {  // the traversal's lane map through this build's permutation (lane_order)
+        uint32_t nl[EC_PER];
+#pragma unroll
+        for (int i = 0; i < EC_PER; ++i) nl[i] = inv[lv[i]];
 #pragma unroll
         for (int i = 0; i < EC_PER; ++i)
-            if (a0 + i < n) lanes[a0 + i] = inv[lanes[a0 + i]];
+            if (a0 + i < n) lanes[a0 + i] = nl[i];
     }
     const uint32_t S0 = base[c0], S1 = base[c1];
     const uint32_t cnt = S1 - S0;
@@ -810,45 +838,17 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
     // ---- skeletons and leaves (BHA:125-137, 159-166, 176-178) ----
     const uint64_t SENT = sentinel_key(J);
     const int shift0 = 2 * (J - D0);
+    // LDS mode: the slots' owners (body, depth) until the child lists reuse the space; the
+    // nodes deeper than D0 are then finished slot by slot (below), 4 slots per thread, instead
+    // of body by body (a body that starts 7 nested cells held its whole wave)
+    uint16_t *s_own = reinterpret_cast<uint16_t *>(s_ch);
 #pragma unroll
-    for (int i = 0; i < EC_PER; ++i) {
+    for (int i = 0; i < EC_PER; ++i) {  // leaves first: their data is already loaded
         const int64_t a = a0 + i;
-        if (a >= n) continue;
-        const uint64_t k = keys_s[a];
-        if (k == SENT) continue;  // not in the tree: no slots
+        if (a >= n || ks[i] == SENT) continue;  // not in the tree: no slots
         const int cp = cps[i], cc = ccs[i];
-        const uint32_t b0 = bases[i];
-        int64_t end = a;
-        for (int L = cc; L > cp; --L) {  // deepest first: ends are nested
-            int64_t b;
-            if (L <= D0) {  // one load: the next depth-L cell starts at a depth-D0 cell start
-                const uint64_t nextcell = ((k >> (2 * (J - L))) + 1) << (2 * (D0 - L));
-                b = (int64_t)cell_start[nextcell] - 1;
-            } else {  // inside a's depth-D0 cell: scan the LDS window, then bounded galloping
-                b = lds_scan<EC_WIN>(win, win_min, c0, end, L);
-                if (b < 0) {
-                    const int64_t limit = (int64_t)cell_start[(k >> shift0) + 1] - 1;
-                    const int shift = 2 * (J - L);
-                    b = run_end(keys_s, limit, c0 + EC_WIN - 1, shift, k >> shift);
-                }
-            }
-            end = b;
-            const bool span = (a >> COM_CHUNK_SHIFT) != (end >> COM_CHUNK_SHIFT);
-            const uint32_t ni = b0 + (uint32_t)(L - cp - 1);
-            const uint32_t nx = base[end + 1];
-            if (span || !lds) {
-                Node nd;
-                nd.comX = 0.0;
-                nd.comY = 0.0;
-                nd.mass = 0.0;
-                nd.next = nx;
-                nd.meta = (uint32_t)(2 * L) | (span ? NODE_SPAN : 0u);  // 2 x depth
-                nodes[ni] = nd;
-            }
-            if (lds)
-                s_next[ni - S0] = span ? EC_SPAN : ((nx - S0) | ((uint32_t)(2 * L) << EC_D2_SHIFT));
-        }
-        const uint32_t li = b0 + (uint32_t)max(0, cc - cp);
+        const uint32_t li = bases[i] + (uint32_t)max(0, cc - cp);
+        if (lds) s_own[li - S0] = EC_OWN_DONE;
         if (cc == J || cp == J) {  // a jitter run's slot: written by the run's replay below
             if (lds) {
                 s_m[li - S0] = 0.0;
@@ -858,10 +858,10 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
             }
             continue;
         }
-        const double mm = m[a];
+        const double mm = ms[i];
         Node leaf;
-        leaf.comX = x[a];  // BHA:176-178
-        leaf.comY = y[a];
+        leaf.comX = xs[i];  // BHA:176-178
+        leaf.comY = ys[i];
         leaf.mass = mm;
         leaf.next = li + 1;
         leaf.meta = NODE_LEAF | (uint32_t)a | (mm == 0.0 ? NODE_SKIP : 0u);
@@ -871,6 +871,126 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
             s_x[li - S0] = leaf.comX;
             s_y[li - S0] = leaf.comY;
             s_next[li - S0] = (li + 1 - S0) | EC_LEAF;
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < EC_PER; ++i) {
+        const int64_t a = a0 + i;
+        const uint64_t k = ks[i];
+        if (a >= n || k == SENT) continue;
+        const int cp = cps[i], cc = ccs[i];
+        const uint32_t b0 = bases[i];
+        int64_t end = a;
+        int top = cc;
+        if (lds) {  // depths D0 < L <= cc: recorded for the slot pass; the rest are done here
+            for (int L = cc; L > max(cp, D0); --L) {
+                const uint32_t ni = b0 + (uint32_t)(L - cp - 1) - S0;
+                s_own[ni] = (uint16_t)((uint32_t)(a - c0) | ((uint32_t)L << EC_OWN_L_SHIFT));
+            }
+            for (int L = min(cc, D0); L > cp; --L) s_own[b0 + (uint32_t)(L - cp - 1) - S0] = EC_OWN_DONE;
+            top = min(cc, D0);
+        }
+        // deepest first (the LDS scans start at the deeper level's end: ends are nested), in
+        // groups of EC_LVL levels whose end and slot loads are all in flight together: the
+        // depth-<= D0 ends and the successors' slots do not depend on each other within a group
+        for (int Lh = top; Lh > cp; Lh -= EC_LVL) {
+            int64_t e[EC_LVL];
+#pragma unroll
+            for (int q = 0; q < EC_LVL; ++q) {  // below depth D0: LDS scans, nested
+                const int L = Lh - q;
+                int64_t b = end;
+                if (L > cp && L > D0) {  // inside a's depth-D0 cell: LDS window, then galloping
+                    b = lds_scan<EC_WIN>(win, win_wmin, win_min, c0, end, L);
+                    if (b < 0) {
+                        const int64_t limit = (int64_t)cell_start[(k >> shift0) + 1] - 1;
+                        const int shift = 2 * (J - L);
+                        b = run_end(keys_s, limit, c0 + EC_WIN - 1, shift, k >> shift);
+                    }
+                    end = b;
+                }
+                e[q] = b;
+            }
+            uint32_t cs[EC_LVL];
+#pragma unroll
+            for (int q = 0; q < EC_LVL; ++q) {  // depth <= D0: the next depth-L cell's start,
+                const int L = Lh - q;           // every load issued unconditionally
+                const bool sh = L > cp && L <= D0;
+                cs[q] = cell_start[sh ? ((k >> (2 * (J - L))) + 1) << (2 * (D0 - L)) : 0];
+            }
+#pragma unroll
+            for (int q = 0; q < EC_LVL; ++q) {
+                const int L = Lh - q;
+                if (L > cp && L <= D0) e[q] = (int64_t)cs[q] - 1;
+            }
+            uint32_t nxs[EC_LVL];
+#pragma unroll
+            for (int q = 0; q < EC_LVL; ++q) nxs[q] = base[Lh - q > cp ? e[q] + 1 : 0];
+#pragma unroll
+            for (int q = 0; q < EC_LVL; ++q) {
+                const int L = Lh - q;
+                if (L <= cp) break;
+                const bool span = (a >> COM_CHUNK_SHIFT) != (e[q] >> COM_CHUNK_SHIFT);
+                const uint32_t ni = b0 + (uint32_t)(L - cp - 1);
+                const uint32_t nx = nxs[q];
+                if (span || !lds) {
+                    Node nd;
+                    nd.comX = 0.0;
+                    nd.comY = 0.0;
+                    nd.mass = 0.0;
+                    nd.next = nx;
+                    nd.meta = (uint32_t)(2 * L) | (span ? NODE_SPAN : 0u);  // 2 x depth
+                    nodes[ni] = nd;
+                }
+                if (lds)
+                    s_next[ni - S0] =
+                        span ? EC_SPAN : ((nx - S0) | ((uint32_t)(2 * L) << EC_D2_SHIFT));
+            }
+        }
+    }
+    if (lds) {  // the nodes below depth D0, by slot (s_own)
+        phase_barrier();
+        constexpr int SL = COM_CAP / EC_TB;
+        static_assert(COM_CAP % EC_TB == 0, "whole slots per thread");
+        int64_t as[SL], e[SL];
+        int Ls[SL];
+#pragma unroll
+        for (int r = 0; r < SL; ++r) {
+            const uint32_t i = threadIdx.x + (uint32_t)r * EC_TB;
+            const uint32_t ow = i < cnt ? s_own[i] : EC_OWN_DONE;
+            const bool live = ow != EC_OWN_DONE;
+            as[r] = c0 + (ow & EC_OWN_BODY_MASK);
+            Ls[r] = live ? (int)(ow >> EC_OWN_L_SHIFT) : -1;
+            int64_t b = as[r];
+            if (live) {  // the LDS window, then bounded galloping over the keys
+                b = lds_scan<EC_WIN>(win, win_wmin, win_min, c0, as[r], Ls[r]);
+                if (b < 0) {
+                    const uint64_t k = keys_s[as[r]];
+                    const int64_t limit = (int64_t)cell_start[(k >> shift0) + 1] - 1;
+                    const int shift = 2 * (J - Ls[r]);
+                    b = run_end(keys_s, limit, c0 + EC_WIN - 1, shift, k >> shift);
+                }
+            }
+            e[r] = b;
+        }
+        uint32_t nxs[SL];
+#pragma unroll
+        for (int r = 0; r < SL; ++r) nxs[r] = base[Ls[r] >= 0 ? e[r] + 1 : 0];
+#pragma unroll
+        for (int r = 0; r < SL; ++r) {
+            if (Ls[r] < 0) continue;
+            const uint32_t i = threadIdx.x + (uint32_t)r * EC_TB;
+            const int L = Ls[r];
+            const bool span = (as[r] >> COM_CHUNK_SHIFT) != (e[r] >> COM_CHUNK_SHIFT);
+            if (span) {
+                Node nd;
+                nd.comX = 0.0;
+                nd.comY = 0.0;
+                nd.mass = 0.0;
+                nd.next = nxs[r];
+                nd.meta = (uint32_t)(2 * L) | NODE_SPAN;  // 2 x depth
+                nodes[S0 + i] = nd;
+            }
+            s_next[i] = span ? EC_SPAN : ((nxs[r] - S0) | ((uint32_t)(2 * L) << EC_D2_SHIFT));
         }
     }
     phase_barrier();
