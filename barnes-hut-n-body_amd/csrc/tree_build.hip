@@ -783,29 +783,29 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
         lmax = max(lmax, ccs[i]);
     }
     {
-        uint8_t *wb = reinterpret_cast<uint8_t *>(win);
+        // one 8-byte word of c(j) + 1 per thread (EC_WIN / 8 threads): the word minimum in
+        // registers, the 64-byte block minimum over 8 neighbouring lanes
         uint8_t *mb = reinterpret_cast<uint8_t *>(win_min);
         uint8_t *wm = reinterpret_cast<uint8_t *>(win_wmin);
-        static_assert(EC_WIN % EC_TB == 0 && EC_TB % 64 == 0, "a wave fills whole blocks");
-        constexpr int R = EC_WIN / EC_TB;
-        int v[R];
+        constexpr int NW = EC_WIN / 8;
+        static_assert(NW <= EC_TB && NW % 64 == 0, "one word per thread, whole waves");
+        const int t = (int)threadIdx.x;
+        if (t < NW) {
+            const int64_t j = c0 + 8 * (int64_t)t;
+            const int64_t valid = n - j;  // bytes past the last body: c = -1
+            // a word that starts below n ends within cpl's 32 bytes of slack past cap
+            uint64_t wv = *reinterpret_cast<const uint64_t *>(cpl + (valid > 0 ? j : 0));
+            // c + 1 per byte without carries (c in [-1, 41]): -1 -> 0
+            wv = ((wv & 0x7F7F7F7F7F7F7F7Full) + 0x0101010101010101ull) ^ (wv & 0x8080808080808080ull);
+            if (valid < 8) wv = valid <= 0 ? 0ull : (wv & ~(~0ull << (8 * valid)));
+            int mv = 0xFF;
 #pragma unroll
-        for (int r = 0; r < R; ++r) {  // every load in flight before the first use
-            const int64_t j = c0 + threadIdx.x + r * EC_TB;  // unconditional loads (a branch
-            const int c = (int)cpl[min(j, n - 1)] + 1;        // per load serialises them)
-            v[r] = j < n ? c : 0;  // past the end: c = -1
-        }
-#pragma unroll
-        for (int r = 0; r < R; ++r) {  // a wave writes block i / 64
-            const int i = threadIdx.x + r * EC_TB;
-            wb[i] = (uint8_t)v[r];
-            int mv = v[r];
+            for (int q = 0; q < 8; ++q) mv = min(mv, (int)((wv >> (8 * q)) & 0xFFu));
+            win[t] = wv;
+            wm[t] = (uint8_t)mv;
 #pragma unroll
             for (int off = 1; off < 8; off <<= 1) mv = min(mv, __shfl_xor(mv, off));
-            if ((threadIdx.x & 7) == 0) wm[i >> 3] = (uint8_t)mv;
-#pragma unroll
-            for (int off = 8; off < 64; off <<= 1) mv = min(mv, __shfl_xor(mv, off));
-            if ((threadIdx.x & 63) == 0) mb[i >> 6] = (uint8_t)mv;
+            if ((t & 7) == 0) mb[t >> 3] = (uint8_t)mv;
         }
     }
     if (threadIdx.x == 0) s_lmax = -1;
