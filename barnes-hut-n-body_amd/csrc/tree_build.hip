@@ -69,15 +69,30 @@ __global__ __launch_bounds__(TB) void k_morton(int64_t n, const double *__restri
     if (!quad_contains(cx, cy, g.root_h, px, py) || (cidx[i] & CIDX_DEAD)) {
         key = sentinel_key(g.J);  // BHA:126 — not inserted (or merged away this call)
     } else {
-        key = 0;
-        for (int d = 0; d < g.J; ++d) {
-            int ix = (px < cx) ? 0 : 1;  // BHA:153
-            int iy = (py < cy) ? 0 : 1;  // BHA:154
-            double hh = g.h[d + 1];
-            cx = ix ? cx + hh : cx - hh;
-            cy = iy ? cy + hh : cy - hh;
-            key = (key << 2) | (uint64_t)(ix | (iy << 1));
-        }
+        // The descent (BHA:153-154 at every depth: digit = p >= cell centre) ends in the depth-J
+        // cell [x0 + i w, x0 + (i + 1) w) that holds p: every centre it compares against is a
+        // grid line x0 + k w, exact in binary64 (dyadic, < 40 significant bits), and p stays in
+        // the current cell, so i = floor((p - x0) / w) in exact arithmetic.  It is taken from
+        // the rounded quotient (off by at most one near a line) and settled by two exact
+        // compares against the grid lines, the same compares the descent makes.
+        const double w = 2.0 * g.h[g.J];
+        const double x0 = cx - g.root_h, y0 = cy - g.root_h;
+        const int64_t top = ((int64_t)1 << g.J) - 1;
+        auto cell = [&](double p, double o) __attribute__((always_inline)) {
+            int64_t c = (int64_t)((p - o) * (1.0 / w));
+            c = c < 0 ? 0 : (c > top ? top : c);
+            if (p < o + (double)c * w) --c;
+            else if (c < top && p >= o + (double)(c + 1) * w) ++c;
+            return (uint64_t)c;
+        };
+        auto spread = [](uint64_t v) __attribute__((always_inline)) {  // bit k -> bit 2k
+            v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+            v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+            v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+            v = (v | (v << 2)) & 0x3333333333333333ull;
+            return (v | (v << 1)) & 0x5555555555555555ull;
+        };
+        key = spread(cell(px, x0)) | (spread(cell(py, y0)) << 1);  // digit = ix | iy << 1
     }
     keys[i] = key;
     keys32[i] = (uint32_t)(key >> key32_shift(g.J));  // the sort key: top 32 of 2J+1 bits
