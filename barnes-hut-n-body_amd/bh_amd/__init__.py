@@ -43,7 +43,7 @@ EXPORTED_SYMBOLS = (
     "bh_nbody3d_create", "bh_nbody3d_destroy", "bh_nbody3d_last_error", "bh_nbody3d_set",
     "bh_nbody3d_step", "bh_nbody3d_accelerations", "bh_nbody3d_get", "bh_nbody3d_last_ms",
     "bh_local_group_create", "bh_local_group_destroy", "bh_create_local",
-    "bh_save_state", "bh_load_state",
+    "bh_save_state", "bh_load_state", "bh_let_stats",
 )
 
 
@@ -118,6 +118,7 @@ def load_library(path: str | None = None):
     lib.bh_synchronize.argtypes = [_VP]
     lib.bh_traversal_stats.argtypes = [_VP, _I64P, _I64P, _I64P]
     lib.bh_traversal_counters.argtypes = [_VP, _I64P]
+    lib.bh_let_stats.argtypes = [_VP, _I64P]
     lib.bh_last_removed.argtypes = [_VP, _I64P, ctypes.c_int64, _I64P]
     lib.bh_shard_range.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    _I64P, _I64P]
@@ -372,6 +373,12 @@ class Engine:
         cx, cy, h = (np.empty(n, dtype=np.float64) for _ in range(3))
         self._check(self._lib.bh_get_quads(self._h, _dp(cx), _dp(cy), _dp(h), n, ctypes.byref(need)))
         return cx, cy, h
+
+    def let_stats(self):
+        """Multi-rank build sharding: LET builds, full builds, last subset size, last LET nodes."""
+        out = np.zeros(4, dtype=np.int64)
+        self._check(self._lib.bh_let_stats(self._h, out.ctypes.data_as(_I64P)))
+        return dict(zip(("let_builds", "full_builds", "subset", "let_nodes"), out.tolist()))
 
     def set_profiling(self, on: bool):
         self._check(self._lib.bh_set_profiling(self._h, 1 if on else 0))

@@ -166,7 +166,9 @@ hipError_t lane_order(const TreeBuffers &b, int64_t n, int J, bool refresh, uint
 // kick (optional, one GPU, no visit counting): the KDK update of the evaluated slots is applied
 // in the kernel's epilogue instead of writing a2 -- KICK_DRIFT = k_kick_drift (BHA:414-422),
 // KICK_ONLY = k_kick (BHA:429-432), same operations in the same order.
-enum KickMode { KICK_NONE = 0, KICK_DRIFT = 1, KICK_ONLY = 2 };
+// KICK_POS (multi-rank LET evaluation, let.hip): no kick; the lane writes (ax, ay, x, y) to
+// a2[4q..4q+3] -- x, y as the build left them (jitter), for the peers' replicated states.
+enum KickMode { KICK_NONE = 0, KICK_DRIFT = 1, KICK_ONLY = 2, KICK_POS = 3 };
 struct KickArgs {
     KickMode mode;
     double *vx, *vy;  // x, y are the traversal's own position arrays
@@ -197,6 +199,59 @@ __host__ __device__ inline int64_t shard_sub(int64_t n, int world, int rounds) {
 // Exactness check of the traversal's in-range sqrt/reciprocal sequences against the IEEE
 // operations on n generated operands; adds the mismatch count to *d_bad.
 hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_bad, hipStream_t s);
+
+// ---- launchers (let.hip): the multi-rank build as a locally essential tree -------------
+// Every rank keeps the full replicated state but builds only the bodies of the depth-LET_P
+// cells within reach of the bodies it evaluates (its pieces); the rest of the tree is the top
+// (depth < LET_P) assembled from every rank's depth-LET_P cell values, with remote cells as
+// childless records every local body provably accepts.  See let.hip.
+constexpr int LET_P = 8;
+constexpr int64_t LET_CELLS = (int64_t)1 << (2 * LET_P);
+struct __attribute__((aligned(32))) LetCell {
+    double comX, comY, mass;
+    uint32_t cnt;  // in-tree bodies of the cell, saturated at 2 (0 empty, 1 leaf, 2 internal)
+    uint32_t tag;  // exchange table: 1 = provided; levels: depth-LET_P cell of a 1-body node
+};
+static_assert(sizeof(LetCell) == 32, "LET cell record must be 32 bytes");
+struct LetPieces {  // rank `rank` owns lanes [(k*world + rank)*sub, +sub) for k < rounds
+    int64_t n, sub;
+    int world, rank, rounds;
+    const uint32_t *lanes;  // lane -> replicated slot (the Hilbert wave map), or null: identity
+};
+struct LetBufs {
+    uint8_t *ecell, *hcell;   // [LET_CELLS] cells of own bodies / cells built locally
+    uint8_t *own;             // [n] replicated slot evaluated by this rank
+    uint32_t *subpos;         // [n] replicated slot -> subset slot (subset bodies)
+    uint32_t *flag_all;       // [1] a non-finite own body: every cell is built
+    uint32_t *sel, *selpos;   // [n + 1] subset flags and their exclusive scan
+    uint32_t *cstart;         // [LET_CELLS + 1] first sorted subset body of each cell
+    LetCell *table, *tables;  // own exchange table, all ranks' tables [world][LET_CELLS]
+    LetCell *levels;          // depths 0..LET_P, level d at ((4^d - 1) / 3)
+    uint32_t *w, *posc, *bsz; // [LET_CELLS + 1] nodes per cell, their scan, block sizes
+    Node *nodes;              // the assembled tree, pre-order
+    uint32_t *lanes;          // [n] lane -> subset slot (own pieces)
+    void *scratch;
+    size_t scratch_bytes;
+};
+// Largest gap^2 (in cells) at which a depth-LET_P cell may still be opened by a body of a cell
+// at that gap; cells beyond it are accepted by every such body.  < 0: the LET does not apply.
+double let_include_gap2(const Geometry &g, double theta2, double soft2);
+size_t let_scratch_bytes(int64_t n);
+// own cells, halo, subset flags + scan + gather into `sub` (vx carries the replicated slot);
+// the subset size is then selpos[n] (read by the host)
+hipError_t let_select(const BodyState &st, const Geometry &g, const LetPieces &pc,
+                      double gap2, const LetBufs &L, const BodyState &sub, hipStream_t s);
+// after tree_build over the subset: the own cells' exchange table
+hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const TreeBuffers &tb,
+                     hipStream_t s);
+// after the exchange (L.tables): top levels, layout, node array, lane map; tree size posc[LET_CELLS]
+hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, const LetBufs &L,
+                        const TreeBuffers &tb, hipStream_t s);
+// KDK of all replicated slots from a2 = (ax, ay, x, y) per lane (BHA:410-432)
+void let_kick_drift(int64_t n, const double *a4, double *x, double *y, double *vx, double *vy,
+                    double dtHalf, double dt, hipStream_t s, const uint32_t *lanes);
+void let_kick(int64_t n, const double *a4, double *x, double *y, double *vx, double *vy,
+              double dtHalf, hipStream_t s, const uint32_t *lanes);
 
 // ---- launchers (direct.hip): theta = 0 all-pairs ---------------------------------
 // Non-empty leaves of the last tree in pre-order (the reference's theta = 0 summation order).

@@ -6,11 +6,14 @@
 // kernel sequence on that stream; the only host round trip is the merge rule's (BHA:463-532)
 // candidate mailbox, and only while heavy bodies exist.
 //
-// Multi-GPU (bh_create_dist): every rank holds the full replicated state and builds the
-// same tree (deterministically, so the jitter mutates every replica identically); force
-// evaluation is sharded by contiguous Morton ranges and the accelerations are all-gathered
-// in place with RCCL over xGMI, after which every rank integrates the full set.  The merge
-// rule is replicated (identical inputs, identical outcome) and needs no exchange.
+// Multi-GPU (bh_create_dist): every rank holds the full replicated state; force evaluation is
+// sharded by contiguous Morton ranges and the accelerations are all-gathered in place with
+// RCCL over xGMI, after which every rank integrates the full set.  The build is sharded too:
+// each rank builds a locally essential tree (let.hip) -- the cells its bodies may open, plus
+// the top assembled from every rank's cell values -- and sends its bodies' (possibly jittered)
+// positions with the accelerations; every BH_LET_REFRESH builds, and at the end of every
+// bh_step call (lastTree, BHA:435), the full tree is built by every rank.  The merge rule is
+// replicated (identical inputs, identical outcome) and needs no exchange.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
@@ -19,6 +22,7 @@
 #include <condition_variable>
 #include <mutex>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <iterator>
 #include <string>
@@ -148,6 +152,28 @@ struct bh_engine {
     int lanes_age = 0;         // builds since the last Hilbert sort
     const uint32_t *a2_lanes = nullptr;  // the last evaluation wrote a2 by lane of this map
 
+    // multi-rank locally essential tree (let.hip): subset state and tree workspace
+    bool let_on = true;         // BH_LET=0 in the environment: the replicated build
+    int let_age = 0;            // LET builds since the last full build
+    int64_t let_builds = 0, full_builds = 0, let_last_sub = 0;
+    bool st_morton = false;     // slots are in the Morton order of a full build (not caller order)
+    bool a2_pos = false;        // the last evaluation wrote (ax, ay, x, y) per slot
+    LetBufs L{};
+    int64_t let_cap = 0;        // n capacity of the per-body LET arrays
+    int64_t let_sub_cap = 0;    // subset capacity of the subset tree workspace
+    int let_J = -1;
+    size_t let_node_cap = 0;
+    BodyState sub_src{}, sub_dst{};
+    uint64_t *s_keys = nullptr, *s_keys_s = nullptr, *s_spl = nullptr;
+    uint32_t *s_keys32 = nullptr, *s_keys32_s = nullptr, *s_idx = nullptr, *s_perm = nullptr;
+    int8_t *s_cpl = nullptr;
+    uint32_t *s_cnt = nullptr, *s_base = nullptr, *s_cell_start = nullptr;
+    uint32_t *s_span_list = nullptr, *s_super_list = nullptr, *s_bcount = nullptr,
+             *s_bstart = nullptr;
+    bh::SpanSlot *s_span_children = nullptr;
+    Node *s_nodes = nullptr;
+    hipEvent_t table_ev = nullptr;
+
     // profiling
     bool profiling = false;
     std::vector<hipEvent_t> ev;
@@ -258,7 +284,8 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         const int64_t padded = (e->comm || e->group) ? shard_sub(cap, e->world, BH_SHARD_ROUNDS) *
                                              e->world * BH_SHARD_ROUNDS
                                        : cap;
-        TRY(dev_alloc(e, e->a2, 2 * padded));
+        // multi-rank: (ax, ay, x, y) per slot for the LET evaluation
+        TRY(dev_alloc(e, e->a2, ((e->comm || e->group) ? 4 : 2) * padded));
         TRY(dev_alloc(e, e->ax, cap));
         TRY(dev_alloc(e, e->ay, cap));
         TRY(dev_alloc(e, e->keys, cap));
@@ -299,6 +326,7 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         e->J_alloc = J;
     }
     size_t cb = std::max(tree_scratch_bytes(e->cap, J), compact_scratch_bytes(e->cap));
+    cb = std::max(cb, let_scratch_bytes(e->cap));
     if (cb > e->scratch_bytes) {
         if (e->scratch) (void)hipFree(e->scratch);
         e->scratch = nullptr;
@@ -396,6 +424,7 @@ int build(bh_engine *e) {
     const bool refresh = use_lanes && (!e->lanes_valid || e->lanes_age >= BH_LANE_REFRESH);
     tb.lanes_remap = use_lanes && !refresh ? e->lanes : nullptr;
     HIPCHK(e, tree_build(tb, n, e->geo, e->stream));
+    ++e->full_builds;
     if (use_lanes) {
         if (refresh) HIPCHK(e, lane_order(tb, n, e->geo.J, true, e->lanes, e->stream));
         e->lanes_valid = true;
@@ -405,6 +434,7 @@ int build(bh_engine *e) {
     }
     e->spl_nb = sort_buckets(n);  // k_prep wrote this build's splitters
     if (n > 0) std::swap(e->st, e->alt);
+    e->st_morton = true;
     e->tree_valid = true;
     return BH_OK;
 }
@@ -444,8 +474,203 @@ int ensure_direct(bh_engine *e) {
 #ifndef BH_FUSE_KICK
 #define BH_FUSE_KICK 1
 #endif
-int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fused = nullptr) {
+
+// ---- multi-rank: the build as a locally essential tree (let.hip) ----------------------
+int pinned_reserve(bh_engine *e, size_t bytes);
+#ifndef BH_LET_REFRESH
+#define BH_LET_REFRESH 32  // LET builds between full builds (the replicated Morton order)
+#endif
+int let_alloc(bh_engine *e, int64_t n_sub) {
+    const int J = e->geo.J;
+    if (e->let_cap < e->cap || !e->L.ecell) {  // per-body and per-cell arrays
+        const int64_t cap = e->cap;
+        LetBufs &L = e->L;
+        TRY(dev_alloc(e, L.ecell, LET_CELLS));
+        TRY(dev_alloc(e, L.hcell, LET_CELLS));
+        TRY(dev_alloc(e, L.flag_all, 1));
+        TRY(dev_alloc(e, L.sel, cap + 1));
+        TRY(dev_alloc(e, L.selpos, cap + 1));
+        TRY(dev_alloc(e, L.cstart, LET_CELLS + 1));
+        TRY(dev_alloc(e, L.table, LET_CELLS));
+        TRY(dev_alloc(e, L.tables, (size_t)e->world * LET_CELLS));
+        TRY(dev_alloc(e, L.levels, ((size_t)1 << (2 * LET_P + 2)) / 3 + 1));
+        TRY(dev_alloc(e, L.w, LET_CELLS + 1));
+        TRY(dev_alloc(e, L.posc, LET_CELLS + 1));
+        TRY(dev_alloc(e, L.bsz, LET_CELLS + 1));
+        TRY(dev_alloc(e, L.lanes, cap));
+        TRY(dev_alloc(e, L.own, cap));
+        TRY(dev_alloc(e, L.subpos, cap));
+        TRY(alloc_state(e, e->sub_src, cap));
+        if (!e->table_ev) HIPCHK(e, hipEventCreateWithFlags(&e->table_ev, hipEventDisableTiming));
+        e->let_cap = cap;
+    }
+    e->L.scratch = e->scratch;
+    e->L.scratch_bytes = e->scratch_bytes;
+    if (n_sub <= e->let_sub_cap && J == e->let_J) return BH_OK;
+    // the subset's tree workspace, grown with headroom (the subset drifts between builds)
+    const int64_t sc = std::min<int64_t>(e->cap, std::max<int64_t>(n_sub + n_sub / 4, 1024));
+    TRY(alloc_state(e, e->sub_dst, sc));
+    TRY(dev_alloc(e, e->s_keys, sc));
+    TRY(dev_alloc(e, e->s_keys_s, sc));
+    TRY(dev_alloc(e, e->s_keys32, sc));
+    TRY(dev_alloc(e, e->s_keys32_s, sc));
+    TRY(dev_alloc(e, e->s_idx, sc));
+    TRY(dev_alloc(e, e->s_perm, sc));
+    TRY(dev_alloc(e, e->s_cpl, sc + 32));
+    TRY(dev_alloc(e, e->s_cnt, sc + 1));
+    TRY(dev_alloc(e, e->s_base, sc + 1));
+    TRY(dev_alloc(e, e->s_cell_start, ((size_t)1 << (2 * std::min(J, CELL_TABLE_MAX_DEPTH))) + 2));
+    const size_t ncap = node_capacity(sc, J);
+    TRY(dev_alloc(e, e->s_nodes, ncap));
+    e->let_node_cap = ncap + 2 * (size_t)LET_CELLS + 64;
+    TRY(dev_alloc(e, e->L.nodes, e->let_node_cap));
+    TRY(dev_alloc(e, e->s_span_list, (size_t)(J + 2) * span_stride_for(sc)));
+    TRY(dev_alloc(e, e->s_span_children, (size_t)(J + 2) * span_stride_for(sc)));
+    TRY(dev_alloc(e, e->s_super_list, (size_t)(J + 2) * span_groups(span_stride_for(sc))));
+    TRY(dev_alloc(e, e->s_spl, (size_t)sort_buckets(sc) + 2));
+    TRY(dev_alloc(e, e->s_bcount, (size_t)sort_buckets(sc) + 2));
+    TRY(dev_alloc(e, e->s_bstart, (size_t)sort_buckets(sc) + 2));
+    HIPCHK(e, hipMemset(e->s_bcount, 0, sizeof(uint32_t) * ((size_t)sort_buckets(sc) + 2)));
+    e->let_sub_cap = sc;
+    e->let_J = J;
+    return BH_OK;
+}
+
+TreeBuffers let_tree_buffers(bh_engine *e) {
+    TreeBuffers b;
+    b.src = e->sub_src;
+    b.dst = e->sub_dst;
+    b.keys = e->s_keys;
+    b.keys_s = e->s_keys_s;
+    b.keys32 = e->s_keys32;
+    b.keys32_s = e->s_keys32_s;
+    b.idx = e->s_idx;
+    b.perm = e->s_perm;
+    b.cpl = e->s_cpl;
+    b.cnt = e->s_cnt;
+    b.base = e->s_base;
+    b.cell_start = e->s_cell_start;
+    b.nodes = e->s_nodes;
+    b.scalars = e->scalars;
+    b.span_list = e->s_span_list;
+    b.span_stride = span_stride_for(e->let_sub_cap);
+    b.span_children = e->s_span_children;
+    b.super_list = e->s_super_list;
+    b.scratch = e->scratch;
+    b.scratch_bytes = e->scratch_bytes;
+    b.spl = e->s_spl;
+    b.spl_nb = 0;  // a fresh subset every build: rocprim sort
+    b.bcount = e->s_bcount;
+    b.bstart = e->s_bstart;
+    return b;
+}
+
+// One LET evaluation; *done = false when it does not apply (the caller builds the full tree).
+int evaluate_let(bh_engine *e, bool *done) {
+    *done = false;
+    const int64_t n = e->n;
+    const double gap2 = let_include_gap2(e->geo, e->p.theta * e->p.theta, e->p.soft2);
+    if (gap2 < 0.0 || n <= 0) return BH_OK;
+    const int R = BH_SHARD_ROUNDS;
+    const int64_t sub = shard_sub(n, e->world, R);
+    // the pieces are lane ranges of the Hilbert wave map when it is current (as in the full
+    // path), else slot ranges; a2 is written by lane either way
+    const uint32_t *lanes = e->lanes_valid ? e->lanes : nullptr;
+    const LetPieces pc{n, sub, e->world, e->rank, R, lanes};
+    TRY(mark(e, -1));
+    if (e->group) {  // peers are done reading our previous table and pieces
+        e->group->barrier();
+        for (bh_engine *peer : e->group->members)
+            if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->gathered_ev, 0));
+    }
+    TRY(let_alloc(e, 0));
+    HIPCHK(e, let_select(e->st, e->geo, pc, gap2, e->L, e->sub_src, e->stream));
+    TRY(pinned_reserve(e, 64));
+    uint32_t *h = static_cast<uint32_t *>(e->pin);
+    HIPCHK(e, hipMemcpyAsync(h, e->L.selpos + n, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    const int64_t n_sub = h[0];
+    if (n_sub > n) {
+        e->err = "LET subset larger than the state";
+        return BH_E_STATE;
+    }
+    TRY(let_alloc(e, n_sub));
+    e->let_last_sub = n_sub;
+    ++e->let_builds;
+    const TreeBuffers sb = let_tree_buffers(e);
+    HIPCHK(e, tree_build(sb, n_sub, e->geo, e->stream));
+    HIPCHK(e, let_table(n_sub, e->geo, e->L, sb, e->stream));
+    const size_t tbytes = sizeof(LetCell) * (size_t)LET_CELLS;
+    if (e->comm) {
+        NCCLCHK(e, ncclAllGather(e->L.table, e->L.tables, tbytes, ncclUint8, e->comm, e->stream));
+    } else {
+        HIPCHK(e, hipEventRecord(e->table_ev, e->stream));
+        e->group->barrier();
+        for (int q = 0; q < e->world; ++q) {
+            bh_engine *peer = e->group->members[q];
+            if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->table_ev, 0));
+            HIPCHK(e, hipMemcpyAsync(e->L.tables + (size_t)q * LET_CELLS, peer->L.table, tbytes,
+                                     hipMemcpyDeviceToDevice, e->stream));
+        }
+    }
+    HIPCHK(e, let_assemble(n_sub, e->geo, pc, e->L, sb, e->stream));
+    TRY(mark(e, 0));
+    const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};
+    const KickArgs ka{KICK_POS, nullptr, nullptr, 0.0, 0.0};
+    for (int k = 0; k < R; ++k) {
+        int64_t lo = 0, hi = 0;
+        bh_shard_range(n, e->rank, e->world, k, &lo, &hi);
+        traverse(e->L.nodes, e->let_node_cap, e->L.posc + LET_CELLS, e->sub_dst.x, e->sub_dst.y,
+                 e->sub_dst.m, e->sub_dst.cidx, lo, hi, e->geo, fp, e->a2, nullptr, e->stream,
+                 &ka, e->L.lanes);
+        HIPCHK(e, hipGetLastError());
+        HIPCHK(e, hipEventRecord(e->round_ev[k], e->stream));
+        HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
+        double *piece = e->a2 + 4 * ((int64_t)k * e->world) * sub;  // round k, rank 0
+        if (e->comm) {
+            NCCLCHK(e, ncclAllGather(piece + 4 * e->rank * sub, piece, (size_t)(4 * sub),
+                                     ncclDouble, e->comm, e->comm_stream));
+        } else {
+            e->group->barrier();
+            for (int q = 0; q < e->world; ++q) {
+                if (q == e->rank) continue;
+                bh_engine *peer = e->group->members[q];
+                HIPCHK(e, hipStreamWaitEvent(e->comm_stream, peer->round_ev[k], 0));
+                const int64_t off = 4 * ((int64_t)k * e->world + q) * sub;
+                HIPCHK(e, hipMemcpyAsync(e->a2 + off, peer->a2 + off, sizeof(double) * 4 * sub,
+                                         hipMemcpyDeviceToDevice, e->comm_stream));
+            }
+        }
+    }
+    TRY(mark(e, 1));
+    HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
+    HIPCHK(e, hipStreamWaitEvent(e->stream, e->gathered_ev, 0));
+    TRY(mark(e, 4));
+    e->a2_pos = true;
+    e->a2_lanes = lanes;
+    e->tree_valid = false;  // the full tree was not built
+    *done = true;
+    return BH_OK;
+}
+
+int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fused = nullptr,
+             bool allow_let = false, bool *let_used = nullptr) {
     if (fused) *fused = false;
+    if (let_used) *let_used = false;
+    e->a2_pos = false;
+    // (the pieces are ranges of the slot order: spatially compact only once a full build has
+    // put the state into Morton order -- after a reset it is the caller's order)
+    if (allow_let && !visits && (e->comm || e->group) && e->let_on && e->p.theta != 0.0 &&
+        e->st_morton && e->let_age < BH_LET_REFRESH) {
+        bool done = false;
+        TRY(evaluate_let(e, &done));
+        if (done) {
+            ++e->let_age;
+            if (let_used) *let_used = true;
+            return BH_OK;
+        }
+    }
+    e->let_age = 0;
     const int64_t n = e->n;
     TRY(mark(e, -1));
     TRY(build(e));
@@ -658,27 +883,39 @@ int restore(bh_engine *e) {
     e->lanes_valid = false;
     e->heavy_possible = true;
     e->tree_valid = false;
+    e->st_morton = false;
     return BH_OK;
 }
 
 // ---- one PhysicsEngine.step() (BHA:405-439) ------------------------------------------
-int step_once(bh_engine *e) {
+// last: the final step of a bh_step call -- its second build is the full tree (lastTree,
+// BHA:435, for getTreeForDebug) also on a multi-rank engine that shards its builds.
+int step_once(bh_engine *e, bool last) {
     const int64_t n = e->n;
     const double dtHalf = e->p.dt * 0.5;  // BHA:412
     if (n > 0) {
         bool fused = false;  // one GPU: the kicks ride in the traversal's epilogue
-        TRY(evaluate(e, nullptr, KICK_DRIFT, &fused));  // a(t)
+        bool let = false;    // multi-rank LET: a2 holds (ax, ay, x, y), positions included
+        TRY(evaluate(e, nullptr, KICK_DRIFT, &fused, true, &let));  // a(t)
         if (!fused) {
             TRY(mark(e, -1));
-            kick_drift(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->p.dt,
-                       e->stream, e->a2_lanes);
+            if (let)
+                let_kick_drift(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->p.dt,
+                               e->stream, e->a2_lanes);
+            else
+                kick_drift(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->p.dt,
+                           e->stream, e->a2_lanes);
             HIPCHK(e, hipGetLastError());
             TRY(mark(e, 2));
         }
-        TRY(evaluate(e, nullptr, KICK_ONLY, &fused));  // a(t+dt)
+        TRY(evaluate(e, nullptr, KICK_ONLY, &fused, !last, &let));  // a(t+dt)
         if (!fused) {
             TRY(mark(e, -1));
-            kick(n, e->a2, e->st.vx, e->st.vy, dtHalf, e->stream, e->a2_lanes);
+            if (let)
+                let_kick(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->stream,
+                         e->a2_lanes);
+            else
+                kick(n, e->a2, e->st.vx, e->st.vy, dtHalf, e->stream, e->a2_lanes);
             HIPCHK(e, hipGetLastError());
             TRY(mark(e, 2));
         }
@@ -772,6 +1009,7 @@ int engine_init(bh_engine *e, const bh_params *p, int device) {
     e->p = *p;
     TRY(make_geometry(e->p, e->geo, e->err));
     e->device = device;
+    if (const char *v = std::getenv("BH_LET")) e->let_on = std::strcmp(v, "0") != 0;
     HIPCHK(e, hipSetDevice(device));
     HIPCHK(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     TRY(dev_alloc(e, e->scalars, 16));
@@ -925,6 +1163,17 @@ void bh_destroy(bh_engine *e) {
     free_state(e->st);
     free_state(e->alt);
     free_state(e->snap);
+    free_state(e->sub_src);
+    free_state(e->sub_dst);
+    if (e->table_ev) (void)hipEventDestroy(e->table_ev);
+    void *lets[] = {e->L.ecell, e->L.hcell, e->L.own, e->L.subpos, e->L.flag_all, e->L.sel, e->L.selpos, e->L.cstart,
+                    e->L.table, e->L.tables, e->L.levels, e->L.w, e->L.posc, e->L.bsz,
+                    e->L.nodes, e->L.lanes, e->s_keys, e->s_keys_s, e->s_spl, e->s_keys32,
+                    e->s_keys32_s, e->s_idx, e->s_perm, e->s_cpl, e->s_cnt, e->s_base,
+                    e->s_cell_start, e->s_span_list, e->s_super_list, e->s_bcount, e->s_bstart,
+                    e->s_span_children, e->s_nodes};
+    for (void *q : lets)
+        if (q) (void)hipFree(q);
     void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->keys32, e->keys32_s, e->idx, e->perm, e->cpl, e->cnt,
                     e->base, e->cell_start, e->nodes, e->span_list, e->super_list,
                     e->span_children, e->scalars, e->visits32, e->contrib32, e->lanes, e->wave_iters, e->wave_blocks, e->heavy, e->keep,
@@ -995,6 +1244,7 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     e->tree_valid = false;  // BHA:348
     e->spl_nb = 0;          // other bodies: the first build sorts from scratch
     e->lanes_valid = false;
+    e->st_morton = false;
     return BH_OK;
 }
 
@@ -1009,7 +1259,7 @@ int bh_step(bh_engine *e, int32_t k) {
         HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, 3 * sizeof(uint32_t), e->stream));
         e->removed.clear();
         e->merge_ran = false;
-        for (int32_t s = 0; s < k; ++s) TRY(step_once(e));
+        for (int32_t s = 0; s < k; ++s) TRY(step_once(e, s + 1 == k));
         HIPCHK(e, hipStreamSynchronize(e->stream));
         // the merge bookkeeping first, so that an error below leaves a compacted state
         const int tree_rc = (e->n > 0 && k > 0) ? check_tree_flags(e) : BH_OK;
@@ -1187,6 +1437,19 @@ int bh_traversal_counters(const bh_engine *e, int64_t *out5) {
     out5[2] = e->stat_wave_iters;
     out5[3] = e->stat_wave_blocks;
     out5[4] = e->stat_waves;
+    return BH_OK;
+}
+
+int bh_let_stats(const bh_engine *e, int64_t *out4) {
+    if (!e || !out4) return BH_E_INVALID;
+    out4[0] = e->let_builds;
+    out4[1] = e->full_builds;
+    out4[2] = e->let_last_sub;
+    uint32_t T = 0;
+    if (e->L.posc &&
+        hipMemcpy(&T, e->L.posc + LET_CELLS, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+        return BH_E_DEVICE;
+    out4[3] = T;
     return BH_OK;
 }
 

@@ -1,0 +1,514 @@
+// Multi-rank tree build as a locally essential tree (LET): the build is sharded instead of
+// replicated.  Replaces, per rank, PhysicsEngine.buildTree (BHA:359-366) for the bodies the rank
+// evaluates in computeAccelerations (BHA:374-395), with forces bit-identical to the full tree.
+//
+// Every rank holds the full replicated state (engine.cpp) and evaluates its pieces of the slot
+// order.  A traversal from body b visits a node iff b opened its parent (BHA:226-236), so a rank
+// needs the full subtree only where its bodies may open nodes:
+//   * own cells: the depth-P cells (P = LET_P) holding a body the rank evaluates;
+//   * the halo: every depth-P cell that some own cell's body might open -- cells farther away
+//     are accepted as a whole (BHA:228 holds for every body of every own cell, with a margin for
+//     jitter and rounding), so their children are never visited;
+//   * the subset = all bodies of own + halo cells (+ own bodies outside the tree): built with the
+//     ordinary pipeline (tree_build.hip); a depth-P cell's subtree depends only on its bodies
+//     (jitter replays stay inside depth-J cells), so those nodes are the full tree's, bit for bit;
+//   * the top (depth < P): a node's centre of mass is a function of its children's values
+//     (BHA:184-200), so every rank computes it from the depth-P cell values all ranks exchange
+//     (32 B per cell, one all-gather), and lays the tree out in pre-order: top nodes, local
+//     subtrees copied with shifted `next`, remote cells as childless records.
+// The traversal kernel then walks this array unchanged (traverse.hip), one lane per own body.
+// Jitter (BHA:146-151) mutates positions during the build: the lanes send x, y with their
+// accelerations, so every replica takes the owner's positions (let_kick*).
+#include <rocprim/device/device_scan.hpp>
+
+#include "bh_device.hpp"
+
+namespace bh {
+namespace {
+
+constexpr int TB = 256;
+inline unsigned grid_for(int64_t n) { return (unsigned)((n + TB - 1) / TB); }
+
+__device__ __forceinline__ uint32_t spread16(uint32_t v) {  // bit k -> bit 2k
+    v = (v | (v << 8)) & 0x00FF00FFu;
+    v = (v | (v << 4)) & 0x0F0F0F0Fu;
+    v = (v | (v << 2)) & 0x33333333u;
+    return (v | (v << 1)) & 0x55555555u;
+}
+__device__ __forceinline__ uint32_t compact16(uint32_t v) {  // bit 2k -> bit k
+    v &= 0x55555555u;
+    v = (v | (v >> 1)) & 0x33333333u;
+    v = (v | (v >> 2)) & 0x0F0F0F0Fu;
+    v = (v | (v >> 4)) & 0x00FF00FFu;
+    return (v | (v >> 8)) & 0x0000FFFFu;
+}
+
+// Column of p on the grid o + k w, clamped to [0, top]: exact for p inside (settled by the same
+// exact grid-line compares as k_morton); outside, the column of p's projection onto the root.
+__device__ __forceinline__ uint32_t grid_col(double p, double o, double w, uint32_t top) {
+    const double q = (p - o) / w;
+    int64_t c;
+    if (!(q >= 0.0)) c = 0;
+    else if (q >= (double)top) c = top;
+    else c = (int64_t)q;
+    if (c > 0 && p < o + (double)c * w) --c;
+    else if (c < (int64_t)top && p >= o + (double)(c + 1) * w) ++c;
+    return (uint32_t)c;
+}
+
+__device__ __forceinline__ bool in_root(const Geometry &g, double x, double y) {  // BHA:61-62
+    return x >= g.root_cx - g.root_h && x < g.root_cx + g.root_h && y >= g.root_cy - g.root_h &&
+           y < g.root_cy + g.root_h;
+}
+
+__device__ __forceinline__ uint32_t cell_of(const Geometry &g, double x, double y) {
+    const double w = 2.0 * g.h[LET_P];
+    const uint32_t top = (1u << LET_P) - 1;
+    return spread16(grid_col(x, g.root_cx - g.root_h, w, top)) |
+           (spread16(grid_col(y, g.root_cy - g.root_h, w, top)) << 1);
+}
+
+
+// Cell centre at depth d of cell index i (BHA:73-81 applied d times, as tree_build's cell_centre).
+__device__ void cell_centre_at(const Geometry &g, uint32_t i, int d, double &cx, double &cy) {
+    cx = g.root_cx;
+    cy = g.root_cy;
+    for (int l = 0; l < d; ++l) {
+        const uint32_t digit = (i >> (2 * (d - 1 - l))) & 3u;
+        const double hh = g.h[l + 1];
+        cx = (digit & 1u) ? cx + hh : cx - hh;
+        cy = (digit & 2u) ? cy + hh : cy - hh;
+    }
+}
+
+__host__ __device__ constexpr int64_t level_off(int d) { return (((int64_t)1 << (2 * d)) - 1) / 3; }
+
+// ---- selection ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t own_lane(const LetPieces &pc, int64_t t) {  // t-th own lane
+    return ((t / pc.sub) * pc.world + pc.rank) * pc.sub + t % pc.sub;
+}
+
+__global__ __launch_bounds__(TB) void k_let_mark(LetPieces pc, const double *__restrict__ x,
+                                                 const double *__restrict__ y,
+                                                 const uint32_t *__restrict__ cidx, Geometry g,
+                                                 uint8_t *__restrict__ own,
+                                                 uint8_t *__restrict__ ecell,
+                                                 uint32_t *__restrict__ flag_all) {
+    const int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (t >= (int64_t)pc.rounds * pc.sub) return;
+    const int64_t q = own_lane(pc, t);
+    if (q >= pc.n) return;
+    const int64_t i = pc.lanes ? (int64_t)pc.lanes[q] : q;
+    own[i] = 1;
+    if (cidx[i] & CIDX_DEAD) return;  // tombstones do not walk
+    const double px = x[i], py = y[i];
+    if (!__builtin_isfinite(px) || !__builtin_isfinite(py)) {
+        *flag_all = 1u;
+        return;
+    }
+    ecell[cell_of(g, px, py)] = 1;  // outside the root: the cell of the projection
+}
+
+// A cell is built locally iff some own cell lies within gap^2 <= gap2 cells of it (gap =
+// whole cells between the two squares per axis).
+__global__ __launch_bounds__(TB) void k_let_halo(const uint8_t *__restrict__ ecell,
+                                                 const uint32_t *__restrict__ flag_all,
+                                                 double gap2, int K,
+                                                 uint8_t *__restrict__ hcell) {
+    const int64_t c = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (c >= LET_CELLS) return;
+    uint8_t h = (*flag_all != 0u) ? 1 : ecell[c];
+    const int ix = (int)compact16((uint32_t)c), iy = (int)compact16((uint32_t)c >> 1);
+    const int top = (1 << LET_P) - 1;
+    for (int dy = -K; dy <= K && !h; ++dy) {
+        const int ny = iy + dy;
+        if (ny < 0 || ny > top) continue;
+        const int gy = abs(dy) > 0 ? abs(dy) - 1 : 0;
+        for (int dx = -K; dx <= K; ++dx) {
+            const int nx = ix + dx;
+            if (nx < 0 || nx > top) continue;
+            const int gx = abs(dx) > 0 ? abs(dx) - 1 : 0;
+            if ((double)(gx * gx + gy * gy) > gap2) continue;
+            if (ecell[spread16((uint32_t)nx) | (spread16((uint32_t)ny) << 1)]) {
+                h = 1;
+                break;
+            }
+        }
+    }
+    hcell[c] = h;
+}
+
+__global__ __launch_bounds__(TB) void k_let_flags(LetPieces pc, const double *__restrict__ x,
+                                                  const double *__restrict__ y,
+                                                  const uint32_t *__restrict__ cidx, Geometry g,
+                                                  const uint8_t *__restrict__ hcell,
+                                                  const uint8_t *__restrict__ own,
+                                                  uint32_t *__restrict__ sel) {
+    const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i > pc.n) return;
+    if (i == pc.n) {
+        sel[i] = 0u;
+        return;
+    }
+    const double px = x[i], py = y[i];
+    uint32_t f;
+    if (!(cidx[i] & CIDX_DEAD) && in_root(g, px, py)) f = hcell[cell_of(g, px, py)];
+    else f = own[i];  // own bodies outside the tree still walk it (or idle)
+    sel[i] = f;
+}
+
+__global__ __launch_bounds__(TB) void k_let_gather(int64_t n, const uint32_t *__restrict__ sel,
+                                                   const uint32_t *__restrict__ pos,
+                                                   BodyState st, BodyState sub) {
+    const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= n || !sel[i]) return;
+    const uint32_t j = pos[i];
+    sub.x[j] = st.x[i];
+    sub.y[j] = st.y[i];
+    sub.vx[j] = __longlong_as_double((long long)i);  // payload: the replicated slot
+    sub.vy[j] = 0.0;
+    sub.m[j] = st.m[i];
+    sub.cidx[j] = st.cidx[i];
+}
+
+// ---- after the subset build ----------------------------------------------------------------
+__global__ __launch_bounds__(TB) void k_let_cells(int64_t n, int J,
+                                                  const uint64_t *__restrict__ keys_s,
+                                                  uint32_t *__restrict__ cstart) {
+    const int64_t bin = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (bin > LET_CELLS) return;
+    const int shift = 2 * (J - LET_P);
+    int64_t lo = 0, hi = n;  // first sorted index with (key >> shift) >= bin (sentinel: 4^P)
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)(keys_s[mid] >> shift) < bin) lo = mid + 1; else hi = mid;
+    }
+    cstart[bin] = (uint32_t)lo;
+}
+
+// depth-P node of a cell with >= 2 subset bodies starting at sorted a: the internal nodes whose
+// first body is a are depths c(a-1)+1 .. c(a) at base[a] + (depth - c(a-1) - 1) (k_prep)
+__device__ __forceinline__ uint32_t cell_node(const TreeBuffers &tb, uint32_t a) {
+    const int cp = a > 0 ? (int)tb.cpl[a - 1] : -1;
+    return tb.base[a] + (uint32_t)(LET_P - cp - 1);
+}
+
+__global__ __launch_bounds__(TB) void k_let_table(LetBufs L, TreeBuffers tb) {
+    const int64_t c = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (c >= LET_CELLS) return;
+    LetCell r{0.0, 0.0, 0.0, 0u, 0u};
+    if (L.ecell[c]) {
+        const uint32_t a = L.cstart[c], cn = L.cstart[c + 1] - a;
+        r.tag = 1u;
+        if (cn == 1) {
+            r.comX = tb.dst.x[a];
+            r.comY = tb.dst.y[a];
+            r.mass = tb.dst.m[a];
+            r.cnt = 1u;
+        } else if (cn >= 2) {
+            const Node nd = tb.nodes[cell_node(tb, a)];
+            r.comX = nd.comX;
+            r.comY = nd.comY;
+            r.mass = nd.mass;
+            r.cnt = 2u;
+        }
+    }
+    L.table[c] = r;
+}
+
+__global__ __launch_bounds__(TB) void k_let_combine(int world, const LetCell *__restrict__ tables,
+                                                    LetCell *__restrict__ lev) {
+    const int64_t c = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (c >= LET_CELLS) return;
+    LetCell r{0.0, 0.0, 0.0, 0u, 0u};
+    for (int q = 0; q < world; ++q) {
+        const LetCell t = tables[(int64_t)q * LET_CELLS + c];
+        if (t.tag) {
+            r = t;
+            break;
+        }
+    }
+    r.tag = r.cnt == 1u ? (uint32_t)c : 0u;
+    lev[c] = r;
+}
+
+// one level of the top, d < P, from level d + 1: computeMass (BHA:184-200) over the children in
+// order 0..3 with the mass > 0 filter; a one-body cell passes its body through (a leaf).
+__global__ __launch_bounds__(TB) void k_let_level(int d, Geometry g, const LetCell *__restrict__ ch,
+                                                  LetCell *__restrict__ lev) {
+    const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= ((int64_t)1 << (2 * d))) return;
+    LetCell c[4];
+    uint32_t total = 0;
+    for (int q = 0; q < 4; ++q) {
+        c[q] = ch[4 * i + q];
+        total += c[q].cnt;
+    }
+    LetCell r{0.0, 0.0, 0.0, 0u, 0u};
+    if (total == 1u) {
+        for (int q = 0; q < 4; ++q)
+            if (c[q].cnt) r = c[q];
+    } else if (total >= 2u) {
+        double mSum = 0.0, cx = 0.0, cy = 0.0;
+        for (int q = 0; q < 4; ++q) {
+            if (c[q].mass > 0.0) {
+                mSum += c[q].mass;
+                cx += c[q].comX * c[q].mass;
+                cy += c[q].comY * c[q].mass;
+            }
+        }
+        r.mass = mSum;
+        if (mSum > 0.0) {
+            r.comX = cx / mSum;
+            r.comY = cy / mSum;
+        } else {
+            cell_centre_at(g, (uint32_t)i, d, r.comX, r.comY);
+        }
+        r.cnt = 2u;
+    }
+    lev[i] = r;
+}
+
+__device__ __forceinline__ bool node_exists(const LetCell *__restrict__ levels, int d, uint32_t i) {
+    if (levels[level_off(d) + i].cnt == 0u) return false;
+    return d == 0 || levels[level_off(d - 1) + (i >> 2)].cnt >= 2u;
+}
+
+// nodes per depth-P cell: its own node(s) (a locally built subtree, or one record) plus the
+// top nodes whose cell range starts at it; pre-order = order of (first cell, depth).
+__global__ __launch_bounds__(TB) void k_let_w(LetBufs L, TreeBuffers tb) {
+    const int64_t c = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (c > LET_CELLS) return;
+    if (c == LET_CELLS) {
+        L.w[c] = 0u;
+        return;
+    }
+    uint32_t bs = 0;
+    if (node_exists(L.levels, LET_P, (uint32_t)c)) {
+        if (L.levels[level_off(LET_P) + c].cnt >= 2u && L.hcell[c]) {
+            const uint32_t ni = cell_node(tb, L.cstart[c]);
+            bs = tb.nodes[ni].next - ni;
+        } else {
+            bs = 1u;
+        }
+    }
+    uint32_t anc = 0;
+    for (int d = 0; d < LET_P; ++d) {
+        const int sh = 2 * (LET_P - d);
+        if (((uint64_t)c & ((1ull << sh) - 1)) == 0 && node_exists(L.levels, d, (uint32_t)(c >> sh)))
+            ++anc;
+    }
+    L.bsz[c] = bs;
+    L.w[c] = bs + anc;
+}
+
+__device__ __forceinline__ uint32_t leaf_slot(const LetBufs &L, uint32_t bc) {
+    // the body of a one-body cell: its subset slot if the cell was built here (self-skip,
+    // BHA:219), else a slot no local body has
+    return L.hcell[bc] ? L.cstart[bc] : NODE_BODY_MASK;
+}
+
+__global__ __launch_bounds__(TB) void k_let_write_top(LetBufs L) {
+    int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (t >= level_off(LET_P)) return;
+    int d = 0;
+    while (t >= ((int64_t)1 << (2 * d))) {
+        t -= (int64_t)1 << (2 * d);
+        ++d;
+    }
+    const uint32_t i = (uint32_t)t;
+    if (!node_exists(L.levels, d, i)) return;
+    const int sh = 2 * (LET_P - d);
+    uint32_t pos = L.posc[(uint64_t)i << sh];
+    for (int d2 = 0; d2 < d; ++d2) {  // ancestors that start at the same cell come first
+        const int s2 = 2 * (d - d2);
+        if ((i & ((1u << s2) - 1u)) == 0u && node_exists(L.levels, d2, i >> s2)) ++pos;
+    }
+    const LetCell v = L.levels[level_off(d) + i];
+    Node nd;
+    nd.comX = v.comX;
+    nd.comY = v.comY;
+    nd.mass = v.mass;
+    if (v.cnt >= 2u) {
+        nd.next = L.posc[((uint64_t)i + 1) << sh];
+        nd.meta = (uint32_t)(2 * d) | (v.mass > 0.0 ? 0u : NODE_SKIP);
+    } else {
+        nd.next = pos + 1;
+        nd.meta = NODE_LEAF | leaf_slot(L, v.tag) | (v.mass == 0.0 ? NODE_SKIP : 0u);
+    }
+    L.nodes[pos] = nd;
+}
+
+// one wave per depth-P cell: the local subtree (next shifted to the new positions), or one record
+__global__ __launch_bounds__(TB) void k_let_write_cells(LetBufs L, TreeBuffers tb) {
+    const int64_t c = (int64_t)blockIdx.x * (TB / 64) + threadIdx.x / 64;
+    const uint32_t lane = threadIdx.x & 63u;
+    if (c >= LET_CELLS) return;
+    const uint32_t bs = L.bsz[c];
+    if (bs == 0u) return;
+    const uint32_t pos = L.posc[c + 1] - bs;
+    const LetCell v = L.levels[level_off(LET_P) + c];
+    if (v.cnt >= 2u && L.hcell[c]) {
+        const uint32_t ni = cell_node(tb, L.cstart[c]);
+        for (uint32_t k = lane; k < bs; k += 64u) {
+            Node nd = tb.nodes[ni + k];
+            nd.next = nd.next - ni + pos;
+            L.nodes[pos + k] = nd;
+        }
+    } else if (lane == 0) {
+        Node nd;
+        nd.comX = v.comX;
+        nd.comY = v.comY;
+        nd.mass = v.mass;
+        nd.next = pos + 1;
+        if (v.cnt >= 2u)  // accepted by every local body: never opened
+            nd.meta = (uint32_t)(2 * LET_P) | (v.mass > 0.0 ? 0u : NODE_SKIP);
+        else
+            nd.meta = NODE_LEAF | leaf_slot(L, (uint32_t)c) | (v.mass == 0.0 ? NODE_SKIP : 0u);
+        L.nodes[pos] = nd;
+    }
+}
+
+__global__ __launch_bounds__(TB) void k_let_subpos(int64_t n_sub, int64_t n,
+                                                   const double *__restrict__ rep,
+                                                   uint32_t *__restrict__ subpos) {
+    const int64_t s = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (s >= n_sub) return;
+    const int64_t i = (int64_t)__double_as_longlong(rep[s]);
+    if (i >= 0 && i < n) subpos[i] = (uint32_t)s;
+}
+
+// own lane -> subset slot of its body
+__global__ __launch_bounds__(TB) void k_let_lanes(LetPieces pc, const uint32_t *__restrict__ subpos,
+                                                  uint32_t *__restrict__ lanes) {
+    const int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (t >= (int64_t)pc.rounds * pc.sub) return;
+    const int64_t q = own_lane(pc, t);
+    if (q >= pc.n) return;
+    lanes[q] = subpos[pc.lanes ? (int64_t)pc.lanes[q] : q];
+}
+
+typedef double double4_t __attribute__((ext_vector_type(4)));
+
+// BHA:410-422 with the owner's (possibly jittered) position: x = x_b + v dt
+__global__ __launch_bounds__(TB) void k_let_kick_drift(int64_t n, const double *__restrict__ a4,
+                                                       double *__restrict__ x,
+                                                       double *__restrict__ y,
+                                                       double *__restrict__ vx,
+                                                       double *__restrict__ vy, double dtHalf,
+                                                       double dt,
+                                                       const uint32_t *__restrict__ lanes) {
+    const int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (q >= n) return;
+    const double4_t a = *reinterpret_cast<const double4_t *>(a4 + 4 * q);
+    const int64_t i = lanes ? (int64_t)lanes[q] : q;
+    const double vxi = vx[i] + a.x * dtHalf;
+    const double vyi = vy[i] + a.y * dtHalf;
+    vx[i] = vxi;
+    vy[i] = vyi;
+    x[i] = a.z + vxi * dt;
+    y[i] = a.w + vyi * dt;
+}
+
+// BHA:429-432; positions = the owner's after the build
+__global__ __launch_bounds__(TB) void k_let_kick(int64_t n, const double *__restrict__ a4,
+                                                 double *__restrict__ x, double *__restrict__ y,
+                                                 double *__restrict__ vx, double *__restrict__ vy,
+                                                 double dtHalf, const uint32_t *__restrict__ lanes) {
+    const int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (q >= n) return;
+    const double4_t a = *reinterpret_cast<const double4_t *>(a4 + 4 * q);
+    const int64_t i = lanes ? (int64_t)lanes[q] : q;
+    vx[i] = vx[i] + a.x * dtHalf;
+    vy[i] = vy[i] + a.y * dtHalf;
+    x[i] = a.z;
+    y[i] = a.w;
+}
+
+}  // namespace
+
+double let_include_gap2(const Geometry &g, double theta2, double soft2) {
+    if (!(theta2 > 0.0) || g.J <= LET_P + 1) return -1.0;
+    // a cell at distance D from the own bodies is accepted by all of them when
+    // theta2 * ((D - m)^2 + soft2) >= s2_P (1 + 1e-6): m covers jitter (<= 2e-3 per axis) and the
+    // rounding of centres of mass; the criterion's own rounding is far inside the 1e-6
+    const double w = 2.0 * g.h[LET_P], m = 0.01;
+    const double q = g.s2[LET_P] * (1.0 + 1e-6) / theta2 - soft2;
+    const double r = (m + std::sqrt(q > 0.0 ? q : 0.0)) / w;
+    const double gap2 = r * r;
+    return gap2 > 16.0 * 16.0 ? -1.0 : gap2;  // a halo this wide: the replicated build
+}
+
+size_t let_scratch_bytes(int64_t n) {
+    size_t a = 0, b = 0;
+    (void)rocprim::exclusive_scan(nullptr, a, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u,
+                                  (size_t)(n + 1), rocprim::plus<uint32_t>());
+    (void)rocprim::exclusive_scan(nullptr, b, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u,
+                                  (size_t)(LET_CELLS + 1), rocprim::plus<uint32_t>());
+    return a > b ? a : b;
+}
+
+hipError_t let_select(const BodyState &st, const Geometry &g, const LetPieces &pc, double gap2,
+                      const LetBufs &L, const BodyState &sub, hipStream_t s) {
+    hipError_t e = hipMemsetAsync(L.ecell, 0, LET_CELLS, s);
+    if (e == hipSuccess) e = hipMemsetAsync(L.flag_all, 0, sizeof(uint32_t), s);
+    if (e == hipSuccess && pc.n > 0) e = hipMemsetAsync(L.own, 0, (size_t)pc.n, s);
+    if (e != hipSuccess) return e;
+    const int64_t marks = (int64_t)pc.rounds * pc.sub;
+    if (marks > 0 && pc.n > 0)
+        k_let_mark<<<grid_for(marks), TB, 0, s>>>(pc, st.x, st.y, st.cidx, g, L.own, L.ecell,
+                                                  L.flag_all);
+    const int K = (int)std::floor(std::sqrt(gap2 > 0.0 ? gap2 : 0.0)) + 1;
+    k_let_halo<<<grid_for(LET_CELLS), TB, 0, s>>>(L.ecell, L.flag_all, gap2, K, L.hcell);
+    k_let_flags<<<grid_for(pc.n + 1), TB, 0, s>>>(pc, st.x, st.y, st.cidx, g, L.hcell, L.own,
+                                                   L.sel);
+    size_t bytes = L.scratch_bytes;
+    e = rocprim::exclusive_scan(L.scratch, bytes, L.sel, L.selpos, 0u, (size_t)(pc.n + 1),
+                                rocprim::plus<uint32_t>(), s);
+    if (e != hipSuccess) return e;
+    if (pc.n > 0) k_let_gather<<<grid_for(pc.n), TB, 0, s>>>(pc.n, L.sel, L.selpos, st, sub);
+    return hipGetLastError();
+}
+
+hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const TreeBuffers &tb,
+                     hipStream_t s) {
+    k_let_cells<<<grid_for(LET_CELLS + 1), TB, 0, s>>>(n_sub, g.J, tb.keys_s, L.cstart);
+    k_let_table<<<grid_for(LET_CELLS), TB, 0, s>>>(L, tb);
+    return hipGetLastError();
+}
+
+hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, const LetBufs &L,
+                        const TreeBuffers &tb, hipStream_t s) {
+    k_let_combine<<<grid_for(LET_CELLS), TB, 0, s>>>(pc.world, L.tables, L.levels + level_off(LET_P));
+    for (int d = LET_P - 1; d >= 0; --d)
+        k_let_level<<<grid_for((int64_t)1 << (2 * d)), TB, 0, s>>>(
+            d, g, L.levels + level_off(d + 1), L.levels + level_off(d));
+    k_let_w<<<grid_for(LET_CELLS + 1), TB, 0, s>>>(L, tb);
+    size_t bytes = L.scratch_bytes;
+    hipError_t e = rocprim::exclusive_scan(L.scratch, bytes, L.w, L.posc, 0u,
+                                           (size_t)(LET_CELLS + 1), rocprim::plus<uint32_t>(), s);
+    if (e != hipSuccess) return e;
+    k_let_write_top<<<grid_for(level_off(LET_P)), TB, 0, s>>>(L);
+    k_let_write_cells<<<(unsigned)(LET_CELLS / (TB / 64)), TB, 0, s>>>(L, tb);
+    // every own slot is in the subset (its cell is an own cell, or it is listed as own); the
+    // clear only keeps a broken invariant from indexing outside the subset
+    e = hipMemsetAsync(L.subpos, 0, sizeof(uint32_t) * (size_t)pc.n, s);
+    if (e != hipSuccess) return e;
+    if (n_sub > 0) k_let_subpos<<<grid_for(n_sub), TB, 0, s>>>(n_sub, pc.n, tb.dst.vx, L.subpos);
+    const int64_t own_lanes = (int64_t)pc.rounds * pc.sub;
+    if (own_lanes > 0 && pc.n > 0)
+        k_let_lanes<<<grid_for(own_lanes), TB, 0, s>>>(pc, L.subpos, L.lanes);
+    return hipGetLastError();
+}
+
+void let_kick_drift(int64_t n, const double *a4, double *x, double *y, double *vx, double *vy,
+                    double dtHalf, double dt, hipStream_t s, const uint32_t *lanes) {
+    if (n > 0) k_let_kick_drift<<<grid_for(n), TB, 0, s>>>(n, a4, x, y, vx, vy, dtHalf, dt, lanes);
+}
+
+void let_kick(int64_t n, const double *a4, double *x, double *y, double *vx, double *vy,
+              double dtHalf, hipStream_t s, const uint32_t *lanes) {
+    if (n > 0) k_let_kick<<<grid_for(n), TB, 0, s>>>(n, a4, x, y, vx, vy, dtHalf, lanes);
+}
+
+}  // namespace bh

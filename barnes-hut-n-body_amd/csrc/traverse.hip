@@ -214,6 +214,14 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     acc.y = fy / bm;
     if (KICK == KICK_NONE) {  // by lane with a lane map (the multi-GPU pieces stay contiguous)
         *reinterpret_cast<double2_t *>(a2 + 2 * q) = acc;
+    } else if (KICK == KICK_POS) {  // multi-rank LET: the position the build left, for the peers
+        typedef double double4_t __attribute__((ext_vector_type(4)));
+        double4_t o;
+        o.x = acc.x;
+        o.y = acc.y;
+        o.z = bx;
+        o.w = by;
+        *reinterpret_cast<double4_t *>(a2 + 4 * q) = o;
     } else {  // k_kick_drift / k_kick (integrate.hip), operation for operation
         const double vxi = kick.vx[p] + acc.x * kick.dtHalf;
         const double vyi = kick.vy[p] + acc.y * kick.dtHalf;
@@ -300,10 +308,12 @@ void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x
     } else if (off32) {
         if (ka.mode == KICK_DRIFT) BH_TRAV(false, true, KICK_DRIFT);
         else if (ka.mode == KICK_ONLY) BH_TRAV(false, true, KICK_ONLY);
+        else if (ka.mode == KICK_POS) BH_TRAV(false, true, KICK_POS);
         else BH_TRAV(false, true, KICK_NONE);
     } else {
         if (ka.mode == KICK_DRIFT) BH_TRAV(false, false, KICK_DRIFT);
         else if (ka.mode == KICK_ONLY) BH_TRAV(false, false, KICK_ONLY);
+        else if (ka.mode == KICK_POS) BH_TRAV(false, false, KICK_POS);
         else BH_TRAV(false, false, KICK_NONE);
     }
 #undef BH_TRAV

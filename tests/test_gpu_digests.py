@@ -60,21 +60,23 @@ def test_c5_all_accelerations_digest():
 
 def test_c4_eight_rank_group_digest():
     """The north-star configuration's decomposition: C4 (1e7 bodies) on 8 in-process ranks
-    (bh_create_local; each rank evaluates its 4 Morton pieces, the pieces are gathered in
-    place), 10 steps: every rank's full state has the oracle's digest."""
+    (bh_create_local; each rank builds the locally essential tree of its 4 Morton pieces and
+    evaluates them, the pieces are gathered in place), 10 steps: every rank's full state has
+    the oracle's digest."""
     want = DIGESTS["c4_k10"]
     world = 8
     arrs = scenes.config_scene(want["scene"])
     group = bh_amd.LocalGroup(world)
     engines = [bh_amd.Engine(bh_amd.default_params(theta=want["theta"]), device=0, rank=r,
                              local_group=group) for r in range(world)]
-    results, errors = [None] * world, []
+    results, stats, errors = [None] * world, [None] * world, []
 
     def run(r):
         try:
             engines[r].reset_bodies(*arrs)
             engines[r].step(want["steps"])
             results[r] = engines[r].get_bodies()
+            stats[r] = engines[r].let_stats()
         except Exception as exc:  # surfaced below
             errors.append(exc)
 
@@ -87,6 +89,10 @@ def test_c4_eight_rank_group_digest():
     assert not any(t.is_alive() for t in threads), "rank thread hung"
     for r in range(world):
         _check_state(results[r], want, f"rank {r}")
+        # the sharded build ran: 18 of the 20 builds are locally essential trees over a part of
+        # the cloud (the first build sorts the caller's order, the last of the call is full)
+        assert stats[r]["let_builds"] == 18 and stats[r]["full_builds"] == 2, stats[r]
+        assert stats[r]["subset"] < want["n"] // 3, stats[r]
     for e in engines:
         e.close()
     group.close()

@@ -671,6 +671,67 @@ def test_multi_rank_decomposition_in_process(world):
         ref.close()
 
 
+def _run_group(world, params, arrs, calls):
+    """Every rank of an in-process group: reset, then bh_step(k) for k in calls; states."""
+    import threading
+    group = bh_amd.LocalGroup(world)
+    engines = [bh_amd.Engine(params, device=0, rank=r, local_group=group) for r in range(world)]
+    results, stats, errors = [None] * world, [None] * world, []
+
+    def run(r):
+        try:
+            engines[r].reset_bodies(*arrs)
+            for k in calls:
+                engines[r].step(k)
+            results[r] = engines[r].get_bodies()
+            stats[r] = engines[r].let_stats()
+        except Exception as exc:  # surfaced below
+            errors.append(exc)
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors
+    assert not any(t.is_alive() for t in threads), "rank thread hung"
+    for e in engines:
+        e.close()
+    group.close()
+    return results, stats
+
+
+@pytest.mark.parametrize("world,scene,theta", [
+    (2, "c2", 0.5), (4, "c2", 0.3), (8, "c2", 1.0), (3, "disks", 0.5), (8, "cloud", 0.5),
+    (5, "cloud", 0.7)])
+def test_let_build_multi_rank_vs_single(world, scene, theta):
+    """The sharded build (let.hip): each rank builds only the cells its bodies can open plus the
+    top from the exchanged cell values, and its forces -- hence every rank's state -- equal the
+    single-GPU engine's bit for bit.  Two bh_step calls (the LET builds run in the middle of a
+    call; the last build of a call is the full tree)."""
+    arrs = {"c2": lambda: scenes.config_scene("c2"),
+            "disks": lambda: scenes.two_disks(60_000, 15_000),
+            "cloud": lambda: scenes.uniform(150_000, 0.5, seed=9)}[scene]()
+    params = bh_amd.default_params(theta=theta)
+    single = bh_amd.Engine(params, device=0)
+    single.reset_bodies(*arrs)
+    for k in (4, 3):
+        single.step(k)
+    want = single.get_bodies()
+    single.close()
+    got, stats = _run_group(world, params, arrs, (4, 3))
+    n = len(arrs[0])
+    for r in range(world):
+        # 8 + 6 builds: the first (caller order after the reset) and the last of each call
+        # are full, the other 11 are LET builds
+        assert stats[r]["let_builds"] == 11 and stats[r]["full_builds"] == 3, stats[r]
+        assert 0 < stats[r]["subset"] <= n and stats[r]["let_nodes"] > 0, stats[r]
+        if scene == "cloud" and world == 8:  # the shard: a fraction of the bodies is built
+            assert stats[r]["subset"] < n // 2, stats[r]
+        for k, name in enumerate(FIELDS):
+            assert bits_equal(got[r][k], want[k]), f"rank {r}: {name}"
+
+
 def test_checkpoint_resume_bit_identical(tmp_path):
     """bh_save_state after 6 steps of a merge-active two-disk scene, bh_load_state into a fresh
     engine, 6 more steps: bit-identical to 12 uninterrupted steps and to the oracle; the file
