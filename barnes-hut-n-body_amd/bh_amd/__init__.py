@@ -43,7 +43,7 @@ EXPORTED_SYMBOLS = (
     "bh_nbody3d_create", "bh_nbody3d_destroy", "bh_nbody3d_last_error", "bh_nbody3d_set",
     "bh_nbody3d_step", "bh_nbody3d_accelerations", "bh_nbody3d_get", "bh_nbody3d_last_ms",
     "bh_local_group_create", "bh_local_group_destroy", "bh_create_local",
-    "bh_save_state", "bh_load_state", "bh_let_stats",
+    "bh_save_state", "bh_load_state", "bh_let_stats", "bh_create_solo",
 )
 
 
@@ -94,6 +94,8 @@ def load_library(path: str | None = None):
     lib.bh_local_group_destroy.restype = None
     lib.bh_create_local.argtypes = [ctypes.POINTER(BhParams), ctypes.c_int, ctypes.c_int, _VP,
                                     ctypes.POINTER(_VP)]
+    lib.bh_create_solo.argtypes = [ctypes.POINTER(BhParams), ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.POINTER(_VP)]
     lib.bh_destroy.argtypes = [_VP]
     lib.bh_destroy.restype = None
     lib.bh_last_error.argtypes = [_VP]
@@ -278,11 +280,14 @@ class Engine:
 
     def __init__(self, params: BhParams | None = None, device: int = 0, rank: int = 0,
                  world: int = 1, unique_id: bytes | None = None,
-                 local_group: "LocalGroup | None" = None):
+                 local_group: "LocalGroup | None" = None, solo: bool = False):
         self._lib = load_library()
         self._h = _VP()
         self.params = params if params is not None else default_params()
-        if local_group is not None:
+        if solo:  # measurement: one rank's share of a `world`-rank step, alone (bh_create_solo)
+            rc = self._lib.bh_create_solo(ctypes.byref(self.params), device, rank, world,
+                                          ctypes.byref(self._h))
+        elif local_group is not None:
             world = local_group.world
             rc = self._lib.bh_create_local(ctypes.byref(self.params), device, rank,
                                            local_group._h, ctypes.byref(self._h))

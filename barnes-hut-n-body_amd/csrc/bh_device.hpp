@@ -252,6 +252,9 @@ void let_kick_drift(int64_t n, const double *a4, double *x, double *y, double *v
                     double dtHalf, double dt, hipStream_t s, const uint32_t *lanes);
 void let_kick(int64_t n, const double *a4, double *x, double *y, double *vx, double *vy,
               double dtHalf, hipStream_t s, const uint32_t *lanes);
+// bh_create_solo (measurement): every lane (0, 0, x, y) before the own pieces are evaluated
+void let_fill_idle(int64_t n, const uint32_t *lanes, const double *x, const double *y, double *a4,
+                   hipStream_t s);
 
 // ---- launchers (direct.hip): theta = 0 all-pairs ---------------------------------
 // Non-empty leaves of the last tree in pre-order (the reference's theta = 0 summation order).

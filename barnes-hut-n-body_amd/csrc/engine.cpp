@@ -173,6 +173,11 @@ struct bh_engine {
     bh::SpanSlot *s_span_children = nullptr;
     Node *s_nodes = nullptr;
     hipEvent_t table_ev = nullptr;
+    // bh_create_solo (measurement): no peers; their cells' values from the last full build
+    bool solo = false;
+    LetCell *solo_table = nullptr;
+    uint8_t *solo_all = nullptr;    // every cell marked
+    uint32_t *solo_cstart = nullptr;
 
     // profiling
     bool profiling = false;
@@ -281,11 +286,11 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(alloc_state(e, e->st, cap));
         TRY(alloc_state(e, e->alt, cap));
         // multi-GPU: rounds x world pieces of whole wavefronts (bh_shard_range)
-        const int64_t padded = (e->comm || e->group) ? shard_sub(cap, e->world, BH_SHARD_ROUNDS) *
+        const int64_t padded = (e->comm || e->group || e->solo) ? shard_sub(cap, e->world, BH_SHARD_ROUNDS) *
                                              e->world * BH_SHARD_ROUNDS
                                        : cap;
         // multi-rank: (ax, ay, x, y) per slot for the LET evaluation
-        TRY(dev_alloc(e, e->a2, ((e->comm || e->group) ? 4 : 2) * padded));
+        TRY(dev_alloc(e, e->a2, ((e->comm || e->group || e->solo) ? 4 : 2) * padded));
         TRY(dev_alloc(e, e->ax, cap));
         TRY(dev_alloc(e, e->ay, cap));
         TRY(dev_alloc(e, e->keys, cap));
@@ -435,6 +440,21 @@ int build(bh_engine *e) {
     e->spl_nb = sort_buckets(n);  // k_prep wrote this build's splitters
     if (n > 0) std::swap(e->st, e->alt);
     e->st_morton = true;
+    if (e->solo && n > 0 && e->p.theta != 0.0) {  // the peers' cell values for later LET builds
+        if (!e->solo_table) {
+            TRY(dev_alloc(e, e->solo_table, LET_CELLS));
+            TRY(dev_alloc(e, e->solo_all, LET_CELLS));
+            TRY(dev_alloc(e, e->solo_cstart, LET_CELLS + 1));
+            HIPCHK(e, hipMemset(e->solo_all, 1, LET_CELLS));
+        }
+        LetBufs Ls{};
+        Ls.ecell = e->solo_all;
+        Ls.cstart = e->solo_cstart;
+        Ls.table = e->solo_table;
+        TreeBuffers tm = tree_buffers(e);
+        tm.dst = e->st;  // the sorted state
+        HIPCHK(e, let_table(n, e->geo, Ls, tm, e->stream));
+    }
     e->tree_valid = true;
     return BH_OK;
 }
@@ -603,6 +623,13 @@ int evaluate_let(bh_engine *e, bool *done) {
     const size_t tbytes = sizeof(LetCell) * (size_t)LET_CELLS;
     if (e->comm) {
         NCCLCHK(e, ncclAllGather(e->L.table, e->L.tables, tbytes, ncclUint8, e->comm, e->stream));
+    } else if (e->solo) {  // own values first, the rest from the last full build
+        HIPCHK(e, hipMemsetAsync(e->L.tables, 0, tbytes * (size_t)e->world, e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->L.tables, e->L.table, tbytes, hipMemcpyDeviceToDevice,
+                                 e->stream));
+        if (e->world > 1 && e->solo_table)
+            HIPCHK(e, hipMemcpyAsync(e->L.tables + LET_CELLS, e->solo_table, tbytes,
+                                     hipMemcpyDeviceToDevice, e->stream));
     } else {
         HIPCHK(e, hipEventRecord(e->table_ev, e->stream));
         e->group->barrier();
@@ -617,6 +644,7 @@ int evaluate_let(bh_engine *e, bool *done) {
     TRY(mark(e, 0));
     const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};
     const KickArgs ka{KICK_POS, nullptr, nullptr, 0.0, 0.0};
+    if (e->solo) let_fill_idle(n, lanes, e->st.x, e->st.y, e->a2, e->stream);
     for (int k = 0; k < R; ++k) {
         int64_t lo = 0, hi = 0;
         bh_shard_range(n, e->rank, e->world, k, &lo, &hi);
@@ -630,7 +658,7 @@ int evaluate_let(bh_engine *e, bool *done) {
         if (e->comm) {
             NCCLCHK(e, ncclAllGather(piece + 4 * e->rank * sub, piece, (size_t)(4 * sub),
                                      ncclDouble, e->comm, e->comm_stream));
-        } else {
+        } else if (e->group) {
             e->group->barrier();
             for (int q = 0; q < e->world; ++q) {
                 if (q == e->rank) continue;
@@ -660,7 +688,7 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
     e->a2_pos = false;
     // (the pieces are ranges of the slot order: spatially compact only once a full build has
     // put the state into Morton order -- after a reset it is the caller's order)
-    if (allow_let && !visits && (e->comm || e->group) && e->let_on && e->p.theta != 0.0 &&
+    if (allow_let && !visits && (e->comm || e->group || e->solo) && e->let_on && e->p.theta != 0.0 &&
         e->st_morton && e->let_age < BH_LET_REFRESH) {
         bool done = false;
         TRY(evaluate_let(e, &done));
@@ -695,7 +723,7 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
             traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, e->st.cidx, lo, hi, e->geo, fp,
                      e->a2, vis ? &counters : nullptr, e->stream, nullptr, lanes);
     };
-    if ((!e->comm && !e->group) || visits) {
+    if ((!e->comm && !e->group && !e->solo) || visits) {
         if (BH_FUSE_KICK && kick != KICK_NONE && !direct && !visits && fused) {
             const KickArgs ka{kick, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
             traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, e->st.cidx, 0, n, e->geo, fp,
@@ -709,6 +737,10 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
         return BH_OK;
     }
     const int64_t sub = shard_sub(n, e->world, BH_SHARD_ROUNDS);
+    if (e->solo)  // measurement: the peers' bodies get no force
+        HIPCHK(e, hipMemsetAsync(e->a2, 0, sizeof(double) * 2 * (size_t)(sub * e->world *
+                                                                         BH_SHARD_ROUNDS),
+                                 e->stream));
     if (e->group) {  // a collective's implicit ordering: peers' copies of our last pieces done
         e->group->barrier();
         for (bh_engine *peer : e->group->members)
@@ -725,7 +757,7 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
         if (e->comm) {
             NCCLCHK(e, ncclAllGather(piece + 2 * e->rank * sub, piece, (size_t)(2 * sub),
                                      ncclDouble, e->comm, e->comm_stream));
-        } else {  // in-process: every member recorded round k, then copy the peers' pieces
+        } else if (e->group) {  // in-process: every member recorded round k, then copy the peers' pieces
             e->group->barrier();
             for (int q = 0; q < e->world; ++q) {
                 if (q == e->rank) continue;
@@ -1148,6 +1180,38 @@ int bh_create_local(const bh_params *p, int device, int rank, bh_local_group *gr
     return BH_OK;
 }
 
+int bh_create_solo(const bh_params *p, int device, int rank, int world, bh_engine **out) {
+    if (!out || world < 1 || rank < 0 || rank >= world) return BH_E_INVALID;
+    *out = nullptr;
+    bh_engine *e = new bh_engine();
+    e->rank = rank;
+    e->world = world;
+    int rc = engine_init(e, p, device);
+    if (rc == BH_OK) {
+        hipError_t hr = hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking);
+        for (int k = 0; k < BH_SHARD_ROUNDS && hr == hipSuccess; ++k)
+            hr = hipEventCreateWithFlags(&e->round_ev[k], hipEventDisableTiming);
+        if (hr == hipSuccess) hr = hipEventCreateWithFlags(&e->gathered_ev, hipEventDisableTiming);
+        if (hr != hipSuccess) {
+            e->err = std::string("comm stream/events: ") + hipGetErrorString(hr);
+            rc = BH_E_DEVICE;
+        }
+    }
+    if (rc == BH_OK) {
+        e->solo = true;
+        const int64_t cap = e->cap;  // the pieces buffer in rounds x world pieces
+        e->cap = 0;
+        rc = ensure_capacity(e, cap);
+    }
+    if (rc != BH_OK) {
+        std::fprintf(stderr, "bh_create_solo: %s\n", e->err.c_str());
+        bh_destroy(e);
+        return rc;
+    }
+    *out = e;
+    return BH_OK;
+}
+
 void bh_destroy(bh_engine *e) {
     if (!e) return;
     (void)hipSetDevice(e->device);
@@ -1166,7 +1230,7 @@ void bh_destroy(bh_engine *e) {
     free_state(e->sub_src);
     free_state(e->sub_dst);
     if (e->table_ev) (void)hipEventDestroy(e->table_ev);
-    void *lets[] = {e->L.ecell, e->L.hcell, e->L.own, e->L.subpos, e->L.flag_all, e->L.sel, e->L.selpos, e->L.cstart,
+    void *lets[] = {e->solo_table, e->solo_all, e->solo_cstart, e->L.ecell, e->L.hcell, e->L.own, e->L.subpos, e->L.flag_all, e->L.sel, e->L.selpos, e->L.cstart,
                     e->L.table, e->L.tables, e->L.levels, e->L.w, e->L.posc, e->L.bsz,
                     e->L.nodes, e->L.lanes, e->s_keys, e->s_keys_s, e->s_spl, e->s_keys32,
                     e->s_keys32_s, e->s_idx, e->s_perm, e->s_cpl, e->s_cnt, e->s_base,

@@ -425,7 +425,27 @@ __global__ __launch_bounds__(TB) void k_let_kick(int64_t n, const double *__rest
     y[i] = a.w;
 }
 
+__global__ __launch_bounds__(TB) void k_let_fill_idle(int64_t n, const uint32_t *__restrict__ lanes,
+                                                      const double *__restrict__ x,
+                                                      const double *__restrict__ y,
+                                                      double *__restrict__ a4) {
+    const int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (q >= n) return;
+    const int64_t i = lanes ? (int64_t)lanes[q] : q;
+    double4_t o;
+    o.x = 0.0;
+    o.y = 0.0;
+    o.z = x[i];
+    o.w = y[i];
+    *reinterpret_cast<double4_t *>(a4 + 4 * q) = o;
+}
+
 }  // namespace
+
+void let_fill_idle(int64_t n, const uint32_t *lanes, const double *x, const double *y, double *a4,
+                   hipStream_t s) {
+    if (n > 0) k_let_fill_idle<<<grid_for(n), TB, 0, s>>>(n, lanes, x, y, a4);
+}
 
 double let_include_gap2(const Geometry &g, double theta2, double soft2) {
     if (!(theta2 > 0.0) || g.J <= LET_P + 1) return -1.0;

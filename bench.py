@@ -6,9 +6,11 @@ colliding galaxy disks (NBodyPanel.kt:83-100 scaled: 8e5 + 2e5 bodies, seeds 1/2
 dt 0.005, G 80, eps^2 1, merge rule on.  One step = the full reference step: two tree builds,
 two force evaluations, kick-drift-kick, merge.  Inputs are resident in HBM before timing.
 
-Multi-GPU (torchrun, one rank per GPU): weak scaling — each rank adds 1e6 bodies to the same
-two-disk geometry (c3x<N>), state is replicated, force evaluation is sharded over ranks by
-Morton range and accelerations are all-gathered by RCCL over xGMI inside the engine.
+Multi-GPU (torchrun, one rank per GPU): the north-star configuration C4 (1e7-body uniform cloud,
+total fixed: strong scaling; `--config c3x` = weak scaling, 1e6 two-disk bodies per GPU).  The
+state is replicated; each rank builds a locally essential tree (only the cells its bodies can
+open, plus the top from every rank's cell values), evaluates its Hilbert-ordered pieces, and
+the (ax, ay, x, y) pieces are all-gathered by RCCL over xGMI inside the engine.
 
 Prints ONE JSON line on rank 0 (see the driver contract in the task statement).
 """
@@ -238,6 +240,7 @@ def main():
     per_rank = None
     if world > 1:
         mine = {k: round(v / max(args.steps, 1), 3) for k, v in phases.items()}
+        mine["let"] = eng.let_stats()  # sharded builds: LET / full builds, subset, LET nodes
         gathered = [None] * world
         dist.all_gather_object(gathered, mine)
         per_rank = gathered
@@ -375,7 +378,8 @@ def main():
                 "soft2": params.soft2,
                 "root": "2400x800",
                 "evals_per_step": 2,
-                "parallelism": f"replicated state, force sharded x{world} (RCCL all-gather)"
+                "parallelism": f"replicated state, build sharded as locally essential trees, "
+                               f"force sharded x{world} (RCCL all-gather)"
                 if world > 1 else "single GPU",
             },
             "phase_ms": {k: round(v, 3) for k, v in phases.items()},

@@ -76,6 +76,14 @@ void bh_local_group_destroy(bh_local_group *g);  /* after its members' bh_destro
 int bh_create_local(const bh_params *p, int device, int rank, bh_local_group *group,
                     bh_engine **out);
 
+/* Measurement only: rank `rank` of a `world`-rank engine running alone on one device -- the
+ * rank's own work of a multi-GPU step (its locally essential tree builds, the traversal of its
+ * pieces, the integration of every body) without peers and without the exchange: the peers'
+ * bodies get zero acceleration and the cell values of the peers' cells come from the last
+ * full build.  Times one GPU's share of the north-star decomposition on a single GPU; the
+ * results are NOT the reference's. */
+int bh_create_solo(const bh_params *p, int device, int rank, int world, bh_engine **out);
+
 void bh_destroy(bh_engine *e);
 const char *bh_last_error(const bh_engine *e);
 
