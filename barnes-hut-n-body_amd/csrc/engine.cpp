@@ -76,6 +76,10 @@ struct bh_engine {
     ncclComm_t comm = nullptr;
     bh_local_group *group = nullptr;             // in-process ranks (test path), or RCCL:
     hipStream_t comm_stream = nullptr;            // all-gathers, overlapping the next round
+    // odd rounds' traversals: at 8 ranks a round is under one dispatch generation of waves, so
+    // consecutive rounds run concurrently on two streams instead of each waiting for the tail
+    hipStream_t stream2 = nullptr;
+    hipEvent_t built_ev = nullptr;
     hipEvent_t round_ev[BH_SHARD_ROUNDS] = {};   // round k's forces written (compute stream)
     hipEvent_t gathered_ev = nullptr;            // every round gathered (comm stream)
 
@@ -585,6 +589,17 @@ TreeBuffers let_tree_buffers(bh_engine *e) {
     return b;
 }
 
+// Stream of round k (even: the engine's stream; odd: stream2, started after the build).
+int round_streams(bh_engine *e) {
+    if (!e->stream2) {
+        HIPCHK(e, hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
+        HIPCHK(e, hipEventCreateWithFlags(&e->built_ev, hipEventDisableTiming));
+    }
+    HIPCHK(e, hipEventRecord(e->built_ev, e->stream));
+    HIPCHK(e, hipStreamWaitEvent(e->stream2, e->built_ev, 0));
+    return BH_OK;
+}
+
 // One LET evaluation; *done = false when it does not apply (the caller builds the full tree).
 int evaluate_let(bh_engine *e, bool *done) {
     *done = false;
@@ -645,14 +660,16 @@ int evaluate_let(bh_engine *e, bool *done) {
     const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};
     const KickArgs ka{KICK_POS, nullptr, nullptr, 0.0, 0.0};
     if (e->solo) let_fill_idle(n, lanes, e->st.x, e->st.y, e->a2, e->stream);
+    TRY(round_streams(e));
     for (int k = 0; k < R; ++k) {
         int64_t lo = 0, hi = 0;
         bh_shard_range(n, e->rank, e->world, k, &lo, &hi);
+        hipStream_t rs = (k & 1) ? e->stream2 : e->stream;
         traverse(e->L.nodes, e->let_node_cap, e->L.posc + LET_CELLS, e->sub_dst.x, e->sub_dst.y,
-                 e->sub_dst.m, e->sub_dst.cidx, lo, hi, e->geo, fp, e->a2, nullptr, e->stream,
+                 e->sub_dst.m, e->sub_dst.cidx, lo, hi, e->geo, fp, e->a2, nullptr, rs,
                  &ka, e->L.lanes);
         HIPCHK(e, hipGetLastError());
-        HIPCHK(e, hipEventRecord(e->round_ev[k], e->stream));
+        HIPCHK(e, hipEventRecord(e->round_ev[k], rs));
         HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
         double *piece = e->a2 + 4 * ((int64_t)k * e->world) * sub;  // round k, rank 0
         if (e->comm) {
@@ -715,13 +732,13 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
     const TraverseCounters counters{visits, e->contrib32, e->wave_iters, e->wave_blocks};
     const uint32_t *lanes = e->lanes_valid ? e->lanes : nullptr;  // [lo, hi): lane ranges
     e->a2_lanes = direct ? nullptr : lanes;
-    auto forces = [&](int64_t lo, int64_t hi, uint32_t *vis) {
+    auto forces = [&](int64_t lo, int64_t hi, uint32_t *vis, hipStream_t fs) {
         if (direct)
             direct_forces(e->leaves, e->leaf_count, e->st.x, e->st.y, e->st.m, lo, hi, fp.G,
-                          fp.soft2, e->a2, e->stream);
+                          fp.soft2, e->a2, fs);
         else
             traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, e->st.cidx, lo, hi, e->geo, fp,
-                     e->a2, vis ? &counters : nullptr, e->stream, nullptr, lanes);
+                     e->a2, vis ? &counters : nullptr, fs, nullptr, lanes);
     };
     if ((!e->comm && !e->group && !e->solo) || visits) {
         if (BH_FUSE_KICK && kick != KICK_NONE && !direct && !visits && fused) {
@@ -730,7 +747,7 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
                      e->a2, nullptr, e->stream, &ka, lanes);
             *fused = true;
         } else {
-            forces(0, n, visits);
+            forces(0, n, visits, e->stream);
         }
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
@@ -746,12 +763,14 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
         for (bh_engine *peer : e->group->members)
             if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->gathered_ev, 0));
     }
+    TRY(round_streams(e));
     for (int k = 0; k < BH_SHARD_ROUNDS; ++k) {
         int64_t lo = 0, hi = 0;
         bh_shard_range(n, e->rank, e->world, k, &lo, &hi);
-        forces(lo, hi, nullptr);
+        hipStream_t rs = (k & 1) ? e->stream2 : e->stream;
+        forces(lo, hi, nullptr, rs);
         HIPCHK(e, hipGetLastError());
-        HIPCHK(e, hipEventRecord(e->round_ev[k], e->stream));
+        HIPCHK(e, hipEventRecord(e->round_ev[k], rs));
         HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
         double *piece = e->a2 + 2 * ((int64_t)k * e->world) * sub;  // round k, rank 0
         if (e->comm) {
@@ -1224,6 +1243,11 @@ void bh_destroy(bh_engine *e) {
         if (ev) (void)hipEventDestroy(ev);
     if (e->gathered_ev) (void)hipEventDestroy(e->gathered_ev);
     if (e->comm_stream) (void)hipStreamDestroy(e->comm_stream);
+    if (e->stream2) {
+        (void)hipStreamSynchronize(e->stream2);
+        (void)hipStreamDestroy(e->stream2);
+    }
+    if (e->built_ev) (void)hipEventDestroy(e->built_ev);
     free_state(e->st);
     free_state(e->alt);
     free_state(e->snap);
