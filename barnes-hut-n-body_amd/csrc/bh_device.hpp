@@ -228,6 +228,7 @@ struct LetBufs {
     LetCell *table, *tables;  // own exchange table, all ranks' tables [world][LET_CELLS]
     LetCell *levels;          // depths 0..LET_P, level d at ((4^d - 1) / 3)
     uint32_t *w, *posc, *bsz; // [LET_CELLS + 1] nodes per cell, their scan, block sizes
+    uint32_t *csrc, *ccnt, *cpos;  // [LET_CELLS + 1] local block: first subset node, nodes, scan
     Node *nodes;              // the assembled tree, pre-order
     uint32_t *lanes;          // [n] lane -> subset slot (own pieces)
     void *scratch;

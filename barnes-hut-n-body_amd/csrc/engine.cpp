@@ -521,6 +521,9 @@ int let_alloc(bh_engine *e, int64_t n_sub) {
         TRY(dev_alloc(e, L.w, LET_CELLS + 1));
         TRY(dev_alloc(e, L.posc, LET_CELLS + 1));
         TRY(dev_alloc(e, L.bsz, LET_CELLS + 1));
+        TRY(dev_alloc(e, L.csrc, LET_CELLS + 1));
+        TRY(dev_alloc(e, L.ccnt, LET_CELLS + 1));
+        TRY(dev_alloc(e, L.cpos, LET_CELLS + 1));
         TRY(dev_alloc(e, L.lanes, cap));
         TRY(dev_alloc(e, L.own, cap));
         TRY(dev_alloc(e, L.subpos, cap));
@@ -1254,7 +1257,7 @@ void bh_destroy(bh_engine *e) {
     free_state(e->sub_src);
     free_state(e->sub_dst);
     if (e->table_ev) (void)hipEventDestroy(e->table_ev);
-    void *lets[] = {e->solo_table, e->solo_all, e->solo_cstart, e->L.ecell, e->L.hcell, e->L.own, e->L.subpos, e->L.flag_all, e->L.sel, e->L.selpos, e->L.cstart,
+    void *lets[] = {e->L.csrc, e->L.ccnt, e->L.cpos, e->solo_table, e->solo_all, e->solo_cstart, e->L.ecell, e->L.hcell, e->L.own, e->L.subpos, e->L.flag_all, e->L.sel, e->L.selpos, e->L.cstart,
                     e->L.table, e->L.tables, e->L.levels, e->L.w, e->L.posc, e->L.bsz,
                     e->L.nodes, e->L.lanes, e->s_keys, e->s_keys_s, e->s_spl, e->s_keys32,
                     e->s_keys32_s, e->s_idx, e->s_perm, e->s_cpl, e->s_cnt, e->s_base,

@@ -19,6 +19,9 @@
 // The traversal kernel then walks this array unchanged (traverse.hip), one lane per own body.
 // Jitter (BHA:146-151) mutates positions during the build: the lanes send x, y with their
 // accelerations, so every replica takes the owner's positions (let_kick*).
+#include <algorithm>
+#include <cmath>
+
 #include <rocprim/device/device_scan.hpp>
 
 #include "bh_device.hpp"
@@ -46,7 +49,7 @@ __device__ __forceinline__ uint32_t compact16(uint32_t v) {  // bit 2k -> bit k
 // Column of p on the grid o + k w, clamped to [0, top]: exact for p inside (settled by the same
 // exact grid-line compares as k_morton); outside, the column of p's projection onto the root.
 __device__ __forceinline__ uint32_t grid_col(double p, double o, double w, uint32_t top) {
-    const double q = (p - o) / w;
+    const double q = (p - o) * (1.0 / w);  // off by at most one: settled below
     int64_t c;
     if (!(q >= 0.0)) c = 0;
     else if (q >= (double)top) c = top;
@@ -138,6 +141,7 @@ __global__ __launch_bounds__(TB) void k_let_halo(const uint8_t *__restrict__ ece
     hcell[c] = h;
 }
 
+// the subset: bodies of built cells, and own bodies outside the tree (they still walk it, or idle)
 __global__ __launch_bounds__(TB) void k_let_flags(LetPieces pc, const double *__restrict__ x,
                                                   const double *__restrict__ y,
                                                   const uint32_t *__restrict__ cidx, Geometry g,
@@ -153,7 +157,7 @@ __global__ __launch_bounds__(TB) void k_let_flags(LetPieces pc, const double *__
     const double px = x[i], py = y[i];
     uint32_t f;
     if (!(cidx[i] & CIDX_DEAD) && in_root(g, px, py)) f = hcell[cell_of(g, px, py)];
-    else f = own[i];  // own bodies outside the tree still walk it (or idle)
+    else f = own[i];
     sel[i] = f;
 }
 
@@ -216,34 +220,11 @@ __global__ __launch_bounds__(TB) void k_let_table(LetBufs L, TreeBuffers tb) {
     L.table[c] = r;
 }
 
-__global__ __launch_bounds__(TB) void k_let_combine(int world, const LetCell *__restrict__ tables,
-                                                    LetCell *__restrict__ lev) {
-    const int64_t c = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (c >= LET_CELLS) return;
-    LetCell r{0.0, 0.0, 0.0, 0u, 0u};
-    for (int q = 0; q < world; ++q) {
-        const LetCell t = tables[(int64_t)q * LET_CELLS + c];
-        if (t.tag) {
-            r = t;
-            break;
-        }
-    }
-    r.tag = r.cnt == 1u ? (uint32_t)c : 0u;
-    lev[c] = r;
-}
-
-// one level of the top, d < P, from level d + 1: computeMass (BHA:184-200) over the children in
-// order 0..3 with the mass > 0 filter; a one-body cell passes its body through (a leaf).
-__global__ __launch_bounds__(TB) void k_let_level(int d, Geometry g, const LetCell *__restrict__ ch,
-                                                  LetCell *__restrict__ lev) {
-    const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (i >= ((int64_t)1 << (2 * d))) return;
-    LetCell c[4];
+// computeMass (BHA:184-200) of a top node from its 4 children in order 0..3 with the mass > 0
+// filter; a one-body cell passes its body through (a leaf).
+__device__ LetCell let_parent(const LetCell *c, int d, uint32_t i, const Geometry &g) {
     uint32_t total = 0;
-    for (int q = 0; q < 4; ++q) {
-        c[q] = ch[4 * i + q];
-        total += c[q].cnt;
-    }
+    for (int q = 0; q < 4; ++q) total += c[q].cnt;
     LetCell r{0.0, 0.0, 0.0, 0u, 0u};
     if (total == 1u) {
         for (int q = 0; q < 4; ++q)
@@ -262,11 +243,66 @@ __global__ __launch_bounds__(TB) void k_let_level(int d, Geometry g, const LetCe
             r.comX = cx / mSum;
             r.comY = cy / mSum;
         } else {
-            cell_centre_at(g, (uint32_t)i, d, r.comX, r.comY);
+            cell_centre_at(g, i, d, r.comX, r.comY);
         }
         r.cnt = 2u;
     }
-    lev[i] = r;
+    return r;
+}
+
+// Depths LET_P .. 4 of one depth-4 cell per workgroup (256 depth-8 cells): the exchanged values
+// (first rank that provided the cell), then the levels up, in LDS.
+static_assert(LET_P == 8, "k_let_top_hi assumes 256 depth-LET_P cells per depth-4 cell");
+__global__ __launch_bounds__(256) void k_let_top_hi(int world, Geometry g,
+                                                    const LetCell *__restrict__ tables,
+                                                    LetCell *__restrict__ levels) {
+    __shared__ LetCell sh[256];
+    const uint32_t b = blockIdx.x, t = threadIdx.x;
+    {
+        const uint32_t c = b * 256u + t;
+        LetCell r{0.0, 0.0, 0.0, 0u, 0u};
+        for (int q = 0; q < world; ++q) {
+            const LetCell v = tables[(int64_t)q * LET_CELLS + c];
+            if (v.tag) {
+                r = v;
+                break;
+            }
+        }
+        r.tag = r.cnt == 1u ? c : 0u;
+        levels[level_off(LET_P) + c] = r;
+        sh[t] = r;
+    }
+    __syncthreads();
+    uint32_t width = 64;  // this workgroup's nodes at depth d
+    for (int d = LET_P - 1; d >= 4; --d, width >>= 2) {
+        LetCell r{};
+        if (t < width) {
+            r = let_parent(sh + 4 * t, d, b * width + t, g);
+            levels[level_off(d) + b * width + t] = r;
+        }
+        __syncthreads();
+        if (t < width) sh[t] = r;  // the level becomes the next level's children
+        __syncthreads();
+    }
+}
+
+// Depths 3 .. 0 (85 nodes) by one workgroup from depth 4.
+__global__ __launch_bounds__(256) void k_let_top_lo(Geometry g, LetCell *__restrict__ levels) {
+    __shared__ LetCell sh[256];
+    const uint32_t t = threadIdx.x;
+    sh[t] = levels[level_off(4) + t];
+    __syncthreads();
+    uint32_t width = 64;
+    for (int d = 3; d >= 0; --d, width >>= 2) {
+        LetCell r{};
+        if (t < width) {
+            r = let_parent(sh + 4 * t, d, t, g);
+            levels[level_off(d) + t] = r;
+        }
+        __syncthreads();
+        if (t < width) sh[t] = r;
+        __syncthreads();
+    }
 }
 
 __device__ __forceinline__ bool node_exists(const LetCell *__restrict__ levels, int d, uint32_t i) {
@@ -281,17 +317,20 @@ __global__ __launch_bounds__(TB) void k_let_w(LetBufs L, TreeBuffers tb) {
     if (c > LET_CELLS) return;
     if (c == LET_CELLS) {
         L.w[c] = 0u;
+        L.ccnt[c] = 0u;
         return;
     }
-    uint32_t bs = 0;
+    uint32_t bs = 0, copy = 0, ni = 0;
     if (node_exists(L.levels, LET_P, (uint32_t)c)) {
         if (L.levels[level_off(LET_P) + c].cnt >= 2u && L.hcell[c]) {
-            const uint32_t ni = cell_node(tb, L.cstart[c]);
-            bs = tb.nodes[ni].next - ni;
+            ni = cell_node(tb, L.cstart[c]);
+            bs = copy = tb.nodes[ni].next - ni;
         } else {
             bs = 1u;
         }
     }
+    L.csrc[c] = ni;
+    L.ccnt[c] = copy;
     uint32_t anc = 0;
     for (int d = 0; d < LET_P; ++d) {
         const int sh = 2 * (LET_P - d);
@@ -339,33 +378,43 @@ __global__ __launch_bounds__(TB) void k_let_write_top(LetBufs L) {
     L.nodes[pos] = nd;
 }
 
-// one wave per depth-P cell: the local subtree (next shifted to the new positions), or one record
-__global__ __launch_bounds__(TB) void k_let_write_cells(LetBufs L, TreeBuffers tb) {
-    const int64_t c = (int64_t)blockIdx.x * (TB / 64) + threadIdx.x / 64;
-    const uint32_t lane = threadIdx.x & 63u;
+// one record per depth-P cell that is not copied: a remote internal cell (accepted by every local
+// body: never opened) or a one-body leaf
+__global__ __launch_bounds__(TB) void k_let_write_cells(LetBufs L) {
+    const int64_t c = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (c >= LET_CELLS) return;
     const uint32_t bs = L.bsz[c];
-    if (bs == 0u) return;
-    const uint32_t pos = L.posc[c + 1] - bs;
+    if (bs != 1u || L.ccnt[c] != 0u) return;
+    const uint32_t pos = L.posc[c + 1] - 1u;
     const LetCell v = L.levels[level_off(LET_P) + c];
-    if (v.cnt >= 2u && L.hcell[c]) {
-        const uint32_t ni = cell_node(tb, L.cstart[c]);
-        for (uint32_t k = lane; k < bs; k += 64u) {
-            Node nd = tb.nodes[ni + k];
-            nd.next = nd.next - ni + pos;
-            L.nodes[pos + k] = nd;
+    Node nd;
+    nd.comX = v.comX;
+    nd.comY = v.comY;
+    nd.mass = v.mass;
+    nd.next = pos + 1;
+    if (v.cnt >= 2u)
+        nd.meta = (uint32_t)(2 * LET_P) | (v.mass > 0.0 ? 0u : NODE_SKIP);
+    else
+        nd.meta = NODE_LEAF | leaf_slot(L, (uint32_t)c) | (v.mass == 0.0 ? NODE_SKIP : 0u);
+    L.nodes[pos] = nd;
+}
+
+// the locally built subtrees, one thread per node (grid-stride over cpos[LET_CELLS] nodes): node t
+// of the concatenated blocks belongs to the cell c with cpos[c] <= t < cpos[c + 1]; its `next`
+// moves with the block
+__global__ __launch_bounds__(TB) void k_let_copy_blocks(LetBufs L, const Node *__restrict__ src) {
+    const uint32_t total = L.cpos[LET_CELLS];
+    for (uint32_t t = blockIdx.x * TB + threadIdx.x; t < total; t += gridDim.x * TB) {
+        uint32_t lo = 0, hi = (uint32_t)LET_CELLS;  // largest c with cpos[c] <= t
+        while (hi - lo > 1) {
+            const uint32_t mid = (lo + hi) >> 1;
+            if (L.cpos[mid] <= t) lo = mid; else hi = mid;
         }
-    } else if (lane == 0) {
-        Node nd;
-        nd.comX = v.comX;
-        nd.comY = v.comY;
-        nd.mass = v.mass;
-        nd.next = pos + 1;
-        if (v.cnt >= 2u)  // accepted by every local body: never opened
-            nd.meta = (uint32_t)(2 * LET_P) | (v.mass > 0.0 ? 0u : NODE_SKIP);
-        else
-            nd.meta = NODE_LEAF | leaf_slot(L, (uint32_t)c) | (v.mass == 0.0 ? NODE_SKIP : 0u);
-        L.nodes[pos] = nd;
+        const uint32_t c = lo, k = t - L.cpos[c];
+        const uint32_t ni = L.csrc[c], dst = L.posc[c + 1] - L.bsz[c];
+        Node nd = src[ni + k];
+        nd.next = nd.next - ni + dst;
+        L.nodes[dst + k] = nd;
     }
 }
 
@@ -379,13 +428,17 @@ __global__ __launch_bounds__(TB) void k_let_subpos(int64_t n_sub, int64_t n,
 }
 
 // own lane -> subset slot of its body
-__global__ __launch_bounds__(TB) void k_let_lanes(LetPieces pc, const uint32_t *__restrict__ subpos,
+__global__ __launch_bounds__(TB) void k_let_lanes(LetPieces pc, uint32_t n_sub,
+                                                  const uint32_t *__restrict__ subpos,
                                                   uint32_t *__restrict__ lanes) {
     const int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (t >= (int64_t)pc.rounds * pc.sub) return;
     const int64_t q = own_lane(pc, t);
     if (q >= pc.n) return;
-    lanes[q] = subpos[pc.lanes ? (int64_t)pc.lanes[q] : q];
+    // every own body is in the subset (its cell is an own cell, or it is listed as own); the
+    // clamp only keeps a broken invariant inside the subset
+    const uint32_t s = subpos[pc.lanes ? (int64_t)pc.lanes[q] : q];
+    lanes[q] = s < n_sub ? s : 0u;
 }
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
@@ -465,7 +518,7 @@ size_t let_scratch_bytes(int64_t n) {
                                   (size_t)(n + 1), rocprim::plus<uint32_t>());
     (void)rocprim::exclusive_scan(nullptr, b, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u,
                                   (size_t)(LET_CELLS + 1), rocprim::plus<uint32_t>());
-    return a > b ? a : b;
+    return std::max(a, b);
 }
 
 hipError_t let_select(const BodyState &st, const Geometry &g, const LetPieces &pc, double gap2,
@@ -499,25 +552,24 @@ hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const T
 
 hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, const LetBufs &L,
                         const TreeBuffers &tb, hipStream_t s) {
-    k_let_combine<<<grid_for(LET_CELLS), TB, 0, s>>>(pc.world, L.tables, L.levels + level_off(LET_P));
-    for (int d = LET_P - 1; d >= 0; --d)
-        k_let_level<<<grid_for((int64_t)1 << (2 * d)), TB, 0, s>>>(
-            d, g, L.levels + level_off(d + 1), L.levels + level_off(d));
+    k_let_top_hi<<<256, 256, 0, s>>>(pc.world, g, L.tables, L.levels);
+    k_let_top_lo<<<1, 256, 0, s>>>(g, L.levels);
     k_let_w<<<grid_for(LET_CELLS + 1), TB, 0, s>>>(L, tb);
     size_t bytes = L.scratch_bytes;
     hipError_t e = rocprim::exclusive_scan(L.scratch, bytes, L.w, L.posc, 0u,
                                            (size_t)(LET_CELLS + 1), rocprim::plus<uint32_t>(), s);
     if (e != hipSuccess) return e;
-    k_let_write_top<<<grid_for(level_off(LET_P)), TB, 0, s>>>(L);
-    k_let_write_cells<<<(unsigned)(LET_CELLS / (TB / 64)), TB, 0, s>>>(L, tb);
-    // every own slot is in the subset (its cell is an own cell, or it is listed as own); the
-    // clear only keeps a broken invariant from indexing outside the subset
-    e = hipMemsetAsync(L.subpos, 0, sizeof(uint32_t) * (size_t)pc.n, s);
+    bytes = L.scratch_bytes;
+    e = rocprim::exclusive_scan(L.scratch, bytes, L.ccnt, L.cpos, 0u, (size_t)(LET_CELLS + 1),
+                                rocprim::plus<uint32_t>(), s);
     if (e != hipSuccess) return e;
+    k_let_write_top<<<grid_for(level_off(LET_P)), TB, 0, s>>>(L);
+    k_let_write_cells<<<grid_for(LET_CELLS), TB, 0, s>>>(L);
+    k_let_copy_blocks<<<2048, TB, 0, s>>>(L, tb.nodes);
     if (n_sub > 0) k_let_subpos<<<grid_for(n_sub), TB, 0, s>>>(n_sub, pc.n, tb.dst.vx, L.subpos);
     const int64_t own_lanes = (int64_t)pc.rounds * pc.sub;
     if (own_lanes > 0 && pc.n > 0)
-        k_let_lanes<<<grid_for(own_lanes), TB, 0, s>>>(pc, L.subpos, L.lanes);
+        k_let_lanes<<<grid_for(own_lanes), TB, 0, s>>>(pc, (uint32_t)n_sub, L.subpos, L.lanes);
     return hipGetLastError();
 }
 

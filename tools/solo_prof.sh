@@ -4,7 +4,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for let in 1 0; do
+for let in ${LETS:-1 0}; do
   BH_LET=$let timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/soloprof$let -o run \
     --output-format csv -- python3 tools/solo_rank.py --world 8 --rank 0 --steps 10 --warmup 2 \
     > gpurun_out/soloprof$let.log 2>&1
