@@ -701,18 +701,42 @@ def _run_group(world, params, arrs, calls):
     return results, stats
 
 
+def _let_scene(name):
+    if name == "c2":
+        return scenes.config_scene("c2")
+    if name == "disks":
+        return scenes.two_disks(60_000, 15_000)
+    if name == "cloud":
+        return scenes.uniform(150_000, 0.5, seed=9)
+    rng = np.random.default_rng(17)
+    x, y, vx, vy, m = (a.copy() for a in scenes.uniform(40_000, 0.5, seed=13))
+    if name == "jitter":  # coincident and < 1e-3 apart pairs: the build moves positions
+        dup = rng.choice(len(x), 300, replace=False)
+        near = rng.choice(len(x), 300, replace=False)
+        ex = np.concatenate([x[dup], x[near] + 3e-4])
+        ey = np.concatenate([y[dup], y[near] - 2e-4])
+    else:  # "outside": bodies around and far outside the root cell walk the tree too
+        ex = np.concatenate([rng.uniform(-900, -1, 60), rng.uniform(2403, 3500, 60),
+                             rng.uniform(0, 2400, 60), [1e7, -1e7]])
+        ey = np.concatenate([rng.uniform(-100, 900, 120), rng.uniform(-1500, -803, 60),
+                             [5.0, 5.0]])
+    k = len(ex)
+    arrs = (np.concatenate([x, ex]), np.concatenate([y, ey]), np.concatenate([vx, np.zeros(k)]),
+            np.concatenate([vy, np.zeros(k)]), np.concatenate([m, np.full(k, 0.5)]))
+    perm = rng.permutation(len(arrs[0]))
+    return tuple(a[perm] for a in arrs)
+
+
 @pytest.mark.parametrize("world,scene,theta", [
     (2, "c2", 0.5), (4, "c2", 0.3), (8, "c2", 1.0), (3, "disks", 0.5), (8, "cloud", 0.5),
-    (5, "cloud", 0.7)])
+    (5, "cloud", 0.7), (4, "jitter", 0.5), (3, "outside", 0.5)])
 def test_let_build_multi_rank_vs_single(world, scene, theta):
     """The sharded build (let.hip): each rank builds only the cells its bodies can open plus the
     top from the exchanged cell values, and its forces -- hence every rank's state -- equal the
     single-GPU engine's bit for bit.  Two bh_step calls (the LET builds run in the middle of a
     call; the last build of a call is the full tree)."""
-    arrs = {"c2": lambda: scenes.config_scene("c2"),
-            "disks": lambda: scenes.two_disks(60_000, 15_000),
-            "cloud": lambda: scenes.uniform(150_000, 0.5, seed=9)}[scene]()
-    params = bh_amd.default_params(theta=theta)
+    arrs = _let_scene(scene)
+    params = bh_amd.default_params(theta=theta, merge_min_dist=0.0 if scene == "jitter" else 8.0)
     single = bh_amd.Engine(params, device=0)
     single.reset_bodies(*arrs)
     for k in (4, 3):
