@@ -381,9 +381,10 @@ class Engine:
 
     def let_stats(self):
         """Multi-rank build sharding: LET builds, full builds, last subset size, last LET nodes."""
-        out = np.zeros(4, dtype=np.int64)
+        out = np.zeros(5, dtype=np.int64)
         self._check(self._lib.bh_let_stats(self._h, out.ctypes.data_as(_I64P)))
-        return dict(zip(("let_builds", "full_builds", "subset", "let_nodes"), out.tolist()))
+        return dict(zip(("let_builds", "full_builds", "subset", "let_nodes", "overflows"),
+                        out.tolist()))
 
     def set_profiling(self, on: bool):
         self._check(self._lib.bh_set_profiling(self._h, 1 if on else 0))

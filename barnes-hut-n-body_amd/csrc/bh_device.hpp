@@ -207,6 +207,8 @@ hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_ba
 // childless records every local body provably accepts.  See let.hip.
 constexpr int LET_P = 8;
 constexpr int64_t LET_CELLS = (int64_t)1 << (2 * LET_P);
+// an exchange table: LET_CELLS cell records + one status record (cnt = subset overflow)
+constexpr int64_t LET_TSTRIDE = LET_CELLS + 1;
 struct __attribute__((aligned(32))) LetCell {
     double comX, comY, mass;
     uint32_t cnt;  // in-tree bodies of the cell, saturated at 2 (0 empty, 1 leaf, 2 internal)
@@ -230,6 +232,7 @@ struct LetBufs {
     uint32_t *w, *posc, *bsz; // [LET_CELLS + 1] nodes per cell, their scan, block sizes
     uint32_t *csrc, *ccnt, *cpos;  // [LET_CELLS + 1] local block: first subset node, nodes, scan
     Node *nodes;              // the assembled tree, pre-order
+    uint32_t node_cap;        // records allocated for it (every write is bounded by it)
     uint32_t *lanes;          // [n] lane -> subset slot (own pieces)
     void *scratch;
     size_t scratch_bytes;
@@ -239,15 +242,19 @@ struct LetBufs {
 double let_include_gap2(const Geometry &g, double theta2, double soft2);
 size_t let_scratch_bytes(int64_t n);
 // own cells, halo, subset flags + scan + gather into `sub` (vx carries the replicated slot);
-// the subset size is then selpos[n] (read by the host)
+// the subset has selpos[n] bodies.  The build runs over a host-chosen capacity S without a host
+// round trip: `sub` is padded with dead bodies (sentinel keys: not in the tree) up to S, and
+// selpos[n] > S is an overflow (the status record of the table; scal[5] = max subset size)
 hipError_t let_select(const BodyState &st, const Geometry &g, const LetPieces &pc,
-                      double gap2, const LetBufs &L, const BodyState &sub, hipStream_t s);
+                      double gap2, const LetBufs &L, const BodyState &sub, int64_t S,
+                      uint32_t *scal, hipStream_t s);
 // after tree_build over the subset: the own cells' exchange table
 hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const TreeBuffers &tb,
                      hipStream_t s);
-// after the exchange (L.tables): top levels, layout, node array, lane map; tree size posc[LET_CELLS]
+// after the exchange (L.tables, LET_TSTRIDE per rank): any rank's overflow -> scal[4]; top
+// levels, layout, node array, lane map; tree size posc[LET_CELLS]
 hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, const LetBufs &L,
-                        const TreeBuffers &tb, hipStream_t s);
+                        const TreeBuffers &tb, uint32_t *scal, hipStream_t s);
 // KDK of all replicated slots from a2 = (ax, ay, x, y) per lane (BHA:410-432)
 void let_kick_drift(int64_t n, const double *a4, double *x, double *y, double *vx, double *vy,
                     double dtHalf, double dt, hipStream_t s, const uint32_t *lanes);

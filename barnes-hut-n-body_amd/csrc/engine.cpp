@@ -160,6 +160,9 @@ struct bh_engine {
     bool let_on = true;         // BH_LET=0 in the environment: the replicated build
     int let_age = 0;            // LET builds since the last full build
     int64_t let_builds = 0, full_builds = 0, let_last_sub = 0;
+    int64_t let_known = 0;       // largest subset of the last bh_step call (0: unknown)
+    int64_t let_overflows = 0;   // calls replayed for a subset overflow
+    uint32_t s_spl_nb = 0;       // splitters of the last LET build (subset bucket sort)
     bool st_morton = false;     // slots are in the Morton order of a full build (not caller order)
     bool a2_pos = false;        // the last evaluation wrote (ax, ay, x, y) per slot
     LetBufs L{};
@@ -446,7 +449,8 @@ int build(bh_engine *e) {
     e->st_morton = true;
     if (e->solo && n > 0 && e->p.theta != 0.0) {  // the peers' cell values for later LET builds
         if (!e->solo_table) {
-            TRY(dev_alloc(e, e->solo_table, LET_CELLS));
+            TRY(dev_alloc(e, e->solo_table, LET_TSTRIDE));
+            HIPCHK(e, hipMemset(e->solo_table, 0, sizeof(LetCell) * LET_TSTRIDE));
             TRY(dev_alloc(e, e->solo_all, LET_CELLS));
             TRY(dev_alloc(e, e->solo_cstart, LET_CELLS + 1));
             HIPCHK(e, hipMemset(e->solo_all, 1, LET_CELLS));
@@ -515,8 +519,8 @@ int let_alloc(bh_engine *e, int64_t n_sub) {
         TRY(dev_alloc(e, L.sel, cap + 1));
         TRY(dev_alloc(e, L.selpos, cap + 1));
         TRY(dev_alloc(e, L.cstart, LET_CELLS + 1));
-        TRY(dev_alloc(e, L.table, LET_CELLS));
-        TRY(dev_alloc(e, L.tables, (size_t)e->world * LET_CELLS));
+        TRY(dev_alloc(e, L.table, LET_TSTRIDE));
+        TRY(dev_alloc(e, L.tables, (size_t)e->world * LET_TSTRIDE));
         TRY(dev_alloc(e, L.levels, ((size_t)1 << (2 * LET_P + 2)) / 3 + 1));
         TRY(dev_alloc(e, L.w, LET_CELLS + 1));
         TRY(dev_alloc(e, L.posc, LET_CELLS + 1));
@@ -551,6 +555,7 @@ int let_alloc(bh_engine *e, int64_t n_sub) {
     TRY(dev_alloc(e, e->s_nodes, ncap));
     e->let_node_cap = ncap + 2 * (size_t)LET_CELLS + 64;
     TRY(dev_alloc(e, e->L.nodes, e->let_node_cap));
+    e->L.node_cap = (uint32_t)std::min<size_t>(e->let_node_cap, 0xFFFFFFF0u);
     TRY(dev_alloc(e, e->s_span_list, (size_t)(J + 2) * span_stride_for(sc)));
     TRY(dev_alloc(e, e->s_span_children, (size_t)(J + 2) * span_stride_for(sc)));
     TRY(dev_alloc(e, e->s_super_list, (size_t)(J + 2) * span_groups(span_stride_for(sc))));
@@ -558,6 +563,7 @@ int let_alloc(bh_engine *e, int64_t n_sub) {
     TRY(dev_alloc(e, e->s_bcount, (size_t)sort_buckets(sc) + 2));
     TRY(dev_alloc(e, e->s_bstart, (size_t)sort_buckets(sc) + 2));
     HIPCHK(e, hipMemset(e->s_bcount, 0, sizeof(uint32_t) * ((size_t)sort_buckets(sc) + 2)));
+    e->s_spl_nb = 0;
     e->let_sub_cap = sc;
     e->let_J = J;
     return BH_OK;
@@ -586,7 +592,9 @@ TreeBuffers let_tree_buffers(bh_engine *e) {
     b.scratch = e->scratch;
     b.scratch_bytes = e->scratch_bytes;
     b.spl = e->s_spl;
-    b.spl_nb = 0;  // a fresh subset every build: rocprim sort
+    // the subset is compacted from the Morton-ordered state, nearly sorted: the adaptive bucket
+    // sort with the previous LET build's splitters (any splitters partition correctly)
+    b.spl_nb = e->s_spl_nb;
     b.bcount = e->s_bcount;
     b.bstart = e->s_bstart;
     return b;
@@ -622,23 +630,29 @@ int evaluate_let(bh_engine *e, bool *done) {
             if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->gathered_ev, 0));
     }
     TRY(let_alloc(e, 0));
-    HIPCHK(e, let_select(e->st, e->geo, pc, gap2, e->L, e->sub_src, e->stream));
-    TRY(pinned_reserve(e, 64));
-    uint32_t *h = static_cast<uint32_t *>(e->pin);
-    HIPCHK(e, hipMemcpyAsync(h, e->L.selpos + n, sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    const int64_t n_sub = h[0];
-    if (n_sub > n) {
-        e->err = "LET subset larger than the state";
-        return BH_E_STATE;
+    // subset capacity: the largest subset of the previous call + headroom, no host round trip;
+    // a subset beyond it is an overflow every rank sees after the exchange, and bh_step replays
+    // the call with the observed size (the first LET build of an engine reads its size once)
+    // (the selection writes sub_src, sized for the whole state; padding up to S = n is harmless)
+    int64_t S = e->let_known > 0 ? std::min<int64_t>(n, e->let_known + e->let_known / 8 + 4096) : n;
+    HIPCHK(e, let_select(e->st, e->geo, pc, gap2, e->L, e->sub_src, S, e->scalars, e->stream));
+    if (e->let_known <= 0) {
+        TRY(pinned_reserve(e, 64));
+        uint32_t *h = static_cast<uint32_t *>(e->pin);
+        HIPCHK(e, hipMemcpyAsync(h, e->L.selpos + n, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                 e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        e->let_known = std::max<int64_t>(h[0], 1);
+        S = std::min<int64_t>(n, e->let_known + e->let_known / 8 + 4096);  // padded above
     }
-    TRY(let_alloc(e, n_sub));
-    e->let_last_sub = n_sub;
+    TRY(let_alloc(e, S));
+    const int64_t n_sub = S;  // padded: bodies past the real subset are dead
     ++e->let_builds;
     const TreeBuffers sb = let_tree_buffers(e);
     HIPCHK(e, tree_build(sb, n_sub, e->geo, e->stream));
+    e->s_spl_nb = sort_buckets(n_sub);  // k_prep wrote this build's splitters
     HIPCHK(e, let_table(n_sub, e->geo, e->L, sb, e->stream));
-    const size_t tbytes = sizeof(LetCell) * (size_t)LET_CELLS;
+    const size_t tbytes = sizeof(LetCell) * (size_t)LET_TSTRIDE;
     if (e->comm) {
         NCCLCHK(e, ncclAllGather(e->L.table, e->L.tables, tbytes, ncclUint8, e->comm, e->stream));
     } else if (e->solo) {  // own values first, the rest from the last full build
@@ -646,7 +660,7 @@ int evaluate_let(bh_engine *e, bool *done) {
         HIPCHK(e, hipMemcpyAsync(e->L.tables, e->L.table, tbytes, hipMemcpyDeviceToDevice,
                                  e->stream));
         if (e->world > 1 && e->solo_table)
-            HIPCHK(e, hipMemcpyAsync(e->L.tables + LET_CELLS, e->solo_table, tbytes,
+            HIPCHK(e, hipMemcpyAsync(e->L.tables + LET_TSTRIDE, e->solo_table, tbytes,
                                      hipMemcpyDeviceToDevice, e->stream));
     } else {
         HIPCHK(e, hipEventRecord(e->table_ev, e->stream));
@@ -654,11 +668,11 @@ int evaluate_let(bh_engine *e, bool *done) {
         for (int q = 0; q < e->world; ++q) {
             bh_engine *peer = e->group->members[q];
             if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->table_ev, 0));
-            HIPCHK(e, hipMemcpyAsync(e->L.tables + (size_t)q * LET_CELLS, peer->L.table, tbytes,
+            HIPCHK(e, hipMemcpyAsync(e->L.tables + (size_t)q * LET_TSTRIDE, peer->L.table, tbytes,
                                      hipMemcpyDeviceToDevice, e->stream));
         }
     }
-    HIPCHK(e, let_assemble(n_sub, e->geo, pc, e->L, sb, e->stream));
+    HIPCHK(e, let_assemble(n_sub, e->geo, pc, e->L, sb, e->scalars, e->stream));
     TRY(mark(e, 0));
     const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};
     const KickArgs ka{KICK_POS, nullptr, nullptr, 0.0, 0.0};
@@ -1343,15 +1357,40 @@ int bh_step(bh_engine *e, int32_t k) {
     if (!e || k < 0) return BH_E_INVALID;
     HIPCHK(e, hipSetDevice(e->device));
     const bool may_merge = k > 0 && e->n > 1 && e->p.merge_min_dist > 0.0 && e->heavy_possible;
-    if (may_merge) TRY(snapshot(e));
+    // a multi-rank call with LET builds may have to be replayed with a larger subset capacity
+    const bool may_let = k > 0 && e->n > 0 && (e->comm || e->group || e->solo) && e->let_on &&
+                         e->p.theta != 0.0;
+    if (may_merge || may_let) TRY(snapshot(e));
+    int let_replays = 0;
     for (;;) {
         e->ev_used = 0;
         e->timings_pending = false;
-        HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, 3 * sizeof(uint32_t), e->stream));
+        // the subset splitters are trusted only within a call (another scene after a reset
+        // would put most of a subset into one bucket): the first LET build sorts with rocprim
+        e->s_spl_nb = 0;
+        HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, 5 * sizeof(uint32_t), e->stream));
         e->removed.clear();
         e->merge_ran = false;
         for (int32_t s = 0; s < k; ++s) TRY(step_once(e, s + 1 == k));
         HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (may_let) {  // LET subset sizes of this call: [4] some rank overflowed, [5] largest
+            uint32_t ls[2] = {0, 0};
+            HIPCHK(e, hipMemcpy(ls, e->scalars + 4, sizeof(ls), hipMemcpyDeviceToHost));
+            if (ls[1] > 0) {
+                e->let_last_sub = ls[1];
+                e->let_known = std::max<int64_t>(ls[1], ls[0] ? e->let_known : 1);
+            }
+            if (ls[0]) {  // every rank saw the overflow (exchanged): all replay the call
+                // (the builds after an overflow saw a damaged state, so a replay can meet a
+                // larger subset than observed; the third replay builds subsets of any size)
+                if (++let_replays >= 3) e->let_known = e->n;
+                ++e->let_overflows;
+                e->removed.clear();
+                e->merge_ran = false;
+                TRY(restore(e));
+                continue;
+            }
+        }
         // the merge bookkeeping first, so that an error below leaves a compacted state
         const int tree_rc = (e->n > 0 && k > 0) ? check_tree_flags(e) : BH_OK;
         uint32_t overflow = 0;
@@ -1533,6 +1572,7 @@ int bh_traversal_counters(const bh_engine *e, int64_t *out5) {
 
 int bh_let_stats(const bh_engine *e, int64_t *out4) {
     if (!e || !out4) return BH_E_INVALID;
+    out4[4] = e->let_overflows;
     out4[0] = e->let_builds;
     out4[1] = e->full_builds;
     out4[2] = e->let_last_sub;

@@ -175,6 +175,41 @@ __global__ __launch_bounds__(TB) void k_let_gather(int64_t n, const uint32_t *__
     sub.cidx[j] = st.cidx[i];
 }
 
+// subset slots [n_real, S) as dead bodies (sentinel keys: never in the tree, never evaluated);
+// the status: overflow when n_real > S (the build then misses bodies: the call is replayed)
+__global__ __launch_bounds__(TB) void k_let_pad(int64_t n, int64_t S, const uint32_t *__restrict__ selpos,
+                                                BodyState sub, LetCell *__restrict__ table,
+                                                uint32_t *__restrict__ scal) {
+    const int64_t j = (int64_t)blockIdx.x * TB + threadIdx.x;
+    const int64_t n_real = selpos[n];
+    if (j == 0) {
+        table[LET_CELLS] = LetCell{0.0, 0.0, 0.0, n_real > S ? 1u : 0u, 0u};
+        atomicMax(scal + 5, (uint32_t)n_real);
+    }
+    if (j >= S || j < n_real) return;
+    sub.x[j] = 0.0;
+    sub.y[j] = 0.0;
+    sub.vx[j] = __longlong_as_double(-1ll);  // no replicated slot
+    sub.vy[j] = 0.0;
+    sub.m[j] = 0.0;
+    sub.cidx[j] = CIDX_DEAD;
+}
+
+__global__ void k_let_overflow(int world, const LetCell *__restrict__ tables,
+                               uint32_t *__restrict__ scal) {
+    for (int q = 0; q < world; ++q)
+        if (tables[(int64_t)q * LET_TSTRIDE + LET_CELLS].cnt) scal[4] = 1u;
+}
+
+// a tree larger than its array can only come from a broken invariant: no walk, and the call is
+// replayed (bh_step) instead of reading past the array
+__global__ void k_let_guard(LetBufs L, uint32_t *__restrict__ scal) {
+    if (L.posc[LET_CELLS] + 1u >= L.node_cap) {
+        scal[4] = 1u;
+        L.posc[LET_CELLS] = 0u;
+    }
+}
+
 // ---- after the subset build ----------------------------------------------------------------
 __global__ __launch_bounds__(TB) void k_let_cells(int64_t n, int J,
                                                   const uint64_t *__restrict__ keys_s,
@@ -262,7 +297,7 @@ __global__ __launch_bounds__(256) void k_let_top_hi(int world, Geometry g,
         const uint32_t c = b * 256u + t;
         LetCell r{0.0, 0.0, 0.0, 0u, 0u};
         for (int q = 0; q < world; ++q) {
-            const LetCell v = tables[(int64_t)q * LET_CELLS + c];
+            const LetCell v = tables[(int64_t)q * LET_TSTRIDE + c];
             if (v.tag) {
                 r = v;
                 break;
@@ -312,19 +347,29 @@ __device__ __forceinline__ bool node_exists(const LetCell *__restrict__ levels, 
 
 // nodes per depth-P cell: its own node(s) (a locally built subtree, or one record) plus the
 // top nodes whose cell range starts at it; pre-order = order of (first cell, depth).
-__global__ __launch_bounds__(TB) void k_let_w(LetBufs L, TreeBuffers tb) {
+__global__ __launch_bounds__(TB) void k_let_w(LetBufs L, TreeBuffers tb,
+                                              uint32_t *__restrict__ scal) {
     const int64_t c = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (c > LET_CELLS) return;
-    if (c == LET_CELLS) {
+    if (c == LET_CELLS || scal[4]) {
+        // after a subset overflow (some rank's subset missed bodies: the call is replayed) the
+        // local cells need not hold what the exchanged counts say: an empty tree
         L.w[c] = 0u;
         L.ccnt[c] = 0u;
+        L.bsz[c] = 0u;
+        L.csrc[c] = 0u;
         return;
     }
     uint32_t bs = 0, copy = 0, ni = 0;
     if (node_exists(L.levels, LET_P, (uint32_t)c)) {
         if (L.levels[level_off(LET_P) + c].cnt >= 2u && L.hcell[c]) {
-            ni = cell_node(tb, L.cstart[c]);
-            bs = copy = tb.nodes[ni].next - ni;
+            if (L.cstart[c + 1] - L.cstart[c] < 2u) {  // cannot happen (replicated positions):
+                scal[4] = 1u;                          // replay rather than read a wrong node
+                bs = 1u;
+            } else {
+                ni = cell_node(tb, L.cstart[c]);
+                bs = copy = tb.nodes[ni].next - ni;
+            }
         } else {
             bs = 1u;
         }
@@ -375,7 +420,7 @@ __global__ __launch_bounds__(TB) void k_let_write_top(LetBufs L) {
         nd.next = pos + 1;
         nd.meta = NODE_LEAF | leaf_slot(L, v.tag) | (v.mass == 0.0 ? NODE_SKIP : 0u);
     }
-    L.nodes[pos] = nd;
+    if (pos < L.node_cap) L.nodes[pos] = nd;
 }
 
 // one record per depth-P cell that is not copied: a remote internal cell (accepted by every local
@@ -396,7 +441,7 @@ __global__ __launch_bounds__(TB) void k_let_write_cells(LetBufs L) {
         nd.meta = (uint32_t)(2 * LET_P) | (v.mass > 0.0 ? 0u : NODE_SKIP);
     else
         nd.meta = NODE_LEAF | leaf_slot(L, (uint32_t)c) | (v.mass == 0.0 ? NODE_SKIP : 0u);
-    L.nodes[pos] = nd;
+    if (pos < L.node_cap) L.nodes[pos] = nd;
 }
 
 // the locally built subtrees, one thread per node (grid-stride over cpos[LET_CELLS] nodes): node t
@@ -414,7 +459,7 @@ __global__ __launch_bounds__(TB) void k_let_copy_blocks(LetBufs L, const Node *_
         const uint32_t ni = L.csrc[c], dst = L.posc[c + 1] - L.bsz[c];
         Node nd = src[ni + k];
         nd.next = nd.next - ni + dst;
-        L.nodes[dst + k] = nd;
+        if (dst + k < L.node_cap) L.nodes[dst + k] = nd;
     }
 }
 
@@ -522,7 +567,8 @@ size_t let_scratch_bytes(int64_t n) {
 }
 
 hipError_t let_select(const BodyState &st, const Geometry &g, const LetPieces &pc, double gap2,
-                      const LetBufs &L, const BodyState &sub, hipStream_t s) {
+                      const LetBufs &L, const BodyState &sub, int64_t S, uint32_t *scal,
+                      hipStream_t s) {
     hipError_t e = hipMemsetAsync(L.ecell, 0, LET_CELLS, s);
     if (e == hipSuccess) e = hipMemsetAsync(L.flag_all, 0, sizeof(uint32_t), s);
     if (e == hipSuccess && pc.n > 0) e = hipMemsetAsync(L.own, 0, (size_t)pc.n, s);
@@ -540,6 +586,7 @@ hipError_t let_select(const BodyState &st, const Geometry &g, const LetPieces &p
                                 rocprim::plus<uint32_t>(), s);
     if (e != hipSuccess) return e;
     if (pc.n > 0) k_let_gather<<<grid_for(pc.n), TB, 0, s>>>(pc.n, L.sel, L.selpos, st, sub);
+    k_let_pad<<<grid_for(S > 0 ? S : 1), TB, 0, s>>>(pc.n, S, L.selpos, sub, L.table, scal);
     return hipGetLastError();
 }
 
@@ -551,10 +598,11 @@ hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const T
 }
 
 hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, const LetBufs &L,
-                        const TreeBuffers &tb, hipStream_t s) {
+                        const TreeBuffers &tb, uint32_t *scal, hipStream_t s) {
+    k_let_overflow<<<1, 1, 0, s>>>(pc.world, L.tables, scal);
     k_let_top_hi<<<256, 256, 0, s>>>(pc.world, g, L.tables, L.levels);
     k_let_top_lo<<<1, 256, 0, s>>>(g, L.levels);
-    k_let_w<<<grid_for(LET_CELLS + 1), TB, 0, s>>>(L, tb);
+    k_let_w<<<grid_for(LET_CELLS + 1), TB, 0, s>>>(L, tb, scal);
     size_t bytes = L.scratch_bytes;
     hipError_t e = rocprim::exclusive_scan(L.scratch, bytes, L.w, L.posc, 0u,
                                            (size_t)(LET_CELLS + 1), rocprim::plus<uint32_t>(), s);
@@ -564,6 +612,7 @@ hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, c
                                 rocprim::plus<uint32_t>(), s);
     if (e != hipSuccess) return e;
     k_let_write_top<<<grid_for(level_off(LET_P)), TB, 0, s>>>(L);
+    k_let_guard<<<1, 1, 0, s>>>(L, scal);
     k_let_write_cells<<<grid_for(LET_CELLS), TB, 0, s>>>(L);
     k_let_copy_blocks<<<2048, TB, 0, s>>>(L, tb.nodes);
     if (n_sub > 0) k_let_subpos<<<grid_for(n_sub), TB, 0, s>>>(n_sub, pc.n, tb.dst.vx, L.subpos);

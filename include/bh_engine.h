@@ -160,11 +160,13 @@ int bh_traversal_stats(const bh_engine *e, int64_t *lane_visits, int64_t *wave_i
  * Lane efficiency = [0] / (64 [2]); force-block lane use = ([1] + bodies) / (64 [3]). */
 int bh_traversal_counters(const bh_engine *e, int64_t *out5);
 
-/* Multi-rank build sharding (locally essential tree): out4[0] LET builds, out4[1] full-tree
- * builds since the engine was created, out4[2] bodies in the last LET build's subset (the
- * cells this rank's bodies can open), out4[3] node records of the last LET tree.  Setting
+/* Multi-rank build sharding (locally essential tree): out5[0] LET builds, out5[1] full-tree
+ * builds since the engine was created, out5[2] bodies in the largest LET subset of the last
+ * bh_step call (the cells this rank's bodies can open), out5[3] node records of the last LET
+ * tree, out5[4] bh_step calls replayed because a subset outgrew its capacity (the capacity
+ * follows the previous call's subsets, so the build needs no host round trip).  Setting
  * BH_LET=0 in the environment before creating an engine keeps every build full. */
-int bh_let_stats(const bh_engine *e, int64_t *out4);
+int bh_let_stats(const bh_engine *e, int64_t *out5);
 
 /* Enable/disable per-phase event timing (default off: no events in the hot loop). */
 int bh_set_profiling(bh_engine *e, int enabled);

@@ -756,6 +756,54 @@ def test_let_build_multi_rank_vs_single(world, scene, theta):
             assert bits_equal(got[r][k], want[k]), f"rank {r}: {name}"
 
 
+def test_let_subset_overflow_replays_the_call():
+    """The LET subset capacity follows the previous call's subsets (no host round trip per
+    build): after a reset to a scene with 4x the bodies every rank's subset outgrows it, every
+    rank sees the overflow through the exchange and the call is replayed -- the states still
+    equal the single-GPU engine's bit for bit."""
+    small = scenes.uniform(50_000, 0.5, seed=21)
+    big = scenes.uniform(200_000, 0.5, seed=22)
+    params = bh_amd.default_params(theta=0.5)
+    single = bh_amd.Engine(params, device=0)
+    single.reset_bodies(*small)
+    single.step(3)
+    single.reset_bodies(*big)
+    single.step(3)
+    want = single.get_bodies()
+    single.close()
+    import threading
+    world = 4
+    group = bh_amd.LocalGroup(world)
+    engines = [bh_amd.Engine(params, device=0, rank=r, local_group=group) for r in range(world)]
+    got, stats, errors = [None] * world, [None] * world, []
+
+    def run(r):
+        try:
+            engines[r].reset_bodies(*small)
+            engines[r].step(3)
+            engines[r].reset_bodies(*big)
+            engines[r].step(3)
+            got[r] = engines[r].get_bodies()
+            stats[r] = engines[r].let_stats()
+        except Exception as exc:  # surfaced below
+            errors.append(exc)
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors
+    assert not any(t.is_alive() for t in threads), "rank thread hung"
+    for e in engines:
+        e.close()
+    group.close()
+    for r in range(world):
+        assert stats[r]["overflows"] >= 1, stats[r]
+        for k, name in enumerate(FIELDS):
+            assert bits_equal(got[r][k], want[k]), f"rank {r}: {name}"
+
+
 def test_checkpoint_resume_bit_identical(tmp_path):
     """bh_save_state after 6 steps of a merge-active two-disk scene, bh_load_state into a fresh
     engine, 6 more steps: bit-identical to 12 uninterrupted steps and to the oracle; the file
