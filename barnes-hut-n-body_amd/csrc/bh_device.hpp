@@ -207,8 +207,11 @@ hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_ba
 // childless records every local body provably accepts.  See let.hip.
 constexpr int LET_P = 8;
 constexpr int64_t LET_CELLS = (int64_t)1 << (2 * LET_P);
-// an exchange table: LET_CELLS cell records + one status record (cnt = subset overflow)
-constexpr int64_t LET_TSTRIDE = LET_CELLS + 1;
+// an exchange table: LET_CELLS cell records, one status record (cnt: 1 = subset overflow, 2 =
+// jitter log overflow; tag: jitter log entries) and the jitter log -- (x, y, -, slot) of the
+// rank's own bodies whose position the build moved (BHA:146-151), so the lanes send only (ax, ay)
+constexpr int64_t LET_JLOG = 16384;
+constexpr int64_t LET_TSTRIDE = LET_CELLS + 1 + LET_JLOG;
 struct __attribute__((aligned(32))) LetCell {
     double comX, comY, mass;
     uint32_t cnt;  // in-tree bodies of the cell, saturated at 2 (0 empty, 1 leaf, 2 internal)
@@ -251,7 +254,13 @@ hipError_t let_select(const BodyState &st, const Geometry &g, const LetPieces &p
 // after tree_build over the subset: the own cells' exchange table
 hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const TreeBuffers &tb,
                      hipStream_t s);
-// after the exchange (L.tables, LET_TSTRIDE per rank): any rank's overflow -> scal[4]; top
+// after the subset build: the own bodies the build moved, into the table's jitter log
+hipError_t let_jitter_log(int64_t n_sub, int64_t n, const BodyState &st, const LetBufs &L,
+                          const TreeBuffers &tb, hipStream_t s);
+// after the exchange: every rank's logged positions into the replicated state
+hipError_t let_jitter_apply(int world, const LetBufs &L, BodyState st, hipStream_t s);
+// after the exchange (L.tables, LET_TSTRIDE per rank): any rank's overflow -> scal[4] (a jitter
+// log overflow also -> scal[6]: the engine switches to the wide exchange); top
 // levels, layout, node array, lane map; tree size posc[LET_CELLS]
 hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, const LetBufs &L,
                         const TreeBuffers &tb, uint32_t *scal, hipStream_t s);

@@ -164,7 +164,8 @@ struct bh_engine {
     int64_t let_overflows = 0;   // calls replayed for a subset overflow
     uint32_t s_spl_nb = 0;       // splitters of the last LET build (subset bucket sort)
     bool st_morton = false;     // slots are in the Morton order of a full build (not caller order)
-    bool a2_pos = false;        // the last evaluation wrote (ax, ay, x, y) per slot
+    bool a2_pos = false;        // the last evaluation wrote (ax, ay, x, y) per lane
+    bool let_wide = false;      // a jitter log overflowed: lanes send (ax, ay, x, y)
     LetBufs L{};
     int64_t let_cap = 0;        // n capacity of the per-body LET arrays
     int64_t let_sub_cap = 0;    // subset capacity of the subset tree workspace
@@ -652,6 +653,7 @@ int evaluate_let(bh_engine *e, bool *done) {
     HIPCHK(e, tree_build(sb, n_sub, e->geo, e->stream));
     e->s_spl_nb = sort_buckets(n_sub);  // k_prep wrote this build's splitters
     HIPCHK(e, let_table(n_sub, e->geo, e->L, sb, e->stream));
+    if (!e->let_wide) HIPCHK(e, let_jitter_log(n_sub, n, e->st, e->L, sb, e->stream));
     const size_t tbytes = sizeof(LetCell) * (size_t)LET_TSTRIDE;
     if (e->comm) {
         NCCLCHK(e, ncclAllGather(e->L.table, e->L.tables, tbytes, ncclUint8, e->comm, e->stream));
@@ -672,11 +674,17 @@ int evaluate_let(bh_engine *e, bool *done) {
                                      hipMemcpyDeviceToDevice, e->stream));
         }
     }
+    if (!e->let_wide) HIPCHK(e, let_jitter_apply(e->world, e->L, e->st, e->stream));
     HIPCHK(e, let_assemble(n_sub, e->geo, pc, e->L, sb, e->scalars, e->stream));
     TRY(mark(e, 0));
     const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};
-    const KickArgs ka{KICK_POS, nullptr, nullptr, 0.0, 0.0};
-    if (e->solo) let_fill_idle(n, lanes, e->st.x, e->st.y, e->a2, e->stream);
+    // (ax, ay) per lane, the jittered positions travelled in the logs; wide: (ax, ay, x, y)
+    const int W = e->let_wide ? 4 : 2;
+    const KickArgs ka{e->let_wide ? KICK_POS : KICK_NONE, nullptr, nullptr, 0.0, 0.0};
+    if (e->solo && e->let_wide) let_fill_idle(n, lanes, e->st.x, e->st.y, e->a2, e->stream);
+    if (e->solo && !e->let_wide)  // measurement: the peers' bodies get no force
+        HIPCHK(e, hipMemsetAsync(e->a2, 0, sizeof(double) * 2 * (size_t)(sub * e->world * R),
+                                 e->stream));
     TRY(round_streams(e));
     for (int k = 0; k < R; ++k) {
         int64_t lo = 0, hi = 0;
@@ -688,9 +696,9 @@ int evaluate_let(bh_engine *e, bool *done) {
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipEventRecord(e->round_ev[k], rs));
         HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
-        double *piece = e->a2 + 4 * ((int64_t)k * e->world) * sub;  // round k, rank 0
+        double *piece = e->a2 + W * ((int64_t)k * e->world) * sub;  // round k, rank 0
         if (e->comm) {
-            NCCLCHK(e, ncclAllGather(piece + 4 * e->rank * sub, piece, (size_t)(4 * sub),
+            NCCLCHK(e, ncclAllGather(piece + W * e->rank * sub, piece, (size_t)(W * sub),
                                      ncclDouble, e->comm, e->comm_stream));
         } else if (e->group) {
             e->group->barrier();
@@ -698,8 +706,8 @@ int evaluate_let(bh_engine *e, bool *done) {
                 if (q == e->rank) continue;
                 bh_engine *peer = e->group->members[q];
                 HIPCHK(e, hipStreamWaitEvent(e->comm_stream, peer->round_ev[k], 0));
-                const int64_t off = 4 * ((int64_t)k * e->world + q) * sub;
-                HIPCHK(e, hipMemcpyAsync(e->a2 + off, peer->a2 + off, sizeof(double) * 4 * sub,
+                const int64_t off = W * ((int64_t)k * e->world + q) * sub;
+                HIPCHK(e, hipMemcpyAsync(e->a2 + off, peer->a2 + off, sizeof(double) * W * sub,
                                          hipMemcpyDeviceToDevice, e->comm_stream));
             }
         }
@@ -708,7 +716,7 @@ int evaluate_let(bh_engine *e, bool *done) {
     HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
     HIPCHK(e, hipStreamWaitEvent(e->stream, e->gathered_ev, 0));
     TRY(mark(e, 4));
-    e->a2_pos = true;
+    e->a2_pos = e->let_wide;
     e->a2_lanes = lanes;
     e->tree_valid = false;  // the full tree was not built
     *done = true;
@@ -967,7 +975,7 @@ int step_once(bh_engine *e, bool last) {
         TRY(evaluate(e, nullptr, KICK_DRIFT, &fused, true, &let));  // a(t)
         if (!fused) {
             TRY(mark(e, -1));
-            if (let)
+            if (let && e->a2_pos)
                 let_kick_drift(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->p.dt,
                                e->stream, e->a2_lanes);
             else
@@ -979,7 +987,7 @@ int step_once(bh_engine *e, bool last) {
         TRY(evaluate(e, nullptr, KICK_ONLY, &fused, !last, &let));  // a(t+dt)
         if (!fused) {
             TRY(mark(e, -1));
-            if (let)
+            if (let && e->a2_pos)
                 let_kick(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->stream,
                          e->a2_lanes);
             else
@@ -1368,14 +1376,16 @@ int bh_step(bh_engine *e, int32_t k) {
         // the subset splitters are trusted only within a call (another scene after a reset
         // would put most of a subset into one bucket): the first LET build sorts with rocprim
         e->s_spl_nb = 0;
-        HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, 5 * sizeof(uint32_t), e->stream));
+        HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, 6 * sizeof(uint32_t), e->stream));
         e->removed.clear();
         e->merge_ran = false;
         for (int32_t s = 0; s < k; ++s) TRY(step_once(e, s + 1 == k));
         HIPCHK(e, hipStreamSynchronize(e->stream));
-        if (may_let) {  // LET subset sizes of this call: [4] some rank overflowed, [5] largest
-            uint32_t ls[2] = {0, 0};
+        if (may_let) {  // LET subset sizes of this call: [4] some rank overflowed, [5] largest,
+                        // [6] a jitter log overflowed (every rank: the wide exchange from now on)
+            uint32_t ls[3] = {0, 0, 0};
             HIPCHK(e, hipMemcpy(ls, e->scalars + 4, sizeof(ls), hipMemcpyDeviceToHost));
+            if (ls[2]) e->let_wide = true;
             if (ls[1] > 0) {
                 e->let_last_sub = ls[1];
                 e->let_known = std::max<int64_t>(ls[1], ls[0] ? e->let_known : 1);

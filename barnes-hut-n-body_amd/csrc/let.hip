@@ -17,8 +17,10 @@
 //     (32 B per cell, one all-gather), and lays the tree out in pre-order: top nodes, local
 //     subtrees copied with shifted `next`, remote cells as childless records.
 // The traversal kernel then walks this array unchanged (traverse.hip), one lane per own body.
-// Jitter (BHA:146-151) mutates positions during the build: the lanes send x, y with their
-// accelerations, so every replica takes the owner's positions (let_kick*).
+// Jitter (BHA:146-151) mutates positions during the build: each rank logs its own bodies that
+// the build moved into its exchange table, and every replica takes those positions before the
+// kick; the lanes send only (ax, ay).  A log overflow switches the engine to the wide exchange
+// -- the lanes send (ax, ay, x, y) and every replica takes the owners' positions (let_kick*).
 #include <algorithm>
 #include <cmath>
 
@@ -197,8 +199,42 @@ __global__ __launch_bounds__(TB) void k_let_pad(int64_t n, int64_t S, const uint
 
 __global__ void k_let_overflow(int world, const LetCell *__restrict__ tables,
                                uint32_t *__restrict__ scal) {
-    for (int q = 0; q < world; ++q)
-        if (tables[(int64_t)q * LET_TSTRIDE + LET_CELLS].cnt) scal[4] = 1u;
+    for (int q = 0; q < world; ++q) {
+        const uint32_t st = tables[(int64_t)q * LET_TSTRIDE + LET_CELLS].cnt;
+        if (st) scal[4] = 1u;
+        if (st & 2u) scal[6] = 1u;
+    }
+}
+
+// own bodies whose position the subset build changed (jitter): logged for the other replicas
+__global__ __launch_bounds__(TB) void k_let_jlog(int64_t n_sub, int64_t n, BodyState sub,
+                                                 const double *__restrict__ x,
+                                                 const double *__restrict__ y,
+                                                 const uint8_t *__restrict__ own,
+                                                 LetCell *__restrict__ table) {
+    const int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (a >= n_sub) return;
+    const int64_t i = (int64_t)__double_as_longlong(sub.vx[a]);
+    if (i < 0 || i >= n || !own[i]) return;
+    const double px = sub.x[a], py = sub.y[a];
+    if (__double_as_longlong(px) == __double_as_longlong(x[i]) &&
+        __double_as_longlong(py) == __double_as_longlong(y[i]))
+        return;
+    const uint32_t k = atomicAdd(&table[LET_CELLS].tag, 1u);
+    if (k < (uint32_t)LET_JLOG) table[LET_CELLS + 1 + k] = LetCell{px, py, 0.0, (uint32_t)i, 0u};
+    else atomicOr(&table[LET_CELLS].cnt, 2u);  // too many: the wide exchange takes over
+}
+
+__global__ __launch_bounds__(TB) void k_let_japply(int world, const LetCell *__restrict__ tables,
+                                                   double *__restrict__ x, double *__restrict__ y) {
+    const int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (t >= (int64_t)world * LET_JLOG) return;
+    const int64_t q = t / LET_JLOG, k = t % LET_JLOG;
+    const LetCell *tq = tables + q * LET_TSTRIDE;
+    if (k >= (int64_t)min(tq[LET_CELLS].tag, (uint32_t)LET_JLOG)) return;
+    const LetCell v = tq[LET_CELLS + 1 + k];
+    x[v.cnt] = v.comX;
+    y[v.cnt] = v.comY;
 }
 
 // a tree larger than its array can only come from a broken invariant: no walk, and the call is
@@ -594,6 +630,18 @@ hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const T
                      hipStream_t s) {
     k_let_cells<<<grid_for(LET_CELLS + 1), TB, 0, s>>>(n_sub, g.J, tb.keys_s, L.cstart);
     k_let_table<<<grid_for(LET_CELLS), TB, 0, s>>>(L, tb);
+    return hipGetLastError();
+}
+
+hipError_t let_jitter_log(int64_t n_sub, int64_t n, const BodyState &st, const LetBufs &L,
+                          const TreeBuffers &tb, hipStream_t s) {
+    if (n_sub > 0)
+        k_let_jlog<<<grid_for(n_sub), TB, 0, s>>>(n_sub, n, tb.dst, st.x, st.y, L.own, L.table);
+    return hipGetLastError();
+}
+
+hipError_t let_jitter_apply(int world, const LetBufs &L, BodyState st, hipStream_t s) {
+    k_let_japply<<<grid_for((int64_t)world * LET_JLOG), TB, 0, s>>>(world, L.tables, st.x, st.y);
     return hipGetLastError();
 }
 

@@ -804,6 +804,29 @@ def test_let_subset_overflow_replays_the_call():
             assert bits_equal(got[r][k], want[k]), f"rank {r}: {name}"
 
 
+def test_let_jitter_log_overflow_switches_to_the_wide_exchange():
+    """Every body a coincident pair: each build moves 30 000 own bodies per rank, past the
+    16 384-entry jitter log, so every rank sees the overflow, the call is replayed with the
+    positions sent beside the accelerations -- and the states still equal the single-GPU
+    engine's bit for bit (the narrow exchange ran before the overflow)."""
+    base = scenes.uniform(30_000, 0.5, seed=31)
+    rng = np.random.default_rng(32)
+    perm = rng.permutation(2 * len(base[0]))
+    arrs = tuple(np.concatenate([a, a])[perm] for a in base)
+    params = bh_amd.default_params(theta=0.5, merge_min_dist=0.0)
+    single = bh_amd.Engine(params, device=0)
+    single.reset_bodies(*arrs)
+    for k in (3, 2):
+        single.step(k)
+    want = single.get_bodies()
+    single.close()
+    got, stats = _run_group(2, params, arrs, (3, 2))
+    for r in range(2):
+        assert stats[r]["overflows"] >= 1, stats[r]
+        for k, name in enumerate(FIELDS):
+            assert bits_equal(got[r][k], want[k]), f"rank {r}: {name}"
+
+
 def test_checkpoint_resume_bit_identical(tmp_path):
     """bh_save_state after 6 steps of a merge-active two-disk scene, bh_load_state into a fresh
     engine, 6 more steps: bit-identical to 12 uninterrupted steps and to the oracle; the file

@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 if [ "${LET_TESTS:-1}" = "1" ]; then
 timeout -k 10 900 python -u -m pytest -x -v --timeout 400 --timeout-method thread \
-  tests/test_gpu_parity.py tests/test_gpu_digests.py -k "${LET_K:-let_build or let_subset or multi_rank or rccl or eight_rank}" \
+  tests/test_gpu_parity.py tests/test_gpu_digests.py -k "${LET_K:-let_ or multi_rank or rccl or eight_rank}" \
   > gpurun_out/let_tests.log 2>&1
 rc=$?; echo "let tests rc=$rc"; tail -15 gpurun_out/let_tests.log
 [ $rc -eq 0 ] || exit $rc
