@@ -228,7 +228,8 @@ struct LetBufs {
     uint8_t *own;             // [n] replicated slot evaluated by this rank
     uint32_t *subpos;         // [n] replicated slot -> subset slot (subset bodies)
     uint32_t *flag_all;       // [1] a non-finite own body: every cell is built
-    uint32_t *sel, *selpos;   // [n + 1] subset flags and their exclusive scan
+    uint8_t *flag8;           // [n] subset flag per replicated slot
+    uint32_t *sel, *selpos;   // [n / 256 + 2] subset count per 256-slot block, its scan
     uint32_t *cstart;         // [LET_CELLS + 1] first sorted subset body of each cell
     LetCell *table, *tables;  // own exchange table, all ranks' tables [world][LET_CELLS]
     LetCell *levels;          // depths 0..LET_P, level d at ((4^d - 1) / 3)
@@ -244,8 +245,9 @@ struct LetBufs {
 // at that gap; cells beyond it are accepted by every such body.  < 0: the LET does not apply.
 double let_include_gap2(const Geometry &g, double theta2, double soft2);
 size_t let_scratch_bytes(int64_t n);
+inline int64_t let_sel_blocks(int64_t n) { return (n + 255) / 256; }
 // own cells, halo, subset flags + scan + gather into `sub` (vx carries the replicated slot);
-// the subset has selpos[n] bodies.  The build runs over a host-chosen capacity S without a host
+// the subset has selpos[let_sel_blocks(n)] bodies.  The build runs over a host-chosen capacity S without a host
 // round trip: `sub` is padded with dead bodies (sentinel keys: not in the tree) up to S, and
 // selpos[n] > S is an overflow (the status record of the table; scal[5] = max subset size)
 hipError_t let_select(const BodyState &st, const Geometry &g, const LetPieces &pc,

@@ -517,8 +517,9 @@ int let_alloc(bh_engine *e, int64_t n_sub) {
         TRY(dev_alloc(e, L.ecell, LET_CELLS));
         TRY(dev_alloc(e, L.hcell, LET_CELLS));
         TRY(dev_alloc(e, L.flag_all, 1));
-        TRY(dev_alloc(e, L.sel, cap + 1));
-        TRY(dev_alloc(e, L.selpos, cap + 1));
+        TRY(dev_alloc(e, L.flag8, cap));
+        TRY(dev_alloc(e, L.sel, let_sel_blocks(cap) + 2));
+        TRY(dev_alloc(e, L.selpos, let_sel_blocks(cap) + 2));
         TRY(dev_alloc(e, L.cstart, LET_CELLS + 1));
         TRY(dev_alloc(e, L.table, LET_TSTRIDE));
         TRY(dev_alloc(e, L.tables, (size_t)e->world * LET_TSTRIDE));
@@ -640,7 +641,7 @@ int evaluate_let(bh_engine *e, bool *done) {
     if (e->let_known <= 0) {
         TRY(pinned_reserve(e, 64));
         uint32_t *h = static_cast<uint32_t *>(e->pin);
-        HIPCHK(e, hipMemcpyAsync(h, e->L.selpos + n, sizeof(uint32_t), hipMemcpyDeviceToHost,
+        HIPCHK(e, hipMemcpyAsync(h, e->L.selpos + let_sel_blocks(n), sizeof(uint32_t), hipMemcpyDeviceToHost,
                                  e->stream));
         HIPCHK(e, hipStreamSynchronize(e->stream));
         e->let_known = std::max<int64_t>(h[0], 1);
@@ -1279,7 +1280,7 @@ void bh_destroy(bh_engine *e) {
     free_state(e->sub_src);
     free_state(e->sub_dst);
     if (e->table_ev) (void)hipEventDestroy(e->table_ev);
-    void *lets[] = {e->L.csrc, e->L.ccnt, e->L.cpos, e->solo_table, e->solo_all, e->solo_cstart, e->L.ecell, e->L.hcell, e->L.own, e->L.subpos, e->L.flag_all, e->L.sel, e->L.selpos, e->L.cstart,
+    void *lets[] = {e->L.csrc, e->L.ccnt, e->L.cpos, e->solo_table, e->solo_all, e->solo_cstart, e->L.ecell, e->L.hcell, e->L.own, e->L.subpos, e->L.flag_all, e->L.flag8, e->L.sel, e->L.selpos, e->L.cstart,
                     e->L.table, e->L.tables, e->L.levels, e->L.w, e->L.posc, e->L.bsz,
                     e->L.nodes, e->L.lanes, e->s_keys, e->s_keys_s, e->s_spl, e->s_keys32,
                     e->s_keys32_s, e->s_idx, e->s_perm, e->s_cpl, e->s_cnt, e->s_base,

@@ -50,14 +50,13 @@ __device__ __forceinline__ uint32_t compact16(uint32_t v) {  // bit 2k -> bit k
 
 // Column of p on the grid o + k w, clamped to [0, top]: exact for p inside (settled by the same
 // exact grid-line compares as k_morton); outside, the column of p's projection onto the root.
-__device__ __forceinline__ uint32_t grid_col(double p, double o, double w, uint32_t top) {
-    const double q = (p - o) * (1.0 / w);  // off by at most one: settled below
-    int64_t c;
-    if (!(q >= 0.0)) c = 0;
-    else if (q >= (double)top) c = top;
-    else c = (int64_t)q;
+__device__ __forceinline__ uint32_t grid_col(double p, double o, double w, int top) {
+    double q = (p - o) * (1.0 / w);  // off by at most one: settled below
+    if (!(q >= 0.0)) q = 0.0;
+    if (q > (double)top) q = (double)top;
+    int c = (int)q;
     if (c > 0 && p < o + (double)c * w) --c;
-    else if (c < (int64_t)top && p >= o + (double)(c + 1) * w) ++c;
+    else if (c < top && p >= o + (double)(c + 1) * w) ++c;
     return (uint32_t)c;
 }
 
@@ -68,7 +67,7 @@ __device__ __forceinline__ bool in_root(const Geometry &g, double x, double y) {
 
 __device__ __forceinline__ uint32_t cell_of(const Geometry &g, double x, double y) {
     const double w = 2.0 * g.h[LET_P];
-    const uint32_t top = (1u << LET_P) - 1;
+    const int top = (1 << LET_P) - 1;
     return spread16(grid_col(x, g.root_cx - g.root_h, w, top)) |
            (spread16(grid_col(y, g.root_cy - g.root_h, w, top)) << 1);
 }
@@ -143,32 +142,48 @@ __global__ __launch_bounds__(TB) void k_let_halo(const uint8_t *__restrict__ ece
     hcell[c] = h;
 }
 
-// the subset: bodies of built cells, and own bodies outside the tree (they still walk it, or idle)
+// the subset: bodies of built cells, and own bodies outside the tree (they still walk it, or
+// idle); a flag byte per slot and the count of every 256-slot block (scanned: block offsets)
+static_assert(TB == 256, "one 256-slot block per workgroup");
 __global__ __launch_bounds__(TB) void k_let_flags(LetPieces pc, const double *__restrict__ x,
                                                   const double *__restrict__ y,
                                                   const uint32_t *__restrict__ cidx, Geometry g,
                                                   const uint8_t *__restrict__ hcell,
                                                   const uint8_t *__restrict__ own,
-                                                  uint32_t *__restrict__ sel) {
+                                                  uint8_t *__restrict__ flag8,
+                                                  uint32_t *__restrict__ bcnt) {
+    __shared__ uint32_t s_w[TB / 64];
     const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (i > pc.n) return;
-    if (i == pc.n) {
-        sel[i] = 0u;
-        return;
+    uint32_t f = 0;
+    if (i < pc.n) {
+        const double px = x[i], py = y[i];
+        if (!(cidx[i] & CIDX_DEAD) && in_root(g, px, py)) f = hcell[cell_of(g, px, py)];
+        else f = own[i];
+        flag8[i] = (uint8_t)f;
     }
-    const double px = x[i], py = y[i];
-    uint32_t f;
-    if (!(cidx[i] & CIDX_DEAD) && in_root(g, px, py)) f = hcell[cell_of(g, px, py)];
-    else f = own[i];
-    sel[i] = f;
+    const uint64_t m = __ballot(f != 0);
+    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        bcnt[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        if (blockIdx.x + 1 == gridDim.x) bcnt[gridDim.x] = 0u;  // the scan's last entry
+    }
 }
 
-__global__ __launch_bounds__(TB) void k_let_gather(int64_t n, const uint32_t *__restrict__ sel,
-                                                   const uint32_t *__restrict__ pos,
+__global__ __launch_bounds__(TB) void k_let_gather(int64_t n, const uint8_t *__restrict__ flag8,
+                                                   const uint32_t *__restrict__ bpos,
                                                    BodyState st, BodyState sub) {
+    __shared__ uint32_t s_w[TB / 64];
     const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (i >= n || !sel[i]) return;
-    const uint32_t j = pos[i];
+    const bool f = i < n && flag8[i];
+    const uint64_t m = __ballot(f);
+    const uint32_t w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) s_w[w] = (uint32_t)__popcll(m);
+    __syncthreads();
+    if (!f) return;
+    uint32_t j = bpos[blockIdx.x];
+    for (uint32_t q = 0; q < w; ++q) j += s_w[q];
+    j += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
     sub.x[j] = st.x[i];
     sub.y[j] = st.y[i];
     sub.vx[j] = __longlong_as_double((long long)i);  // payload: the replicated slot
@@ -179,11 +194,11 @@ __global__ __launch_bounds__(TB) void k_let_gather(int64_t n, const uint32_t *__
 
 // subset slots [n_real, S) as dead bodies (sentinel keys: never in the tree, never evaluated);
 // the status: overflow when n_real > S (the build then misses bodies: the call is replayed)
-__global__ __launch_bounds__(TB) void k_let_pad(int64_t n, int64_t S, const uint32_t *__restrict__ selpos,
+__global__ __launch_bounds__(TB) void k_let_pad(int64_t S, const uint32_t *__restrict__ count,
                                                 BodyState sub, LetCell *__restrict__ table,
                                                 uint32_t *__restrict__ scal) {
     const int64_t j = (int64_t)blockIdx.x * TB + threadIdx.x;
-    const int64_t n_real = selpos[n];
+    const int64_t n_real = *count;
     if (j == 0) {
         table[LET_CELLS] = LetCell{0.0, 0.0, 0.0, n_real > S ? 1u : 0u, 0u};
         atomicMax(scal + 5, (uint32_t)n_real);
@@ -485,13 +500,36 @@ __global__ __launch_bounds__(TB) void k_let_write_cells(LetBufs L) {
 // moves with the block
 __global__ __launch_bounds__(TB) void k_let_copy_blocks(LetBufs L, const Node *__restrict__ src) {
     const uint32_t total = L.cpos[LET_CELLS];
-    for (uint32_t t = blockIdx.x * TB + threadIdx.x; t < total; t += gridDim.x * TB) {
-        uint32_t lo = 0, hi = (uint32_t)LET_CELLS;  // largest c with cpos[c] <= t
-        while (hi - lo > 1) {
-            const uint32_t mid = (lo + hi) >> 1;
-            if (L.cpos[mid] <= t) lo = mid; else hi = mid;
+    const uint32_t lane = threadIdx.x & 63u, stride = gridDim.x * TB;
+    for (uint32_t base = blockIdx.x * TB + (threadIdx.x & ~63u); base < total; base += stride) {
+        uint32_t c = 0;
+        if (lane == 0) {  // the wave's first node: largest c with cpos[c] <= base
+            uint32_t lo = 0, hi = (uint32_t)LET_CELLS;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (L.cpos[mid] <= base) lo = mid; else hi = mid;
+            }
+            c = lo;
         }
-        const uint32_t c = lo, k = t - L.cpos[c];
+        c = __shfl(c, 0);
+        const uint32_t t = base + lane;
+        if (t >= total) continue;
+        if (L.cpos[c + 1] <= t) {  // gallop from the wave's cell (empty cells lie between pieces)
+            uint32_t lo = c + 1, step = 1, hi;
+            for (;;) {  // cpos[lo] <= t holds
+                hi = lo + step;
+                if (hi >= (uint32_t)LET_CELLS || L.cpos[hi] > t) break;
+                lo = hi;
+                step <<= 1;
+            }
+            if (hi > (uint32_t)LET_CELLS) hi = (uint32_t)LET_CELLS;
+            while (hi - lo > 1) {
+                const uint32_t mid = (lo + hi) >> 1;
+                if (L.cpos[mid] <= t) lo = mid; else hi = mid;
+            }
+            c = lo;
+        }
+        const uint32_t k = t - L.cpos[c];
         const uint32_t ni = L.csrc[c], dst = L.posc[c + 1] - L.bsz[c];
         Node nd = src[ni + k];
         nd.next = nd.next - ni + dst;
@@ -608,21 +646,22 @@ hipError_t let_select(const BodyState &st, const Geometry &g, const LetPieces &p
     hipError_t e = hipMemsetAsync(L.ecell, 0, LET_CELLS, s);
     if (e == hipSuccess) e = hipMemsetAsync(L.flag_all, 0, sizeof(uint32_t), s);
     if (e == hipSuccess && pc.n > 0) e = hipMemsetAsync(L.own, 0, (size_t)pc.n, s);
-    if (e != hipSuccess) return e;
+    if (e != hipSuccess || pc.n <= 0) return e;
     const int64_t marks = (int64_t)pc.rounds * pc.sub;
-    if (marks > 0 && pc.n > 0)
+    if (marks > 0)
         k_let_mark<<<grid_for(marks), TB, 0, s>>>(pc, st.x, st.y, st.cidx, g, L.own, L.ecell,
                                                   L.flag_all);
     const int K = (int)std::floor(std::sqrt(gap2 > 0.0 ? gap2 : 0.0)) + 1;
     k_let_halo<<<grid_for(LET_CELLS), TB, 0, s>>>(L.ecell, L.flag_all, gap2, K, L.hcell);
-    k_let_flags<<<grid_for(pc.n + 1), TB, 0, s>>>(pc, st.x, st.y, st.cidx, g, L.hcell, L.own,
-                                                   L.sel);
+    const int64_t nb = let_sel_blocks(pc.n);
+    k_let_flags<<<(unsigned)nb, TB, 0, s>>>(pc, st.x, st.y, st.cidx, g, L.hcell, L.own, L.flag8,
+                                            L.sel);
     size_t bytes = L.scratch_bytes;
-    e = rocprim::exclusive_scan(L.scratch, bytes, L.sel, L.selpos, 0u, (size_t)(pc.n + 1),
+    e = rocprim::exclusive_scan(L.scratch, bytes, L.sel, L.selpos, 0u, (size_t)(nb + 1),
                                 rocprim::plus<uint32_t>(), s);
     if (e != hipSuccess) return e;
-    if (pc.n > 0) k_let_gather<<<grid_for(pc.n), TB, 0, s>>>(pc.n, L.sel, L.selpos, st, sub);
-    k_let_pad<<<grid_for(S > 0 ? S : 1), TB, 0, s>>>(pc.n, S, L.selpos, sub, L.table, scal);
+    k_let_gather<<<(unsigned)nb, TB, 0, s>>>(pc.n, L.flag8, L.selpos, st, sub);
+    k_let_pad<<<grid_for(S > 0 ? S : 1), TB, 0, s>>>(S, L.selpos + nb, sub, L.table, scal);
     return hipGetLastError();
 }
 
