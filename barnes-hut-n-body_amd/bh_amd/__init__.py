@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "bh_num_bodies", "bh_get_bodies", "bh_compute_accelerations", "bh_get_quads",
     "bh_last_timings", "bh_last_tree_nodes", "bh_traverse_kernel_ms",
     "bh_traverse_kernel_samples", "bh_set_profiling",
-    "bh_synchronize", "bh_shard_range", "bh_traversal_stats", "bh_traversal_counters", "bh_last_removed",
+    "bh_synchronize", "bh_shard_range", "bh_gather_slot", "bh_traversal_stats", "bh_traversal_counters", "bh_last_removed",
     "bh_selftest_fast_math", "bh_scene_galaxy_disk", "bh_scene_kepler_disk", "bh_scene_uniform",
     "bh_nbody3d_create", "bh_nbody3d_destroy", "bh_nbody3d_last_error", "bh_nbody3d_set",
     "bh_nbody3d_step", "bh_nbody3d_accelerations", "bh_nbody3d_get", "bh_nbody3d_last_ms",
@@ -124,6 +124,8 @@ def load_library(path: str | None = None):
     lib.bh_last_removed.argtypes = [_VP, _I64P, ctypes.c_int64, _I64P]
     lib.bh_shard_range.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    _I64P, _I64P]
+    lib.bh_gather_slot.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int64]
+    lib.bh_gather_slot.restype = ctypes.c_int64
     lib.bh_selftest_fast_math.argtypes = [ctypes.c_int, ctypes.c_int64, ctypes.c_uint64, _I64P]
     _F = ctypes.POINTER(ctypes.c_float)
     lib.bh_nbody3d_create.argtypes = [ctypes.c_int, ctypes.POINTER(_VP)]
@@ -167,9 +169,10 @@ SHARD_ROUNDS = 4  # BH_SHARD_ROUNDS (include/bh_engine.h)
 
 
 def shard_range(n: int, rank: int, world: int, round: int = 0):
-    """Morton-order piece [lo, hi) of bodies whose forces `rank` evaluates in round `round`
-    of a multi-GPU evaluation (bh_shard_range); pieces of round k sit at
-    [(k * world + r) * sub, + sub), so round k's all-gather is in place."""
+    """Lanes [lo, hi) (Hilbert wave order) whose forces `rank` evaluates in round `round` of a
+    multi-GPU evaluation (bh_shard_range): rank r owns [(r * rounds) * sub, + rounds * sub), one
+    contiguous region; the accelerations of lane q sit at gather_slot(n, world, q), where round
+    k's pieces are adjacent, so round k's all-gather is in place."""
     lo = ctypes.c_int64(0)
     hi = ctypes.c_int64(0)
     rc = load_library().bh_shard_range(int(n), int(rank), int(world), int(round),
@@ -177,6 +180,14 @@ def shard_range(n: int, rank: int, world: int, round: int = 0):
     if rc != BH_OK:
         raise BhError(rc, "bh_shard_range: invalid arguments")
     return lo.value, hi.value
+
+
+def gather_slot(n: int, world: int, lane: int) -> int:
+    """Slot of lane `lane` in the exchange buffer of a multi-GPU evaluation (bh_gather_slot)."""
+    g = load_library().bh_gather_slot(int(n), int(world), int(lane))
+    if g < 0:
+        raise BhError(BH_E_INVALID, "bh_gather_slot: invalid arguments")
+    return g
 
 
 class NBody3D:

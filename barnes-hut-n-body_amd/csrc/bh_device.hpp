@@ -195,6 +195,19 @@ __host__ __device__ inline int64_t shard_sub(int64_t n, int world, int rounds) {
     const int64_t c = (n + parts - 1) / parts;
     return (c + 63) / 64 * 64;
 }
+// Rank r owns lanes [r * rounds * sub, +rounds * sub); lane q = (r * rounds + k) * sub + i of
+// round k sits in the exchange buffer at slot (k * world + r) * sub + i, so that the pieces of a
+// round are adjacent (in-place all-gather).  sub == 0: the identity (one GPU).
+struct GatherLayout {
+    int64_t sub;
+    int world, rounds;
+};
+__host__ __device__ inline int64_t gather_slot(const GatherLayout &L, int64_t q) {
+    if (L.sub == 0) return q;
+    const int64_t piece = q / L.sub, i = q - piece * L.sub;
+    const int64_t r = piece / L.rounds, k = piece - r * L.rounds;
+    return (k * L.world + r) * L.sub + i;
+}
 
 // Exactness check of the traversal's in-range sqrt/reciprocal sequences against the IEEE
 // operations on n generated operands; adds the mismatch count to *d_bad.
@@ -268,12 +281,13 @@ hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, c
                         const TreeBuffers &tb, uint32_t *scal, hipStream_t s);
 // KDK of all replicated slots from a2 = (ax, ay, x, y) per lane (BHA:410-432)
 void let_kick_drift(int64_t n, const double *a4, double *x, double *y, double *vx, double *vy,
-                    double dtHalf, double dt, hipStream_t s, const uint32_t *lanes);
+                    double dtHalf, double dt, hipStream_t s, const uint32_t *lanes,
+                    GatherLayout gl);
 void let_kick(int64_t n, const double *a4, double *x, double *y, double *vx, double *vy,
-              double dtHalf, hipStream_t s, const uint32_t *lanes);
+              double dtHalf, hipStream_t s, const uint32_t *lanes, GatherLayout gl);
 // bh_create_solo (measurement): every lane (0, 0, x, y) before the own pieces are evaluated
 void let_fill_idle(int64_t n, const uint32_t *lanes, const double *x, const double *y, double *a4,
-                   hipStream_t s);
+                   hipStream_t s, GatherLayout gl);
 
 // ---- launchers (direct.hip): theta = 0 all-pairs ---------------------------------
 // Non-empty leaves of the last tree in pre-order (the reference's theta = 0 summation order).
@@ -292,16 +306,19 @@ void direct_forces(const LeafList &L, const uint32_t *d_count, const double *x, 
 
 // ---- launchers (integrate.hip) ---------------------------------------------------
 // a2 indexed by traversal lane when lanes != null (lane i holds body slot lanes[i])
+// lane q's acceleration at a2[2 * gather_slot(gl, q)]
 void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
-                double dtHalf, double dt, hipStream_t s, const uint32_t *lanes = nullptr);
+                double dtHalf, double dt, hipStream_t s, const uint32_t *lanes = nullptr,
+                GatherLayout gl = GatherLayout{0, 1, 1});
 void kick(int64_t n, const double *a2, double *vx, double *vy, double dtHalf, hipStream_t s,
-          const uint32_t *lanes = nullptr);
+          const uint32_t *lanes = nullptr, GatherLayout gl = GatherLayout{0, 1, 1});
 void iota_u32(uint32_t *p, int64_t n, hipStream_t s);
 // caller-order copies: dst_k[cidx[s]] = src_k[s]
 void scatter_to_caller(int64_t n, const uint32_t *cidx, int k, const double *const *src,
                        double *const *dst, hipStream_t s);
 void scatter_acc_to_caller(int64_t n, const uint32_t *cidx, const double *a2, double *ax,
-                           double *ay, hipStream_t s, const uint32_t *lanes = nullptr);
+                           double *ay, hipStream_t s, const uint32_t *lanes = nullptr,
+                           GatherLayout gl = GatherLayout{0, 1, 1});
 
 struct MergePair {
     uint32_t h_cidx, v_cidx;  // heavy body and candidate victim, caller indices

@@ -155,6 +155,7 @@ struct bh_engine {
     bool lanes_valid = false;  // the map is a permutation of the current slots
     int lanes_age = 0;         // builds since the last Hilbert sort
     const uint32_t *a2_lanes = nullptr;  // the last evaluation wrote a2 by lane of this map
+    GatherLayout a2_layout{0, 1, 1};     // ... at the lane's gather slot (multi-rank rounds)
 
     // multi-rank locally essential tree (let.hip): subset state and tree workspace
     bool let_on = true;         // BH_LET=0 in the environment: the replicated build
@@ -682,7 +683,8 @@ int evaluate_let(bh_engine *e, bool *done) {
     // (ax, ay) per lane, the jittered positions travelled in the logs; wide: (ax, ay, x, y)
     const int W = e->let_wide ? 4 : 2;
     const KickArgs ka{e->let_wide ? KICK_POS : KICK_NONE, nullptr, nullptr, 0.0, 0.0};
-    if (e->solo && e->let_wide) let_fill_idle(n, lanes, e->st.x, e->st.y, e->a2, e->stream);
+    const GatherLayout gl{sub, e->world, R};
+    if (e->solo && e->let_wide) let_fill_idle(n, lanes, e->st.x, e->st.y, e->a2, e->stream, gl);
     if (e->solo && !e->let_wide)  // measurement: the peers' bodies get no force
         HIPCHK(e, hipMemsetAsync(e->a2, 0, sizeof(double) * 2 * (size_t)(sub * e->world * R),
                                  e->stream));
@@ -691,8 +693,10 @@ int evaluate_let(bh_engine *e, bool *done) {
         int64_t lo = 0, hi = 0;
         bh_shard_range(n, e->rank, e->world, k, &lo, &hi);
         hipStream_t rs = (k & 1) ? e->stream2 : e->stream;
+        // lane q of the piece writes slot gather_slot(q) = q - lo + gather_slot(lo)
+        double *a2r = e->a2 + W * (gather_slot(gl, lo) - lo);
         traverse(e->L.nodes, e->let_node_cap, e->L.posc + LET_CELLS, e->sub_dst.x, e->sub_dst.y,
-                 e->sub_dst.m, e->sub_dst.cidx, lo, hi, e->geo, fp, e->a2, nullptr, rs,
+                 e->sub_dst.m, e->sub_dst.cidx, lo, hi, e->geo, fp, a2r, nullptr, rs,
                  &ka, e->L.lanes);
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipEventRecord(e->round_ev[k], rs));
@@ -719,6 +723,7 @@ int evaluate_let(bh_engine *e, bool *done) {
     TRY(mark(e, 4));
     e->a2_pos = e->let_wide;
     e->a2_lanes = lanes;
+    e->a2_layout = gl;
     e->tree_valid = false;  // the full tree was not built
     *done = true;
     return BH_OK;
@@ -758,13 +763,14 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
     const TraverseCounters counters{visits, e->contrib32, e->wave_iters, e->wave_blocks};
     const uint32_t *lanes = e->lanes_valid ? e->lanes : nullptr;  // [lo, hi): lane ranges
     e->a2_lanes = direct ? nullptr : lanes;
-    auto forces = [&](int64_t lo, int64_t hi, uint32_t *vis, hipStream_t fs) {
+    e->a2_layout = GatherLayout{0, 1, 1};
+    auto forces = [&](int64_t lo, int64_t hi, uint32_t *vis, hipStream_t fs, double *a2) {
         if (direct)
             direct_forces(e->leaves, e->leaf_count, e->st.x, e->st.y, e->st.m, lo, hi, fp.G,
-                          fp.soft2, e->a2, fs);
+                          fp.soft2, a2, fs);
         else
             traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, e->st.cidx, lo, hi, e->geo, fp,
-                     e->a2, vis ? &counters : nullptr, fs, nullptr, lanes);
+                     a2, vis ? &counters : nullptr, fs, nullptr, lanes);
     };
     if ((!e->comm && !e->group && !e->solo) || visits) {
         if (BH_FUSE_KICK && kick != KICK_NONE && !direct && !visits && fused) {
@@ -773,7 +779,7 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
                      e->a2, nullptr, e->stream, &ka, lanes);
             *fused = true;
         } else {
-            forces(0, n, visits, e->stream);
+            forces(0, n, visits, e->stream, e->a2);
         }
         HIPCHK(e, hipGetLastError());
         TRY(mark(e, 1));
@@ -790,11 +796,13 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
             if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->gathered_ev, 0));
     }
     TRY(round_streams(e));
+    const GatherLayout gl{sub, e->world, BH_SHARD_ROUNDS};
+    e->a2_layout = gl;
     for (int k = 0; k < BH_SHARD_ROUNDS; ++k) {
         int64_t lo = 0, hi = 0;
         bh_shard_range(n, e->rank, e->world, k, &lo, &hi);
         hipStream_t rs = (k & 1) ? e->stream2 : e->stream;
-        forces(lo, hi, nullptr, rs);
+        forces(lo, hi, nullptr, rs, e->a2 + 2 * (gather_slot(gl, lo) - lo));
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipEventRecord(e->round_ev[k], rs));
         HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
@@ -978,10 +986,10 @@ int step_once(bh_engine *e, bool last) {
             TRY(mark(e, -1));
             if (let && e->a2_pos)
                 let_kick_drift(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->p.dt,
-                               e->stream, e->a2_lanes);
+                               e->stream, e->a2_lanes, e->a2_layout);
             else
                 kick_drift(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->p.dt,
-                           e->stream, e->a2_lanes);
+                           e->stream, e->a2_lanes, e->a2_layout);
             HIPCHK(e, hipGetLastError());
             TRY(mark(e, 2));
         }
@@ -990,9 +998,9 @@ int step_once(bh_engine *e, bool last) {
             TRY(mark(e, -1));
             if (let && e->a2_pos)
                 let_kick(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->stream,
-                         e->a2_lanes);
+                         e->a2_lanes, e->a2_layout);
             else
-                kick(n, e->a2, e->st.vx, e->st.vy, dtHalf, e->stream, e->a2_lanes);
+                kick(n, e->a2, e->st.vx, e->st.vy, dtHalf, e->stream, e->a2_lanes, e->a2_layout);
             HIPCHK(e, hipGetLastError());
             TRY(mark(e, 2));
         }
@@ -1456,7 +1464,8 @@ int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visi
     HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
     if (n > 0) {
         TRY(evaluate(e, visits ? e->visits32 : nullptr));
-        scatter_acc_to_caller(n, e->st.cidx, e->a2, e->ax, e->ay, e->stream, e->a2_lanes);
+        scatter_acc_to_caller(n, e->st.cidx, e->a2, e->ax, e->ay, e->stream, e->a2_lanes,
+                              e->a2_layout);
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipStreamSynchronize(e->stream));
         TRY(check_tree_flags(e));
@@ -1606,9 +1615,15 @@ int bh_shard_range(int64_t n, int rank, int world, int round, int64_t *lo, int64
         round >= BH_SHARD_ROUNDS || !lo || !hi)
         return BH_E_INVALID;
     const int64_t sub = shard_sub(n, world, BH_SHARD_ROUNDS);  // whole wavefronts
-    *lo = std::min<int64_t>(n, ((int64_t)round * world + rank) * sub);
+    *lo = std::min<int64_t>(n, ((int64_t)rank * BH_SHARD_ROUNDS + round) * sub);  // own range
     *hi = std::min<int64_t>(n, *lo + sub);
     return BH_OK;
+}
+
+int64_t bh_gather_slot(int64_t n, int world, int64_t lane) {
+    if (n < 0 || world < 1 || lane < 0) return -1;
+    return gather_slot(GatherLayout{shard_sub(n, world, BH_SHARD_ROUNDS), world, BH_SHARD_ROUNDS},
+                       lane);
 }
 
 int bh_selftest_fast_math(int device, int64_t n, uint64_t seed, int64_t *mismatches) {

@@ -19,10 +19,11 @@ __global__ __launch_bounds__(TB) void k_kick_drift(int64_t n, const double *__re
                                                    double *__restrict__ x, double *__restrict__ y,
                                                    double *__restrict__ vx,
                                                    double *__restrict__ vy, double dtHalf,
-                                                   double dt, const uint32_t *__restrict__ lanes) {
+                                                   double dt, const uint32_t *__restrict__ lanes,
+                                                   GatherLayout gl) {
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
-    const double2_t a = *reinterpret_cast<const double2_t *>(a2 + 2 * i);
+    const double2_t a = *reinterpret_cast<const double2_t *>(a2 + 2 * gather_slot(gl, i));
     const int64_t p = lanes ? (int64_t)lanes[i] : i;
     double vxi = vx[p] + a.x * dtHalf;
     double vyi = vy[p] + a.y * dtHalf;
@@ -35,10 +36,11 @@ __global__ __launch_bounds__(TB) void k_kick_drift(int64_t n, const double *__re
 // BHA:429-432
 __global__ __launch_bounds__(TB) void k_kick(int64_t n, const double *__restrict__ a2,
                                              double *__restrict__ vx, double *__restrict__ vy,
-                                             double dtHalf, const uint32_t *__restrict__ lanes) {
+                                             double dtHalf, const uint32_t *__restrict__ lanes,
+                                             GatherLayout gl) {
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
-    const double2_t a = *reinterpret_cast<const double2_t *>(a2 + 2 * i);
+    const double2_t a = *reinterpret_cast<const double2_t *>(a2 + 2 * gather_slot(gl, i));
     const int64_t p = lanes ? (int64_t)lanes[i] : i;
     vx[p] = vx[p] + a.x * dtHalf;
     vy[p] = vy[p] + a.y * dtHalf;
@@ -67,13 +69,15 @@ __global__ __launch_bounds__(TB) void k_scatter_acc(int64_t n, const uint32_t *_
                                                     const double *__restrict__ a2,
                                                     double *__restrict__ ax,
                                                     double *__restrict__ ay,
-                                                    const uint32_t *__restrict__ lanes) {
+                                                    const uint32_t *__restrict__ lanes,
+                                                    GatherLayout gl) {
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
     const uint32_t o = cidx[lanes ? (int64_t)lanes[i] : i];
     if (o & CIDX_DEAD) return;  // a tombstone has no caller slot
-    ax[o] = a2[2 * i];
-    ay[o] = a2[2 * i + 1];
+    const int64_t g = gather_slot(gl, i);
+    ax[o] = a2[2 * g];
+    ay[o] = a2[2 * g + 1];
 }
 
 // heavy bodies: m > mergeMaxMass (BHA:474), live ones only; appended in any order (the
@@ -536,13 +540,13 @@ hipError_t compact_lanes(int64_t n, const uint32_t *lanes, const uint32_t *keep,
 }
 
 void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
-                double dtHalf, double dt, hipStream_t s, const uint32_t *lanes) {
-    if (n > 0) k_kick_drift<<<grid_for(n), TB, 0, s>>>(n, a2, x, y, vx, vy, dtHalf, dt, lanes);
+                double dtHalf, double dt, hipStream_t s, const uint32_t *lanes, GatherLayout gl) {
+    if (n > 0) k_kick_drift<<<grid_for(n), TB, 0, s>>>(n, a2, x, y, vx, vy, dtHalf, dt, lanes, gl);
 }
 
 void kick(int64_t n, const double *a2, double *vx, double *vy, double dtHalf, hipStream_t s,
-          const uint32_t *lanes) {
-    if (n > 0) k_kick<<<grid_for(n), TB, 0, s>>>(n, a2, vx, vy, dtHalf, lanes);
+          const uint32_t *lanes, GatherLayout gl) {
+    if (n > 0) k_kick<<<grid_for(n), TB, 0, s>>>(n, a2, vx, vy, dtHalf, lanes, gl);
 }
 
 void iota_u32(uint32_t *p, int64_t n, hipStream_t s) {
@@ -561,8 +565,8 @@ void scatter_to_caller(int64_t n, const uint32_t *cidx, int k, const double *con
 }
 
 void scatter_acc_to_caller(int64_t n, const uint32_t *cidx, const double *a2, double *ax,
-                           double *ay, hipStream_t s, const uint32_t *lanes) {
-    if (n > 0) k_scatter_acc<<<grid_for(n), TB, 0, s>>>(n, cidx, a2, ax, ay, lanes);
+                           double *ay, hipStream_t s, const uint32_t *lanes, GatherLayout gl) {
+    if (n > 0) k_scatter_acc<<<grid_for(n), TB, 0, s>>>(n, cidx, a2, ax, ay, lanes, gl);
 }
 
 void merge_candidates(int64_t n, const double *x, const double *y, const double *m,

@@ -89,7 +89,7 @@ __host__ __device__ constexpr int64_t level_off(int d) { return (((int64_t)1 << 
 
 // ---- selection ---------------------------------------------------------------------------
 __device__ __forceinline__ int64_t own_lane(const LetPieces &pc, int64_t t) {  // t-th own lane
-    return ((t / pc.sub) * pc.world + pc.rank) * pc.sub + t % pc.sub;
+    return (int64_t)pc.rank * pc.rounds * pc.sub + t;  // one contiguous range per rank
 }
 
 __global__ __launch_bounds__(TB) void k_let_mark(LetPieces pc, const double *__restrict__ x,
@@ -569,10 +569,11 @@ __global__ __launch_bounds__(TB) void k_let_kick_drift(int64_t n, const double *
                                                        double *__restrict__ vx,
                                                        double *__restrict__ vy, double dtHalf,
                                                        double dt,
-                                                       const uint32_t *__restrict__ lanes) {
+                                                       const uint32_t *__restrict__ lanes,
+                                                       GatherLayout gl) {
     const int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (q >= n) return;
-    const double4_t a = *reinterpret_cast<const double4_t *>(a4 + 4 * q);
+    const double4_t a = *reinterpret_cast<const double4_t *>(a4 + 4 * gather_slot(gl, q));
     const int64_t i = lanes ? (int64_t)lanes[q] : q;
     const double vxi = vx[i] + a.x * dtHalf;
     const double vyi = vy[i] + a.y * dtHalf;
@@ -586,10 +587,11 @@ __global__ __launch_bounds__(TB) void k_let_kick_drift(int64_t n, const double *
 __global__ __launch_bounds__(TB) void k_let_kick(int64_t n, const double *__restrict__ a4,
                                                  double *__restrict__ x, double *__restrict__ y,
                                                  double *__restrict__ vx, double *__restrict__ vy,
-                                                 double dtHalf, const uint32_t *__restrict__ lanes) {
+                                                 double dtHalf, const uint32_t *__restrict__ lanes,
+                                                 GatherLayout gl) {
     const int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (q >= n) return;
-    const double4_t a = *reinterpret_cast<const double4_t *>(a4 + 4 * q);
+    const double4_t a = *reinterpret_cast<const double4_t *>(a4 + 4 * gather_slot(gl, q));
     const int64_t i = lanes ? (int64_t)lanes[q] : q;
     vx[i] = vx[i] + a.x * dtHalf;
     vy[i] = vy[i] + a.y * dtHalf;
@@ -600,7 +602,7 @@ __global__ __launch_bounds__(TB) void k_let_kick(int64_t n, const double *__rest
 __global__ __launch_bounds__(TB) void k_let_fill_idle(int64_t n, const uint32_t *__restrict__ lanes,
                                                       const double *__restrict__ x,
                                                       const double *__restrict__ y,
-                                                      double *__restrict__ a4) {
+                                                      double *__restrict__ a4, GatherLayout gl) {
     const int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (q >= n) return;
     const int64_t i = lanes ? (int64_t)lanes[q] : q;
@@ -609,14 +611,14 @@ __global__ __launch_bounds__(TB) void k_let_fill_idle(int64_t n, const uint32_t 
     o.y = 0.0;
     o.z = x[i];
     o.w = y[i];
-    *reinterpret_cast<double4_t *>(a4 + 4 * q) = o;
+    *reinterpret_cast<double4_t *>(a4 + 4 * gather_slot(gl, q)) = o;
 }
 
 }  // namespace
 
 void let_fill_idle(int64_t n, const uint32_t *lanes, const double *x, const double *y, double *a4,
-                   hipStream_t s) {
-    if (n > 0) k_let_fill_idle<<<grid_for(n), TB, 0, s>>>(n, lanes, x, y, a4);
+                   hipStream_t s, GatherLayout gl) {
+    if (n > 0) k_let_fill_idle<<<grid_for(n), TB, 0, s>>>(n, lanes, x, y, a4, gl);
 }
 
 double let_include_gap2(const Geometry &g, double theta2, double soft2) {
@@ -710,13 +712,15 @@ hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, c
 }
 
 void let_kick_drift(int64_t n, const double *a4, double *x, double *y, double *vx, double *vy,
-                    double dtHalf, double dt, hipStream_t s, const uint32_t *lanes) {
-    if (n > 0) k_let_kick_drift<<<grid_for(n), TB, 0, s>>>(n, a4, x, y, vx, vy, dtHalf, dt, lanes);
+                    double dtHalf, double dt, hipStream_t s, const uint32_t *lanes,
+                    GatherLayout gl) {
+    if (n > 0)
+        k_let_kick_drift<<<grid_for(n), TB, 0, s>>>(n, a4, x, y, vx, vy, dtHalf, dt, lanes, gl);
 }
 
 void let_kick(int64_t n, const double *a4, double *x, double *y, double *vx, double *vy,
-              double dtHalf, hipStream_t s, const uint32_t *lanes) {
-    if (n > 0) k_let_kick<<<grid_for(n), TB, 0, s>>>(n, a4, x, y, vx, vy, dtHalf, lanes);
+              double dtHalf, hipStream_t s, const uint32_t *lanes, GatherLayout gl) {
+    if (n > 0) k_let_kick<<<grid_for(n), TB, 0, s>>>(n, a4, x, y, vx, vy, dtHalf, lanes, gl);
 }
 
 }  // namespace bh

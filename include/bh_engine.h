@@ -171,13 +171,18 @@ int bh_let_stats(const bh_engine *e, int64_t *out5);
 /* Enable/disable per-phase event timing (default off: no events in the hot loop). */
 int bh_set_profiling(bh_engine *e, int enabled);
 
-/* Multi-GPU force evaluation runs in BH_SHARD_ROUNDS rounds.  Round k of rank r evaluates
- * the Morton-order bodies [lo, hi) = [(k * world + r) * sub, + sub) clipped to n, with
- * sub = ceil(n / (world * rounds)) rounded up to whole wavefronts; the (ax, ay) of round k
- * are all-gathered in place (one ncclAllGather of 2 * sub doubles per rank) on a second
- * stream while round k + 1 is evaluated.  Host-only; used by the engine itself. */
+/* Multi-GPU force evaluation runs in BH_SHARD_ROUNDS rounds.  Rank r owns the contiguous
+ * lanes [r * rounds * sub, (r + 1) * rounds * sub) of the Hilbert wave order (one spatial
+ * region: its locally essential tree has one halo), and round k evaluates its lanes
+ * [lo, hi) = [(r * rounds + k) * sub, + sub) clipped to n, with sub = ceil(n / (world * rounds))
+ * rounded up to whole wavefronts.  The accelerations of lane q are written to the exchange
+ * buffer at bh_gather_slot(n, world, q) = (k * world + r) * sub + i (q = (r * rounds + k) * sub
+ * + i): the pieces of round k are adjacent there and are all-gathered in place (one
+ * ncclAllGather per round) on a second stream while round k + 1 is evaluated.  Host-only; used
+ * by the engine itself. */
 #define BH_SHARD_ROUNDS 4
 int bh_shard_range(int64_t n, int rank, int world, int round, int64_t *lo, int64_t *hi);
+int64_t bh_gather_slot(int64_t n, int world, int64_t lane);
 
 /* Diagnostic: checks, on HIP device `device`, the traversal's reduced-range exact sequences
  * for sqrt(d2), 1/sqrt(d2) and 1/d2 (traverse.hip) bit-for-bit against the IEEE operations on

@@ -45,20 +45,28 @@ def test_default_params_match_config_kt():
 
 @pytest.mark.parametrize("n,world", [(0, 1), (1, 2), (7, 2), (1000, 3), (1_000_003, 8), (5, 8)])
 def test_shard_ranges_partition_the_bodies(n, world):
-    """Pieces (round k, rank r) tile [0, n) in the order k-major, r-minor, each a whole
-    number of wavefronts except the last non-empty one: round k's in-place all-gather
-    (ranks' pieces of one round are adjacent) covers exactly that round."""
+    """Pieces (rank r, round k) tile [0, n) in the order r-major, k-minor -- every rank owns one
+    contiguous range of lanes -- each a whole number of wavefronts except the last non-empty
+    one; in the exchange buffer the pieces of round k are adjacent (in-place all-gather) and
+    the slots are a permutation of the lanes."""
     pieces = []
-    for k in range(bh_amd.SHARD_ROUNDS):
-        for r in range(world):
+    for r in range(world):
+        for k in range(bh_amd.SHARD_ROUNDS):
             lo, hi = bh_amd.shard_range(n, r, world, k)
             assert 0 <= lo <= hi <= n
-            pieces.append((lo, hi))
-    assert pieces[0][0] == 0 and pieces[-1][1] == n
-    assert all(pieces[i][1] == pieces[i + 1][0] for i in range(len(pieces) - 1))
-    sub = pieces[0][1] - pieces[0][0]
+            pieces.append((r, k, lo, hi))
+    assert pieces[0][2] == 0 and pieces[-1][3] == n
+    assert all(pieces[i][3] == pieces[i + 1][2] for i in range(len(pieces) - 1))
+    sub = pieces[0][3] - pieces[0][2]
     assert sub % 64 == 0 or n <= 64
-    assert all(hi - lo in (sub, 0) or hi == n for lo, hi in pieces)
+    assert all(hi - lo in (sub, 0) or hi == n for _, _, lo, hi in pieces)
+    if n <= 5000:
+        slots = [bh_amd.gather_slot(n, world, q) for q in range(n)]
+        assert len(set(slots)) == n
+        for r, k, lo, hi in pieces:
+            if hi > lo:
+                assert bh_amd.gather_slot(n, world, lo) == (k * world + r) * sub
+                assert slots[lo:hi] == list(range(slots[lo], slots[lo] + hi - lo))
 
 
 def test_shard_range_rejects_bad_arguments():

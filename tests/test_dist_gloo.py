@@ -2,7 +2,8 @@
 
 The engine's multi-GPU step (engine.cpp `evaluate`, bh_create_dist) keeps the state replicated,
 builds the same tree on every rank and evaluates forces in BH_SHARD_ROUNDS rounds: in round k
-a rank evaluates its Morton-sorted piece bh_shard_range(n, rank, world, k), and the round's
+a rank evaluates its Morton-sorted piece bh_shard_range(n, rank, world, k) (each rank owns one
+contiguous range; the piece's slots in the buffer are bh_gather_slot), and the round's
 interleaved (ax, ay) pieces are all-gathered in place (RCCL on the GPU box, overlapping the
 next round) into the slot-indexed buffer, which is scattered back through the sort
 permutation.  This test runs exactly that decomposition with gloo in place of RCCL and the
@@ -69,18 +70,19 @@ def _worker(rank, world, port, out_dir):
         lo, hi = bh_amd.shard_range(n, rank, world, k)
         if hi > lo:
             ax, ay = ref.accelerations(subset=perm[lo:hi])  # this rank's piece of round k
-            a2[2 * lo:2 * hi:2] = ax
-            a2[2 * lo + 1:2 * hi:2] = ay
+            g = bh_amd.gather_slot(n, world, lo)  # the piece's slots in the exchange buffer
+            a2[2 * g:2 * (g + hi - lo):2] = ax
+            a2[2 * g + 1:2 * (g + hi - lo):2] = ay
         base = 2 * k * world * sub  # in place: rank r's piece sits at base + 2 * r * sub
         send = torch.from_numpy(a2[base + 2 * rank * sub:base + 2 * (rank + 1) * sub].copy())
         gathered = [torch.zeros(2 * sub, dtype=torch.float64) for _ in range(world)]
         dist.all_gather(gathered, send)
         a2[base:base + 2 * world * sub] = torch.cat(gathered).numpy()
-    a_sorted = a2
+    slots = np.array([bh_amd.gather_slot(n, world, q) for q in range(n)])
     full_ax = np.empty(n)
     full_ay = np.empty(n)
-    full_ax[perm] = a_sorted[0:2 * n:2]
-    full_ay[perm] = a_sorted[1:2 * n:2]
+    full_ax[perm] = a2[2 * slots]
+    full_ay[perm] = a2[2 * slots + 1]
     np.save(os.path.join(out_dir, f"ax{rank}.npy"), full_ax)
     np.save(os.path.join(out_dir, f"ay{rank}.npy"), full_ay)
     dist.barrier()
