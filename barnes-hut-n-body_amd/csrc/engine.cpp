@@ -158,7 +158,12 @@ struct bh_engine {
     GatherLayout a2_layout{0, 1, 1};     // ... at the lane's gather slot (multi-rank rounds)
 
     // multi-rank locally essential tree (let.hip): subset state and tree workspace
-    bool let_on = true;         // BH_LET=0 in the environment: the replicated build
+    // BH_LET unset: LET builds from 4 ranks up (at 2 ranks the subset is over half the bodies
+    // and the selection / exchange / copy outweigh the smaller build: solo C4 step 10.45 ms
+    // with LET against 10.15 replicated; 4 ranks 6.07 vs 6.82, 8 ranks 4.03 vs 5.15);
+    // BH_LET=1 at any world size, BH_LET=0 never
+    bool let_on = true;
+    bool let_forced = false;
     int let_age = 0;            // LET builds since the last full build
     int64_t let_builds = 0, full_builds = 0, let_last_sub = 0;
     int64_t let_known = 0;       // largest subset of the last bh_step call (0: unknown)
@@ -603,6 +608,8 @@ TreeBuffers let_tree_buffers(bh_engine *e) {
     return b;
 }
 
+bool let_active(const bh_engine *e) { return e->let_on && (e->let_forced || e->world >= 4); }
+
 // Stream of round k (even: the engine's stream; odd: stream2, started after the build).
 int round_streams(bh_engine *e) {
     if (!e->stream2) {
@@ -736,7 +743,8 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
     e->a2_pos = false;
     // (the pieces are ranges of the slot order: spatially compact only once a full build has
     // put the state into Morton order -- after a reset it is the caller's order)
-    if (allow_let && !visits && (e->comm || e->group || e->solo) && e->let_on && e->p.theta != 0.0 &&
+    if (allow_let && !visits && (e->comm || e->group || e->solo) && let_active(e) &&
+        e->p.theta != 0.0 &&
         e->st_morton && e->let_age < BH_LET_REFRESH) {
         bool done = false;
         TRY(evaluate_let(e, &done));
@@ -1094,7 +1102,10 @@ int engine_init(bh_engine *e, const bh_params *p, int device) {
     e->p = *p;
     TRY(make_geometry(e->p, e->geo, e->err));
     e->device = device;
-    if (const char *v = std::getenv("BH_LET")) e->let_on = std::strcmp(v, "0") != 0;
+    if (const char *v = std::getenv("BH_LET")) {
+        e->let_on = std::strcmp(v, "0") != 0;
+        e->let_forced = std::strcmp(v, "1") == 0;
+    }
     HIPCHK(e, hipSetDevice(device));
     HIPCHK(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     TRY(dev_alloc(e, e->scalars, 16));
@@ -1375,7 +1386,7 @@ int bh_step(bh_engine *e, int32_t k) {
     HIPCHK(e, hipSetDevice(e->device));
     const bool may_merge = k > 0 && e->n > 1 && e->p.merge_min_dist > 0.0 && e->heavy_possible;
     // a multi-rank call with LET builds may have to be replayed with a larger subset capacity
-    const bool may_let = k > 0 && e->n > 0 && (e->comm || e->group || e->solo) && e->let_on &&
+    const bool may_let = k > 0 && e->n > 0 && (e->comm || e->group || e->solo) && let_active(e) &&
                          e->p.theta != 0.0;
     if (may_merge || may_let) TRY(snapshot(e));
     int let_replays = 0;

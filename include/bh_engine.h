@@ -164,8 +164,9 @@ int bh_traversal_counters(const bh_engine *e, int64_t *out5);
  * builds since the engine was created, out5[2] bodies in the largest LET subset of the last
  * bh_step call (the cells this rank's bodies can open), out5[3] node records of the last LET
  * tree, out5[4] bh_step calls replayed because a subset outgrew its capacity (the capacity
- * follows the previous call's subsets, so the build needs no host round trip).  Setting
- * BH_LET=0 in the environment before creating an engine keeps every build full. */
+ * follows the previous call's subsets, so the build needs no host round trip).  LET builds run
+ * from 4 ranks up; BH_LET=1 in the environment before creating an engine enables them at any
+ * world size, BH_LET=0 keeps every build full. */
 int bh_let_stats(const bh_engine *e, int64_t *out5);
 
 /* Enable/disable per-phase event timing (default off: no events in the hot loop). */

@@ -730,11 +730,12 @@ def _let_scene(name):
 @pytest.mark.parametrize("world,scene,theta", [
     (2, "c2", 0.5), (4, "c2", 0.3), (8, "c2", 1.0), (3, "disks", 0.5), (8, "cloud", 0.5),
     (5, "cloud", 0.7), (4, "jitter", 0.5), (3, "outside", 0.5)])
-def test_let_build_multi_rank_vs_single(world, scene, theta):
+def test_let_build_multi_rank_vs_single(world, scene, theta, monkeypatch):
     """The sharded build (let.hip): each rank builds only the cells its bodies can open plus the
     top from the exchanged cell values, and its forces -- hence every rank's state -- equal the
     single-GPU engine's bit for bit.  Two bh_step calls (the LET builds run in the middle of a
     call; the last build of a call is the full tree)."""
+    monkeypatch.setenv("BH_LET", "1")  # LET builds at every world size (default: from 4 ranks)
     arrs = _let_scene(scene)
     params = bh_amd.default_params(theta=theta, merge_min_dist=0.0 if scene == "jitter" else 8.0)
     single = bh_amd.Engine(params, device=0)
@@ -804,11 +805,12 @@ def test_let_subset_overflow_replays_the_call():
             assert bits_equal(got[r][k], want[k]), f"rank {r}: {name}"
 
 
-def test_let_jitter_log_overflow_switches_to_the_wide_exchange():
+def test_let_jitter_log_overflow_switches_to_the_wide_exchange(monkeypatch):
     """Every body a coincident pair: each build moves 30 000 own bodies per rank, past the
     16 384-entry jitter log, so every rank sees the overflow, the call is replayed with the
     positions sent beside the accelerations -- and the states still equal the single-GPU
     engine's bit for bit (the narrow exchange ran before the overflow)."""
+    monkeypatch.setenv("BH_LET", "1")
     base = scenes.uniform(30_000, 0.5, seed=31)
     rng = np.random.default_rng(32)
     perm = rng.permutation(2 * len(base[0]))
