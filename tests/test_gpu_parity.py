@@ -757,6 +757,24 @@ def test_let_build_multi_rank_vs_single(world, scene, theta, monkeypatch):
             assert bits_equal(got[r][k], want[k]), f"rank {r}: {name}"
 
 
+def test_let_refresh_full_build_inside_a_call():
+    """20 steps in one call = 40 builds: a full build sorts the caller's order, 32 LET builds,
+    the refresh full build (the replicas' slot order), 5 more LET builds, the call's last build
+    full -- every rank's state equals the single-GPU engine's bit for bit."""
+    arrs = scenes.uniform(120_000, 0.5, seed=41)
+    params = bh_amd.default_params(theta=0.5)
+    single = bh_amd.Engine(params, device=0)
+    single.reset_bodies(*arrs)
+    single.step(20)
+    want = single.get_bodies()
+    single.close()
+    got, stats = _run_group(4, params, arrs, (20,))
+    for r in range(4):
+        assert stats[r]["let_builds"] == 37 and stats[r]["full_builds"] == 3, stats[r]
+        for k, name in enumerate(FIELDS):
+            assert bits_equal(got[r][k], want[k]), f"rank {r}: {name}"
+
+
 def test_let_subset_overflow_replays_the_call():
     """The LET subset capacity follows the previous call's subsets (no host round trip per
     build): after a reset to a scene with 4x the bodies every rank's subset outgrows it, every
