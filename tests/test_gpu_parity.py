@@ -556,9 +556,12 @@ def test_theta0_direct_c5_sampled():
     assert bits_equal(ax, rax) and bits_equal(ay, ray)
 
 
-def test_rccl_path_single_rank():
+@pytest.mark.parametrize("let", ["0", "1"])
+def test_rccl_path_single_rank(let, monkeypatch):
     """The multi-GPU evaluation path (shard range, in-place ncclAllGather of (ax, ay) over an
-    RCCL communicator) on one rank: bit-identical to the oracle, tree walk and theta = 0."""
+    RCCL communicator; with BH_LET=1 also the LET builds and the ncclAllGather of the cell
+    tables) on one rank: bit-identical to the oracle, tree walk and theta = 0."""
+    monkeypatch.setenv("BH_LET", let)
     uid = bh_amd.comm_unique_id()
     arrs = scenes.config_scene("c1_code")
     for theta in (0.5, 0.0):
