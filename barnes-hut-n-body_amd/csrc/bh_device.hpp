@@ -166,13 +166,18 @@ hipError_t lane_order(const TreeBuffers &b, int64_t n, int J, bool refresh, uint
 // kick (optional, one GPU, no visit counting): the KDK update of the evaluated slots is applied
 // in the kernel's epilogue instead of writing a2 -- KICK_DRIFT = k_kick_drift (BHA:414-422),
 // KICK_ONLY = k_kick (BHA:429-432), same operations in the same order.
-// KICK_POS (multi-rank LET evaluation, let.hip): no kick; the lane writes (ax, ay, x, y) to
-// a2[4q..4q+3] -- x, y as the build left them (jitter), for the peers' replicated states.
-enum KickMode { KICK_NONE = 0, KICK_DRIFT = 1, KICK_ONLY = 2, KICK_POS = 3 };
+// KICK_OWN_DRIFT / KICK_OWN_ONLY (multi-rank LET, owner integration): the lane applies
+// k_kick_drift / k_kick to its own body in the replicated state (velocities at slot rep[q]) and
+// writes the body's new position (x + v dt, or x as the build left it) to a2[2q..2q+1] -- the
+// peers take positions from the exchange, velocities once per call (engine.cpp).
+enum KickMode {
+    KICK_NONE = 0, KICK_DRIFT = 1, KICK_ONLY = 2, KICK_OWN_DRIFT = 3, KICK_OWN_ONLY = 4
+};
 struct KickArgs {
     KickMode mode;
-    double *vx, *vy;  // x, y are the traversal's own position arrays
+    double *vx, *vy;  // x, y are the traversal's own position arrays (KICK_OWN_*: replicated v)
     double dtHalf, dt;
+    const uint32_t *rep = nullptr;  // KICK_OWN_*: lane -> replicated slot (null: the lane)
 };
 // Diagnostic counters of the counting walk (all per evaluation): per body, the non-empty
 // nodes visited (BHA:216 passed) and the point-force contributions (accepted internal nodes
@@ -220,11 +225,8 @@ hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_ba
 // childless records every local body provably accepts.  See let.hip.
 constexpr int LET_P = 8;
 constexpr int64_t LET_CELLS = (int64_t)1 << (2 * LET_P);
-// an exchange table: LET_CELLS cell records, one status record (cnt: 1 = subset overflow, 2 =
-// jitter log overflow; tag: jitter log entries) and the jitter log -- (x, y, -, slot) of the
-// rank's own bodies whose position the build moved (BHA:146-151), so the lanes send only (ax, ay)
-constexpr int64_t LET_JLOG = 16384;
-constexpr int64_t LET_TSTRIDE = LET_CELLS + 1 + LET_JLOG;
+// an exchange table: LET_CELLS cell records + one status record (cnt = subset overflow)
+constexpr int64_t LET_TSTRIDE = LET_CELLS + 1;
 struct __attribute__((aligned(32))) LetCell {
     double comX, comY, mass;
     uint32_t cnt;  // in-tree bodies of the cell, saturated at 2 (0 empty, 1 leaf, 2 internal)
@@ -269,25 +271,21 @@ hipError_t let_select(const BodyState &st, const Geometry &g, const LetPieces &p
 // after tree_build over the subset: the own cells' exchange table
 hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const TreeBuffers &tb,
                      hipStream_t s);
-// after the subset build: the own bodies the build moved, into the table's jitter log
-hipError_t let_jitter_log(int64_t n_sub, int64_t n, const BodyState &st, const LetBufs &L,
-                          const TreeBuffers &tb, hipStream_t s);
-// after the exchange: every rank's logged positions into the replicated state
-hipError_t let_jitter_apply(int world, const LetBufs &L, BodyState st, hipStream_t s);
-// after the exchange (L.tables, LET_TSTRIDE per rank): any rank's overflow -> scal[4] (a jitter
-// log overflow also -> scal[6]: the engine switches to the wide exchange); top
+// after the exchange (L.tables, LET_TSTRIDE per rank): any rank's overflow -> scal[4]; top
 // levels, layout, node array, lane map; tree size posc[LET_CELLS]
 hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, const LetBufs &L,
                         const TreeBuffers &tb, uint32_t *scal, hipStream_t s);
-// KDK of all replicated slots from a2 = (ax, ay, x, y) per lane (BHA:410-432)
-void let_kick_drift(int64_t n, const double *a4, double *x, double *y, double *vx, double *vy,
-                    double dtHalf, double dt, hipStream_t s, const uint32_t *lanes,
-                    GatherLayout gl);
-void let_kick(int64_t n, const double *a4, double *x, double *y, double *vx, double *vy,
-              double dtHalf, hipStream_t s, const uint32_t *lanes, GatherLayout gl);
-// bh_create_solo (measurement): every lane (0, 0, x, y) before the own pieces are evaluated
-void let_fill_idle(int64_t n, const uint32_t *lanes, const double *x, const double *y, double *a4,
-                   hipStream_t s, GatherLayout gl);
+// owner integration: a2 (gather slots) holds every lane's (x, y) -> the replicated state; the
+// solo fill writes the current positions of all lanes first
+void let_set_pos(int64_t n, const uint32_t *lanes, const double *a2, GatherLayout gl, double *x,
+                 double *y, hipStream_t s);
+void let_fill_pos(int64_t n, const uint32_t *lanes, const double *x, const double *y, double *a2,
+                  GatherLayout gl, hipStream_t s);
+// velocity exchange of the owner integration: own lanes' (vx, vy) into a2, all lanes' back out
+void let_pack_vel(const LetPieces &pc, const double *vx, const double *vy, double *a2,
+                  GatherLayout gl, hipStream_t s);
+void let_unpack_vel(int64_t n, const uint32_t *lanes, const double *a2, GatherLayout gl,
+                    double *vx, double *vy, hipStream_t s);
 
 // ---- launchers (direct.hip): theta = 0 all-pairs ---------------------------------
 // Non-empty leaves of the last tree in pre-order (the reference's theta = 0 summation order).

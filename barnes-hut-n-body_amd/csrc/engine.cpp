@@ -170,8 +170,8 @@ struct bh_engine {
     int64_t let_overflows = 0;   // calls replayed for a subset overflow
     uint32_t s_spl_nb = 0;       // splitters of the last LET build (subset bucket sort)
     bool st_morton = false;     // slots are in the Morton order of a full build (not caller order)
-    bool a2_pos = false;        // the last evaluation wrote (ax, ay, x, y) per lane
-    bool let_wide = false;      // a jitter log overflowed: lanes send (ax, ay, x, y)
+    bool vel_stale = false;     // LET evaluations integrated only own bodies: velocities of the
+                                // others are exchanged before the next full build
     LetBufs L{};
     int64_t let_cap = 0;        // n capacity of the per-body LET arrays
     int64_t let_sub_cap = 0;    // subset capacity of the subset tree workspace
@@ -303,8 +303,7 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         const int64_t padded = (e->comm || e->group || e->solo) ? shard_sub(cap, e->world, BH_SHARD_ROUNDS) *
                                              e->world * BH_SHARD_ROUNDS
                                        : cap;
-        // multi-rank: (ax, ay, x, y) per slot for the LET evaluation
-        TRY(dev_alloc(e, e->a2, ((e->comm || e->group || e->solo) ? 4 : 2) * padded));
+        TRY(dev_alloc(e, e->a2, 2 * padded));
         TRY(dev_alloc(e, e->ax, cap));
         TRY(dev_alloc(e, e->ay, cap));
         TRY(dev_alloc(e, e->keys, cap));
@@ -621,9 +620,60 @@ int round_streams(bh_engine *e) {
     return BH_OK;
 }
 
-// One LET evaluation; *done = false when it does not apply (the caller builds the full tree).
-int evaluate_let(bh_engine *e, bool *done) {
+// Velocities after owner-integrated LET evaluations: every rank holds current velocities of its
+// own bodies only; before a full build (which permutes and re-assigns the bodies) the owners'
+// (vx, vy) are all-gathered once, in the same rounds and slots as the forces.
+int sync_velocities(bh_engine *e) {
+    if (!e->vel_stale) return BH_OK;
+    e->vel_stale = false;
+    const int64_t n = e->n;
+    if (n <= 0 || e->solo) return BH_OK;  // solo: no peers (their bodies keep their velocities)
+    const int R = BH_SHARD_ROUNDS;
+    const int64_t sub = shard_sub(n, e->world, R);
+    const uint32_t *lanes = e->lanes_valid ? e->lanes : nullptr;
+    const LetPieces pc{n, sub, e->world, e->rank, R, lanes};
+    const GatherLayout gl{sub, e->world, R};
+    if (e->group) {  // peers are done reading our previous pieces
+        e->group->barrier();
+        for (bh_engine *peer : e->group->members)
+            if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->gathered_ev, 0));
+    }
+    let_pack_vel(pc, e->st.vx, e->st.vy, e->a2, gl, e->stream);
+    HIPCHK(e, hipGetLastError());
+    HIPCHK(e, hipEventRecord(e->round_ev[0], e->stream));
+    HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[0], 0));
+    if (e->group) e->group->barrier();
+    for (int k = 0; k < R; ++k) {
+        double *piece = e->a2 + 2 * ((int64_t)k * e->world) * sub;
+        if (e->comm) {
+            NCCLCHK(e, ncclAllGather(piece + 2 * e->rank * sub, piece, (size_t)(2 * sub),
+                                     ncclDouble, e->comm, e->comm_stream));
+        } else {
+            for (int q = 0; q < e->world; ++q) {
+                if (q == e->rank) continue;
+                bh_engine *peer = e->group->members[q];
+                if (k == 0) HIPCHK(e, hipStreamWaitEvent(e->comm_stream, peer->round_ev[0], 0));
+                const int64_t off = 2 * ((int64_t)k * e->world + q) * sub;
+                HIPCHK(e, hipMemcpyAsync(e->a2 + off, peer->a2 + off, sizeof(double) * 2 * sub,
+                                         hipMemcpyDeviceToDevice, e->comm_stream));
+            }
+        }
+    }
+    HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
+    HIPCHK(e, hipStreamWaitEvent(e->stream, e->gathered_ev, 0));
+    let_unpack_vel(n, lanes, e->a2, gl, e->st.vx, e->st.vy, e->stream);
+    HIPCHK(e, hipGetLastError());
+    return BH_OK;
+}
+
+// One LET evaluation with its integration (kick: KICK_DRIFT after a(t), KICK_ONLY after
+// a(t+dt)); *done = false when it does not apply (the caller builds the full tree).  Each lane
+// kicks its own body (velocity in the replicated state, owner only) and sends the body's new
+// position -- drifted, or as the build left it (jitter, BHA:146-151) -- so every replica takes
+// all positions from the exchange.
+int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     *done = false;
+    if (kick != KICK_DRIFT && kick != KICK_ONLY) return BH_OK;
     const int64_t n = e->n;
     const double gap2 = let_include_gap2(e->geo, e->p.theta * e->p.theta, e->p.soft2);
     if (gap2 < 0.0 || n <= 0) return BH_OK;
@@ -662,7 +712,6 @@ int evaluate_let(bh_engine *e, bool *done) {
     HIPCHK(e, tree_build(sb, n_sub, e->geo, e->stream));
     e->s_spl_nb = sort_buckets(n_sub);  // k_prep wrote this build's splitters
     HIPCHK(e, let_table(n_sub, e->geo, e->L, sb, e->stream));
-    if (!e->let_wide) HIPCHK(e, let_jitter_log(n_sub, n, e->st, e->L, sb, e->stream));
     const size_t tbytes = sizeof(LetCell) * (size_t)LET_TSTRIDE;
     if (e->comm) {
         NCCLCHK(e, ncclAllGather(e->L.table, e->L.tables, tbytes, ncclUint8, e->comm, e->stream));
@@ -683,18 +732,15 @@ int evaluate_let(bh_engine *e, bool *done) {
                                      hipMemcpyDeviceToDevice, e->stream));
         }
     }
-    if (!e->let_wide) HIPCHK(e, let_jitter_apply(e->world, e->L, e->st, e->stream));
     HIPCHK(e, let_assemble(n_sub, e->geo, pc, e->L, sb, e->scalars, e->stream));
     TRY(mark(e, 0));
     const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};
-    // (ax, ay) per lane, the jittered positions travelled in the logs; wide: (ax, ay, x, y)
-    const int W = e->let_wide ? 4 : 2;
-    const KickArgs ka{e->let_wide ? KICK_POS : KICK_NONE, nullptr, nullptr, 0.0, 0.0};
+    const int W = 2;  // (x, y) per lane
+    const KickArgs ka{kick == KICK_DRIFT ? KICK_OWN_DRIFT : KICK_OWN_ONLY, e->st.vx, e->st.vy,
+                      e->p.dt * 0.5, e->p.dt, lanes};  // BHA:412
     const GatherLayout gl{sub, e->world, R};
-    if (e->solo && e->let_wide) let_fill_idle(n, lanes, e->st.x, e->st.y, e->a2, e->stream, gl);
-    if (e->solo && !e->let_wide)  // measurement: the peers' bodies get no force
-        HIPCHK(e, hipMemsetAsync(e->a2, 0, sizeof(double) * 2 * (size_t)(sub * e->world * R),
-                                 e->stream));
+    if (e->solo)  // measurement: the peers' bodies keep their positions
+        let_fill_pos(n, lanes, e->st.x, e->st.y, e->a2, gl, e->stream);
     TRY(round_streams(e));
     for (int k = 0; k < R; ++k) {
         int64_t lo = 0, hi = 0;
@@ -728,7 +774,10 @@ int evaluate_let(bh_engine *e, bool *done) {
     HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
     HIPCHK(e, hipStreamWaitEvent(e->stream, e->gathered_ev, 0));
     TRY(mark(e, 4));
-    e->a2_pos = e->let_wide;
+    let_set_pos(n, lanes, e->a2, gl, e->st.x, e->st.y, e->stream);  // every body's new position
+    HIPCHK(e, hipGetLastError());
+    TRY(mark(e, 2));
+    e->vel_stale = true;
     e->a2_lanes = lanes;
     e->a2_layout = gl;
     e->tree_valid = false;  // the full tree was not built
@@ -740,22 +789,23 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
              bool allow_let = false, bool *let_used = nullptr) {
     if (fused) *fused = false;
     if (let_used) *let_used = false;
-    e->a2_pos = false;
     // (the pieces are ranges of the slot order: spatially compact only once a full build has
     // put the state into Morton order -- after a reset it is the caller's order)
     if (allow_let && !visits && (e->comm || e->group || e->solo) && let_active(e) &&
         e->p.theta != 0.0 &&
         e->st_morton && e->let_age < BH_LET_REFRESH) {
         bool done = false;
-        TRY(evaluate_let(e, &done));
+        TRY(evaluate_let(e, kick, &done));
         if (done) {
             ++e->let_age;
             if (let_used) *let_used = true;
+            if (fused) *fused = true;  // integrated in the evaluation
             return BH_OK;
         }
     }
     e->let_age = 0;
     const int64_t n = e->n;
+    TRY(sync_velocities(e));  // before the full build permutes the state
     TRY(mark(e, -1));
     TRY(build(e));
     TRY(mark(e, 0));
@@ -977,6 +1027,7 @@ int restore(bh_engine *e) {
     e->heavy_possible = true;
     e->tree_valid = false;
     e->st_morton = false;
+    e->vel_stale = false;  // the snapshot is a consistent replica
     return BH_OK;
 }
 
@@ -988,27 +1039,19 @@ int step_once(bh_engine *e, bool last) {
     const double dtHalf = e->p.dt * 0.5;  // BHA:412
     if (n > 0) {
         bool fused = false;  // one GPU: the kicks ride in the traversal's epilogue
-        bool let = false;    // multi-rank LET: a2 holds (ax, ay, x, y), positions included
-        TRY(evaluate(e, nullptr, KICK_DRIFT, &fused, true, &let));  // a(t)
+        // (multi-rank LET evaluations integrate their own bodies too: fused)
+        TRY(evaluate(e, nullptr, KICK_DRIFT, &fused, true));  // a(t)
         if (!fused) {
             TRY(mark(e, -1));
-            if (let && e->a2_pos)
-                let_kick_drift(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->p.dt,
-                               e->stream, e->a2_lanes, e->a2_layout);
-            else
-                kick_drift(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->p.dt,
-                           e->stream, e->a2_lanes, e->a2_layout);
+            kick_drift(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->p.dt,
+                       e->stream, e->a2_lanes, e->a2_layout);
             HIPCHK(e, hipGetLastError());
             TRY(mark(e, 2));
         }
-        TRY(evaluate(e, nullptr, KICK_ONLY, &fused, !last, &let));  // a(t+dt)
+        TRY(evaluate(e, nullptr, KICK_ONLY, &fused, !last));  // a(t+dt)
         if (!fused) {
             TRY(mark(e, -1));
-            if (let && e->a2_pos)
-                let_kick(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->stream,
-                         e->a2_lanes, e->a2_layout);
-            else
-                kick(n, e->a2, e->st.vx, e->st.vy, dtHalf, e->stream, e->a2_lanes, e->a2_layout);
+            kick(n, e->a2, e->st.vx, e->st.vy, dtHalf, e->stream, e->a2_lanes, e->a2_layout);
             HIPCHK(e, hipGetLastError());
             TRY(mark(e, 2));
         }
@@ -1378,6 +1421,7 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     e->spl_nb = 0;          // other bodies: the first build sorts from scratch
     e->lanes_valid = false;
     e->st_morton = false;
+    e->vel_stale = false;
     return BH_OK;
 }
 
@@ -1396,16 +1440,14 @@ int bh_step(bh_engine *e, int32_t k) {
         // the subset splitters are trusted only within a call (another scene after a reset
         // would put most of a subset into one bucket): the first LET build sorts with rocprim
         e->s_spl_nb = 0;
-        HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, 6 * sizeof(uint32_t), e->stream));
+        HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, 5 * sizeof(uint32_t), e->stream));
         e->removed.clear();
         e->merge_ran = false;
         for (int32_t s = 0; s < k; ++s) TRY(step_once(e, s + 1 == k));
         HIPCHK(e, hipStreamSynchronize(e->stream));
-        if (may_let) {  // LET subset sizes of this call: [4] some rank overflowed, [5] largest,
-                        // [6] a jitter log overflowed (every rank: the wide exchange from now on)
-            uint32_t ls[3] = {0, 0, 0};
+        if (may_let) {  // LET subset sizes of this call: [4] some rank overflowed, [5] largest
+            uint32_t ls[2] = {0, 0};
             HIPCHK(e, hipMemcpy(ls, e->scalars + 4, sizeof(ls), hipMemcpyDeviceToHost));
-            if (ls[2]) e->let_wide = true;
             if (ls[1] > 0) {
                 e->let_last_sub = ls[1];
                 e->let_known = std::max<int64_t>(ls[1], ls[0] ? e->let_known : 1);

@@ -17,10 +17,10 @@
 //     (32 B per cell, one all-gather), and lays the tree out in pre-order: top nodes, local
 //     subtrees copied with shifted `next`, remote cells as childless records.
 // The traversal kernel then walks this array unchanged (traverse.hip), one lane per own body.
-// Jitter (BHA:146-151) mutates positions during the build: each rank logs its own bodies that
-// the build moved into its exchange table, and every replica takes those positions before the
-// kick; the lanes send only (ax, ay).  A log overflow switches the engine to the wide exchange
-// -- the lanes send (ax, ay, x, y) and every replica takes the owners' positions (let_kick*).
+// Jitter (BHA:146-151) mutates positions during the build: each lane kicks its own body in the
+// traversal's epilogue and sends the body's new position (x + v dt, or x as the build left it),
+// and every replica takes all positions from the exchange (let_set_pos); velocities stay with
+// the owners until the next full build (engine.cpp sync_velocities).
 #include <algorithm>
 #include <cmath>
 
@@ -214,42 +214,8 @@ __global__ __launch_bounds__(TB) void k_let_pad(int64_t S, const uint32_t *__res
 
 __global__ void k_let_overflow(int world, const LetCell *__restrict__ tables,
                                uint32_t *__restrict__ scal) {
-    for (int q = 0; q < world; ++q) {
-        const uint32_t st = tables[(int64_t)q * LET_TSTRIDE + LET_CELLS].cnt;
-        if (st) scal[4] = 1u;
-        if (st & 2u) scal[6] = 1u;
-    }
-}
-
-// own bodies whose position the subset build changed (jitter): logged for the other replicas
-__global__ __launch_bounds__(TB) void k_let_jlog(int64_t n_sub, int64_t n, BodyState sub,
-                                                 const double *__restrict__ x,
-                                                 const double *__restrict__ y,
-                                                 const uint8_t *__restrict__ own,
-                                                 LetCell *__restrict__ table) {
-    const int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (a >= n_sub) return;
-    const int64_t i = (int64_t)__double_as_longlong(sub.vx[a]);
-    if (i < 0 || i >= n || !own[i]) return;
-    const double px = sub.x[a], py = sub.y[a];
-    if (__double_as_longlong(px) == __double_as_longlong(x[i]) &&
-        __double_as_longlong(py) == __double_as_longlong(y[i]))
-        return;
-    const uint32_t k = atomicAdd(&table[LET_CELLS].tag, 1u);
-    if (k < (uint32_t)LET_JLOG) table[LET_CELLS + 1 + k] = LetCell{px, py, 0.0, (uint32_t)i, 0u};
-    else atomicOr(&table[LET_CELLS].cnt, 2u);  // too many: the wide exchange takes over
-}
-
-__global__ __launch_bounds__(TB) void k_let_japply(int world, const LetCell *__restrict__ tables,
-                                                   double *__restrict__ x, double *__restrict__ y) {
-    const int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (t >= (int64_t)world * LET_JLOG) return;
-    const int64_t q = t / LET_JLOG, k = t % LET_JLOG;
-    const LetCell *tq = tables + q * LET_TSTRIDE;
-    if (k >= (int64_t)min(tq[LET_CELLS].tag, (uint32_t)LET_JLOG)) return;
-    const LetCell v = tq[LET_CELLS + 1 + k];
-    x[v.cnt] = v.comX;
-    y[v.cnt] = v.comY;
+    for (int q = 0; q < world; ++q)
+        if (tables[(int64_t)q * LET_TSTRIDE + LET_CELLS].cnt) scal[4] = 1u;
 }
 
 // a tree larger than its array can only come from a broken invariant: no walk, and the call is
@@ -560,65 +526,61 @@ __global__ __launch_bounds__(TB) void k_let_lanes(LetPieces pc, uint32_t n_sub,
     lanes[q] = s < n_sub ? s : 0u;
 }
 
-typedef double double4_t __attribute__((ext_vector_type(4)));
-
-// BHA:410-422 with the owner's (possibly jittered) position: x = x_b + v dt
-__global__ __launch_bounds__(TB) void k_let_kick_drift(int64_t n, const double *__restrict__ a4,
-                                                       double *__restrict__ x,
-                                                       double *__restrict__ y,
-                                                       double *__restrict__ vx,
-                                                       double *__restrict__ vy, double dtHalf,
-                                                       double dt,
-                                                       const uint32_t *__restrict__ lanes,
-                                                       GatherLayout gl) {
+__global__ __launch_bounds__(TB) void k_let_set_pos(int64_t n, const uint32_t *__restrict__ lanes,
+                                                    const double *__restrict__ a2, GatherLayout gl,
+                                                    double *__restrict__ x, double *__restrict__ y) {
     const int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (q >= n) return;
-    const double4_t a = *reinterpret_cast<const double4_t *>(a4 + 4 * gather_slot(gl, q));
-    const int64_t i = lanes ? (int64_t)lanes[q] : q;
-    const double vxi = vx[i] + a.x * dtHalf;
-    const double vyi = vy[i] + a.y * dtHalf;
-    vx[i] = vxi;
-    vy[i] = vyi;
-    x[i] = a.z + vxi * dt;
-    y[i] = a.w + vyi * dt;
+    const int64_t i = lanes ? (int64_t)lanes[q] : q, g = gather_slot(gl, q);
+    x[i] = a2[2 * g];
+    y[i] = a2[2 * g + 1];
 }
 
-// BHA:429-432; positions = the owner's after the build
-__global__ __launch_bounds__(TB) void k_let_kick(int64_t n, const double *__restrict__ a4,
-                                                 double *__restrict__ x, double *__restrict__ y,
-                                                 double *__restrict__ vx, double *__restrict__ vy,
-                                                 double dtHalf, const uint32_t *__restrict__ lanes,
-                                                 GatherLayout gl) {
+__global__ __launch_bounds__(TB) void k_let_fill_pos(int64_t n, const uint32_t *__restrict__ lanes,
+                                                     const double *__restrict__ x,
+                                                     const double *__restrict__ y,
+                                                     double *__restrict__ a2, GatherLayout gl) {
     const int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (q >= n) return;
-    const double4_t a = *reinterpret_cast<const double4_t *>(a4 + 4 * gather_slot(gl, q));
-    const int64_t i = lanes ? (int64_t)lanes[q] : q;
-    vx[i] = vx[i] + a.x * dtHalf;
-    vy[i] = vy[i] + a.y * dtHalf;
-    x[i] = a.z;
-    y[i] = a.w;
+    const int64_t i = lanes ? (int64_t)lanes[q] : q, g = gather_slot(gl, q);
+    a2[2 * g] = x[i];
+    a2[2 * g + 1] = y[i];
 }
 
-__global__ __launch_bounds__(TB) void k_let_fill_idle(int64_t n, const uint32_t *__restrict__ lanes,
-                                                      const double *__restrict__ x,
-                                                      const double *__restrict__ y,
-                                                      double *__restrict__ a4, GatherLayout gl) {
-    const int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (q >= n) return;
-    const int64_t i = lanes ? (int64_t)lanes[q] : q;
-    double4_t o;
-    o.x = 0.0;
-    o.y = 0.0;
-    o.z = x[i];
-    o.w = y[i];
-    *reinterpret_cast<double4_t *>(a4 + 4 * gather_slot(gl, q)) = o;
+__global__ __launch_bounds__(TB) void k_let_pack_vel(LetPieces pc, const double *__restrict__ vx,
+                                                     const double *__restrict__ vy,
+                                                     double *__restrict__ a2, GatherLayout gl) {
+    const int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (t >= (int64_t)pc.rounds * pc.sub) return;
+    const int64_t q = own_lane(pc, t);
+    if (q >= pc.n) return;
+    const int64_t i = pc.lanes ? (int64_t)pc.lanes[q] : q, g = gather_slot(gl, q);
+    a2[2 * g] = vx[i];
+    a2[2 * g + 1] = vy[i];
 }
 
 }  // namespace
 
-void let_fill_idle(int64_t n, const uint32_t *lanes, const double *x, const double *y, double *a4,
-                   hipStream_t s, GatherLayout gl) {
-    if (n > 0) k_let_fill_idle<<<grid_for(n), TB, 0, s>>>(n, lanes, x, y, a4, gl);
+void let_set_pos(int64_t n, const uint32_t *lanes, const double *a2, GatherLayout gl, double *x,
+                 double *y, hipStream_t s) {
+    if (n > 0) k_let_set_pos<<<grid_for(n), TB, 0, s>>>(n, lanes, a2, gl, x, y);
+}
+
+void let_fill_pos(int64_t n, const uint32_t *lanes, const double *x, const double *y, double *a2,
+                  GatherLayout gl, hipStream_t s) {
+    if (n > 0) k_let_fill_pos<<<grid_for(n), TB, 0, s>>>(n, lanes, x, y, a2, gl);
+}
+
+void let_pack_vel(const LetPieces &pc, const double *vx, const double *vy, double *a2,
+                  GatherLayout gl, hipStream_t s) {
+    const int64_t m = (int64_t)pc.rounds * pc.sub;
+    if (m > 0 && pc.n > 0) k_let_pack_vel<<<grid_for(m), TB, 0, s>>>(pc, vx, vy, a2, gl);
+}
+
+void let_unpack_vel(int64_t n, const uint32_t *lanes, const double *a2, GatherLayout gl,
+                    double *vx, double *vy, hipStream_t s) {
+    // the same copy as the positions' (lane's gather slot -> its body's slot)
+    if (n > 0) k_let_set_pos<<<grid_for(n), TB, 0, s>>>(n, lanes, a2, gl, vx, vy);
 }
 
 double let_include_gap2(const Geometry &g, double theta2, double soft2) {
@@ -674,18 +636,6 @@ hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const T
     return hipGetLastError();
 }
 
-hipError_t let_jitter_log(int64_t n_sub, int64_t n, const BodyState &st, const LetBufs &L,
-                          const TreeBuffers &tb, hipStream_t s) {
-    if (n_sub > 0)
-        k_let_jlog<<<grid_for(n_sub), TB, 0, s>>>(n_sub, n, tb.dst, st.x, st.y, L.own, L.table);
-    return hipGetLastError();
-}
-
-hipError_t let_jitter_apply(int world, const LetBufs &L, BodyState st, hipStream_t s) {
-    k_let_japply<<<grid_for((int64_t)world * LET_JLOG), TB, 0, s>>>(world, L.tables, st.x, st.y);
-    return hipGetLastError();
-}
-
 hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, const LetBufs &L,
                         const TreeBuffers &tb, uint32_t *scal, hipStream_t s) {
     k_let_overflow<<<1, 1, 0, s>>>(pc.world, L.tables, scal);
@@ -709,18 +659,6 @@ hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, c
     if (own_lanes > 0 && pc.n > 0)
         k_let_lanes<<<grid_for(own_lanes), TB, 0, s>>>(pc, (uint32_t)n_sub, L.subpos, L.lanes);
     return hipGetLastError();
-}
-
-void let_kick_drift(int64_t n, const double *a4, double *x, double *y, double *vx, double *vy,
-                    double dtHalf, double dt, hipStream_t s, const uint32_t *lanes,
-                    GatherLayout gl) {
-    if (n > 0)
-        k_let_kick_drift<<<grid_for(n), TB, 0, s>>>(n, a4, x, y, vx, vy, dtHalf, dt, lanes, gl);
-}
-
-void let_kick(int64_t n, const double *a4, double *x, double *y, double *vx, double *vy,
-              double dtHalf, hipStream_t s, const uint32_t *lanes, GatherLayout gl) {
-    if (n > 0) k_let_kick<<<grid_for(n), TB, 0, s>>>(n, a4, x, y, vx, vy, dtHalf, lanes, gl);
 }
 
 }  // namespace bh

@@ -214,14 +214,23 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     acc.y = fy / bm;
     if (KICK == KICK_NONE) {  // by lane with a lane map (the multi-GPU pieces stay contiguous)
         *reinterpret_cast<double2_t *>(a2 + 2 * q) = acc;
-    } else if (KICK == KICK_POS) {  // multi-rank LET: the position the build left, for the peers
-        typedef double double4_t __attribute__((ext_vector_type(4)));
-        double4_t o;
-        o.x = acc.x;
-        o.y = acc.y;
-        o.z = bx;
-        o.w = by;
-        *reinterpret_cast<double4_t *>(a2 + 4 * q) = o;
+    } else if (KICK == KICK_OWN_DRIFT || KICK == KICK_OWN_ONLY) {
+        // k_kick_drift / k_kick of the own body, operation for operation (BHA:414-432); the new
+        // position goes to the exchange, the velocity stays with the owner
+        const int64_t r = kick.rep ? (int64_t)kick.rep[q] : q;
+        const double vxi = kick.vx[r] + acc.x * kick.dtHalf;
+        const double vyi = kick.vy[r] + acc.y * kick.dtHalf;
+        kick.vx[r] = vxi;
+        kick.vy[r] = vyi;
+        double2_t o;
+        if (KICK == KICK_OWN_DRIFT) {
+            o.x = bx + vxi * kick.dt;
+            o.y = by + vyi * kick.dt;
+        } else {
+            o.x = bx;
+            o.y = by;
+        }
+        *reinterpret_cast<double2_t *>(a2 + 2 * q) = o;
     } else {  // k_kick_drift / k_kick (integrate.hip), operation for operation
         const double vxi = kick.vx[p] + acc.x * kick.dtHalf;
         const double vyi = kick.vy[p] + acc.y * kick.dtHalf;
@@ -297,7 +306,7 @@ void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x
     unsigned grid = (unsigned)((hi - lo + TB - 1) / TB);
     // node records addressed by a 32-bit byte offset while the array stays below 4 GiB
     const bool off32 = node_cap * sizeof(Node) < (size_t(1) << 32);
-    const KickArgs ka = kick ? *kick : KickArgs{KICK_NONE, nullptr, nullptr, 0.0, 0.0};
+    const KickArgs ka = kick ? *kick : KickArgs{KICK_NONE, nullptr, nullptr, 0.0, 0.0, nullptr};
     const TraverseCounters tc = cnt ? *cnt : TraverseCounters{nullptr, nullptr, nullptr, nullptr};
 #define BH_TRAV(C, O, K) \
     k_traverse<C, O, K><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, tc, ka, \
@@ -308,12 +317,14 @@ void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x
     } else if (off32) {
         if (ka.mode == KICK_DRIFT) BH_TRAV(false, true, KICK_DRIFT);
         else if (ka.mode == KICK_ONLY) BH_TRAV(false, true, KICK_ONLY);
-        else if (ka.mode == KICK_POS) BH_TRAV(false, true, KICK_POS);
+        else if (ka.mode == KICK_OWN_DRIFT) BH_TRAV(false, true, KICK_OWN_DRIFT);
+        else if (ka.mode == KICK_OWN_ONLY) BH_TRAV(false, true, KICK_OWN_ONLY);
         else BH_TRAV(false, true, KICK_NONE);
     } else {
         if (ka.mode == KICK_DRIFT) BH_TRAV(false, false, KICK_DRIFT);
         else if (ka.mode == KICK_ONLY) BH_TRAV(false, false, KICK_ONLY);
-        else if (ka.mode == KICK_POS) BH_TRAV(false, false, KICK_POS);
+        else if (ka.mode == KICK_OWN_DRIFT) BH_TRAV(false, false, KICK_OWN_DRIFT);
+        else if (ka.mode == KICK_OWN_ONLY) BH_TRAV(false, false, KICK_OWN_ONLY);
         else BH_TRAV(false, false, KICK_NONE);
     }
 #undef BH_TRAV
