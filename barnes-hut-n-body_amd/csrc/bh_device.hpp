@@ -187,6 +187,9 @@ struct TraverseCounters {
     uint32_t *visits, *contrib;
     uint32_t *wave_iters, *wave_blocks;
 };
+// A lane mapped to LANE_IDLE neither walks nor writes (the LET evaluation after a subset
+// overflow, whose call is replayed).
+constexpr uint32_t LANE_IDLE = 0xFFFFFFFFu;
 // lanes (nullable): lane -> body slot map (the Hilbert grouping made by lane_order in
 // tree_build.hip); [lo, hi) is then a range of lanes and a2 is written by lane; null = lane q
 // walks slot q and a2 is written by slot.
@@ -278,7 +281,7 @@ hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, c
 // owner integration: a2 (gather slots) holds every lane's (x, y) -> the replicated state; the
 // solo fill writes the current positions of all lanes first
 void let_set_pos(int64_t n, const uint32_t *lanes, const double *a2, GatherLayout gl, double *x,
-                 double *y, hipStream_t s);
+                 double *y, const uint32_t *skip, hipStream_t s);
 void let_fill_pos(int64_t n, const uint32_t *lanes, const double *x, const double *y, double *a2,
                   GatherLayout gl, hipStream_t s);
 // velocity exchange of the owner integration: own lanes' (vx, vy) into a2, all lanes' back out

@@ -774,7 +774,7 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
     HIPCHK(e, hipStreamWaitEvent(e->stream, e->gathered_ev, 0));
     TRY(mark(e, 4));
-    let_set_pos(n, lanes, e->a2, gl, e->st.x, e->st.y, e->stream);  // every body's new position
+    let_set_pos(n, lanes, e->a2, gl, e->st.x, e->st.y, e->scalars + 4, e->stream);  // new positions
     HIPCHK(e, hipGetLastError());
     TRY(mark(e, 2));
     e->vel_stale = true;

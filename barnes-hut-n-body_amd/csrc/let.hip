@@ -515,6 +515,7 @@ __global__ __launch_bounds__(TB) void k_let_subpos(int64_t n_sub, int64_t n,
 // own lane -> subset slot of its body
 __global__ __launch_bounds__(TB) void k_let_lanes(LetPieces pc, uint32_t n_sub,
                                                   const uint32_t *__restrict__ subpos,
+                                                  const uint32_t *__restrict__ scal,
                                                   uint32_t *__restrict__ lanes) {
     const int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (t >= (int64_t)pc.rounds * pc.sub) return;
@@ -523,14 +524,16 @@ __global__ __launch_bounds__(TB) void k_let_lanes(LetPieces pc, uint32_t n_sub,
     // every own body is in the subset (its cell is an own cell, or it is listed as own); the
     // clamp only keeps a broken invariant inside the subset
     const uint32_t s = subpos[pc.lanes ? (int64_t)pc.lanes[q] : q];
-    lanes[q] = s < n_sub ? s : 0u;
+    // after a subset overflow (the call is replayed) the lanes sit out: no walk, no kick
+    lanes[q] = scal[4] ? LANE_IDLE : (s < n_sub ? s : 0u);
 }
 
 __global__ __launch_bounds__(TB) void k_let_set_pos(int64_t n, const uint32_t *__restrict__ lanes,
                                                     const double *__restrict__ a2, GatherLayout gl,
-                                                    double *__restrict__ x, double *__restrict__ y) {
+                                                    double *__restrict__ x, double *__restrict__ y,
+                                                    const uint32_t *__restrict__ skip) {
     const int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (q >= n) return;
+    if (q >= n || (skip && *skip)) return;  // skip: a subset overflow left the state as it was
     const int64_t i = lanes ? (int64_t)lanes[q] : q, g = gather_slot(gl, q);
     x[i] = a2[2 * g];
     y[i] = a2[2 * g + 1];
@@ -562,8 +565,8 @@ __global__ __launch_bounds__(TB) void k_let_pack_vel(LetPieces pc, const double 
 }  // namespace
 
 void let_set_pos(int64_t n, const uint32_t *lanes, const double *a2, GatherLayout gl, double *x,
-                 double *y, hipStream_t s) {
-    if (n > 0) k_let_set_pos<<<grid_for(n), TB, 0, s>>>(n, lanes, a2, gl, x, y);
+                 double *y, const uint32_t *skip, hipStream_t s) {
+    if (n > 0) k_let_set_pos<<<grid_for(n), TB, 0, s>>>(n, lanes, a2, gl, x, y, skip);
 }
 
 void let_fill_pos(int64_t n, const uint32_t *lanes, const double *x, const double *y, double *a2,
@@ -580,7 +583,7 @@ void let_pack_vel(const LetPieces &pc, const double *vx, const double *vy, doubl
 void let_unpack_vel(int64_t n, const uint32_t *lanes, const double *a2, GatherLayout gl,
                     double *vx, double *vy, hipStream_t s) {
     // the same copy as the positions' (lane's gather slot -> its body's slot)
-    if (n > 0) k_let_set_pos<<<grid_for(n), TB, 0, s>>>(n, lanes, a2, gl, vx, vy);
+    if (n > 0) k_let_set_pos<<<grid_for(n), TB, 0, s>>>(n, lanes, a2, gl, vx, vy, nullptr);
 }
 
 double let_include_gap2(const Geometry &g, double theta2, double soft2) {
@@ -657,7 +660,8 @@ hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, c
     if (n_sub > 0) k_let_subpos<<<grid_for(n_sub), TB, 0, s>>>(n_sub, pc.n, tb.dst.vx, L.subpos);
     const int64_t own_lanes = (int64_t)pc.rounds * pc.sub;
     if (own_lanes > 0 && pc.n > 0)
-        k_let_lanes<<<grid_for(own_lanes), TB, 0, s>>>(pc, (uint32_t)n_sub, L.subpos, L.lanes);
+        k_let_lanes<<<grid_for(own_lanes), TB, 0, s>>>(pc, (uint32_t)n_sub, L.subpos, scal,
+                                                        L.lanes);
     return hipGetLastError();
 }
 

@@ -165,8 +165,9 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     const uint64_t t_start = wall_clock64();
 #endif
     const int64_t q = lo + (int64_t)xcd_block<BH_TRAV_XCD_RUN>() * TB + threadIdx.x;  // lane
-    const bool valid = q < hi;
-    const int64_t p = lanes && valid ? (int64_t)lanes[q] : q;  // its body's slot
+    const uint32_t lp = lanes && q < hi ? lanes[q] : (uint32_t)q;
+    const bool valid = q < hi && (!lanes || lp != LANE_IDLE);
+    const int64_t p = lanes ? (int64_t)lp : q;  // its body's slot
     // A body merged away earlier in this bh_step call (a tombstone until the call's compaction)
     // needs no force: it does not walk.  Tombstones sort to the tail with the out-of-root
     // bodies and are flung across the domain by the heavy body that absorbed them, so a tail

@@ -9,8 +9,8 @@ two force evaluations, kick-drift-kick, merge.  Inputs are resident in HBM befor
 Multi-GPU (torchrun, one rank per GPU): the north-star configuration C4 (1e7-body uniform cloud,
 total fixed: strong scaling; `--config c3x` = weak scaling, 1e6 two-disk bodies per GPU).  The
 state is replicated; each rank builds a locally essential tree (only the cells its bodies can
-open, plus the top from every rank's cell values), evaluates its Hilbert-ordered pieces, and
-the (ax, ay) pieces are all-gathered by RCCL over xGMI inside the engine.
+open, plus the top from every rank's cell values), evaluates and integrates its Hilbert-ordered
+lane range, and the new positions are all-gathered by RCCL over xGMI inside the engine.
 
 Prints ONE JSON line on rank 0 (see the driver contract in the task statement).
 """
