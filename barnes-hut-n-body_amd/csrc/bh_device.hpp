@@ -19,6 +19,8 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 
+#include "bh_engine.h"  // BH_SHARD_ROUNDS
+
 namespace bh {
 
 struct __attribute__((aligned(32))) Node {
@@ -203,18 +205,24 @@ __host__ __device__ inline int64_t shard_sub(int64_t n, int world, int rounds) {
     const int64_t c = (n + parts - 1) / parts;
     return (c + 63) / 64 * 64;
 }
-// Rank r owns lanes [r * rounds * sub, +rounds * sub); lane q = (r * rounds + k) * sub + i of
-// round k sits in the exchange buffer at slot (k * world + r) * sub + i, so that the pieces of a
-// round are adjacent (in-place all-gather).  sub == 0: the identity (one GPU).
+// Rank r owns lanes [r * span, (r + 1) * span), span = rounds * sub; its round k is the lanes
+// [r * span + off[k], r * span + off[k + 1]) (whole wavefronts; rounds of unequal size: the
+// first ones fill the GPU, the last ones are small so that little of the exchange is exposed).
+// Lane q = r * span + off[k] + i sits in the exchange buffer at world * off[k] + r * size_k + i,
+// so that the pieces of a round are adjacent (in-place all-gather).  span == 0: the identity.
 struct GatherLayout {
-    int64_t sub;
-    int world, rounds;
+    int64_t span;
+    int64_t off[BH_SHARD_ROUNDS + 1];
+    int world;
 };
+GatherLayout shard_layout(int64_t n, int world);  // engine.cpp (bh_shard_range's layout)
 __host__ __device__ inline int64_t gather_slot(const GatherLayout &L, int64_t q) {
-    if (L.sub == 0) return q;
-    const int64_t piece = q / L.sub, i = q - piece * L.sub;
-    const int64_t r = piece / L.rounds, k = piece - r * L.rounds;
-    return (k * L.world + r) * L.sub + i;
+    if (L.span == 0) return q;
+    const int64_t r = q / L.span, t = q - r * L.span;
+    int k = 0;
+#pragma unroll
+    for (int j = 1; j < BH_SHARD_ROUNDS; ++j) k += t >= L.off[j] ? 1 : 0;
+    return L.world * L.off[k] + r * (L.off[k + 1] - L.off[k]) + (t - L.off[k]);
 }
 
 // Exactness check of the traversal's in-range sqrt/reciprocal sequences against the IEEE
@@ -310,16 +318,16 @@ void direct_forces(const LeafList &L, const uint32_t *d_count, const double *x, 
 // lane q's acceleration at a2[2 * gather_slot(gl, q)]
 void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
                 double dtHalf, double dt, hipStream_t s, const uint32_t *lanes = nullptr,
-                GatherLayout gl = GatherLayout{0, 1, 1});
+                GatherLayout gl = GatherLayout{});
 void kick(int64_t n, const double *a2, double *vx, double *vy, double dtHalf, hipStream_t s,
-          const uint32_t *lanes = nullptr, GatherLayout gl = GatherLayout{0, 1, 1});
+          const uint32_t *lanes = nullptr, GatherLayout gl = GatherLayout{});
 void iota_u32(uint32_t *p, int64_t n, hipStream_t s);
 // caller-order copies: dst_k[cidx[s]] = src_k[s]
 void scatter_to_caller(int64_t n, const uint32_t *cidx, int k, const double *const *src,
                        double *const *dst, hipStream_t s);
 void scatter_acc_to_caller(int64_t n, const uint32_t *cidx, const double *a2, double *ax,
                            double *ay, hipStream_t s, const uint32_t *lanes = nullptr,
-                           GatherLayout gl = GatherLayout{0, 1, 1});
+                           GatherLayout gl = GatherLayout{});
 
 struct MergePair {
     uint32_t h_cidx, v_cidx;  // heavy body and candidate victim, caller indices

@@ -155,7 +155,7 @@ struct bh_engine {
     bool lanes_valid = false;  // the map is a permutation of the current slots
     int lanes_age = 0;         // builds since the last Hilbert sort
     const uint32_t *a2_lanes = nullptr;  // the last evaluation wrote a2 by lane of this map
-    GatherLayout a2_layout{0, 1, 1};     // ... at the lane's gather slot (multi-rank rounds)
+    GatherLayout a2_layout{};            // ... at the lane's gather slot (multi-rank rounds)
 
     // multi-rank locally essential tree (let.hip): subset state and tree workspace
     // BH_LET unset: LET builds from 4 ranks up (at 2 ranks the subset is over half the bodies
@@ -508,6 +508,9 @@ int ensure_direct(bh_engine *e) {
 #ifndef BH_FUSE_KICK
 #define BH_FUSE_KICK 1
 #endif
+#ifndef BH_ROUND_WEIGHTS
+#define BH_ROUND_WEIGHTS 1, 1, 1, 1  // relative sizes of a rank's rounds (BH_ROUND_FRACS)
+#endif
 
 // ---- multi-rank: the build as a locally essential tree (let.hip) ----------------------
 int pinned_reserve(bh_engine *e, size_t bytes);
@@ -620,6 +623,30 @@ int round_streams(bh_engine *e) {
     return BH_OK;
 }
 
+// Round k's in-place all-gather of W doubles per lane on the comm stream (RCCL), or the peers'
+// pieces copied in (in-process group: the caller has passed a barrier after every member
+// recorded round_ev[ev_round]; ev_round < 0: the peers' events were waited for already).
+int gather_round(bh_engine *e, const GatherLayout &gl, int k, int W, int ev_round) {
+    const int64_t size = gl.off[k + 1] - gl.off[k];
+    double *piece = e->a2 + W * (int64_t)e->world * gl.off[k];  // round k, rank 0
+    if (size <= 0) return BH_OK;
+    if (e->comm) {
+        NCCLCHK(e, ncclAllGather(piece + W * e->rank * size, piece, (size_t)(W * size),
+                                 ncclDouble, e->comm, e->comm_stream));
+    } else if (e->group) {
+        for (int q = 0; q < e->world; ++q) {
+            if (q == e->rank) continue;
+            bh_engine *peer = e->group->members[q];
+            if (ev_round >= 0)
+                HIPCHK(e, hipStreamWaitEvent(e->comm_stream, peer->round_ev[ev_round], 0));
+            const int64_t off = W * ((int64_t)e->world * gl.off[k] + q * size);
+            HIPCHK(e, hipMemcpyAsync(e->a2 + off, peer->a2 + off, sizeof(double) * W * size,
+                                     hipMemcpyDeviceToDevice, e->comm_stream));
+        }
+    }
+    return BH_OK;
+}
+
 // Velocities after owner-integrated LET evaluations: every rank holds current velocities of its
 // own bodies only; before a full build (which permutes and re-assigns the bodies) the owners'
 // (vx, vy) are all-gathered once, in the same rounds and slots as the forces.
@@ -632,7 +659,7 @@ int sync_velocities(bh_engine *e) {
     const int64_t sub = shard_sub(n, e->world, R);
     const uint32_t *lanes = e->lanes_valid ? e->lanes : nullptr;
     const LetPieces pc{n, sub, e->world, e->rank, R, lanes};
-    const GatherLayout gl{sub, e->world, R};
+    const GatherLayout gl = shard_layout(n, e->world);
     if (e->group) {  // peers are done reading our previous pieces
         e->group->barrier();
         for (bh_engine *peer : e->group->members)
@@ -643,22 +670,7 @@ int sync_velocities(bh_engine *e) {
     HIPCHK(e, hipEventRecord(e->round_ev[0], e->stream));
     HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[0], 0));
     if (e->group) e->group->barrier();
-    for (int k = 0; k < R; ++k) {
-        double *piece = e->a2 + 2 * ((int64_t)k * e->world) * sub;
-        if (e->comm) {
-            NCCLCHK(e, ncclAllGather(piece + 2 * e->rank * sub, piece, (size_t)(2 * sub),
-                                     ncclDouble, e->comm, e->comm_stream));
-        } else {
-            for (int q = 0; q < e->world; ++q) {
-                if (q == e->rank) continue;
-                bh_engine *peer = e->group->members[q];
-                if (k == 0) HIPCHK(e, hipStreamWaitEvent(e->comm_stream, peer->round_ev[0], 0));
-                const int64_t off = 2 * ((int64_t)k * e->world + q) * sub;
-                HIPCHK(e, hipMemcpyAsync(e->a2 + off, peer->a2 + off, sizeof(double) * 2 * sub,
-                                         hipMemcpyDeviceToDevice, e->comm_stream));
-            }
-        }
-    }
+    for (int k = 0; k < R; ++k) TRY(gather_round(e, gl, k, 2, k == 0 ? 0 : -1));
     HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
     HIPCHK(e, hipStreamWaitEvent(e->stream, e->gathered_ev, 0));
     let_unpack_vel(n, lanes, e->a2, gl, e->st.vx, e->st.vy, e->stream);
@@ -738,7 +750,7 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     const int W = 2;  // (x, y) per lane
     const KickArgs ka{kick == KICK_DRIFT ? KICK_OWN_DRIFT : KICK_OWN_ONLY, e->st.vx, e->st.vy,
                       e->p.dt * 0.5, e->p.dt, lanes};  // BHA:412
-    const GatherLayout gl{sub, e->world, R};
+    const GatherLayout gl = shard_layout(n, e->world);
     if (e->solo)  // measurement: the peers' bodies keep their positions
         let_fill_pos(n, lanes, e->st.x, e->st.y, e->a2, gl, e->stream);
     TRY(round_streams(e));
@@ -754,21 +766,8 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipEventRecord(e->round_ev[k], rs));
         HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
-        double *piece = e->a2 + W * ((int64_t)k * e->world) * sub;  // round k, rank 0
-        if (e->comm) {
-            NCCLCHK(e, ncclAllGather(piece + W * e->rank * sub, piece, (size_t)(W * sub),
-                                     ncclDouble, e->comm, e->comm_stream));
-        } else if (e->group) {
-            e->group->barrier();
-            for (int q = 0; q < e->world; ++q) {
-                if (q == e->rank) continue;
-                bh_engine *peer = e->group->members[q];
-                HIPCHK(e, hipStreamWaitEvent(e->comm_stream, peer->round_ev[k], 0));
-                const int64_t off = W * ((int64_t)k * e->world + q) * sub;
-                HIPCHK(e, hipMemcpyAsync(e->a2 + off, peer->a2 + off, sizeof(double) * W * sub,
-                                         hipMemcpyDeviceToDevice, e->comm_stream));
-            }
-        }
+        if (e->group) e->group->barrier();
+        TRY(gather_round(e, gl, k, W, k));
     }
     TRY(mark(e, 1));
     HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
@@ -821,7 +820,7 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
     const TraverseCounters counters{visits, e->contrib32, e->wave_iters, e->wave_blocks};
     const uint32_t *lanes = e->lanes_valid ? e->lanes : nullptr;  // [lo, hi): lane ranges
     e->a2_lanes = direct ? nullptr : lanes;
-    e->a2_layout = GatherLayout{0, 1, 1};
+    e->a2_layout = GatherLayout{};
     auto forces = [&](int64_t lo, int64_t hi, uint32_t *vis, hipStream_t fs, double *a2) {
         if (direct)
             direct_forces(e->leaves, e->leaf_count, e->st.x, e->st.y, e->st.m, lo, hi, fp.G,
@@ -854,7 +853,7 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
             if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->gathered_ev, 0));
     }
     TRY(round_streams(e));
-    const GatherLayout gl{sub, e->world, BH_SHARD_ROUNDS};
+    const GatherLayout gl = shard_layout(n, e->world);
     e->a2_layout = gl;
     for (int k = 0; k < BH_SHARD_ROUNDS; ++k) {
         int64_t lo = 0, hi = 0;
@@ -864,21 +863,8 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipEventRecord(e->round_ev[k], rs));
         HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
-        double *piece = e->a2 + 2 * ((int64_t)k * e->world) * sub;  // round k, rank 0
-        if (e->comm) {
-            NCCLCHK(e, ncclAllGather(piece + 2 * e->rank * sub, piece, (size_t)(2 * sub),
-                                     ncclDouble, e->comm, e->comm_stream));
-        } else if (e->group) {  // in-process: every member recorded round k, then copy the peers' pieces
-            e->group->barrier();
-            for (int q = 0; q < e->world; ++q) {
-                if (q == e->rank) continue;
-                bh_engine *peer = e->group->members[q];
-                HIPCHK(e, hipStreamWaitEvent(e->comm_stream, peer->round_ev[k], 0));
-                const int64_t off = 2 * ((int64_t)k * e->world + q) * sub;
-                HIPCHK(e, hipMemcpyAsync(e->a2 + off, peer->a2 + off, sizeof(double) * 2 * sub,
-                                         hipMemcpyDeviceToDevice, e->comm_stream));
-            }
-        }
+        if (e->group) e->group->barrier();  // every member recorded round k
+        TRY(gather_round(e, gl, k, 2, k));
     }
     TRY(mark(e, 1));
     HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
@@ -1164,6 +1150,51 @@ void free_state(BodyState &s) {
 }
 
 }  // namespace
+
+// Round sizes of a rank's lane range (BH_ROUND_FRACS="a,b,c,d": relative weights; default
+// below): whole wavefronts, the same on every rank (bh_shard_range, bh_gather_slot).
+static const double *round_cum() {
+    struct Cum {
+        double c[BH_SHARD_ROUNDS + 1];
+        Cum() {
+            double w[BH_SHARD_ROUNDS] = {BH_ROUND_WEIGHTS};
+            if (const char *v = std::getenv("BH_ROUND_FRACS")) {
+                double t[BH_SHARD_ROUNDS];
+                int k = 0;
+                const char *p = v;
+                while (k < BH_SHARD_ROUNDS && *p) {
+                    char *end = nullptr;
+                    t[k] = std::strtod(p, &end);
+                    if (end == p || !(t[k] > 0.0)) break;
+                    ++k;
+                    p = *end == ',' ? end + 1 : end;
+                }
+                if (k == BH_SHARD_ROUNDS)
+                    for (int j = 0; j < k; ++j) w[j] = t[j];
+            }
+            double tot = 0.0;
+            for (double x : w) tot += x;
+            c[0] = 0.0;
+            for (int j = 0; j < BH_SHARD_ROUNDS; ++j) c[j + 1] = c[j] + w[j] / tot;
+        }
+    };
+    static const Cum cum;  // thread-safe initialisation (the in-process ranks are threads)
+    return cum.c;
+}
+
+GatherLayout bh::shard_layout(int64_t n, int world) {
+    GatherLayout L{};
+    const int64_t sub = shard_sub(n, world, BH_SHARD_ROUNDS);
+    L.span = sub * BH_SHARD_ROUNDS;
+    L.world = world;
+    const double *cum = round_cum();
+    L.off[0] = 0;
+    for (int k = 1; k < BH_SHARD_ROUNDS; ++k)
+        L.off[k] = std::max<int64_t>(L.off[k - 1],
+                                     std::min<int64_t>(L.span, (int64_t)(cum[k] * (double)L.span) / 64 * 64));
+    L.off[BH_SHARD_ROUNDS] = L.span;
+    return L;
+}
 
 void bh::set_error(bh_engine *e, const std::string &msg) {
     if (e) e->err = msg;
@@ -1667,16 +1698,15 @@ int bh_shard_range(int64_t n, int rank, int world, int round, int64_t *lo, int64
     if (n < 0 || world < 1 || rank < 0 || rank >= world || round < 0 ||
         round >= BH_SHARD_ROUNDS || !lo || !hi)
         return BH_E_INVALID;
-    const int64_t sub = shard_sub(n, world, BH_SHARD_ROUNDS);  // whole wavefronts
-    *lo = std::min<int64_t>(n, ((int64_t)rank * BH_SHARD_ROUNDS + round) * sub);  // own range
-    *hi = std::min<int64_t>(n, *lo + sub);
+    const GatherLayout L = shard_layout(n, world);  // whole wavefronts
+    *lo = std::min<int64_t>(n, (int64_t)rank * L.span + L.off[round]);  // in the own range
+    *hi = std::min<int64_t>(n, (int64_t)rank * L.span + L.off[round + 1]);
     return BH_OK;
 }
 
 int64_t bh_gather_slot(int64_t n, int world, int64_t lane) {
     if (n < 0 || world < 1 || lane < 0) return -1;
-    return gather_slot(GatherLayout{shard_sub(n, world, BH_SHARD_ROUNDS), world, BH_SHARD_ROUNDS},
-                       lane);
+    return gather_slot(shard_layout(n, world), lane);
 }
 
 int bh_selftest_fast_math(int device, int64_t n, uint64_t seed, int64_t *mismatches) {
