@@ -79,6 +79,13 @@ __device__ __forceinline__ bool lane_self_ok(double Gm, double bm) {
     return __builtin_fabs(Gm * bm) < 0x1p400;
 }
 
+// The fast criterion forms s2 = s2_0 * 2^-2d by an exponent-field subtraction (traverse.hip):
+// exact while the result stays normal, i.e. for every 2d <= 255 (NODE_DEPTH2_MASK) when
+// s2_0 >= 2^-760; finite s2_0 only.
+__device__ __forceinline__ bool fast_s2_ok(double s2root) {
+    return s2root >= 0x1p-760 && s2root <= 0x1p1000;
+}
+
 __device__ __forceinline__ bool lane_fast_ok(double bx, double by, double soft2) {
     return __builtin_fabs(bx) < 0x1p250 && __builtin_fabs(by) < 0x1p250 && soft2 >= 0x1p-600 &&
            soft2 <= 0x1p500;

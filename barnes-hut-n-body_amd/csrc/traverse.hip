@@ -93,8 +93,19 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
             // (a power-of-two scaling commutes with rounding), and s2 < t2 <=> s2_0 < t2 * 4^d:
             // the scaling of t2 is exact too (up from a subnormal included) or overflows to
             // +inf where s2 < t2 holds anyway.  The record carries 2d: one scalar mask.
-            const double t2 = __builtin_ldexp(theta2 * d2, (int)(meta & NODE_DEPTH2_MASK));
-            const uint64_t acc_m = __builtin_amdgcn_ballot_w64(s2root < t2);  // BHA:226-228
+            // Fast path: s2 itself, the reference's own comparison, built on the scalar unit by
+            // subtracting 2d from s2_0's exponent field (exact: s2_0 >= 2^-760 keeps it normal
+            // for every 2d <= 255, fast_s2_ok) -- one v_ldexp_f64 less per internal node.
+            uint64_t acc_m;
+            if (FAST) {
+                const uint64_t s2b = (uint64_t)__double_as_longlong(s2root) -
+                                     ((uint64_t)(meta & NODE_DEPTH2_MASK) << 52);
+                acc_m = __builtin_amdgcn_ballot_w64(__longlong_as_double((long long)s2b) <
+                                                    theta2 * d2);  // BHA:226-228
+            } else {
+                const double t2 = __builtin_ldexp(theta2 * d2, (int)(meta & NODE_DEPTH2_MASK));
+                acc_m = __builtin_amdgcn_ballot_w64(s2root < t2);  // BHA:226-228
+            }
             contrib_m = act_m & acc_m;
             open_m = act_m & ~acc_m;
         }
@@ -186,7 +197,7 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     // lane is active for node `cur` iff cur >= resume; invalid lanes and tombstones never are.
     const uint32_t resume = walks ? 0u : 0xFFFFFFFFu;
     const uint32_t T = __builtin_amdgcn_readfirstlane(*d_T);
-    const bool fast =
+    const bool fast = fast_s2_ok(s2root) &&
         __ballot(walks && !(lane_fast_ok(bx, by, soft2) && lane_self_ok(Gm, bm))) == 0ull;
     if (fast)
         walk<true, COUNT, OFF32>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx,
