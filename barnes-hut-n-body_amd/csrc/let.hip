@@ -463,32 +463,51 @@ __global__ __launch_bounds__(TB) void k_let_write_cells(LetBufs L) {
 
 // the locally built subtrees, one thread per node (grid-stride over cpos[LET_CELLS] nodes): node t
 // of the concatenated blocks belongs to the cell c with cpos[c] <= t < cpos[c + 1]; its `next`
-// moves with the block
+// moves with the block.  The cell is found by the whole wave: a 64-ary search for the cell of
+// the wave's first node (three rounds of 64 parallel loads instead of a 16-step chain of
+// dependent loads by one lane), then each lane's own cell in the 64-cell window after it
+// (one load, a binary search over the window by lane shuffles); a lane past the window (many
+// empty cells between two pieces) gallops from the window's end.
+#ifndef BH_LET_COPY_GRID
+#define BH_LET_COPY_GRID 8192  // workgroups of the grid-stride copy (one search per 64 nodes)
+#endif
 __global__ __launch_bounds__(TB) void k_let_copy_blocks(LetBufs L, const Node *__restrict__ src) {
     const uint32_t total = L.cpos[LET_CELLS];
     const uint32_t lane = threadIdx.x & 63u, stride = gridDim.x * TB;
+    constexpr uint32_t NC = (uint32_t)LET_CELLS;
     for (uint32_t base = blockIdx.x * TB + (threadIdx.x & ~63u); base < total; base += stride) {
-        uint32_t c = 0;
-        if (lane == 0) {  // the wave's first node: largest c with cpos[c] <= base
-            uint32_t lo = 0, hi = (uint32_t)LET_CELLS;
-            while (hi - lo > 1) {
-                const uint32_t mid = (lo + hi) >> 1;
-                if (L.cpos[mid] <= base) lo = mid; else hi = mid;
-            }
-            c = lo;
+        // largest c < NC with cpos[c] <= base (cpos is non-decreasing, cpos[0] = 0): the lanes
+        // whose probe satisfies it form a prefix, its length picks the next range
+        uint32_t c0 = 0, span = NC;
+        while (span > 1u) {
+            const uint32_t step = (span + 63u) >> 6;
+            const bool in = lane * step < span;
+            const bool le = in && L.cpos[c0 + lane * step] <= base;
+            const uint32_t k = (uint32_t)__popcll(__ballot(le));  // >= 1
+            c0 += (k - 1u) * step;
+            const uint32_t rest = span - (k - 1u) * step;
+            span = rest < step ? rest : step;
         }
-        c = __shfl(c, 0);
         const uint32_t t = base + lane;
+        // the window: cells c0 .. c0 + 63 (past the last cell: never <= t)
+        const uint32_t w = c0 + lane < NC ? L.cpos[c0 + lane] : 0xFFFFFFFFu;
+        uint32_t j = 0;  // largest j with w_j <= t (w_0 = cpos[c0] <= base <= t)
+#pragma unroll
+        for (uint32_t sft = 32; sft >= 1u; sft >>= 1) {
+            const uint32_t wj = (uint32_t)__shfl((int)w, (int)(j + sft));
+            if (wj <= t) j += sft;
+        }
         if (t >= total) continue;
-        if (L.cpos[c + 1] <= t) {  // gallop from the wave's cell (empty cells lie between pieces)
+        uint32_t c = c0 + j;
+        if (j == 63u && c + 1u < NC && L.cpos[c + 1] <= t) {  // past the window: gallop
             uint32_t lo = c + 1, step = 1, hi;
             for (;;) {  // cpos[lo] <= t holds
                 hi = lo + step;
-                if (hi >= (uint32_t)LET_CELLS || L.cpos[hi] > t) break;
+                if (hi >= NC || L.cpos[hi] > t) break;
                 lo = hi;
                 step <<= 1;
             }
-            if (hi > (uint32_t)LET_CELLS) hi = (uint32_t)LET_CELLS;
+            if (hi > NC) hi = NC;
             while (hi - lo > 1) {
                 const uint32_t mid = (lo + hi) >> 1;
                 if (L.cpos[mid] <= t) lo = mid; else hi = mid;
@@ -656,7 +675,7 @@ hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, c
     k_let_write_top<<<grid_for(level_off(LET_P)), TB, 0, s>>>(L);
     k_let_guard<<<1, 1, 0, s>>>(L, scal);
     k_let_write_cells<<<grid_for(LET_CELLS), TB, 0, s>>>(L);
-    k_let_copy_blocks<<<2048, TB, 0, s>>>(L, tb.nodes);
+    k_let_copy_blocks<<<BH_LET_COPY_GRID, TB, 0, s>>>(L, tb.nodes);
     if (n_sub > 0) k_let_subpos<<<grid_for(n_sub), TB, 0, s>>>(n_sub, pc.n, tb.dst.vx, L.subpos);
     const int64_t own_lanes = (int64_t)pc.rounds * pc.sub;
     if (own_lanes > 0 && pc.n > 0)
