@@ -145,27 +145,31 @@ __global__ __launch_bounds__(TB) void k_let_halo(const uint8_t *__restrict__ ece
 // the subset: bodies of built cells, and own bodies outside the tree (they still walk it, or
 // idle); a flag byte per slot and the count of every 256-slot block (scanned: block offsets)
 static_assert(TB == 256, "one 256-slot block per workgroup");
-__global__ __launch_bounds__(TB) void k_let_flags(LetPieces pc, const double *__restrict__ x,
+// One wave per 256-slot block, four slots per lane (slot base + lane + 64 u): four independent
+// position loads and cell lookups in flight per lane, the block's count from four ballots.
+__global__ __launch_bounds__(64) void k_let_flags(LetPieces pc, const double *__restrict__ x,
                                                   const double *__restrict__ y,
                                                   const uint32_t *__restrict__ cidx, Geometry g,
                                                   const uint8_t *__restrict__ hcell,
                                                   const uint8_t *__restrict__ own,
                                                   uint8_t *__restrict__ flag8,
                                                   uint32_t *__restrict__ bcnt) {
-    __shared__ uint32_t s_w[TB / 64];
-    const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
-    uint32_t f = 0;
-    if (i < pc.n) {
-        const double px = x[i], py = y[i];
-        if (!(cidx[i] & CIDX_DEAD) && in_root(g, px, py)) f = hcell[cell_of(g, px, py)];
-        else f = own[i];
-        flag8[i] = (uint8_t)f;
+    const int64_t b0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    uint32_t count = 0;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int64_t i = b0 + 64 * u;
+        uint32_t f = 0;
+        if (i < pc.n) {
+            const double px = x[i], py = y[i];
+            if (!(cidx[i] & CIDX_DEAD) && in_root(g, px, py)) f = hcell[cell_of(g, px, py)];
+            else f = own[i];
+            flag8[i] = (uint8_t)f;
+        }
+        count += (uint32_t)__popcll(__ballot(f != 0));
     }
-    const uint64_t m = __ballot(f != 0);
-    if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = (uint32_t)__popcll(m);
-    __syncthreads();
     if (threadIdx.x == 0) {
-        bcnt[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+        bcnt[blockIdx.x] = count;
         if (blockIdx.x + 1 == gridDim.x) bcnt[gridDim.x] = 0u;  // the scan's last entry
     }
 }
@@ -640,7 +644,7 @@ hipError_t let_select(const BodyState &st, const Geometry &g, const LetPieces &p
     const int K = (int)std::floor(std::sqrt(gap2 > 0.0 ? gap2 : 0.0)) + 1;
     k_let_halo<<<grid_for(LET_CELLS), TB, 0, s>>>(L.ecell, L.flag_all, gap2, K, L.hcell);
     const int64_t nb = let_sel_blocks(pc.n);
-    k_let_flags<<<(unsigned)nb, TB, 0, s>>>(pc, st.x, st.y, st.cidx, g, L.hcell, L.own, L.flag8,
+    k_let_flags<<<(unsigned)nb, 64, 0, s>>>(pc, st.x, st.y, st.cidx, g, L.hcell, L.own, L.flag8,
                                             L.sel);
     size_t bytes = L.scratch_bytes;
     e = rocprim::exclusive_scan(L.scratch, bytes, L.sel, L.selpos, 0u, (size_t)(nb + 1),
