@@ -317,12 +317,19 @@ __global__ __launch_bounds__(256) void k_let_top_hi(int world, Geometry g,
     {
         const uint32_t c = b * 256u + t;
         LetCell r{0.0, 0.0, 0.0, 0u, 0u};
-        for (int q = 0; q < world; ++q) {
-            const LetCell v = tables[(int64_t)q * LET_TSTRIDE + c];
-            if (v.tag) {
-                r = v;
-                break;
-            }
+        // the ranks' entries four at a time: independent loads in flight, the first tagged wins
+        bool found = false;
+        for (int q0 = 0; q0 < world && !found; q0 += 4) {
+            LetCell v[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (q0 + j < world) v[j] = tables[(int64_t)(q0 + j) * LET_TSTRIDE + c];
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (!found && q0 + j < world && v[j].tag) {
+                    r = v[j];
+                    found = true;
+                }
         }
         r.tag = r.cnt == 1u ? c : 0u;
         levels[level_off(LET_P) + c] = r;
