@@ -637,13 +637,31 @@ size_t let_scratch_bytes(int64_t n) {
     return std::max(a, b);
 }
 
+// The selection's three clears in one launch (16-byte stores; the buffers are hipMalloc'd):
+// own[0, n), ecell[0, LET_CELLS), *flag_all.
+static_assert(LET_CELLS % 16 == 0, "ecell is cleared in 16-byte stores");
+__global__ __launch_bounds__(TB) void k_let_clear(int64_t n, uint8_t *__restrict__ own,
+                                                  uint8_t *__restrict__ ecell,
+                                                  uint32_t *__restrict__ flag_all) {
+    const int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    const int64_t nv = n >> 4;
+    if (t < nv) reinterpret_cast<uint4 *>(own)[t] = z;
+    if (t < (n & 15)) own[(nv << 4) + t] = 0;
+    if (t < LET_CELLS / 16) reinterpret_cast<uint4 *>(ecell)[t] = z;
+    if (t == 0) *flag_all = 0u;
+}
+
 hipError_t let_select(const BodyState &st, const Geometry &g, const LetPieces &pc, double gap2,
                       const LetBufs &L, const BodyState &sub, int64_t S, uint32_t *scal,
                       hipStream_t s) {
-    hipError_t e = hipMemsetAsync(L.ecell, 0, LET_CELLS, s);
-    if (e == hipSuccess) e = hipMemsetAsync(L.flag_all, 0, sizeof(uint32_t), s);
-    if (e == hipSuccess && pc.n > 0) e = hipMemsetAsync(L.own, 0, (size_t)pc.n, s);
-    if (e != hipSuccess || pc.n <= 0) return e;
+    if (pc.n <= 0) {
+        hipError_t e = hipMemsetAsync(L.ecell, 0, LET_CELLS, s);
+        return e == hipSuccess ? hipMemsetAsync(L.flag_all, 0, sizeof(uint32_t), s) : e;
+    }
+    const int64_t clear = std::max<int64_t>(pc.n >> 4, LET_CELLS / 16);
+    k_let_clear<<<grid_for(clear), TB, 0, s>>>(pc.n, L.own, L.ecell, L.flag_all);
+    hipError_t e;
     const int64_t marks = (int64_t)pc.rounds * pc.sub;
     if (marks > 0)
         k_let_mark<<<grid_for(marks), TB, 0, s>>>(pc, st.x, st.y, st.cidx, g, L.own, L.ecell,
