@@ -43,7 +43,8 @@ EXPORTED_SYMBOLS = (
     "bh_nbody3d_create", "bh_nbody3d_destroy", "bh_nbody3d_last_error", "bh_nbody3d_set",
     "bh_nbody3d_step", "bh_nbody3d_accelerations", "bh_nbody3d_get", "bh_nbody3d_last_ms",
     "bh_local_group_create", "bh_local_group_destroy", "bh_create_local",
-    "bh_save_state", "bh_load_state", "bh_let_stats", "bh_create_solo",
+    "bh_save_state", "bh_load_state", "bh_let_stats", "bh_create_solo", "bh_comm_ranks",
+    "bh_debug_inject",
 )
 
 
@@ -121,6 +122,9 @@ def load_library(path: str | None = None):
     lib.bh_traversal_stats.argtypes = [_VP, _I64P, _I64P, _I64P]
     lib.bh_traversal_counters.argtypes = [_VP, _I64P]
     lib.bh_let_stats.argtypes = [_VP, _I64P]
+    lib.bh_comm_ranks.argtypes = [_VP, ctypes.POINTER(ctypes.c_int32),
+                                  ctypes.POINTER(ctypes.c_int32)]
+    lib.bh_debug_inject.argtypes = [_VP, ctypes.c_int]
     lib.bh_last_removed.argtypes = [_VP, _I64P, ctypes.c_int64, _I64P]
     lib.bh_shard_range.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    _I64P, _I64P]
@@ -396,6 +400,17 @@ class Engine:
         self._check(self._lib.bh_let_stats(self._h, out.ctypes.data_as(_I64P)))
         return dict(zip(("let_builds", "full_builds", "subset", "let_nodes", "overflows"),
                         out.tolist()))
+
+    def comm_ranks(self):
+        """(ncclCommCount, ncclCommUserRank) of the engine's RCCL communicator; (0, rank) for
+        an engine without one (bh_comm_ranks)."""
+        c, r = ctypes.c_int32(0), ctypes.c_int32(0)
+        self._check(self._lib.bh_comm_ranks(self._h, ctypes.byref(c), ctypes.byref(r)))
+        return c.value, r.value
+
+    def debug_inject(self, what: int = 1):
+        """Test hook (bh_debug_inject): 1 = the next LET build of this rank trips its guard."""
+        self._check(self._lib.bh_debug_inject(self._h, int(what)))
 
     def set_profiling(self, on: bool):
         self._check(self._lib.bh_set_profiling(self._h, 1 if on else 0))

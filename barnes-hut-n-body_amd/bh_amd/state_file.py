@@ -1,6 +1,6 @@
 """Reader / writer of the engine's on-disk state format (bh_save_state / bh_load_state, layout in
-csrc/state_io.cpp): 80-byte little-endian header (magic "BHSTATE1", header size 64, flags,
-bh_params, N) followed by x, y, vx, vy, m as fp64 arrays in the caller's list order.  Host-only
+csrc/state_io.cpp): 80-byte little-endian header (magic "BHSTATE1", the uint32 size 64 of the
+block from byte 16 to the body arrays, flags, bh_params, N) followed by x, y, vx, vy, m as fp64 arrays in the caller's list order.  Host-only
 (numpy); used to inspect checkpoints and to build fixtures without a GPU."""
 from __future__ import annotations
 

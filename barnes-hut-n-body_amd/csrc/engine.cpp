@@ -6,13 +6,15 @@
 // kernel sequence on that stream; the only host round trip is the merge rule's (BHA:463-532)
 // candidate mailbox, and only while heavy bodies exist.
 //
-// Multi-GPU (bh_create_dist): every rank holds the full replicated state; force evaluation is
-// sharded by contiguous Morton ranges and the accelerations are all-gathered in place with
-// RCCL over xGMI, after which every rank integrates the full set.  The build is sharded too:
-// each rank builds a locally essential tree (let.hip) -- the cells its bodies may open, plus
-// the top assembled from every rank's cell values -- and sends its bodies' (possibly jittered)
-// positions with the accelerations; every BH_LET_REFRESH builds, and at the end of every
-// bh_step call (lastTree, BHA:435), the full tree is built by every rank.  The merge rule is
+// Multi-GPU (bh_create_dist): every rank holds a replica of the state and owns one contiguous
+// range of the Hilbert wave order.  The build is sharded: each rank builds a locally essential
+// tree (let.hip) -- the cells its bodies may open, plus the top assembled from every rank's cell
+// values (one all-gather of the cell tables) -- evaluates its range, kicks (and drifts) its own
+// bodies in the traversal's epilogue, and the new positions (16 B per body) are all-gathered in
+// place with RCCL over xGMI; velocities stay with their owners until the next full build, before
+// which they are all-gathered.  Every BH_LET_REFRESH builds, after a reset and for the last build
+// of every bh_step call (lastTree, BHA:435) the full tree is built by every rank; its
+// accelerations are all-gathered and every rank integrates every body.  The merge rule is
 // replicated (identical inputs, identical outcome) and needs no exchange.
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
@@ -187,6 +189,7 @@ struct bh_engine {
     bh::SpanSlot *s_span_children = nullptr;
     Node *s_nodes = nullptr;
     hipEvent_t table_ev = nullptr;
+    bool inject_guard = false;  // bh_debug_inject(1): the next LET build trips k_let_guard
     // bh_create_solo (measurement): no peers; their cells' values from the last full build
     bool solo = false;
     LetCell *solo_table = nullptr;
@@ -744,7 +747,16 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
                                      hipMemcpyDeviceToDevice, e->stream));
         }
     }
-    HIPCHK(e, let_assemble(n_sub, e->geo, pc, e->L, sb, e->scalars, e->stream));
+    {
+        // bh_debug_inject: a node array of one record makes k_let_guard fire on this rank only,
+        // exactly as a broken invariant would (empty tree, idle lanes, replay flag set)
+        const uint32_t node_cap = e->L.node_cap;
+        if (e->inject_guard) e->L.node_cap = 1u;
+        e->inject_guard = false;
+        const hipError_t rc = let_assemble(n_sub, e->geo, pc, e->L, sb, e->scalars, e->stream);
+        e->L.node_cap = node_cap;
+        HIPCHK(e, rc);
+    }
     TRY(mark(e, 0));
     const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};
     const int W = 2;  // (x, y) per lane
@@ -1017,6 +1029,38 @@ int restore(bh_engine *e) {
     return BH_OK;
 }
 
+// End of a bh_step call with LET builds (every rank's stream is idle): the call's LET status words
+// scalars[4] (some subset overflowed, or a rank-local guard fired) and scalars[5] (largest subset),
+// max-reduced over the ranks, so that every rank replays the call or none does.
+int agree_let_flags(bh_engine *e, uint32_t ls[2], uint32_t *own_sub) {
+    HIPCHK(e, hipMemcpy(ls, e->scalars + 4, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
+    *own_sub = ls[1];
+    if (e->comm) {
+        NCCLCHK(e, ncclAllReduce(e->scalars + 4, e->scalars + 4, 2, ncclUint32, ncclMax, e->comm,
+                                 e->stream));
+        HIPCHK(e, hipMemcpyAsync(ls, e->scalars + 4, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                 e->stream));
+        HIPCHK(e, hipStreamSynchronize(e->stream));
+        return BH_OK;
+    }
+    if (!e->group) return BH_OK;  // solo: no peers
+    e->group->barrier();          // every member's call is complete on the device
+    for (bh_engine *peer : e->group->members) {
+        if (peer == e) continue;
+        uint32_t q[2] = {0, 0};
+        const hipError_t rc = hipMemcpy(q, peer->scalars + 4, sizeof(q), hipMemcpyDeviceToHost);
+        if (rc != hipSuccess) {  // still pass the second barrier: the peers wait for it
+            e->group->barrier();
+            e->err = std::string("agree_let_flags: ") + hipGetErrorString(rc);
+            return BH_E_DEVICE;
+        }
+        ls[0] = std::max(ls[0], q[0]);
+        ls[1] = std::max(ls[1], q[1]);
+    }
+    e->group->barrier();  // nobody clears its flags (a replay) before every member has read them
+    return BH_OK;
+}
+
 // ---- one PhysicsEngine.step() (BHA:405-439) ------------------------------------------
 // last: the final step of a bh_step call -- its second build is the full tree (lastTree,
 // BHA:435, for getTreeForDebug) also on a multi-rank engine that shards its builds.
@@ -1200,6 +1244,52 @@ void bh::set_error(bh_engine *e, const std::string &msg) {
     if (e) e->err = msg;
 }
 
+// The per-process settings that decide which collectives a step issues and how large each piece
+// is -- BH_LET (LET builds: the cell-table all-gather) and BH_ROUND_FRACS (the round sizes of
+// bh_shard_range / bh_gather_slot) -- must be equal on every rank, or the collectives stop
+// matching and the run hangs.  Min- and max-reduced over the ranks at creation: every rank sees
+// the same comparison, so all of them fail together on a mismatch.
+static int agree_settings(bh_engine *e) {
+    constexpr int K = 2 + BH_SHARD_ROUNDS + 1;
+    double v[K];
+    v[0] = e->let_on ? 1.0 : 0.0;
+    v[1] = e->let_forced ? 1.0 : 0.0;
+    const double *cum = round_cum();
+    for (int j = 0; j <= BH_SHARD_ROUNDS; ++j) v[2 + j] = cum[j];
+    double *d = nullptr;
+    if (hipMalloc((void **)&d, sizeof(double) * 3 * K) != hipSuccess) {
+        e->err = "agree_settings: hipMalloc";
+        return BH_E_DEVICE;
+    }
+    double lo[K], hi[K];
+    ncclResult_t nr = ncclSuccess;
+    hipError_t hr = hipMemcpyAsync(d, v, sizeof(v), hipMemcpyHostToDevice, e->stream);
+    if (hr == hipSuccess) nr = ncclAllReduce(d, d + K, K, ncclFloat64, ncclMin, e->comm, e->stream);
+    if (hr == hipSuccess && nr == ncclSuccess)
+        nr = ncclAllReduce(d, d + 2 * K, K, ncclFloat64, ncclMax, e->comm, e->stream);
+    if (hr == hipSuccess && nr == ncclSuccess)
+        hr = hipMemcpyAsync(lo, d + K, sizeof(lo), hipMemcpyDeviceToHost, e->stream);
+    if (hr == hipSuccess && nr == ncclSuccess)
+        hr = hipMemcpyAsync(hi, d + 2 * K, sizeof(hi), hipMemcpyDeviceToHost, e->stream);
+    if (hr == hipSuccess) hr = hipStreamSynchronize(e->stream);
+    (void)hipFree(d);
+    if (nr != ncclSuccess) {
+        e->err = std::string("agree_settings: ") + ncclGetErrorString(nr);
+        return BH_E_COMM;
+    }
+    if (hr != hipSuccess) {
+        e->err = std::string("agree_settings: ") + hipGetErrorString(hr);
+        return BH_E_DEVICE;
+    }
+    for (int j = 0; j < K; ++j)
+        if (lo[j] != hi[j]) {
+            e->err = "BH_LET / BH_ROUND_FRACS differ between ranks: every rank must run with the "
+                     "same settings";
+            return BH_E_INVALID;
+        }
+    return BH_OK;
+}
+
 // =========================================================================================
 extern "C" {
 
@@ -1261,6 +1351,7 @@ int bh_create_dist(const bh_params *p, int device, int rank, int world, const vo
             e->cap = 0;
             rc = ensure_capacity(e, cap);
         }
+        if (rc == BH_OK) rc = agree_settings(e);
     }
     if (rc != BH_OK) {
         std::fprintf(stderr, "bh_create_dist: %s\n", e->err.c_str());
@@ -1478,9 +1569,13 @@ int bh_step(bh_engine *e, int32_t k) {
         HIPCHK(e, hipStreamSynchronize(e->stream));
         if (may_let) {  // LET subset sizes of this call: [4] some rank overflowed, [5] largest
             uint32_t ls[2] = {0, 0};
-            HIPCHK(e, hipMemcpy(ls, e->scalars + 4, sizeof(ls), hipMemcpyDeviceToHost));
+            // [4] can be set after the cell tables were exchanged (k_let_guard, k_let_w): on one
+            // rank only.  Every rank must take the same decision, or one replays alone and issues
+            // collectives its peers never match -- so the flags are max-reduced over the ranks.
+            uint32_t own_sub = 0;
+            TRY(agree_let_flags(e, ls, &own_sub));
             if (ls[1] > 0) {
-                e->let_last_sub = ls[1];
+                e->let_last_sub = own_sub;
                 e->let_known = std::max<int64_t>(ls[1], ls[0] ? e->let_known : 1);
             }
             if (ls[0]) {  // every rank saw the overflow (exchanged): all replay the call
@@ -1728,6 +1823,29 @@ int bh_synchronize(bh_engine *e) {
     if (!e) return BH_E_INVALID;
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    return BH_OK;
+}
+
+int bh_comm_ranks(const bh_engine *e, int32_t *nranks, int32_t *rank) {
+    if (!e || !nranks || !rank) return BH_E_INVALID;
+    *nranks = 0;
+    *rank = e->rank;
+    if (!e->comm) return BH_OK;
+    int c = 0, r = 0;
+    if (ncclCommCount(e->comm, &c) != ncclSuccess || ncclCommUserRank(e->comm, &r) != ncclSuccess)
+        return BH_E_COMM;
+    *nranks = c;
+    *rank = r;
+    return BH_OK;
+}
+
+int bh_debug_inject(bh_engine *e, int what) {
+    if (!e) return BH_E_INVALID;
+    if (what != 1) {
+        e->err = "bh_debug_inject: unknown fault";
+        return BH_E_INVALID;
+    }
+    e->inject_guard = true;
     return BH_OK;
 }
 

@@ -4,7 +4,8 @@
 //
 //   offset  size        field
 //   0       8           magic "BHSTATE1"
-//   8       4           uint32 header bytes (= 64)
+//   8       4           uint32 size of the block from byte 16 to the body arrays (= 64): the
+//                       body arrays start at byte 16 + this field = 80
 //   12      4           uint32 flags (0)
 //   16      8 x 4       double G, dt, theta, soft2                (CFG:11,14,23,20)
 //   48      4 x 2       int32 width_px, height_px                 (CFG:5,8)
@@ -17,6 +18,7 @@
 // saved list reproduces every later step exactly.
 #include <cstdio>
 #include <cstring>
+#include <new>
 #include <string>
 #include <vector>
 
@@ -110,7 +112,7 @@ int bh_load_state(bh_engine *e, const char *path) {
         return bad("not a BHSTATE1 file");
     uint32_t hb = 0;
     std::memcpy(&hb, hdr + 8, 4);
-    if (hb != kHeaderBytes) return bad("unknown header size");
+    if (hb != kHeaderBytes) return bad("unknown header block size");
     bh_params p;
     std::memcpy(&p.G, hdr + 16, 8);
     std::memcpy(&p.dt, hdr + 24, 8);
@@ -123,7 +125,18 @@ int bh_load_state(bh_engine *e, const char *path) {
     int64_t n = 0;
     std::memcpy(&n, hdr + 72, 8);
     if (n < 0 || n > ((int64_t)1 << 40)) return bad("body count out of range");
-    std::vector<double> a((size_t)(5 * n) + 1);
+    // the file must be exactly the header plus 5 N doubles -- checked before allocating, so a
+    // corrupt or hostile N cannot ask for memory the file does not back
+    if (std::fseek(in.f, 0, SEEK_END) != 0) return bad("cannot seek");
+    const long len = std::ftell(in.f);
+    if (len < 0 || (int64_t)len != 80 + 40 * n) return bad("file length does not match N");
+    if (std::fseek(in.f, 80, SEEK_SET) != 0) return bad("cannot seek");
+    std::vector<double> a;
+    try {
+        a.resize((size_t)(5 * n) + 1);
+    } catch (const std::bad_alloc &) {
+        return bad("not enough host memory for the body arrays");
+    }
     if (n > 0 && std::fread(a.data(), sizeof(double), (size_t)(5 * n), in.f) != (size_t)(5 * n))
         return bad("truncated body arrays");
     int rc = bh_set_params(e, &p);

@@ -6,19 +6,31 @@ colliding galaxy disks (NBodyPanel.kt:83-100 scaled: 8e5 + 2e5 bodies, seeds 1/2
 dt 0.005, G 80, eps^2 1, merge rule on.  One step = the full reference step: two tree builds,
 two force evaluations, kick-drift-kick, merge.  Inputs are resident in HBM before timing.
 
-Multi-GPU (torchrun, one rank per GPU): the north-star configuration C4 (1e7-body uniform cloud,
-total fixed: strong scaling; `--config c3x` = weak scaling, 1e6 two-disk bodies per GPU).  The
-state is replicated; each rank builds a locally essential tree (only the cells its bodies can
-open, plus the top from every rank's cell values), evaluates and integrates its Hilbert-ordered
-lane range, and the new positions are all-gathered by RCCL over xGMI inside the engine.
+Multi-GPU (one rank per GPU): the north-star configuration C4 (1e7-body uniform cloud, total
+fixed: strong scaling; `--config c3x` = weak scaling, 1e6 two-disk bodies per GPU).  The state is
+replicated; each rank builds a locally essential tree (only the cells its bodies can open, plus
+the top from every rank's cell values), evaluates and integrates its Hilbert-ordered lane range,
+and the new positions are all-gathered by RCCL over xGMI inside the engine.
+  * `python bench.py --gpus N` (N > 1) outside torchrun starts `python -m torch.distributed.run
+    --nproc-per-node N ... bench.py ...` as a CHILD process before anything touches the GPU and
+    exits with its status (`--dry-run` prints that command); inside torchrun, WORLD_SIZE must
+    equal --gpus, and RCCL's own communicator size (ncclCommCount) must equal it too.
+  * After the timed region every rank checks itself (`--verify`, on by default): the engine is
+    reset to a committed golden configuration -- C4 x 10 steps on N > 1 GPUs (the north-star
+    scene through the sharded path), C3 x 10 steps on one GPU -- and the SHA-256 of every final
+    SoA field must equal tests/golden/digests.json (made by the CPU oracle) on every rank; a
+    mismatch prints the line with "verify" and exits non-zero.
 
 Prints ONE JSON line on rank 0 (see the driver contract in the task statement).
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -36,7 +48,9 @@ BODY_EVAL_BYTES = 40   # body read (x, y, m) + acceleration write (ax, ay) per e
 
 def parse():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (default: WORLD_SIZE under torchrun, else 1); N > 1 outside "
+                         "torchrun launches torchrun as a child process")
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", default=None,
@@ -51,7 +65,36 @@ def parse():
                     help="diagnostic: no HIP events in the timed region (no kernel times)")
     ap.add_argument("--cpu-steps", type=int, default=1)
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--verify", dest="verify", action="store_true", default=None,
+                    help="golden-digest self-check after the timed region (default on)")
+    ap.add_argument("--no-verify", dest="verify", action="store_false")
+    ap.add_argument("--no-single-gpu", action="store_true",
+                    help="N > 1: skip rank 0's one-GPU run of the same workload")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="print the launch plan (the torchrun child command for N > 1) and exit")
     return ap.parse_args()
+
+
+def _free_port() -> int:
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        return sk.getsockname()[1]
+
+
+def spawn_torchrun(args) -> int:
+    """`--gpus N` (N > 1) without torchrun: run the same command under torch.distributed.run as
+    a child process -- nothing in this process has touched the GPU, and no exec replaces it --
+    relaying the child's output (rank 0 prints the JSON line) and returning its exit status."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           "--master-port", str(_free_port()), os.path.abspath(__file__)]
+    cmd += [a for a in sys.argv[1:] if a != "--dry-run"]
+    if args.dry_run:
+        print(json.dumps({"launch": "torchrun child", "cmd": cmd}), flush=True)
+        return 0
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver
+    return subprocess.run(cmd, env=env).returncode
 
 
 def committed_traffic(config, kernel):
@@ -167,9 +210,133 @@ WORKLOAD_DESC = {
 }
 
 
+GOLDEN = os.path.join(ROOT, "tests", "golden", "digests.json")
+FIELDS = ("x", "y", "vx", "vy", "m")
+
+
+def _sha(a) -> str:
+    import numpy as np
+    return hashlib.sha256(np.ascontiguousarray(a, dtype="<f8").tobytes()).hexdigest()
+
+
+def verify_leg(bh_amd, eng, case, arrs, dist, rank, world):
+    """Reset the engine to the golden configuration `case` of tests/golden/digests.json, run its
+    steps in one bh_step call and compare the SHA-256 of every final SoA field (little-endian
+    fp64, caller order) with the oracle's; the digests of all ranks are compared as well."""
+    with open(GOLDEN) as fh:
+        want = json.load(fh)[case]
+    t0 = time.perf_counter()
+    eng.set_params(bh_amd.default_params(theta=want["theta"]))
+    eng.reset_bodies(*arrs)
+    eng.step(want["steps"])
+    state = eng.get_bodies()
+    mine = {"n": len(state[0])}
+    mine.update({f: _sha(a) for f, a in zip(FIELDS, state)})
+    match = mine["n"] == want["n"] and all(mine[f] == want[f] for f in FIELDS)
+    agree = True
+    if world > 1:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, mine)
+        agree = all(g == gathered[0] for g in gathered)
+        match = match and all(g["n"] == want["n"] and all(g[f] == want[f] for f in FIELDS)
+                              for g in gathered)
+    return {"case": case, "steps": want["steps"], "n": want["n"], "digest_match": bool(match),
+            "ranks_agree": bool(agree), "ranks": world,
+            "bad_fields": [f for f in FIELDS if mine[f] != want[f]],
+            "seconds": round(time.perf_counter() - t0, 3),
+            "source": "tests/golden/digests.json (SHA-256 of the CPU oracle's final state)"}
+
+
+def cpu_baseline_leg(args, arrs, scene_name, direct):
+    """The reference CPU path, restated in C (oracle/bh_oracle.c: serial pointer-tree build,
+    `threads` workers on an atomic body queue, BHA:359-395), on a bounded sample of the same
+    workload, timed on this host's cores."""
+    import numpy as np
+    import oracle
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    n0 = len(arrs[0])
+    if direct:
+        # theta = 0: one evaluation of a body subsample through the oracle's tree walk (every
+        # leaf visited), scaled to body-steps/s (2 evaluations per step)
+        ref = oracle.Oracle(*arrs, theta=0.0, threads=threads)
+        sample = np.arange(0, n0, max(1, n0 // 4096), dtype=np.int64)
+        c0 = time.perf_counter()
+        ref.accelerations(subset=sample)
+        c1 = time.perf_counter()
+        ref.close()
+        return {"value": round(len(sample) / (2.0 * (c1 - c0)), 1), "unit": "body-steps/s",
+                "cores": threads, "kind": "port",
+                "sample": f"one theta=0 evaluation of {len(sample)} of {n0} bodies (every leaf of "
+                          f"the tree) with the C restatement (oracle/bh_oracle.c), scaled by 2 "
+                          f"evaluations per step; includes the serial tree build",
+                "seconds": round(c1 - c0, 3)}
+    if n0 > 2_000_000:
+        # C4-sized: a full CPU step takes minutes, so one evaluation is timed in its two parts --
+        # the serial tree build of all bodies and the walk of every 128th body -- and one step
+        # is extrapolated as 2 x (build + walk of all bodies)
+        ref = oracle.Oracle(*arrs, theta=args.theta, threads=threads)
+        sample = np.arange(0, n0, 128, dtype=np.int64)
+        c0 = time.perf_counter()
+        ref.accelerations(subset=sample)
+        c1 = time.perf_counter()
+        t_build, t_walk_sample = ref.last_timing()
+        ref.close()
+        step_s = 2.0 * (t_build + t_walk_sample * n0 / len(sample))
+        return {"value": round(n0 / step_s, 1), "unit": "body-steps/s", "cores": threads,
+                "kind": "port",
+                "sample": f"{scene_name} ({n0} bodies), one evaluation with the C restatement "
+                          f"(oracle/bh_oracle.c): serial tree build of all bodies "
+                          f"{t_build:.2f} s, walk of every 128th body ({len(sample)} bodies, "
+                          f"{threads} workers) {t_walk_sample:.3f} s; one step extrapolated as "
+                          f"2 x (build + walk of all bodies) = {step_s:.1f} s",
+                "seconds": round(c1 - c0, 3)}
+    ref = oracle.Oracle(*arrs, theta=args.theta, threads=threads)
+    ref.step(1)  # same first step the GPU warmup took; bounded sample follows
+    c0 = time.perf_counter()
+    ref.step(args.cpu_steps)
+    c1 = time.perf_counter()
+    nb = ref.num_bodies()
+    ref.close()
+    return {"value": round(nb * args.cpu_steps / (c1 - c0), 1), "unit": "body-steps/s",
+            "cores": threads, "kind": "port",
+            "sample": f"{args.cpu_steps} full step(s) of {scene_name} ({nb} bodies) with the C "
+                      f"restatement of the reference CPU path (oracle/bh_oracle.c: serial "
+                      f"pointer-tree build, {threads} workers on an atomic body queue)",
+            "seconds": round(c1 - c0, 3)}
+
+
+def single_gpu_leg(bh_amd, params, device, arrs, steps, warmup):
+    """Rank 0 of a multi-GPU run: the same workload on its one GPU with the single-GPU engine
+    (a reference point for the driver's scaling curve; the N = 1 bench line runs C3)."""
+    eng = bh_amd.Engine(params, device=device)
+    eng.reset_bodies(*arrs)
+    if warmup > 0:
+        eng.step(warmup)
+    n0 = eng.num_bodies()
+    eng.synchronize()
+    t0 = time.perf_counter()
+    eng.step(steps)
+    eng.synchronize()
+    el = time.perf_counter() - t0
+    n1 = eng.num_bodies()
+    eng.close()
+    return {"value": round(0.5 * (n0 + n1) * steps / el, 1), "unit": "body-steps/s",
+            "ms_per_step": round(1e3 * el / max(steps, 1), 4), "n_gpus": 1,
+            "note": "rank 0's GPU alone, single-GPU engine, same scene / steps / warmup"}
+
+
 def main():
     args = parse()
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus is not None and args.gpus > 1:
+        sys.exit(spawn_torchrun(args))  # before anything touches the GPU
+    world = int(env_world) if env_world is not None else 1
+    if args.gpus is None:
+        args.gpus = world
+    if args.gpus != world:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: refusing to measure a "
+              f"different number of GPUs than asked", file=sys.stderr)
+        sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.config is None:  # BASELINE's metric on one GPU; the north-star cloud on N > 1
@@ -177,8 +344,12 @@ def main():
     if args.theta is None:
         args.theta = 0.0 if args.config == "c5" else 0.5
     direct = args.theta == 0.0
-    if args.gpus != world and world > 1:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}", file=sys.stderr)
+    if args.verify is None:
+        args.verify = True
+    if args.dry_run:
+        print(json.dumps({"launch": "in-process", "world": world, "config": args.config,
+                          "theta": args.theta, "verify": args.verify}), flush=True)
+        return
 
     import numpy as np
     import torch
@@ -191,10 +362,20 @@ def main():
     torch.cuda.set_device(local_rank)
 
     params = bh_amd.default_params(theta=args.theta)
+    rccl = None
     if world > 1:
         uid = [bh_amd.comm_unique_id() if rank == 0 else None]
         dist.broadcast_object_list(uid, src=0)
         eng = bh_amd.Engine(params, device=local_rank, rank=rank, world=world, unique_id=uid[0])
+        nr, ur = eng.comm_ranks()
+        views = [None] * world
+        dist.all_gather_object(views, [nr, ur])
+        rccl = {"comm_count": nr, "user_ranks": [v[1] for v in views]}
+        if any(v[0] != world for v in views) or sorted(v[1] for v in views) != list(range(world)):
+            if rank == 0:
+                print(f"bench.py: RCCL communicator {views} does not span the {world} ranks",
+                      file=sys.stderr)
+            sys.exit(3)
     else:
         eng = bh_amd.Engine(params, device=local_rank)
 
@@ -267,12 +448,13 @@ def main():
         extra = {"interactions_per_s": round(flops_per_launch / FLOP_PER_INTERACTION /
                                              (trav_ms * 1e-3)) if trav_ms > 0 else 0}
     else:
-        kernel = "k_traverse"
+        kernel = "k_traverse" if world == 1 else "k_traverse (one rank's 4 rounds, 2 streams)"
         cs = [c for c in (cnt_start, cnt_end) if c]
         contrib = float(np.mean([c["contrib_per_body"] for c in cs])) if cs else 0.0
         vbar = float(np.mean([c["vbar"] for c in cs])) if cs else 0.0
-        # world > 1: one launch per round evaluates 1 / (world * rounds) of the bodies
-        bodies_per_launch = bodies / (world * (bh_amd.SHARD_ROUNDS if world > 1 else 1))
+        # world > 1: one timed interval spans a rank's 4 round launches (its 1 / world of the
+        # bodies), from the first round's start to the last even round's end on its stream
+        bodies_per_launch = bodies / world
         flops_per_launch = FLOP_PER_INTERACTION * contrib * bodies_per_launch
         node_bytes = (NODE_BYTES * vbar + BODY_EVAL_BYTES) * bodies_per_launch
         extra = {
@@ -312,47 +494,23 @@ def main():
     }
     roofline.update(extra)
 
+    # rank 0's extra legs; the other ranks wait at the next collective
+    single = None
+    if rank == 0 and world > 1 and not args.no_single_gpu:
+        single = single_gpu_leg(bh_amd, params, local_rank, arrs, args.steps, args.warmup)
     cpu_baseline = None
-    if rank == 0 and world == 1 and not args.no_cpu_baseline and direct:
-        # theta = 0: one evaluation of a body subsample through the oracle's tree walk (every
-        # leaf visited), scaled to body-steps/s (2 evaluations per step)
-        import oracle
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        ref = oracle.Oracle(*arrs, theta=0.0, threads=threads)
-        sample = np.arange(0, n0, max(1, n0 // 4096), dtype=np.int64)
-        c0 = time.perf_counter()
-        ref.accelerations(subset=sample)
-        c1 = time.perf_counter()
-        cpu_baseline = {
-            "value": round(len(sample) / (2.0 * (c1 - c0)), 1),
-            "unit": "body-steps/s",
-            "cores": threads,
-            "kind": "port",
-            "sample": f"one theta=0 evaluation of {len(sample)} of {n0} bodies (every leaf of the "
-                      f"tree) with the C restatement (oracle/bh_oracle.c), scaled by 2 "
-                      f"evaluations per step; includes the serial tree build",
-            "seconds": round(c1 - c0, 3),
-        }
-        ref.close()
-    elif rank == 0 and world == 1 and not args.no_cpu_baseline:
-        import oracle
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        ref = oracle.Oracle(*arrs, theta=args.theta, threads=threads)
-        ref.step(1)  # same first step the GPU warmup took; bounded sample follows
-        c0 = time.perf_counter()
-        ref.step(args.cpu_steps)
-        c1 = time.perf_counter()
-        cpu_baseline = {
-            "value": round(ref.num_bodies() * args.cpu_steps / (c1 - c0), 1),
-            "unit": "body-steps/s",
-            "cores": threads,
-            "kind": "port",
-            "sample": f"{args.cpu_steps} full step(s) of {scene_name} ({ref.num_bodies()} bodies) "
-                      f"with the C restatement of the reference CPU path (oracle/bh_oracle.c: "
-                      f"serial pointer-tree build, {threads} workers on an atomic body queue)",
-            "seconds": round(c1 - c0, 3),
-        }
-        ref.close()
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu_baseline = cpu_baseline_leg(args, arrs, scene_name, direct)
+
+    verify = None
+    if world > 1:
+        dist.barrier()  # rank 0's extra legs are done: the verify leg's collectives start together
+    if args.verify:
+        from bh_amd import scenes
+        case = "c4_k10" if world > 1 else "c3_k10"
+        golden_scene = "c4" if world > 1 else "c3"
+        varrs = arrs if scene_name == golden_scene else scenes.config_scene(golden_scene)
+        verify = verify_leg(bh_amd, eng, case, varrs, dist, rank, world)
 
     if rank == 0:
         line = {
@@ -385,13 +543,23 @@ def main():
             "phase_ms": {k: round(v, 3) for k, v in phases.items()},
             "roofline": roofline,
             "cpu_baseline": cpu_baseline,
+            "verify": verify,
         }
+        if rccl is not None:
+            line["rccl"] = rccl
+        if single is not None:
+            line["single_gpu_same_workload"] = single
         if per_rank is not None:
             line["per_rank_phase_ms_per_step"] = per_rank
         print(json.dumps(line), flush=True)
     eng.close()
     if world > 1:
+        dist.barrier()
         dist.destroy_process_group()
+    if verify is not None and not (verify["digest_match"] and verify["ranks_agree"]):
+        if rank == 0:
+            print(f"bench.py: VERIFY FAILED: {verify}", file=sys.stderr)
+        sys.exit(4)
 
 
 if __name__ == "__main__":

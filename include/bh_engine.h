@@ -59,12 +59,34 @@ int bh_create(const bh_params *p, int device, bh_engine **out);
 
 /* Multi-GPU member: one process per GPU; `unique_id` is the 128-byte RCCL id produced by
  * bh_comm_unique_id() on rank 0 and broadcast by the caller (e.g. torch.distributed).
- * Every rank holds the full replicated state; force evaluation is sharded over ranks by
- * Morton-ordered body ranges and the accelerations are all-gathered over xGMI.  world == 1
- * with a non-NULL id runs the same RCCL path on one rank (used to test it on one GPU). */
+ * Replaces computeAccelerations' fan-out over worker threads (BHA:374-395) by a fan-out over
+ * GPUs.  Every rank holds a replica of the state and owns one contiguous range of the Hilbert
+ * wave order (bh_shard_range).  Per force evaluation a rank either
+ *   - builds a locally essential tree (from 4 ranks up, or BH_LET=1): only the depth-8 cells its
+ *     bodies can open, plus the top computed from every rank's cell values (one all-gather of
+ *     2 MB cell tables); it evaluates its range, kicks (and drifts) its own bodies, and the new
+ *     positions -- 16 B per body -- are all-gathered over RCCL in BH_SHARD_ROUNDS rounds into
+ *     every replica; velocities stay with their owners and are all-gathered before the next
+ *     full build; or
+ *   - builds the full tree (the first build after a reset, every 32 builds, the last build of a
+ *     bh_step call): it evaluates its range and the accelerations are all-gathered, after which
+ *     every rank integrates every body.
+ * The merge rule is replicated (identical inputs).  world == 1 with a non-NULL id runs the same
+ * RCCL path on one rank (used to test it on one GPU).  BH_LET and BH_ROUND_FRACS must be equal
+ * on every rank (checked at creation: BH_E_INVALID on every rank otherwise). */
 int bh_create_dist(const bh_params *p, int device, int rank, int world, const void *unique_id,
                    bh_engine **out);
 int bh_comm_unique_id(void *out128);
+
+/* RCCL's own view of the engine's communicator: *nranks = ncclCommCount, *rank =
+ * ncclCommUserRank; *nranks = 0 (and *rank = the engine's rank) for an engine without one
+ * (single GPU, in-process group, solo). */
+int bh_comm_ranks(const bh_engine *e, int32_t *nranks, int32_t *rank);
+
+/* Test hook: what == 1 -- the next locally essential tree build of this rank trips the node
+ * array guard (let.hip k_let_guard), as a broken invariant on one rank would; the call must then
+ * be replayed by every rank of the group alike. */
+int bh_debug_inject(bh_engine *e, int what);
 
 /* In-process rank group (testing the multi-GPU decomposition on one device, where RCCL refuses
  * several ranks): `world` engines of one process, each driven by its own host thread with
@@ -96,8 +118,11 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
                     const double *vy, const double *m);
 
 /* On-disk state (checkpoint / resume): the Config fields and the body list in the caller's
- * order as one little-endian file ("BHSTATE1" magic, 64-byte header of bh_params + N, then
- * x[N], y[N], vx[N], vy[N], m[N] fp64; layout in csrc/state_io.cpp).  Loading = bh_set_params
+ * order as one little-endian file: an 80-byte header -- the 8-byte magic "BHSTATE1", a uint32
+ * holding the size of the block that follows the first 16 bytes (64: the bh_params fields and
+ * the int64 N), a uint32 flags word (0), that block -- then x[N], y[N], vx[N], vy[N], m[N] fp64
+ * from byte 16 + 64 = 80 (layout in csrc/state_io.cpp).  A file whose length is not
+ * 80 + 40 N is rejected (BH_E_INVALID) before anything is allocated.  Loading = bh_set_params
  * + bh_reset_bodies (resetBodies, BHA:342-349) of the saved list, so a resumed run is
  * bit-identical to an uninterrupted one.  The file is written to path.tmp, then renamed. */
 int bh_save_state(bh_engine *e, const char *path);

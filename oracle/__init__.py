@@ -64,6 +64,8 @@ def load():
     lib.oracle_quads.argtypes = [ctypes.c_void_p, _D, _D, _D, ctypes.c_int64]
     lib.oracle_quads.restype = ctypes.c_int64
     lib.oracle_tree_stats.argtypes = [ctypes.c_void_p, _I64P, _I64P]
+    lib.oracle_last_timing.argtypes = [ctypes.c_void_p, _D, _D]
+    lib.oracle_last_timing.restype = None
     lib.oracle_group_union.argtypes = [ctypes.c_void_p, _I64P, ctypes.c_int64, ctypes.c_int, _I64P,
                                        _I64P]
     lib.oracle_group_union.restype = ctypes.c_int64
@@ -143,6 +145,12 @@ class Oracle:
         vis = np.empty(cnt, dtype=np.int64)
         self._lib.oracle_accel(self._h, cnt, sp, _dp(ax), _dp(ay), vis.ctypes.data_as(_I64P))
         return (ax, ay, vis) if visits else (ax, ay)
+
+    def last_timing(self):
+        """(build seconds, walk seconds) of the last accelerations() call."""
+        b, w = ctypes.c_double(0.0), ctypes.c_double(0.0)
+        self._lib.oracle_last_timing(self._h, ctypes.byref(b), ctypes.byref(w))
+        return b.value, w.value
 
     def quads(self):
         n = self._lib.oracle_quads(self._h, None, None, None, 0)

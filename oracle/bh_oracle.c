@@ -31,6 +31,7 @@
 #include <stdint.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <unistd.h>
 
 #include "bh_oracle.h"
@@ -224,7 +225,14 @@ struct oracle_engine {
     Tree tree;       /* last built tree (BHA:304 lastTree) */
     int tree_valid;
     int threads;
+    double t_build, t_walk; /* seconds of the last oracle_accel's build and walk (bench.py) */
 };
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
 
 /* BHA:359-366 — root Quad(W/2, H/2, max(W,H)/2 + 2); insert in list order. */
 static void build_tree(oracle_engine *e) {
@@ -433,9 +441,13 @@ int oracle_step(oracle_engine *e, int k) {
 int oracle_accel(oracle_engine *e, int64_t count, const int64_t *subset, double *ax, double *ay,
                  int64_t *visits) {
     ensure_acc(e);
+    const double t0 = now_s();
     build_tree(e);
+    const double t1 = now_s();
     if (!subset) count = e->n;
     compute_accelerations(e, subset, count);
+    e->t_build = t1 - t0;
+    e->t_walk = now_s() - t1;
     for (int64_t k = 0; k < count; ++k) {
         int64_t i = subset ? subset[k] : k;
         if (ax) ax[k] = e->ax[i];
@@ -443,6 +455,12 @@ int oracle_accel(oracle_engine *e, int64_t count, const int64_t *subset, double 
         if (visits) visits[k] = e->visits[i];
     }
     return 0;
+}
+
+/* Timing of the last oracle_accel (the CPU baseline's bounded sample, bench.py). */
+void oracle_last_timing(const oracle_engine *e, double *build_s, double *walk_s) {
+    *build_s = e->t_build;
+    *walk_s = e->t_walk;
 }
 
 /* BHA:265-274 visitQuads on getTreeForDebug() (BHA:329-332). */

@@ -34,6 +34,8 @@ int oracle_step(oracle_engine *e, int k);
 int oracle_accel(oracle_engine *e, int64_t count, const int64_t *subset, double *ax, double *ay,
                  int64_t *visits);
 int64_t oracle_quads(oracle_engine *e, double *cx, double *cy, double *h, int64_t cap);
+/* seconds spent by the last oracle_accel in the serial tree build and in the walk */
+void oracle_last_timing(const oracle_engine *e, double *build_s, double *walk_s);
 void oracle_tree_stats(oracle_engine *e, int64_t *n_nodes, int64_t *n_nonempty);
 /* analysis: wave-union iterations of groups of `group` consecutive bodies of `order` */
 int64_t oracle_group_union(oracle_engine *e, const int64_t *order, int64_t count, int group,

@@ -826,6 +826,114 @@ def test_let_subset_overflow_replays_the_call():
             assert bits_equal(got[r][k], want[k]), f"rank {r}: {name}"
 
 
+def _nonpositive_scene(kind):
+    """A 120 000-body cloud with non-positive masses for the LET halo rule (let.hip
+    let_include_gap2): the rule needs every cell's centre of mass inside its cell, which holds
+    only because computeMass skips children of mass <= 0 (BHA:189-192) -- a cell of non-positive
+    bodies becomes a mass-0 record that no walk visits (BHA:216).  "negative": 40 squares of
+    3 .. 40 px whose bodies all have negative mass (both near and far from any rank's range),
+    3 % negative singles, out-of-root bodies of both signs, two heavy bodies (merges active).
+    "zero": as "negative" plus zero-mass bodies, whose a = 0/0 makes them NaN after the first
+    kick (the reference's behaviour), so every later LET build selects every cell."""
+    rng = np.random.default_rng(57 if kind == "negative" else 58)
+    x, y, vx, vy, m = (a.copy() for a in scenes.uniform(120_000, 0.5, seed=56))
+    for _ in range(40):
+        cx, cy = rng.uniform(0, 2400), rng.uniform(0, 800)
+        half = rng.uniform(1.5, 20.0)
+        inside = (np.abs(x - cx) < half) & (np.abs(y - cy) < half)
+        m[inside] = -rng.uniform(0.1, 0.9, inside.sum())
+    singles = rng.choice(len(x), 3600, replace=False)
+    m[singles] = -0.5
+    if kind == "zero":
+        m[rng.choice(len(x), 200, replace=False)] = 0.0
+    ex = np.concatenate([rng.uniform(-600, -1, 40), rng.uniform(2405, 3000, 40), [1200.0, 800.0]])
+    ey = np.concatenate([rng.uniform(-300, 1100, 80), [400.0, 200.0]])
+    em = np.concatenate([np.where(rng.random(80) < 0.5, -0.7, 0.7), [6000.0, 5000.0]])
+    k = len(ex)
+    arrs = (np.concatenate([x, ex]), np.concatenate([y, ey]), np.concatenate([vx, np.zeros(k)]),
+            np.concatenate([vy, np.zeros(k)]), np.concatenate([m, em]))
+    perm = rng.permutation(len(arrs[0]))
+    return tuple(a[perm] for a in arrs)
+
+
+@pytest.mark.parametrize("world,kind", [(4, "negative"), (8, "negative"), (4, "zero")])
+def test_let_nonpositive_masses(world, kind, monkeypatch):
+    """The LET's halo rule with zero and negative masses: cells whose bodies are all negative
+    (mass-0 records) inside and beyond the halo, negative singles and out-of-root bodies, merges
+    active -- every rank of the group equals the single-GPU engine bit for bit, and the
+    single-GPU engine equals the oracle (NaN payloads of the zero-mass bodies as "both NaN")."""
+    monkeypatch.setenv("BH_LET", "1")
+    arrs = _nonpositive_scene(kind)
+    params = bh_amd.default_params(theta=0.5)
+    single = bh_amd.Engine(params, device=0)
+    single.reset_bodies(*arrs)
+    ref = oracle.Oracle(*arrs, theta=0.5, threads=16)
+    for k in (4, 3):
+        single.step(k)
+        ref.step(k)
+    want = single.get_bodies()
+    _assert_state_equal(single, ref, nan_ok=(kind == "zero"))
+    single.close()
+    ref.close()
+    got, stats = _run_group(world, params, arrs, (4, 3))
+    assert len(want[0]) < len(arrs[0])  # the heavy bodies merged
+    for r in range(world):
+        assert stats[r]["let_builds"] == 11 and stats[r]["full_builds"] == 3, stats[r]
+        if kind == "negative":  # sharded: the halo rule ran, not the select-everything fallback
+            assert stats[r]["subset"] < 0.75 * len(want[0]), stats[r]
+        for k, name in enumerate(FIELDS):
+            assert np.array_equal(got[r][k].view(np.int64), want[k].view(np.int64)), \
+                f"rank {r}: {name}"
+
+
+def test_let_guard_on_one_rank_replays_every_rank(monkeypatch):
+    """A rank-local LET fault (k_let_guard tripped on rank 1 only, after the cell tables were
+    exchanged: bh_debug_inject) is max-reduced over the ranks at the end of the call, so every
+    rank replays it -- none hangs in an unmatched exchange -- and the states still equal the
+    single-GPU engine's bit for bit."""
+    import threading
+    monkeypatch.setenv("BH_LET", "1")
+    arrs = scenes.uniform(80_000, 0.5, seed=61)
+    params = bh_amd.default_params(theta=0.5)
+    single = bh_amd.Engine(params, device=0)
+    single.reset_bodies(*arrs)
+    single.step(3)
+    single.step(2)
+    want = single.get_bodies()
+    single.close()
+    world = 3
+    group = bh_amd.LocalGroup(world)
+    engines = [bh_amd.Engine(params, device=0, rank=r, local_group=group) for r in range(world)]
+    got, stats, errors = [None] * world, [None] * world, []
+
+    def run(r):
+        try:
+            engines[r].reset_bodies(*arrs)
+            if r == 1:
+                engines[r].debug_inject(1)
+            engines[r].step(3)
+            engines[r].step(2)
+            got[r] = engines[r].get_bodies()
+            stats[r] = engines[r].let_stats()
+        except Exception as exc:  # surfaced below
+            errors.append(exc)
+
+    threads = [threading.Thread(target=run, args=(r,)) for r in range(world)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors
+    assert not any(t.is_alive() for t in threads), "rank thread hung"
+    for e in engines:
+        e.close()
+    group.close()
+    for r in range(world):
+        assert stats[r]["overflows"] == 1, stats[r]  # the same single replay on every rank
+        for k, name in enumerate(FIELDS):
+            assert bits_equal(got[r][k], want[k]), f"rank {r}: {name}"
+
+
 def test_let_every_body_in_a_coincident_pair(monkeypatch):
     """Every body a coincident pair: each build moves every body (the h < 1e-3 jitter,
     BHA:146-151) -- on the rank that owns it and on every rank whose halo holds it; the owners'
