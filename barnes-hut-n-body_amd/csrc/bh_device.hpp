@@ -35,6 +35,11 @@ static_assert(sizeof(Node) == 32, "node record must be 32 bytes");
 // meta bits
 constexpr uint32_t NODE_LEAF = 1u << 31;             // leaf holding one body (BHA:97)
 constexpr uint32_t NODE_SKIP = 1u << 30;             // mass == 0.0: never visited (BHA:216)
+// An internal node of mass 0 (every child of mass <= 0, filtered out by computeMass, BHA:189-192)
+// carries NODE_SKIP | NODE_LEAF: the reference returns there (BHA:216) and never reaches its
+// children -- which may hold negative-mass bodies -- so the exact walk skips it, and the fast
+// walk (which tests no flag) takes it as a leaf: an exact +-0 term, and the cursor moves past the
+// subtree.  Such a node is told from a real leaf by next > index + 1.
 constexpr uint32_t NODE_BODY_MASK = (1u << 30) - 1;  // leaf: body slot (Morton position)
 constexpr uint32_t NODE_DEPTH2_MASK = 0xFFu;         // internal: 2 x depth (root = 0)
 constexpr int NODE_JMASK_SHIFT = 8;                  // jitter cell: children that got subdivided
@@ -306,9 +311,10 @@ struct LeafList {
     uint32_t *slot;  // body slot (self-skip)
 };
 size_t leaf_select_bytes(int64_t node_cap);
+// cover: 2 (node_cap + 1) int32 of scratch (leaves under a mass-0 node are never visited)
 hipError_t leaf_list_build(const Node *nodes, const uint32_t *d_T, int64_t node_cap,
                            uint8_t *flags, uint32_t *sel, uint32_t *d_count, const LeafList &L,
-                           int64_t n, void *tmp, size_t tmp_bytes, hipStream_t s);
+                           int64_t n, int32_t *cover, void *tmp, size_t tmp_bytes, hipStream_t s);
 void direct_forces(const LeafList &L, const uint32_t *d_count, const double *x, const double *y,
                    const double *m, int64_t lo, int64_t hi, double G, double soft2, double *a2,
                    hipStream_t s);

@@ -9,6 +9,7 @@
 // body) reads them as broadcasts in sequence order — the reference's order, so the result is
 // bit-identical to the tree walk — with no criterion, cursor or ballot in the loop.  Bound by
 // fp64 VALU issue (one v_rsq_f64 and ~35 fp64 ops per interaction).
+#include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_select.hpp>
 #include <rocprim/iterator/counting_iterator.hpp>
 
@@ -24,8 +25,25 @@ constexpr int TB = 256;
 #endif
 constexpr int TILE = BH_DIRECT_TILE;
 
+// The subtree [i + 1, next) of every mass-0 internal node (NODE_SKIP with descendants): the
+// reference returns at that node (BHA:216) and never reaches its leaves -- which can hold
+// negative masses -- so they must not enter the leaf sequence.  +1 / -1 at the range ends, then
+// a prefix sum counts the covering mass-0 ancestors of every node.
+__global__ __launch_bounds__(TB) void k_leaf_cover(const Node *__restrict__ nodes,
+                                                   const uint32_t *__restrict__ d_T,
+                                                   int32_t *__restrict__ cover, int64_t cap) {
+    const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= cap || i >= (int64_t)*d_T) return;
+    const Node nd = nodes[i];
+    if ((nd.meta & NODE_SKIP) && (int64_t)nd.next > i + 1) {
+        atomicAdd(cover + i + 1, 1);
+        atomicAdd(cover + min((int64_t)nd.next, cap), -1);
+    }
+}
+
 __global__ __launch_bounds__(TB) void k_leaf_flags(const Node *__restrict__ nodes,
                                                    const uint32_t *__restrict__ d_T,
+                                                   const int32_t *__restrict__ covered,
                                                    uint8_t *__restrict__ flags, int64_t cap) {
     const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= cap) return;
@@ -33,7 +51,8 @@ __global__ __launch_bounds__(TB) void k_leaf_flags(const Node *__restrict__ node
     uint8_t f = 0;
     if (i < (int64_t)T) {
         const uint32_t meta = nodes[i].meta;
-        f = (meta & NODE_LEAF) && !(meta & NODE_SKIP);  // BHA:216 (mass == 0 never visited)
+        // BHA:216: mass == 0 never visited, nor is anything below a massless node
+        f = (meta & NODE_LEAF) && !(meta & NODE_SKIP) && covered[i] == 0;
     }
     flags[i] = f;
 }
@@ -160,20 +179,30 @@ __global__ __launch_bounds__(TB) void k_direct(LeafList L, const uint32_t *__res
 }  // namespace
 
 size_t leaf_select_bytes(int64_t node_cap) {
-    size_t b = 0;
+    size_t b = 0, c = 0;
     (void)rocprim::select(nullptr, b, rocprim::counting_iterator<uint32_t>(0),
                           (const uint8_t *)nullptr, (uint32_t *)nullptr, (uint32_t *)nullptr,
                           (size_t)node_cap);
-    return b;
+    (void)rocprim::inclusive_scan(nullptr, c, (const int32_t *)nullptr, (int32_t *)nullptr,
+                                  (size_t)node_cap, rocprim::plus<int32_t>());
+    return b > c ? b : c;
 }
 
 hipError_t leaf_list_build(const Node *nodes, const uint32_t *d_T, int64_t node_cap,
                            uint8_t *flags, uint32_t *sel, uint32_t *d_count, const LeafList &L,
-                           int64_t n, void *tmp, size_t tmp_bytes, hipStream_t s) {
+                           int64_t n, int32_t *cover, void *tmp, size_t tmp_bytes, hipStream_t s) {
     if (node_cap <= 0) return hipSuccess;
-    k_leaf_flags<<<(unsigned)((node_cap + TB - 1) / TB), TB, 0, s>>>(nodes, d_T, flags, node_cap);
-    hipError_t st = rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<uint32_t>(0),
-                                    flags, sel, d_count, (size_t)node_cap, s);
+    const unsigned grid = (unsigned)((node_cap + TB - 1) / TB);
+    int32_t *covered = cover + node_cap + 1;
+    hipError_t st = hipMemsetAsync(cover, 0, sizeof(int32_t) * (size_t)(node_cap + 1), s);
+    if (st != hipSuccess) return st;
+    k_leaf_cover<<<grid, TB, 0, s>>>(nodes, d_T, cover, node_cap);
+    st = rocprim::inclusive_scan(tmp, tmp_bytes, cover, covered, (size_t)node_cap,
+                                 rocprim::plus<int32_t>(), s);
+    if (st != hipSuccess) return st;
+    k_leaf_flags<<<grid, TB, 0, s>>>(nodes, d_T, covered, flags, node_cap);
+    st = rocprim::select(tmp, tmp_bytes, rocprim::counting_iterator<uint32_t>(0),
+                         flags, sel, d_count, (size_t)node_cap, s);
     if (st != hipSuccess) return st;
     if (n > 0) k_leaf_gather<<<(unsigned)((n + TB - 1) / TB), TB, 0, s>>>(nodes, sel, d_count, L);
     return hipGetLastError();

@@ -144,6 +144,7 @@ struct bh_engine {
     // theta = 0 all-pairs path (direct.hip), allocated on first use
     uint8_t *leaf_flags = nullptr;
     uint32_t *leaf_sel = nullptr, *leaf_count = nullptr;
+    int32_t *leaf_cover = nullptr;  // 2 (node_cap + 1): subtrees of massless nodes
     LeafList leaves{nullptr, nullptr, nullptr};
     void *leaf_tmp = nullptr;
     size_t leaf_tmp_bytes = 0;
@@ -482,6 +483,7 @@ int ensure_direct(bh_engine *e) {
     TRY(dev_alloc(e, e->leaf_flags, e->node_cap));
     TRY(dev_alloc(e, e->leaf_sel, (size_t)e->node_cap));
     TRY(dev_alloc(e, e->leaf_count, 1));
+    TRY(dev_alloc(e, e->leaf_cover, 2 * ((size_t)e->node_cap + 1)));
     TRY(dev_alloc(e, e->leaves.xy, 2 * (size_t)e->cap));
     TRY(dev_alloc(e, e->leaves.m, (size_t)e->cap));
     TRY(dev_alloc(e, e->leaves.slot, (size_t)e->cap));
@@ -826,8 +828,8 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
     if (direct) {
         TRY(ensure_direct(e));
         HIPCHK(e, leaf_list_build(e->nodes, d_T, (int64_t)e->node_cap, e->leaf_flags, e->leaf_sel,
-                                  e->leaf_count, e->leaves, n, e->leaf_tmp, e->leaf_tmp_bytes,
-                                  e->stream));
+                                  e->leaf_count, e->leaves, n, e->leaf_cover, e->leaf_tmp,
+                                  e->leaf_tmp_bytes, e->stream));
     }
     const TraverseCounters counters{visits, e->contrib32, e->wave_iters, e->wave_blocks};
     const uint32_t *lanes = e->lanes_valid ? e->lanes : nullptr;  // [lo, hi): lane ranges
@@ -1476,7 +1478,7 @@ void bh_destroy(bh_engine *e) {
                     e->base, e->cell_start, e->nodes, e->span_list, e->super_list,
                     e->span_children, e->scalars, e->visits32, e->contrib32, e->lanes, e->wave_iters, e->wave_blocks, e->heavy, e->keep,
                     e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->mbits, e->mslot, e->scratch,
-                    e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaves.xy, e->leaves.m,
+                    e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaf_cover, e->leaves.xy, e->leaves.m,
                     e->leaves.slot, e->leaf_tmp, e->spl, e->bcount, e->bstart};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);

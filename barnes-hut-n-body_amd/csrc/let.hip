@@ -443,7 +443,7 @@ __global__ __launch_bounds__(TB) void k_let_write_top(LetBufs L) {
     nd.mass = v.mass;
     if (v.cnt >= 2u) {
         nd.next = L.posc[((uint64_t)i + 1) << sh];
-        nd.meta = (uint32_t)(2 * d) | (v.mass > 0.0 ? 0u : NODE_SKIP);
+        nd.meta = (uint32_t)(2 * d) | (v.mass > 0.0 ? 0u : NODE_SKIP | NODE_LEAF);
     } else {
         nd.next = pos + 1;
         nd.meta = NODE_LEAF | leaf_slot(L, v.tag) | (v.mass == 0.0 ? NODE_SKIP : 0u);
@@ -466,7 +466,7 @@ __global__ __launch_bounds__(TB) void k_let_write_cells(LetBufs L) {
     nd.mass = v.mass;
     nd.next = pos + 1;
     if (v.cnt >= 2u)
-        nd.meta = (uint32_t)(2 * LET_P) | (v.mass > 0.0 ? 0u : NODE_SKIP);
+        nd.meta = (uint32_t)(2 * LET_P) | (v.mass > 0.0 ? 0u : NODE_SKIP | NODE_LEAF);
     else
         nd.meta = NODE_LEAF | leaf_slot(L, (uint32_t)c) | (v.mass == 0.0 ? NODE_SKIP : 0u);
     if (pos < L.node_cap) L.nodes[pos] = nd;

@@ -64,9 +64,10 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
         asm volatile("" : "+s"(meta));  // keep the flag tests scalar (s_bitcmp)
         uint32_t next = rec[6];
         next = next > cur ? next : cur + 1;  // structural guard: the cursor always advances
-        // mass == 0.0 (BHA:216): not visited.  The fast path needs no test: such a node's
-        // terms are exact +-0 (mass 0, finite f) and opening it only walks massless children,
-        // so the sums are unchanged -- only the visit-counting variant must skip it.
+        // mass == 0.0 (BHA:216): not visited.  The fast path needs no test: a massless leaf's
+        // term is an exact +-0 (mass 0, finite f), and a massless internal node carries the leaf
+        // flag too (bh_device.hpp NODE_SKIP), so the wave never descends below it -- only the
+        // visit-counting variant must skip it.
         if ((!FAST || COUNT) && (meta & NODE_SKIP)) {
             cur = next;
             nrec = OFF32 ? nload_off(nodes, cur) : nload(nodes + cur);

@@ -689,9 +689,9 @@ __device__ __forceinline__ void node_com(Node *nodes, uint32_t ni, const Geometr
     if (mSum > 0.0) {
         nd.comX = cx / mSum;
         nd.comY = cy / mSum;
-    } else {  // BHA:197-199 (never visited: mass == 0)
+    } else {  // BHA:197-199 (never visited: mass == 0; a skip-leaf, see NODE_SKIP)
         cell_centre(g, key, L, nd.comX, nd.comY);
-        nd.meta |= NODE_SKIP;
+        nd.meta |= NODE_SKIP | NODE_LEAF;
     }
     nodes[ni] = nd;
 }
@@ -1138,7 +1138,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
             nd.next = (nx & EC_NEXT_MASK) + S0;
             nd.meta = ((nx >> EC_D2_SHIFT) & 0xFFu) |
                       (((nx >> EC_JMASK_SHIFT) & 0xFu) << NODE_JMASK_SHIFT) |
-                      (mSum > 0.0 ? 0u : NODE_SKIP);
+                      (mSum > 0.0 ? 0u : NODE_SKIP | NODE_LEAF);
             nodes[S0 + i] = nd;
         }
     }
@@ -1333,7 +1333,7 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span(int J, const uint32_t *__r
             dst->mass = mSum;
             dst->comX = ox;  // massless: never visited (the cell centre is not recorded)
             dst->comY = oy;
-            if (!(mSum > 0.0)) dst->meta |= NODE_SKIP;
+            if (!(mSum > 0.0)) dst->meta |= NODE_SKIP | NODE_LEAF;  // a skip-leaf
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): LDS results visible; stores fly on
         __builtin_amdgcn_s_barrier();
@@ -1390,7 +1390,7 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span_top(int J,
             dst->mass = mSum;
             dst->comX = mSum > 0.0 ? cx / mSum : 0.0;
             dst->comY = mSum > 0.0 ? cy / mSum : 0.0;
-            if (!(mSum > 0.0)) dst->meta |= NODE_SKIP;
+            if (!(mSum > 0.0)) dst->meta |= NODE_SKIP | NODE_LEAF;  // a skip-leaf
         }
         __syncthreads();
     }

@@ -1,0 +1,138 @@
+/*
+ * bh_jni.c -- JNI glue of the Kotlin drop-in PhysicsEngine: the seven
+ * `external fun`s of `object Native` (class `Native`, default package).  Every native only moves
+ * Java arrays in and out and calls the matching bh_shim_* helper (bh_shim.c), whose logic
+ * tests/c/abi_harness.c runs against the oracle; errors become java.lang.RuntimeException with
+ * bh_last_error's text.
+ *
+ * Build where a JDK exists (none in this image, so it is not part of __graft_entry__.build()):
+ *   make -C barnes-hut-n-body_amd jni JAVA_HOME=/path/to/jdk     -> lib/libbh_jni.so
+ * then run the Kotlin app with -Djava.library.path=barnes-hut-n-body_amd/lib.
+ */
+#include <jni.h>
+#include <stdint.h>
+#include <stdlib.h>
+
+#include "bh_shim.h"
+
+static void throw_rt(JNIEnv *env, const bh_engine *e, const char *what) {
+    jclass rt = (*env)->FindClass(env, "java/lang/RuntimeException");
+    if (rt) (*env)->ThrowNew(env, rt, e ? bh_last_error(e) : what);
+}
+
+/* external fun create(device: Int): Long */
+JNIEXPORT jlong JNICALL Java_Native_create(JNIEnv *env, jobject self, jint device) {
+    (void)self;
+    bh_engine *e = NULL;
+    if (bh_shim_create((int)device, &e) != BH_OK) {
+        throw_rt(env, NULL, "bh_create failed (no HIP device?)");
+        return 0;
+    }
+    return (jlong)(intptr_t)e;
+}
+
+/* external fun setParams(h: Long, G: Double, dt: Double, theta: Double, soft2: Double,
+ *                        w: Int, hgt: Int, mergeMaxMass: Double, mergeMinDist: Double) */
+JNIEXPORT void JNICALL Java_Native_setParams(JNIEnv *env, jobject self, jlong h, jdouble G,
+                                             jdouble dt, jdouble theta, jdouble soft2, jint w,
+                                             jint hgt, jdouble mm, jdouble md) {
+    (void)self;
+    bh_engine *e = (bh_engine *)(intptr_t)h;
+    if (bh_shim_set_params(e, G, dt, theta, soft2, w, hgt, mm, md) != BH_OK)
+        throw_rt(env, e, "setParams");
+}
+
+/* external fun reset(h: Long, n: Int, soa: DoubleArray) */
+JNIEXPORT void JNICALL Java_Native_reset(JNIEnv *env, jobject self, jlong h, jint n,
+                                         jdoubleArray soa) {
+    (void)self;
+    bh_engine *e = (bh_engine *)(intptr_t)h;
+    if (n < 0 || (*env)->GetArrayLength(env, soa) < 5 * (jsize)n) {
+        throw_rt(env, NULL, "reset: the SoA array must hold 5 n doubles");
+        return;
+    }
+    jdouble *a = (*env)->GetPrimitiveArrayCritical(env, soa, NULL);
+    const int rc = bh_shim_reset(e, (int64_t)n, a);
+    (*env)->ReleasePrimitiveArrayCritical(env, soa, a, JNI_ABORT); /* read only */
+    if (rc != BH_OK) throw_rt(env, e, "reset");
+}
+
+/* external fun step(h: Long, k: Int) */
+JNIEXPORT void JNICALL Java_Native_step(JNIEnv *env, jobject self, jlong h, jint k) {
+    (void)self;
+    bh_engine *e = (bh_engine *)(intptr_t)h;
+    if (bh_shim_step(e, (int32_t)k) != BH_OK) throw_rt(env, e, "step");
+}
+
+/* external fun get(h: Long): DoubleArray  (SoA, length 5 N) */
+JNIEXPORT jdoubleArray JNICALL Java_Native_get(JNIEnv *env, jobject self, jlong h) {
+    (void)self;
+    bh_engine *e = (bh_engine *)(intptr_t)h;
+    int64_t n = 0;
+    int rc = bh_shim_get(e, NULL, 0, &n);
+    if (rc != BH_OK && rc != BH_E_CAPACITY) {
+        throw_rt(env, e, "get");
+        return NULL;
+    }
+    jdoubleArray out = (*env)->NewDoubleArray(env, (jsize)(5 * n));
+    if (!out || n == 0) return out;
+    jdouble *a = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
+    rc = bh_shim_get(e, a, n, &n);
+    (*env)->ReleasePrimitiveArrayCritical(env, out, a, 0);
+    if (rc != BH_OK) throw_rt(env, e, "get");
+    return out;
+}
+
+/* external fun quads(h: Long): DoubleArray  ([cx0, cy0, h0, cx1, ...], visitQuads order) */
+JNIEXPORT jdoubleArray JNICALL Java_Native_quads(JNIEnv *env, jobject self, jlong h) {
+    (void)self;
+    bh_engine *e = (bh_engine *)(intptr_t)h;
+    int64_t nq = 0;
+    int rc = bh_shim_quads(e, NULL, 0, &nq); /* builds the tree if the cache was dropped */
+    if (rc != BH_OK && rc != BH_E_CAPACITY) {
+        throw_rt(env, e, "quads");
+        return NULL;
+    }
+    double *q = (double *)malloc(sizeof(double) * (size_t)(3 * nq + 1));
+    if (!q) {
+        throw_rt(env, NULL, "quads: out of memory");
+        return NULL;
+    }
+    rc = bh_shim_quads(e, q, nq, &nq);
+    jdoubleArray out = NULL;
+    if (rc == BH_OK) {
+        out = (*env)->NewDoubleArray(env, (jsize)(3 * nq));
+        if (out) (*env)->SetDoubleArrayRegion(env, out, 0, (jsize)(3 * nq), q);
+    } else {
+        throw_rt(env, e, "quads");
+    }
+    free(q);
+    return out;
+}
+
+/* external fun lastRemoved(h: Long): IntArray */
+JNIEXPORT jintArray JNICALL Java_Native_lastRemoved(JNIEnv *env, jobject self, jlong h) {
+    (void)self;
+    const bh_engine *e = (const bh_engine *)(intptr_t)h;
+    int64_t cnt = 0;
+    int rc = bh_shim_last_removed(e, NULL, 0, &cnt);
+    if (rc != BH_OK && rc != BH_E_CAPACITY) {
+        throw_rt(env, e, "lastRemoved");
+        return NULL;
+    }
+    int32_t *idx = (int32_t *)malloc(sizeof(int32_t) * (size_t)(cnt + 1));
+    if (!idx) {
+        throw_rt(env, NULL, "lastRemoved: out of memory");
+        return NULL;
+    }
+    rc = bh_shim_last_removed(e, idx, cnt, &cnt);
+    jintArray out = NULL;
+    if (rc == BH_OK) {
+        out = (*env)->NewIntArray(env, (jsize)cnt);
+        if (out) (*env)->SetIntArrayRegion(env, out, 0, (jsize)cnt, (const jint *)idx);
+    } else {
+        throw_rt(env, e, "lastRemoved");
+    }
+    free(idx);
+    return out;
+}

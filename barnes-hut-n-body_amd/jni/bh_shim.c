@@ -1,0 +1,81 @@
+/* The Kotlin drop-in's native logic over the C-ABI (see bh_shim.h). */
+#include "bh_shim.h"
+
+#include <stdlib.h>
+
+int bh_shim_create(int device, bh_engine **out) {
+    bh_params p;
+    bh_default_params(&p); /* Config.kt defaults (CFG:5-23); setParams follows before any step */
+    return bh_create(&p, device, out);
+}
+
+int bh_shim_set_params(bh_engine *e, double G, double dt, double theta, double soft2,
+                       int32_t width_px, int32_t height_px, double merge_max_mass,
+                       double merge_min_dist) {
+    bh_params p;
+    p.G = G;
+    p.dt = dt;
+    p.theta = theta;
+    p.soft2 = soft2;
+    p.width_px = width_px;
+    p.height_px = height_px;
+    p.merge_max_mass = merge_max_mass;
+    p.merge_min_dist = merge_min_dist;
+    return bh_set_params(e, &p);
+}
+
+int bh_shim_reset(bh_engine *e, int64_t n, const double *soa) {
+    if (n < 0 || (n > 0 && !soa)) return BH_E_INVALID;
+    return bh_reset_bodies(e, n, soa, soa + n, soa + 2 * n, soa + 3 * n, soa + 4 * n);
+}
+
+int bh_shim_step(bh_engine *e, int32_t k) { return bh_step(e, k); }
+
+int bh_shim_get(bh_engine *e, double *soa, int64_t cap, int64_t *n) {
+    const int64_t cnt = bh_num_bodies(e);
+    if (n) *n = cnt;
+    if (cnt < 0) return BH_E_INVALID;
+    if (cap < cnt || (cnt > 0 && !soa)) return BH_E_CAPACITY;
+    int64_t got = 0;
+    if (cnt == 0) return BH_OK;
+    return bh_get_bodies(e, soa, soa + cnt, soa + 2 * cnt, soa + 3 * cnt, soa + 4 * cnt, cnt, &got);
+}
+
+int bh_shim_quads(bh_engine *e, double *q, int64_t cap, int64_t *nq) {
+    int64_t need = 0;
+    int rc = bh_get_quads(e, NULL, NULL, NULL, 0, &need);
+    if (rc != BH_OK && rc != BH_E_CAPACITY) return rc;
+    if (nq) *nq = need;
+    if (cap < need || (need > 0 && !q)) return BH_E_CAPACITY;
+    if (need == 0) return BH_OK;
+    double *tmp = (double *)malloc(sizeof(double) * 3 * (size_t)need);
+    if (!tmp) return BH_E_INVALID;
+    int64_t got = 0;
+    rc = bh_get_quads(e, tmp, tmp + need, tmp + 2 * need, need, &got);
+    if (rc == BH_OK) {
+        for (int64_t i = 0; i < got; ++i) { /* BHTree.fromQuads reads triples */
+            q[3 * i] = tmp[i];
+            q[3 * i + 1] = tmp[need + i];
+            q[3 * i + 2] = tmp[2 * need + i];
+        }
+        if (nq) *nq = got;
+    }
+    free(tmp);
+    return rc;
+}
+
+int bh_shim_last_removed(const bh_engine *e, int32_t *idx, int64_t cap, int64_t *count) {
+    int64_t need = 0;
+    int rc = bh_last_removed(e, NULL, 0, &need);
+    if (rc != BH_OK && rc != BH_E_CAPACITY) return rc;
+    if (count) *count = need;
+    if (cap < need || (need > 0 && !idx)) return BH_E_CAPACITY;
+    if (need == 0) return BH_OK;
+    int64_t *tmp = (int64_t *)malloc(sizeof(int64_t) * (size_t)need);
+    if (!tmp) return BH_E_INVALID;
+    rc = bh_last_removed(e, tmp, need, &need);
+    if (rc == BH_OK)
+        for (int64_t i = 0; i < need; ++i) idx[i] = (int32_t)tmp[i]; /* list sizes fit a jint */
+    free(tmp);
+    return rc;
+}

@@ -1,46 +1,29 @@
-"""Multi-rank decomposition on CPU (torch.distributed / gloo, world_size 2).
+"""The multi-GPU exchange protocol, multi-process on CPU (torch.distributed / gloo, world 2 and 3).
 
-The engine's multi-GPU step (engine.cpp `evaluate`, bh_create_dist) keeps the state replicated,
-builds the same tree on every rank and evaluates forces in BH_SHARD_ROUNDS rounds: in round k
-a rank evaluates its Morton-sorted piece bh_shard_range(n, rank, world, k) (each rank owns one
-contiguous range; the piece's slots in the buffer are bh_gather_slot), and the round's
-interleaved (ax, ay) pieces are all-gathered in place (RCCL on the GPU box, overlapping the
-next round) into the slot-indexed buffer, which is scattered back through the sort
-permutation.  This test runs exactly that decomposition with gloo in place of RCCL and the
-oracle in place of the HIP traversal, and requires the gathered result to be bit-identical to
-a single-process evaluation.
+bh_create_dist engines (engine.cpp evaluate / evaluate_let / sync_velocities, let.hip) keep the
+state replicated and, per force evaluation, either build a locally essential tree and exchange
+2 MB cell tables plus 16 B positions per body (owner kick), or build the full tree and exchange
+accelerations; velocities follow before every full build.  tests/let_mirror.py runs exactly
+that protocol -- the same pieces (bh_shard_range), the same in-place round layout
+(bh_gather_slot), the same cell tables and halo rule -- with gloo in place of RCCL and the
+pure-Python tree in place of the HIP kernels, one process per rank.  Every rank's final state
+after two bh_step calls (LET builds, the full build that ends each call, merges, jitter,
+out-of-root bodies) must equal the C oracle's serial PhysicsEngine.step() (BHA:405-439) bit for
+bit.
 """
+import json
 import os
 import socket
 
 import numpy as np
 import pytest
-import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
-
-def morton_order(x, y, W=2400, H=800):
-    """Stable sort permutation by the engine's keys (exact descent, BHA:153-154, 360-361)."""
-    cx0, cy0, h0 = W / 2.0, H / 2.0, max(W, H) / 2.0 + 2.0
-    hs = [h0]
-    while not hs[-1] < 1e-3:
-        hs.append(hs[-1] / 2.0)
-    J = len(hs) - 1
-    hs.append(hs[-1] / 2.0)
-    inside = (x >= cx0 - h0) & (x < cx0 + h0) & (y >= cy0 - h0) & (y < cy0 + h0)
-    key = np.zeros(len(x), dtype=np.uint64)
-    cx = np.full(len(x), cx0)
-    cy = np.full(len(x), cy0)
-    for d in range(J):
-        ix = ~(x < cx)
-        iy = ~(y < cy)
-        hh = hs[d + 1]
-        cx = np.where(ix, cx + hh, cx - hh)
-        cy = np.where(iy, cy + hh, cy - hh)
-        key = (key << np.uint64(2)) | (ix.astype(np.uint64) | (iy.astype(np.uint64) << np.uint64(1)))
-    key = np.where(inside, key, np.uint64(1) << np.uint64(2 * J))
-    return np.argsort(key, kind="stable")
+FIELDS = ("x", "y", "vx", "vy", "m")
+PARAMS = dict(G=80.0, dt=0.005, theta=0.5, soft2=1.0, width_px=2400, height_px=800,
+              merge_max_mass=4000.0, merge_min_dist=8.0)
+CALLS = (3, 2)
 
 
 def _free_port():
@@ -49,69 +32,83 @@ def _free_port():
         return s.getsockname()[1]
 
 
+def scene():
+    """Two galaxy disks (NBodyPanel.kt:83-100, 2200 + 700 bodies: every rank owns lanes at
+    world 3) plus: five light bodies inside the big disk's merge radius (merges in the first
+    step), a coincident pair and a pair 4e-4 apart (the h < 1e-3 jitter, BHA:146-151), two
+    bodies outside the root (BHA:126), and a cluster of negative masses (mass-0 cells,
+    BHA:189-192)."""
+    from bh_amd import scenes
+    x, y, vx, vy, m = scenes.two_disks(2200, 700)
+    ex = [1203.0, 1200.0, 1195.5, 1201.0, 1206.0, 700.0, 700.0, 1500.0, 1500.0004, -40.0, 2600.0]
+    ey = [400.0, 405.0, 398.0, 393.5, 404.0, 650.0, 650.0, 120.0, 119.9997, 300.0, 900.0]
+    ex += list(2000.0 + 3.0 * np.arange(8) % 9)
+    ey += list(700.0 + np.arange(8) // 3 * 2.5)
+    k = len(ex)
+    em = [0.5] * 11 + [-0.4] * 8
+    return (np.concatenate([x, ex]), np.concatenate([y, ey]), np.concatenate([vx, np.zeros(k)]),
+            np.concatenate([vy, np.zeros(k)]), np.concatenate([m, em]))
+
+
 def _worker(rank, world, port, out_dir):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-    sys.path[:0] = [root, os.path.join(root, "barnes-hut-n-body_amd")]
-    import bh_amd
-    import oracle
-    from bh_amd import scenes
+    sys.path[:0] = [root, os.path.join(root, "barnes-hut-n-body_amd"), os.path.dirname(__file__)]
+    from let_mirror import MirrorRank
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
-    arrs = scenes.two_disks(700, 250)
-    ref = oracle.Oracle(*arrs, theta=0.5, threads=1)
-    x, y = arrs[0], arrs[1]
-    perm = morton_order(x, y)
-    n = len(x)
-    sub = bh_amd.shard_range(n, 0, world, 0)[1]  # whole wavefronts per piece (engine.cpp)
-    a2 = np.zeros(2 * sub * world * bh_amd.SHARD_ROUNDS)  # slot-indexed, interleaved
-    for k in range(bh_amd.SHARD_ROUNDS):
-        lo, hi = bh_amd.shard_range(n, rank, world, k)
-        if hi > lo:
-            ax, ay = ref.accelerations(subset=perm[lo:hi])  # this rank's piece of round k
-            g = bh_amd.gather_slot(n, world, lo)  # the piece's slots in the exchange buffer
-            a2[2 * g:2 * (g + hi - lo):2] = ax
-            a2[2 * g + 1:2 * (g + hi - lo):2] = ay
-        base = 2 * k * world * sub  # in place: rank r's piece sits at base + 2 * r * sub
-        send = torch.from_numpy(a2[base + 2 * rank * sub:base + 2 * (rank + 1) * sub].copy())
-        gathered = [torch.zeros(2 * sub, dtype=torch.float64) for _ in range(world)]
-        dist.all_gather(gathered, send)
-        a2[base:base + 2 * world * sub] = torch.cat(gathered).numpy()
-    slots = np.array([bh_amd.gather_slot(n, world, q) for q in range(n)])
-    full_ax = np.empty(n)
-    full_ay = np.empty(n)
-    full_ax[perm] = a2[2 * slots]
-    full_ay[perm] = a2[2 * slots + 1]
-    np.save(os.path.join(out_dir, f"ax{rank}.npy"), full_ax)
-    np.save(os.path.join(out_dir, f"ay{rank}.npy"), full_ay)
+    mr = MirrorRank(PARAMS, rank, world, dist)
+    mr.reset_bodies(*scene())
+    for k in CALLS:
+        mr.step(k)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), *mr.get_bodies())
+    with open(os.path.join(out_dir, f"stats{rank}.json"), "w") as fh:
+        json.dump(mr.stats, fh)
     dist.barrier()
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world", [2, 3])
-def test_sharded_evaluation_matches_single_process(tmp_path, world):
-    import bh_amd  # noqa: F401  (library must load before spawning)
+def test_exchange_protocol_matches_the_reference_step(tmp_path, world):
+    import bh_amd  # noqa: F401  (the engine library's host-only shard layout must load)
     import oracle
-    from bh_amd import scenes
 
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
-    arrs = scenes.two_disks(700, 250)
-    ax, ay = oracle.Oracle(*arrs, theta=0.5, threads=1).accelerations()
+    arrs = scene()
+    ref = oracle.Oracle(*arrs, threads=1, **PARAMS)
+    for k in CALLS:
+        ref.step(k)
+    want = ref.get_bodies()
+    assert len(want[0]) < len(arrs[0])  # the merge rule removed bodies
     for r in range(world):
-        gx = np.load(tmp_path / f"ax{r}.npy")
-        gy = np.load(tmp_path / f"ay{r}.npy")
-        assert np.array_equal(gx.view(np.int64), ax.view(np.int64)), f"rank {r} ax"
-        assert np.array_equal(gy.view(np.int64), ay.view(np.int64)), f"rank {r} ay"
+        got = np.load(tmp_path / f"rank{r}.npz")
+        stats = json.load(open(tmp_path / f"stats{r}.json"))
+        # per call: the first build after the reset / the call's last build are full, the rest
+        # are LET builds; velocities are gathered before every full build that follows LET ones
+        assert stats["let"] == 2 * sum(CALLS) - len(CALLS) - 1 and stats["full"] == len(CALLS) + 1
+        assert stats["vel_syncs"] == len(CALLS)
+        assert stats["merged"] == len(arrs[0]) - len(want[0])
+        # every rank owns bodies; at world 3 a rank builds a part of the scene only
+        assert 0 < stats["max_subset"] <= len(arrs[0])
+        if world == 3:
+            assert stats["max_subset"] < len(arrs[0]), stats
+        for k, name in enumerate(FIELDS):
+            a = got[f"arr_{k}"]
+            assert a.shape == want[k].shape, f"rank {r}: {name} length"
+            bad = np.flatnonzero(a.view(np.int64) != want[k].view(np.int64))
+            assert len(bad) == 0, f"rank {r}: {name} differs at {bad[:5]}"
 
 
 def test_morton_order_matches_tree_preorder():
-    """The sort order used to shard is the tree's leaf pre-order (child 0..3 = ascending
-    Morton digit, BHA:73-81): leaves appear in sorted order in visitQuads' walk."""
+    """The slot order the pieces are cut from is the tree's leaf pre-order (child 0..3 =
+    ascending Morton digit, BHA:73-81)."""
+    import sys
+    sys.path.insert(0, os.path.dirname(__file__))
+    from let_mirror import Geometry
     from bh_amd import scenes
     x, y, *_ = scenes.uniform(64, 1.0, seed=2)
-    perm = morton_order(x, y)
-    # consecutive sorted bodies must never be "out of order" w.r.t. the first differing level
+    perm = np.argsort(Geometry(2400, 800).keys(x, y, np.zeros(64, dtype=bool)), kind="stable")
     cx0, cy0 = 1200.0, 400.0
     q = [(x[i] >= cx0) + 2 * (y[i] >= cy0) for i in perm]
     assert q == sorted(q)

@@ -856,6 +856,27 @@ def _nonpositive_scene(kind):
     return tuple(a[perm] for a in arrs)
 
 
+@pytest.mark.parametrize("theta", [0.0, 0.5, 1.0])
+def test_massless_cells_of_negative_bodies_are_not_entered(theta):
+    """Cells whose bodies all have negative mass get mass 0 (computeMass keeps children of mass
+    > 0 only, BHA:189-192), and accumulateForce returns at mass == 0 (BHA:216): the negative
+    bodies inside are never reached -- neither by the fast walk (the massless node is a
+    skip-leaf) nor by the theta = 0 leaf list (leaves below a massless node are dropped).
+    One evaluation and 3 steps, bit-identical to the oracle."""
+    rng = np.random.default_rng(71)
+    x, y, vx, vy, m = (a.copy() for a in scenes.uniform(30_000, 0.5, seed=70))
+    for _ in range(25):
+        cx, cy, half = rng.uniform(0, 2400), rng.uniform(0, 800), rng.uniform(2.0, 30.0)
+        inside = (np.abs(x - cx) < half) & (np.abs(y - cy) < half)
+        m[inside] = -rng.uniform(0.1, 0.9, inside.sum())
+    arrs = (x, y, vx, vy, m)
+    eng, ref = _pair(arrs, theta=theta)
+    _assert_acc_equal(eng, ref)
+    eng.step(3)
+    ref.step(3)
+    _assert_state_equal(eng, ref)
+
+
 @pytest.mark.parametrize("world,kind", [(4, "negative"), (8, "negative"), (4, "zero")])
 def test_let_nonpositive_masses(world, kind, monkeypatch):
     """The LET's halo rule with zero and negative masses: cells whose bodies are all negative

@@ -147,7 +147,19 @@ CROSS = [
     ("kepler", lambda: scenes.kepler_disk(250, seed=3), dict(theta=0.5), 3),
     ("uniform", lambda: scenes.uniform(300, 0.7, seed=4), dict(theta=0.5), 3),
     ("screen_1920", lambda: scenes.two_disks(200, 60), dict(theta=0.5, width_px=1920, height_px=1080), 3),
+    ("negative_cells", lambda: _negative_cells(), dict(theta=0.5), 3),
+    ("negative_cells_theta0", lambda: _negative_cells(), dict(theta=0.0), 2),
 ]
+
+
+def _negative_cells():
+    """A cloud with clusters of negative-mass bodies: their cells get mass 0 (only children of
+    mass > 0 count, BHA:189-192) and are never entered (BHA:216)."""
+    x, y, vx, vy, m = (a.copy() for a in scenes.uniform(300, 0.5, seed=9))
+    for cx, cy, half in ((600.0, 300.0, 160.0), (1800.0, 500.0, 90.0), (1200.0, 100.0, 40.0)):
+        inside = (np.abs(x - cx) < half) & (np.abs(y - cy) < half)
+        m[inside] = -0.3
+    return x, y, vx, vy, m
 
 
 @pytest.mark.parametrize("name,make,over,k", CROSS, ids=[c[0] for c in CROSS])
