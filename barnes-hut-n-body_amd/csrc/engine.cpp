@@ -191,6 +191,14 @@ struct bh_engine {
     Node *s_nodes = nullptr;
     hipEvent_t table_ev = nullptr;
     bool inject_guard = false;  // bh_debug_inject(1): the next LET build trips k_let_guard
+    // Between LET evaluations the new positions stay in the exchange buffer (a2, by lane of
+    // pos_lanes at pos_layout's gather slots): the next selection reads them there, and the
+    // replica's x, y are written only when something else needs them (materialize_positions)
+    bool pos_pending = false;
+    const uint32_t *pos_lanes = nullptr;
+    GatherLayout pos_layout{};
+    uint32_t *inv_lanes = nullptr;  // slot -> lane of the wave map (the selection's reads)
+    bool inv_valid = false;
     // bh_create_solo (measurement): no peers; their cells' values from the last full build
     bool solo = false;
     LetCell *solo_table = nullptr;
@@ -323,6 +331,7 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(dev_alloc(e, e->contrib32, cap));
         TRY(dev_alloc(e, e->lanes, cap));
         e->lanes_valid = false;
+        e->inv_valid = false;
         TRY(dev_alloc(e, e->wave_iters, cap / 64 + 2));
         TRY(dev_alloc(e, e->wave_blocks, cap / 64 + 2));
         TRY(dev_alloc(e, e->heavy, cap));
@@ -447,6 +456,7 @@ int build(bh_engine *e) {
     tb.lanes_remap = use_lanes && !refresh ? e->lanes : nullptr;
     HIPCHK(e, tree_build(tb, n, e->geo, e->stream));
     ++e->full_builds;
+    e->inv_valid = false;  // the map follows this build's permutation
     if (use_lanes) {
         if (refresh) HIPCHK(e, lane_order(tb, n, e->geo.J, true, e->lanes, e->stream));
         e->lanes_valid = true;
@@ -544,6 +554,8 @@ int let_alloc(bh_engine *e, int64_t n_sub) {
         TRY(dev_alloc(e, L.ccnt, LET_CELLS + 1));
         TRY(dev_alloc(e, L.cpos, LET_CELLS + 1));
         TRY(dev_alloc(e, L.lanes, cap));
+        TRY(dev_alloc(e, e->inv_lanes, cap));
+        e->inv_valid = false;
         TRY(dev_alloc(e, L.own, cap));
         TRY(dev_alloc(e, L.subpos, cap));
         TRY(alloc_state(e, e->sub_src, cap));
@@ -652,6 +664,20 @@ int gather_round(bh_engine *e, const GatherLayout &gl, int k, int W, int ev_roun
     return BH_OK;
 }
 
+// The positions a sequence of LET evaluations left in the exchange buffer -> the replica (every
+// body's slot), before anything but the next selection reads x, y (a full build, the merge rule,
+// the copy-out) or reuses a2 (accelerations, the velocity exchange).  A subset overflow (scalars[4],
+// the call is replayed) leaves the replica as it was.
+int materialize_positions(bh_engine *e) {
+    if (!e->pos_pending) return BH_OK;
+    e->pos_pending = false;
+    if (e->n <= 0) return BH_OK;
+    let_set_pos(e->n, e->pos_lanes, e->a2, e->pos_layout, e->st.x, e->st.y, e->scalars + 4,
+                e->stream);
+    HIPCHK(e, hipGetLastError());
+    return BH_OK;
+}
+
 // Velocities after owner-integrated LET evaluations: every rank holds current velocities of its
 // own bodies only; before a full build (which permutes and re-assigns the bodies) the owners'
 // (vx, vy) are all-gathered once, in the same rounds and slots as the forces.
@@ -712,7 +738,18 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     // the call with the observed size (the first LET build of an engine reads its size once)
     // (the selection writes sub_src, sized for the whole state; padding up to S = n is harmless)
     int64_t S = e->let_known > 0 ? std::min<int64_t>(n, e->let_known + e->let_known / 8 + 4096) : n;
-    HIPCHK(e, let_select(e->st, e->geo, pc, gap2, e->L, e->sub_src, S, e->scalars, e->stream));
+    PosSrc ps{nullptr, GatherLayout{}, nullptr};
+    if (e->pos_pending && lanes != e->pos_lanes) TRY(materialize_positions(e));  // map changed
+    if (e->pos_pending) {  // the previous LET evaluation's positions, straight from a2
+        if (lanes && !e->inv_valid) {
+            let_inv_lanes(n, lanes, e->inv_lanes, e->stream);
+            HIPCHK(e, hipGetLastError());
+            e->inv_valid = true;
+        }
+        ps = PosSrc{e->a2, e->pos_layout, lanes ? e->inv_lanes : nullptr};
+    }
+    HIPCHK(e, let_select(e->st, ps, e->geo, pc, gap2, e->L, e->sub_src, S, e->scalars,
+                         e->stream));
     if (e->let_known <= 0) {
         TRY(pinned_reserve(e, 64));
         uint32_t *h = static_cast<uint32_t *>(e->pin);
@@ -765,8 +802,8 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     const KickArgs ka{kick == KICK_DRIFT ? KICK_OWN_DRIFT : KICK_OWN_ONLY, e->st.vx, e->st.vy,
                       e->p.dt * 0.5, e->p.dt, lanes};  // BHA:412
     const GatherLayout gl = shard_layout(n, e->world);
-    if (e->solo)  // measurement: the peers' bodies keep their positions
-        let_fill_pos(n, lanes, e->st.x, e->st.y, e->a2, gl, e->stream);
+    // measurement: the peers' bodies keep their positions (already in a2 after a LET evaluation)
+    if (e->solo && !e->pos_pending) let_fill_pos(n, lanes, e->st.x, e->st.y, e->a2, gl, e->stream);
     TRY(round_streams(e));
     for (int k = 0; k < R; ++k) {
         int64_t lo = 0, hi = 0;
@@ -787,9 +824,9 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
     HIPCHK(e, hipStreamWaitEvent(e->stream, e->gathered_ev, 0));
     TRY(mark(e, 4));
-    let_set_pos(n, lanes, e->a2, gl, e->st.x, e->st.y, e->scalars + 4, e->stream);  // new positions
-    HIPCHK(e, hipGetLastError());
-    TRY(mark(e, 2));
+    e->pos_pending = true;  // every body's new position is in a2 (by lane, gather slots)
+    e->pos_lanes = lanes;
+    e->pos_layout = gl;
     e->vel_stale = true;
     e->a2_lanes = lanes;
     e->a2_layout = gl;
@@ -818,7 +855,8 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
     }
     e->let_age = 0;
     const int64_t n = e->n;
-    TRY(sync_velocities(e));  // before the full build permutes the state
+    TRY(materialize_positions(e));  // the replica's x, y; a2 is free again
+    TRY(sync_velocities(e));        // before the full build permutes the state
     TRY(mark(e, -1));
     TRY(build(e));
     TRY(mark(e, 0));
@@ -939,6 +977,7 @@ int merge_bufs(bh_engine *e) {
 
 int merge(bh_engine *e) {
     if (e->p.merge_min_dist <= 0.0 || e->n <= 1 || !e->heavy_possible) return BH_OK;  // BHA:465
+    TRY(materialize_positions(e));
     TRY(mark(e, -1));
     TRY(merge_bufs(e));
     const double minD2 = e->p.merge_min_dist * e->p.merge_min_dist;  // BHA:468
@@ -961,6 +1000,7 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
     e->removed.clear();
     if (!e->merge_ran) return BH_OK;
     e->merge_ran = false;
+    TRY(materialize_positions(e));
     TRY(pinned_reserve(e, 64));
     uint32_t *h = static_cast<uint32_t *>(e->pin);
     HIPCHK(e, hipMemcpyAsync(h, e->scalars, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
@@ -986,6 +1026,7 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
         HIPCHK(e, compact_lanes(n, e->lanes, e->keep, e->pos, e->idx, e->keys32, e->keys32_s,
                                 e->scratch, e->scratch_bytes, e->stream));
         std::swap(e->lanes, e->keys32_s);
+        e->inv_valid = false;
     }
     e->n = n - (int64_t)nd;
     e->removed.assign(dead.begin(), dead.end());
@@ -1011,6 +1052,7 @@ int copy_state(bh_engine *e, const BodyState &src, const BodyState &dst, int64_t
 }
 
 int snapshot(bh_engine *e) {
+    TRY(materialize_positions(e));
     if (e->snap_cap < e->cap) {
         TRY(alloc_state(e, e->snap, (size_t)e->cap));
         e->snap_cap = e->cap;
@@ -1024,6 +1066,8 @@ int restore(bh_engine *e) {
     e->n = e->snap_n;
     e->spl_nb = 0;  // the splitters describe the discarded builds' order
     e->lanes_valid = false;
+    e->inv_valid = false;
+    e->pos_pending = false;  // the snapshot holds every position
     e->heavy_possible = true;
     e->tree_valid = false;
     e->st_morton = false;
@@ -1466,7 +1510,7 @@ void bh_destroy(bh_engine *e) {
     free_state(e->sub_src);
     free_state(e->sub_dst);
     if (e->table_ev) (void)hipEventDestroy(e->table_ev);
-    void *lets[] = {e->L.csrc, e->L.ccnt, e->L.cpos, e->solo_table, e->solo_all, e->solo_cstart, e->L.ecell, e->L.hcell, e->L.own, e->L.subpos, e->L.flag_all, e->L.flag8, e->L.sel, e->L.selpos, e->L.cstart,
+    void *lets[] = {e->inv_lanes, e->L.csrc, e->L.ccnt, e->L.cpos, e->solo_table, e->solo_all, e->solo_cstart, e->L.ecell, e->L.hcell, e->L.own, e->L.subpos, e->L.flag_all, e->L.flag8, e->L.sel, e->L.selpos, e->L.cstart,
                     e->L.table, e->L.tables, e->L.levels, e->L.w, e->L.posc, e->L.bsz,
                     e->L.nodes, e->L.lanes, e->s_keys, e->s_keys_s, e->s_spl, e->s_keys32,
                     e->s_keys32_s, e->s_idx, e->s_perm, e->s_cpl, e->s_cnt, e->s_base,
@@ -1500,10 +1544,12 @@ int bh_set_params(bh_engine *e, const bh_params *p) {
         e->heavy_possible = true;
     e->p = *p;
     if (geo_changed) {
+        TRY(materialize_positions(e));
         e->geo = g;
         e->tree_valid = false;
         e->spl_nb = 0;  // keys change meaning
         e->lanes_valid = false;
+        e->inv_valid = false;
         if (g.J != e->J_alloc) {  // tree workspace sized for another depth; the state stays
             HIPCHK(e, hipStreamSynchronize(e->stream));
             TRY(ensure_capacity(e, e->n));
@@ -1546,6 +1592,8 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     e->lanes_valid = false;
     e->st_morton = false;
     e->vel_stale = false;
+    e->pos_pending = false;
+    e->inv_valid = false;
     return BH_OK;
 }
 
@@ -1620,6 +1668,7 @@ int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, do
     if (n_out) *n_out = e->n;
     if (cap < e->n) return BH_E_CAPACITY;
     HIPCHK(e, hipSetDevice(e->device));
+    TRY(materialize_positions(e));
     const int64_t n = e->n;
     if (n > 0) {  // back to caller (list) order, staged in the second state buffer
         const double *src[5] = {e->st.x, e->st.y, e->st.vx, e->st.vy, e->st.m};
@@ -1688,6 +1737,7 @@ int bh_get_quads(bh_engine *e, double *cx, double *cy, double *h, int64_t cap, i
     if (!e || cap < 0 || (cap > 0 && (!cx || !cy || !h))) return BH_E_INVALID;
     HIPCHK(e, hipSetDevice(e->device));
     const int64_t n = e->n;
+    TRY(materialize_positions(e));
     if (!e->tree_valid) {  // getTreeForDebug builds a fresh tree (BHA:329-332)
         HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
         TRY(build(e));

@@ -92,7 +92,21 @@ __device__ __forceinline__ int64_t own_lane(const LetPieces &pc, int64_t t) {  /
     return (int64_t)pc.rank * pc.rounds * pc.sub + t;  // one contiguous range per rank
 }
 
-__global__ __launch_bounds__(TB) void k_let_mark(LetPieces pc, const double *__restrict__ x,
+__device__ __forceinline__ void slot_pos(const PosSrc &ps, const double *__restrict__ x,
+                                         const double *__restrict__ y, int64_t i, double &px,
+                                         double &py) {
+    if (ps.a2) {
+        const int64_t g = gather_slot(ps.gl, ps.inv ? (int64_t)ps.inv[i] : i);
+        px = ps.a2[2 * g];
+        py = ps.a2[2 * g + 1];
+    } else {
+        px = x[i];
+        py = y[i];
+    }
+}
+
+__global__ __launch_bounds__(TB) void k_let_mark(LetPieces pc, PosSrc ps,
+                                                 const double *__restrict__ x,
                                                  const double *__restrict__ y,
                                                  const uint32_t *__restrict__ cidx, Geometry g,
                                                  uint8_t *__restrict__ own,
@@ -105,7 +119,15 @@ __global__ __launch_bounds__(TB) void k_let_mark(LetPieces pc, const double *__r
     const int64_t i = pc.lanes ? (int64_t)pc.lanes[q] : q;
     own[i] = 1;
     if (cidx[i] & CIDX_DEAD) return;  // tombstones do not walk
-    const double px = x[i], py = y[i];
+    double px, py;
+    if (ps.a2) {  // lane q's position in the exchange buffer
+        const int64_t gs = gather_slot(ps.gl, q);
+        px = ps.a2[2 * gs];
+        py = ps.a2[2 * gs + 1];
+    } else {
+        px = x[i];
+        py = y[i];
+    }
     if (!__builtin_isfinite(px) || !__builtin_isfinite(py)) {
         *flag_all = 1u;
         return;
@@ -147,7 +169,8 @@ __global__ __launch_bounds__(TB) void k_let_halo(const uint8_t *__restrict__ ece
 static_assert(TB == 256, "one 256-slot block per workgroup");
 // One wave per 256-slot block, four slots per lane (slot base + lane + 64 u): four independent
 // position loads and cell lookups in flight per lane, the block's count from four ballots.
-__global__ __launch_bounds__(64) void k_let_flags(LetPieces pc, const double *__restrict__ x,
+__global__ __launch_bounds__(64) void k_let_flags(LetPieces pc, PosSrc ps,
+                                                  const double *__restrict__ x,
                                                   const double *__restrict__ y,
                                                   const uint32_t *__restrict__ cidx, Geometry g,
                                                   const uint8_t *__restrict__ hcell,
@@ -161,7 +184,8 @@ __global__ __launch_bounds__(64) void k_let_flags(LetPieces pc, const double *__
         const int64_t i = b0 + 64 * u;
         uint32_t f = 0;
         if (i < pc.n) {
-            const double px = x[i], py = y[i];
+            double px, py;
+            slot_pos(ps, x, y, i, px, py);
             if (!(cidx[i] & CIDX_DEAD) && in_root(g, px, py)) f = hcell[cell_of(g, px, py)];
             else f = own[i];
             flag8[i] = (uint8_t)f;
@@ -174,7 +198,8 @@ __global__ __launch_bounds__(64) void k_let_flags(LetPieces pc, const double *__
     }
 }
 
-__global__ __launch_bounds__(TB) void k_let_gather(int64_t n, const uint8_t *__restrict__ flag8,
+__global__ __launch_bounds__(TB) void k_let_gather(int64_t n, PosSrc ps,
+                                                   const uint8_t *__restrict__ flag8,
                                                    const uint32_t *__restrict__ bpos,
                                                    BodyState st, BodyState sub) {
     __shared__ uint32_t s_w[TB / 64];
@@ -188,8 +213,10 @@ __global__ __launch_bounds__(TB) void k_let_gather(int64_t n, const uint8_t *__r
     uint32_t j = bpos[blockIdx.x];
     for (uint32_t q = 0; q < w; ++q) j += s_w[q];
     j += __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-    sub.x[j] = st.x[i];
-    sub.y[j] = st.y[i];
+    double px, py;
+    slot_pos(ps, st.x, st.y, i, px, py);
+    sub.x[j] = px;
+    sub.y[j] = py;
     sub.vx[j] = __longlong_as_double((long long)i);  // payload: the replicated slot
     sub.vy[j] = 0.0;
     sub.m[j] = st.m[i];
@@ -592,7 +619,17 @@ __global__ __launch_bounds__(TB) void k_let_pack_vel(LetPieces pc, const double 
     a2[2 * g + 1] = vy[i];
 }
 
+__global__ __launch_bounds__(TB) void k_let_inv_lanes(int64_t n, const uint32_t *__restrict__ lanes,
+                                                      uint32_t *__restrict__ inv) {
+    const int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (q < n) inv[lanes[q]] = (uint32_t)q;
+}
+
 }  // namespace
+
+void let_inv_lanes(int64_t n, const uint32_t *lanes, uint32_t *inv, hipStream_t s) {
+    if (n > 0) k_let_inv_lanes<<<grid_for(n), TB, 0, s>>>(n, lanes, inv);
+}
 
 void let_set_pos(int64_t n, const uint32_t *lanes, const double *a2, GatherLayout gl, double *x,
                  double *y, const uint32_t *skip, hipStream_t s) {
@@ -652,9 +689,9 @@ __global__ __launch_bounds__(TB) void k_let_clear(int64_t n, uint8_t *__restrict
     if (t == 0) *flag_all = 0u;
 }
 
-hipError_t let_select(const BodyState &st, const Geometry &g, const LetPieces &pc, double gap2,
-                      const LetBufs &L, const BodyState &sub, int64_t S, uint32_t *scal,
-                      hipStream_t s) {
+hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
+                      const LetPieces &pc, double gap2, const LetBufs &L, const BodyState &sub,
+                      int64_t S, uint32_t *scal, hipStream_t s) {
     if (pc.n <= 0) {
         hipError_t e = hipMemsetAsync(L.ecell, 0, LET_CELLS, s);
         return e == hipSuccess ? hipMemsetAsync(L.flag_all, 0, sizeof(uint32_t), s) : e;
@@ -664,18 +701,18 @@ hipError_t let_select(const BodyState &st, const Geometry &g, const LetPieces &p
     hipError_t e;
     const int64_t marks = (int64_t)pc.rounds * pc.sub;
     if (marks > 0)
-        k_let_mark<<<grid_for(marks), TB, 0, s>>>(pc, st.x, st.y, st.cidx, g, L.own, L.ecell,
-                                                  L.flag_all);
+        k_let_mark<<<grid_for(marks), TB, 0, s>>>(pc, ps, st.x, st.y, st.cidx, g, L.own,
+                                                  L.ecell, L.flag_all);
     const int K = (int)std::floor(std::sqrt(gap2 > 0.0 ? gap2 : 0.0)) + 1;
     k_let_halo<<<grid_for(LET_CELLS), TB, 0, s>>>(L.ecell, L.flag_all, gap2, K, L.hcell);
     const int64_t nb = let_sel_blocks(pc.n);
-    k_let_flags<<<(unsigned)nb, 64, 0, s>>>(pc, st.x, st.y, st.cidx, g, L.hcell, L.own, L.flag8,
-                                            L.sel);
+    k_let_flags<<<(unsigned)nb, 64, 0, s>>>(pc, ps, st.x, st.y, st.cidx, g, L.hcell, L.own,
+                                            L.flag8, L.sel);
     size_t bytes = L.scratch_bytes;
     e = rocprim::exclusive_scan(L.scratch, bytes, L.sel, L.selpos, 0u, (size_t)(nb + 1),
                                 rocprim::plus<uint32_t>(), s);
     if (e != hipSuccess) return e;
-    k_let_gather<<<(unsigned)nb, TB, 0, s>>>(pc.n, L.flag8, L.selpos, st, sub);
+    k_let_gather<<<(unsigned)nb, TB, 0, s>>>(pc.n, ps, L.flag8, L.selpos, st, sub);
     k_let_pad<<<grid_for(S > 0 ? S : 1), TB, 0, s>>>(S, L.selpos + nb, sub, L.table, scal);
     return hipGetLastError();
 }
