@@ -282,18 +282,20 @@ inline int64_t let_sel_blocks(int64_t n) { return (n + 255) / 256; }
 // round trip: `sub` is padded with dead bodies (sentinel keys: not in the tree) up to S, and
 // selpos[n] > S is an overflow (the status record of the table; scal[5] = max subset size)
 // Where the selection reads body positions: the replica (a2 == null), or -- between LET
-// evaluations, whose new positions are not copied into the replica -- the exchange buffer, lane
-// q's position at a2[2 gather_slot(gl, q)], slot i's lane inv[i] (null: identity).
+// evaluations, whose new positions are not copied into the replica -- the exchange buffer: lane
+// q's position at a2[2 gather_slot(gl, q)], and slot i's at a2[2 gslot[i]] (gslot: the gather
+// slot of the lane that holds slot i, made once per lane map by let_gather_slots).
 struct PosSrc {
     const double *a2;
     GatherLayout gl;
-    const uint32_t *inv;
+    const uint32_t *gslot;
 };
 hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
                       const LetPieces &pc, double gap2, const LetBufs &L, const BodyState &sub,
                       int64_t S, uint32_t *scal, hipStream_t s);
-// inv[lanes[q]] = q: slot -> lane of the wave map
-void let_inv_lanes(int64_t n, const uint32_t *lanes, uint32_t *inv, hipStream_t s);
+// gslot[lanes[q]] = gather_slot(gl, q) (lanes null: the identity map)
+void let_gather_slots(int64_t n, const uint32_t *lanes, GatherLayout gl, uint32_t *gslot,
+                      hipStream_t s);
 // after tree_build over the subset: the own cells' exchange table
 hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const TreeBuffers &tb,
                      hipStream_t s);

@@ -197,8 +197,8 @@ struct bh_engine {
     bool pos_pending = false;
     const uint32_t *pos_lanes = nullptr;
     GatherLayout pos_layout{};
-    uint32_t *inv_lanes = nullptr;  // slot -> lane of the wave map (the selection's reads)
-    bool inv_valid = false;
+    uint32_t *inv_lanes = nullptr;  // slot -> gather slot of its lane (the selection's reads)
+    bool inv_valid = false;         // ... for the current lane map, n and layout
     // bh_create_solo (measurement): no peers; their cells' values from the last full build
     bool solo = false;
     LetCell *solo_table = nullptr;
@@ -741,12 +741,12 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     PosSrc ps{nullptr, GatherLayout{}, nullptr};
     if (e->pos_pending && lanes != e->pos_lanes) TRY(materialize_positions(e));  // map changed
     if (e->pos_pending) {  // the previous LET evaluation's positions, straight from a2
-        if (lanes && !e->inv_valid) {
-            let_inv_lanes(n, lanes, e->inv_lanes, e->stream);
+        if (!e->inv_valid) {  // per lane map: each slot's position in the exchange buffer
+            let_gather_slots(n, lanes, e->pos_layout, e->inv_lanes, e->stream);
             HIPCHK(e, hipGetLastError());
             e->inv_valid = true;
         }
-        ps = PosSrc{e->a2, e->pos_layout, lanes ? e->inv_lanes : nullptr};
+        ps = PosSrc{e->a2, e->pos_layout, e->inv_lanes};
     }
     HIPCHK(e, let_select(e->st, ps, e->geo, pc, gap2, e->L, e->sub_src, S, e->scalars,
                          e->stream));
@@ -1029,6 +1029,7 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
         e->inv_valid = false;
     }
     e->n = n - (int64_t)nd;
+    e->inv_valid = false;  // another n: another exchange layout
     e->removed.assign(dead.begin(), dead.end());
     e->tree_valid = false;  // BHA:526
     HIPCHK(e, hipStreamSynchronize(e->stream));

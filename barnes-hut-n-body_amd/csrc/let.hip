@@ -96,7 +96,7 @@ __device__ __forceinline__ void slot_pos(const PosSrc &ps, const double *__restr
                                          const double *__restrict__ y, int64_t i, double &px,
                                          double &py) {
     if (ps.a2) {
-        const int64_t g = gather_slot(ps.gl, ps.inv ? (int64_t)ps.inv[i] : i);
+        const int64_t g = ps.gslot[i];
         px = ps.a2[2 * g];
         py = ps.a2[2 * g + 1];
     } else {
@@ -619,16 +619,19 @@ __global__ __launch_bounds__(TB) void k_let_pack_vel(LetPieces pc, const double 
     a2[2 * g + 1] = vy[i];
 }
 
-__global__ __launch_bounds__(TB) void k_let_inv_lanes(int64_t n, const uint32_t *__restrict__ lanes,
-                                                      uint32_t *__restrict__ inv) {
+__global__ __launch_bounds__(TB) void k_let_gather_slots(int64_t n,
+                                                         const uint32_t *__restrict__ lanes,
+                                                         GatherLayout gl,
+                                                         uint32_t *__restrict__ gslot) {
     const int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (q < n) inv[lanes[q]] = (uint32_t)q;
+    if (q < n) gslot[lanes ? (int64_t)lanes[q] : q] = (uint32_t)gather_slot(gl, q);
 }
 
 }  // namespace
 
-void let_inv_lanes(int64_t n, const uint32_t *lanes, uint32_t *inv, hipStream_t s) {
-    if (n > 0) k_let_inv_lanes<<<grid_for(n), TB, 0, s>>>(n, lanes, inv);
+void let_gather_slots(int64_t n, const uint32_t *lanes, GatherLayout gl, uint32_t *gslot,
+                      hipStream_t s) {
+    if (n > 0) k_let_gather_slots<<<grid_for(n), TB, 0, s>>>(n, lanes, gl, gslot);
 }
 
 void let_set_pos(int64_t n, const uint32_t *lanes, const double *a2, GatherLayout gl, double *x,
