@@ -161,6 +161,9 @@ struct TreeBuffers {
 int cell_table_depth(int J, int64_t n);
 size_t tree_scratch_bytes(int64_t n, int J);
 hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStream_t s);
+// dst.v[a] = src.v[perm[a]]: the velocities of a build made with src.vx = null (k_prep skips them)
+void permute_velocities(int64_t n, const uint32_t *perm, const double *svx, const double *svy,
+                        double *dvx, double *dvy, hipStream_t s);
 // After a tree_build: lanes = the bodies in Hilbert order of their cells (refresh), or the
 // previous lane map carried through this build's permutation (k_prep leaves old slot -> new
 // slot in keys32).  Uses keys32 / keys32_s / idx.
@@ -200,10 +203,21 @@ constexpr uint32_t LANE_IDLE = 0xFFFFFFFFu;
 // lanes (nullable): lane -> body slot map (the Hilbert grouping made by lane_order in
 // tree_build.hip); [lo, hi) is then a range of lanes and a2 is written by lane; null = lane q
 // walks slot q and a2 is written by slot.
+// Longest-first dispatch of the traversal's waves (traverse.hip wave_order): `cost` receives
+// every wave's duration (wall-clock ticks) and `order` the dispatch order of the XCD runs of
+// waves, costliest first, made from the previous evaluation's costs.  Only the order in which
+// waves start changes -- every body's sum is the same.
+struct WaveOrder {
+    const uint32_t *order = nullptr;
+    uint32_t *cost = nullptr;
+};
+size_t wave_order_runs(int64_t n);  // runs of a launch over n lanes (0: too many to order)
+hipError_t wave_order(const uint32_t *cost, int64_t n, uint32_t *order, hipStream_t s);
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
               const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, const TraverseCounters *cnt,
-              hipStream_t s, const KickArgs *kick = nullptr, const uint32_t *lanes = nullptr);
+              hipStream_t s, const KickArgs *kick = nullptr, const uint32_t *lanes = nullptr,
+              const WaveOrder *wo = nullptr);
 // multi-GPU shard pieces (bh_shard_range): `rounds` x `world` pieces of whole wavefronts
 __host__ __device__ inline int64_t shard_sub(int64_t n, int world, int rounds) {
     const int64_t parts = (int64_t)world * rounds;

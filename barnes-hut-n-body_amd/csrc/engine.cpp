@@ -191,6 +191,22 @@ struct bh_engine {
     Node *s_nodes = nullptr;
     hipEvent_t table_ev = nullptr;
     bool inject_guard = false;  // bh_debug_inject(1): the next LET build trips k_let_guard
+    // pipelined step (one GPU): the next step's first build runs on stream2 while this step's
+    // second traversal runs; it builds into nodes_alt / alt, and the traversal reads copies of
+    // what that build and the merge rule overwrite (masses, flags, lane map, node count)
+    Node *nodes_alt = nullptr;
+    size_t nodes_alt_cap = 0;
+    double *m_trav = nullptr;
+    uint32_t *cidx_trav = nullptr, *lanes_trav = nullptr, *T_trav = nullptr;
+    int64_t trav_cap = 0;
+    bool prebuilt = false;  // the current step's first build was made by the previous step
+    hipEvent_t pipe_ev[2] = {nullptr, nullptr};
+    // one GPU: the previous evaluation's wave durations and the longest-first run order
+    // (slot 0: the one-GPU launch over all lanes; 1 + k: LET round k's piece)
+    uint32_t *wave_cost = nullptr, *run_order = nullptr;
+    int64_t cost_stride = 0, order_stride = 0;
+    int64_t order_n[1 + BH_SHARD_ROUNDS] = {};  // run_order slot j: a permutation of the runs
+                                               // of a launch over order_n[j] lanes (0: none)
     // Between LET evaluations the new positions stay in the exchange buffer (a2, by lane of
     // pos_lanes at pos_layout's gather slots): the next selection reads them there, and the
     // replica's x, y are written only when something else needs them (materialize_positions)
@@ -334,6 +350,13 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         e->inv_valid = false;
         TRY(dev_alloc(e, e->wave_iters, cap / 64 + 2));
         TRY(dev_alloc(e, e->wave_blocks, cap / 64 + 2));
+        e->cost_stride = cap / 64 + 2;
+        e->order_stride = (int64_t)wave_order_runs(cap) + 1;
+        TRY(dev_alloc(e, e->wave_cost, (size_t)(e->cost_stride * (1 + BH_SHARD_ROUNDS))));
+        HIPCHK(e, hipMemset(e->wave_cost, 0,
+                            sizeof(uint32_t) * (size_t)(e->cost_stride * (1 + BH_SHARD_ROUNDS))));
+        TRY(dev_alloc(e, e->run_order, (size_t)(e->order_stride * (1 + BH_SHARD_ROUNDS))));
+        for (int64_t &o : e->order_n) o = 0;
         TRY(dev_alloc(e, e->heavy, cap));
         TRY(dev_alloc(e, e->keep, cap));
         TRY(dev_alloc(e, e->pos, cap));
@@ -446,27 +469,34 @@ int collect_timings(bh_engine *e) {
 #ifndef BH_LANE_REFRESH
 #define BH_LANE_REFRESH 16  // builds between Hilbert re-sorts of the lane map (0: Morton lanes)
 #endif
-int build(bh_engine *e) {
+// overlap: the pipelined step's build on stream `s` -- into nodes_alt and alt without the
+// velocities (permute_velocities follows) and without the final swap (the caller swaps)
+int build_into(bh_engine *e, hipStream_t s, bool overlap) {
     const int64_t n = e->n;
     TreeBuffers tb = tree_buffers(e);
+    if (overlap) {
+        tb.src.vx = tb.src.vy = nullptr;
+        tb.nodes = e->nodes_alt;
+    }
     // Hilbert waves (every rank alike): re-sorted every BH_LANE_REFRESH builds, carried through
     // the build's permutation by k_emit_com in between
     const bool use_lanes = BH_LANE_REFRESH > 0 && n > 0 && e->p.theta != 0.0;
     const bool refresh = use_lanes && (!e->lanes_valid || e->lanes_age >= BH_LANE_REFRESH);
     tb.lanes_remap = use_lanes && !refresh ? e->lanes : nullptr;
-    HIPCHK(e, tree_build(tb, n, e->geo, e->stream));
+    HIPCHK(e, tree_build(tb, n, e->geo, s));
     ++e->full_builds;
     e->inv_valid = false;  // the map follows this build's permutation
     if (use_lanes) {
-        if (refresh) HIPCHK(e, lane_order(tb, n, e->geo.J, true, e->lanes, e->stream));
+        if (refresh) HIPCHK(e, lane_order(tb, n, e->geo.J, true, e->lanes, s));
         e->lanes_valid = true;
         e->lanes_age = refresh ? 1 : e->lanes_age + 1;
     } else {
         e->lanes_valid = false;  // this build's permutation was not applied to the map
     }
     e->spl_nb = sort_buckets(n);  // k_prep wrote this build's splitters
-    if (n > 0) std::swap(e->st, e->alt);
     e->st_morton = true;
+    if (overlap) return BH_OK;
+    if (n > 0) std::swap(e->st, e->alt);
     if (e->solo && n > 0 && e->p.theta != 0.0) {  // the peers' cell values for later LET builds
         if (!e->solo_table) {
             TRY(dev_alloc(e, e->solo_table, LET_TSTRIDE));
@@ -486,6 +516,8 @@ int build(bh_engine *e) {
     e->tree_valid = true;
     return BH_OK;
 }
+
+int build(bh_engine *e) { return build_into(e, e->stream, false); }
 
 // theta = 0 workspace: flags per node slot, selected indices and the leaf list per body.
 int ensure_direct(bh_engine *e) {
@@ -714,6 +746,9 @@ int sync_velocities(bh_engine *e) {
 // kicks its own body (velocity in the replicated state, owner only) and sends the body's new
 // position -- drifted, or as the build left it (jitter, BHA:146-151) -- so every replica takes
 // all positions from the exchange.
+int wave_order_for(bh_engine *e, int slot, int64_t lanes, hipStream_t s, WaveOrder &wo);
+int wave_order_next(bh_engine *e, int slot, int64_t lanes, hipStream_t s);
+
 int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     *done = false;
     if (kick != KICK_DRIFT && kick != KICK_ONLY) return BH_OK;
@@ -811,10 +846,13 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         hipStream_t rs = (k & 1) ? e->stream2 : e->stream;
         // lane q of the piece writes slot gather_slot(q) = q - lo + gather_slot(lo)
         double *a2r = e->a2 + W * (gather_slot(gl, lo) - lo);
+        WaveOrder wo;
+        TRY(wave_order_for(e, 1 + k, hi - lo, rs, wo));
         traverse(e->L.nodes, e->let_node_cap, e->L.posc + LET_CELLS, e->sub_dst.x, e->sub_dst.y,
                  e->sub_dst.m, e->sub_dst.cidx, lo, hi, e->geo, fp, a2r, nullptr, rs,
-                 &ka, e->L.lanes);
+                 &ka, e->L.lanes, &wo);
         HIPCHK(e, hipGetLastError());
+        TRY(wave_order_next(e, 1 + k, hi - lo, rs));
         HIPCHK(e, hipEventRecord(e->round_ev[k], rs));
         HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
         if (e->group) e->group->barrier();
@@ -832,6 +870,38 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     e->a2_layout = gl;
     e->tree_valid = false;  // the full tree was not built
     *done = true;
+    return BH_OK;
+}
+
+// Longest-first wave dispatch for a one-GPU traversal over all n lanes (traverse.hip).
+#ifndef BH_TRAV_LPT
+#define BH_TRAV_LPT 1
+#endif
+// The order for the next launch is made right after each launch (wave_order_next), off the
+// traversal's timed interval; a launch over another lane count first makes its own.
+// slot: 0 for the one-GPU launch, 1 + k for LET round k; lanes: the launch's lane count.
+// Below BH_LPT_MIN_LANES every wave starts at once anyway (8192 wave slots per GPU).
+#ifndef BH_LPT_MIN_LANES
+#define BH_LPT_MIN_LANES 131072
+#endif
+int wave_order_for(bh_engine *e, int slot, int64_t lanes, hipStream_t s, WaveOrder &wo) {
+    wo = WaveOrder{};
+    if (!BH_TRAV_LPT || lanes < BH_LPT_MIN_LANES || wave_order_runs(lanes) == 0) return BH_OK;
+    uint32_t *cost = e->wave_cost + slot * e->cost_stride;
+    uint32_t *order = e->run_order + slot * e->order_stride;
+    if (e->order_n[slot] != lanes) {  // the order must be a permutation of this launch's runs
+        HIPCHK(e, wave_order(cost, lanes, order, s));
+        e->order_n[slot] = lanes;
+    }
+    wo.order = order;
+    wo.cost = cost;
+    return BH_OK;
+}
+
+int wave_order_next(bh_engine *e, int slot, int64_t lanes, hipStream_t s) {
+    if (!BH_TRAV_LPT || lanes <= 0 || e->order_n[slot] != lanes) return BH_OK;
+    HIPCHK(e, wave_order(e->wave_cost + slot * e->cost_stride, lanes,
+                         e->run_order + slot * e->order_stride, s));
     return BH_OK;
 }
 
@@ -855,11 +925,15 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
     }
     e->let_age = 0;
     const int64_t n = e->n;
-    TRY(materialize_positions(e));  // the replica's x, y; a2 is free again
-    TRY(sync_velocities(e));        // before the full build permutes the state
-    TRY(mark(e, -1));
-    TRY(build(e));
-    TRY(mark(e, 0));
+    if (e->prebuilt) {  // the pipelined step built this tree (single GPU: nothing deferred)
+        e->prebuilt = false;
+    } else {
+        TRY(materialize_positions(e));  // the replica's x, y; a2 is free again
+        TRY(sync_velocities(e));        // before the full build permutes the state
+        TRY(mark(e, -1));
+        TRY(build(e));
+        TRY(mark(e, 0));
+    }
     ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};  // BHA:378
     const uint32_t *d_T = e->base + n;
     const bool direct = fp.theta2 == 0.0 && !visits;
@@ -884,9 +958,14 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
     if ((!e->comm && !e->group && !e->solo) || visits) {
         if (BH_FUSE_KICK && kick != KICK_NONE && !direct && !visits && fused) {
             const KickArgs ka{kick, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
+            WaveOrder wo;
+            TRY(wave_order_for(e, 0, n, e->stream, wo));
             traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, e->st.cidx, 0, n, e->geo, fp,
-                     e->a2, nullptr, e->stream, &ka, lanes);
+                     e->a2, nullptr, e->stream, &ka, lanes, &wo);
             *fused = true;
+            HIPCHK(e, hipGetLastError());
+            TRY(mark(e, 1));
+            return wave_order_next(e, 0, n, e->stream);
         } else {
             forces(0, n, visits, e->stream, e->a2);
         }
@@ -975,19 +1054,22 @@ int merge_bufs(bh_engine *e) {
     return BH_OK;
 }
 
-int merge(bh_engine *e) {
+// s: the engine's stream, or stream2 in the pipelined step (no phase marks there)
+int merge(bh_engine *e, hipStream_t s = nullptr) {
     if (e->p.merge_min_dist <= 0.0 || e->n <= 1 || !e->heavy_possible) return BH_OK;  // BHA:465
+    const bool marks = !s;
+    if (!s) s = e->stream;
     TRY(materialize_positions(e));
-    TRY(mark(e, -1));
+    if (marks) TRY(mark(e, -1));
     TRY(merge_bufs(e));
     const double minD2 = e->p.merge_min_dist * e->p.merge_min_dist;  // BHA:468
     merge_candidates(e->n, e->st.x, e->st.y, e->st.m, e->st.cidx, e->p.merge_max_mass, minD2,
-                     e->heavy, e->box, e->box_cap, e->stream);
+                     e->heavy, e->box, e->box_cap, s);
     merge_replay(e->box, e->box_cap, e->st.m, e->st.cidx, e->scalars, e->dlog, e->rkeys, e->ridx,
-                 e->mbits, e->mslot, e->n, e->stream);
+                 e->mbits, e->mslot, e->n, s);
     HIPCHK(e, hipGetLastError());
     e->merge_ran = true;
-    TRY(mark(e, 3));
+    if (marks) TRY(mark(e, 3));
     return BH_OK;
 }
 
@@ -1108,12 +1190,104 @@ int agree_let_flags(bh_engine *e, uint32_t ls[2], uint32_t *own_sub) {
     return BH_OK;
 }
 
+// ---- the pipelined step (one GPU) -----------------------------------------------------
+// Step s's second traversal (a(t+dt), BHA:421-433) and step s+1's first build (BHA:359, over the
+// same positions after the merge rule, BHA:438) are independent: the kick writes only
+// velocities, the merge rule only masses and flags, and the build reads neither velocities nor
+// the traversal's output.  So the merge rule and the next build run on stream2 while the
+// traversal runs -- the build kernels (single-workgroup span passes, scans, sorts: ~260 us of
+// mostly under-filled launches per build at C3) fill the chip next to the traversal's tail.
+// The traversal reads copies of what they overwrite (masses, flags, lane map, node count) and
+// the build writes the other node array; the velocities follow the build's permutation once
+// the kick is done.  Every kernel sees the inputs of the sequential order: bit-identical.
+#ifndef BH_PIPELINE
+#define BH_PIPELINE 1
+#endif
+bool pipelined(const bh_engine *e, bool last) {
+    return BH_PIPELINE && BH_FUSE_KICK && !last && e->n > 0 && !e->comm && !e->group &&
+           !e->solo && e->p.theta != 0.0;
+}
+
+int pipe_alloc(bh_engine *e) {
+    if (e->nodes_alt_cap < e->node_cap) {
+        TRY(dev_alloc(e, e->nodes_alt, e->node_cap));
+        e->nodes_alt_cap = e->node_cap;
+    }
+    if (e->trav_cap < e->cap) {
+        TRY(dev_alloc(e, e->m_trav, (size_t)e->cap));
+        TRY(dev_alloc(e, e->cidx_trav, (size_t)e->cap));
+        TRY(dev_alloc(e, e->lanes_trav, (size_t)e->cap));
+        if (!e->T_trav) TRY(dev_alloc(e, e->T_trav, 1));
+        e->trav_cap = e->cap;
+    }
+    for (hipEvent_t &ev : e->pipe_ev)
+        if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    if (!e->stream2) {
+        HIPCHK(e, hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
+        HIPCHK(e, hipEventCreateWithFlags(&e->built_ev, hipEventDisableTiming));
+    }
+    return BH_OK;
+}
+
+// The second evaluation of a pipelined step: build, second traversal with the fused kick, and
+// next step's first build; e->prebuilt tells the next evaluation its tree is there.
+int evaluate_pipelined(bh_engine *e) {
+    const int64_t n = e->n;
+    TRY(mark(e, -1));
+    TRY(build(e));
+    TRY(mark(e, 0));
+    hipStream_t s = e->stream;
+    const bool lanes = e->lanes_valid;
+    HIPCHK(e, hipMemcpyAsync(e->m_trav, e->st.m, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
+    HIPCHK(e, hipMemcpyAsync(e->cidx_trav, e->st.cidx, sizeof(uint32_t) * n,
+                             hipMemcpyDeviceToDevice, s));
+    if (lanes)
+        HIPCHK(e, hipMemcpyAsync(e->lanes_trav, e->lanes, sizeof(uint32_t) * n,
+                                 hipMemcpyDeviceToDevice, s));
+    HIPCHK(e, hipMemcpyAsync(e->T_trav, e->base + n, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    HIPCHK(e, hipEventRecord(e->pipe_ev[0], s));
+    HIPCHK(e, hipStreamWaitEvent(e->stream2, e->pipe_ev[0], 0));
+    const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};  // BHA:378
+    const KickArgs ka{KICK_ONLY, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
+    WaveOrder wo;
+    TRY(wave_order_for(e, 0, n, s, wo));
+    traverse(e->nodes, e->node_cap, e->T_trav, e->st.x, e->st.y, e->m_trav, e->cidx_trav, 0, n,
+             e->geo, fp, e->a2, nullptr, s, &ka, lanes ? e->lanes_trav : nullptr, &wo);
+    HIPCHK(e, hipGetLastError());
+    TRY(mark(e, 1));
+    TRY(wave_order_next(e, 0, n, s));
+    TRY(merge(e, e->stream2));                      // BHA:438
+    TRY(build_into(e, e->stream2, true));           // step s+1's first tree (BHA:359)
+    HIPCHK(e, hipEventRecord(e->pipe_ev[1], e->stream2));
+    HIPCHK(e, hipStreamWaitEvent(s, e->pipe_ev[1], 0));
+    permute_velocities(n, e->perm, e->st.vx, e->st.vy, e->alt.vx, e->alt.vy, s);
+    HIPCHK(e, hipGetLastError());
+    TRY(mark(e, 0));  // the wait for the overlapped build and the velocity permutation
+    std::swap(e->st, e->alt);
+    std::swap(e->nodes, e->nodes_alt);
+    std::swap(e->node_cap, e->nodes_alt_cap);
+    e->prebuilt = true;
+    return BH_OK;
+}
+
 // ---- one PhysicsEngine.step() (BHA:405-439) ------------------------------------------
 // last: the final step of a bh_step call -- its second build is the full tree (lastTree,
 // BHA:435, for getTreeForDebug) also on a multi-rank engine that shards its builds.
 int step_once(bh_engine *e, bool last) {
     const int64_t n = e->n;
     const double dtHalf = e->p.dt * 0.5;  // BHA:412
+    if (pipelined(e, last)) {
+        TRY(pipe_alloc(e));
+        bool fused = false;
+        TRY(evaluate(e, nullptr, KICK_DRIFT, &fused, true));  // a(t), kick + drift fused
+        if (!fused) {
+            e->err = "pipelined step: the first evaluation did not fuse its kick";
+            return BH_E_STATE;
+        }
+        TRY(evaluate_pipelined(e));  // a(t+dt), the kick, the merge rule and the next tree
+        e->tree_valid = true;
+        return BH_OK;
+    }
     if (n > 0) {
         bool fused = false;  // one GPU: the kicks ride in the traversal's epilogue
         // (multi-rank LET evaluations integrate their own bodies too: fused)
@@ -1505,6 +1679,8 @@ void bh_destroy(bh_engine *e) {
         (void)hipStreamDestroy(e->stream2);
     }
     if (e->built_ev) (void)hipEventDestroy(e->built_ev);
+    for (hipEvent_t ev : e->pipe_ev)
+        if (ev) (void)hipEventDestroy(ev);
     free_state(e->st);
     free_state(e->alt);
     free_state(e->snap);
@@ -1524,7 +1700,8 @@ void bh_destroy(bh_engine *e) {
                     e->span_children, e->scalars, e->visits32, e->contrib32, e->lanes, e->wave_iters, e->wave_blocks, e->heavy, e->keep,
                     e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->mbits, e->mslot, e->scratch,
                     e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaf_cover, e->leaves.xy, e->leaves.m,
-                    e->leaves.slot, e->leaf_tmp, e->spl, e->bcount, e->bstart};
+                    e->leaves.slot, e->leaf_tmp, e->spl, e->bcount, e->bstart, e->nodes_alt, e->wave_cost, e->run_order,
+                    e->m_trav, e->cidx_trav, e->lanes_trav, e->T_trav};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     for (hipEvent_t ev : e->ev) (void)hipEventDestroy(ev);
@@ -1616,6 +1793,7 @@ int bh_step(bh_engine *e, int32_t k) {
         HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, 5 * sizeof(uint32_t), e->stream));
         e->removed.clear();
         e->merge_ran = false;
+        e->prebuilt = false;
         for (int32_t s = 0; s < k; ++s) TRY(step_once(e, s + 1 == k));
         HIPCHK(e, hipStreamSynchronize(e->stream));
         if (may_let) {  // LET subset sizes of this call: [4] some rank overflowed, [5] largest

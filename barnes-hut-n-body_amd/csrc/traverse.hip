@@ -172,11 +172,17 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
                                                  int64_t lo, int64_t hi, ForceParams fp,
                                                  Geometry g, double *__restrict__ a2,
                                                  TraverseCounters cnt, KickArgs kick,
-                                                 const uint32_t *__restrict__ lanes) {
-#ifdef BH_TRAV_TIMING
+                                                 const uint32_t *__restrict__ lanes,
+                                                 WaveOrder wo) {
+#if defined(BH_TRAV_TIMING)
     const uint64_t t_start = wall_clock64();
+#else
+    const uint64_t t_start = wo.cost ? wall_clock64() : 0;
 #endif
-    const int64_t q = lo + (int64_t)xcd_block<BH_TRAV_XCD_RUN>() * TB + threadIdx.x;  // lane
+    uint32_t v = xcd_block<BH_TRAV_XCD_RUN>();
+    if (wo.order)  // the v-th run to start is the order[v]-th run of waves (wave_order)
+        v = wo.order[v / BH_TRAV_XCD_RUN] * BH_TRAV_XCD_RUN + v % BH_TRAV_XCD_RUN;
+    const int64_t q = lo + (int64_t)v * TB + threadIdx.x;  // lane
     const uint32_t lp = lanes && q < hi ? lanes[q] : (uint32_t)q;
     const bool valid = q < hi && (!lanes || lp != LANE_IDLE);
     const int64_t p = lanes ? (int64_t)lp : q;  // its body's slot
@@ -206,6 +212,9 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     else
         walk<false, COUNT, OFF32>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx,
                                   fy, nvis, niters, ncontrib, nblocks);
+    if (wo.cost && threadIdx.x == 0 && q < hi)
+        wo.cost[(q - lo) >> 6] = (uint32_t)(wall_clock64() - t_start < 0xFFFFFFull
+                                                  ? wall_clock64() - t_start : 0xFFFFFFull);
     if (COUNT && (threadIdx.x & 63) == 0) {
         cnt.wave_iters[(q - lo) >> 6] = niters;
         cnt.wave_blocks[(q - lo) >> 6] = nblocks;
@@ -304,7 +313,64 @@ __global__ __launch_bounds__(STB) void k_selftest_math(int64_t n, uint64_t seed,
     if (local) atomicAdd(bad, (unsigned long long)local);
 }
 
+// Dispatch order of the XCD runs (BH_TRAV_XCD_RUN consecutive waves, one XCD's L2): costliest
+// first by the previous evaluation's wave durations, ties (no costs yet: all zero) in run order.
+// The waves of a launch come in two to three dispatch generations at C3 whose durations span
+// 170-540 us: in run order the dense disk centres start late and end the kernel alone.
+constexpr int WO_TB = 1024;
+constexpr int WO_MAX_RUNS = 4096;
+
+__global__ __launch_bounds__(WO_TB) void k_wave_order(const uint32_t *__restrict__ cost,
+                                                      uint32_t waves, uint32_t runs,
+                                                      uint32_t *__restrict__ order) {
+    __shared__ uint64_t key[WO_MAX_RUNS];
+    uint32_t P = 1;
+    while (P < runs) P <<= 1;
+    for (uint32_t r = threadIdx.x; r < P; r += WO_TB) {
+        uint64_t k = ~0ull;
+        if (r < runs) {
+            uint32_t sum = 0;
+            const uint32_t w0 = r * BH_TRAV_XCD_RUN;
+            const uint32_t w1 = min(w0 + (uint32_t)BH_TRAV_XCD_RUN, waves);
+            for (uint32_t w = w0; w < w1; ++w) sum += cost[w];  // <= 64 x 2^24
+            k = ((uint64_t)(~sum) << 32) | r;
+        }
+        key[r] = k;
+    }
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t i = threadIdx.x; i < P; i += WO_TB) {
+                const uint32_t l = i ^ j;
+                if (l > i) {
+                    const uint64_t a = key[i], b = key[l];
+                    if (((i & k) == 0) == (a > b)) {
+                        key[i] = b;
+                        key[l] = a;
+                    }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t r = threadIdx.x; r < runs; r += WO_TB) order[r] = (uint32_t)key[r];
+}
+
 }  // namespace
+
+size_t wave_order_runs(int64_t n) {
+    const int64_t waves = (n + TB - 1) / TB;
+    const int64_t G = 8 * (int64_t)BH_TRAV_XCD_RUN;  // xcd_block remaps whole groups only
+    const int64_t runs = (waves + G - 1) / G * 8;
+    return runs <= WO_MAX_RUNS ? (size_t)runs : 0;
+}
+
+hipError_t wave_order(const uint32_t *cost, int64_t n, uint32_t *order, hipStream_t s) {
+    const size_t runs = wave_order_runs(n);
+    if (runs == 0) return hipErrorInvalidValue;
+    k_wave_order<<<1, WO_TB, 0, s>>>(cost, (uint32_t)((n + TB - 1) / TB), (uint32_t)runs, order);
+    return hipGetLastError();
+}
 
 hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_bad, hipStream_t s) {
     k_selftest_math<<<4096, STB, 0, s>>>(n, seed, d_bad);
@@ -314,16 +380,19 @@ hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_ba
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
               const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, const TraverseCounters *cnt,
-              hipStream_t s, const KickArgs *kick, const uint32_t *lanes) {
+              hipStream_t s, const KickArgs *kick, const uint32_t *lanes, const WaveOrder *wo) {
     if (hi <= lo) return;
     unsigned grid = (unsigned)((hi - lo + TB - 1) / TB);
+    const WaveOrder w = wo && wave_order_runs(hi - lo) ? *wo : WaveOrder{};
+    if (w.order)  // whole runs: every run index the order maps to exists in the grid
+        grid = (unsigned)(wave_order_runs(hi - lo) * BH_TRAV_XCD_RUN);
     // node records addressed by a 32-bit byte offset while the array stays below 4 GiB
     const bool off32 = node_cap * sizeof(Node) < (size_t(1) << 32);
     const KickArgs ka = kick ? *kick : KickArgs{KICK_NONE, nullptr, nullptr, 0.0, 0.0, nullptr};
     const TraverseCounters tc = cnt ? *cnt : TraverseCounters{nullptr, nullptr, nullptr, nullptr};
 #define BH_TRAV(C, O, K) \
     k_traverse<C, O, K><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, tc, ka, \
-                                            lanes)
+                                            lanes, w)
     if (cnt) {  // diagnostic counting walk: accelerations out, never fused
         if (off32) BH_TRAV(true, true, KICK_NONE);
         else BH_TRAV(true, false, KICK_NONE);

@@ -422,8 +422,10 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
         spl[a / SORT_B] = ((k >> key32_shift(J)) << 32) | (uint64_t)a;
     dst.x[a] = src.x[i];
     dst.y[a] = src.y[i];
-    dst.vx[a] = src.vx[i];
-    dst.vy[a] = src.vy[i];
+    if (src.vx) {  // null: the velocities are still being written (the pipelined step)
+        dst.vx[a] = src.vx[i];
+        dst.vy[a] = src.vy[i];
+    }
     dst.m[a] = src.m[i];
     dst.cidx[a] = src.cidx[i];
     int c_cur = -1, c_prev = -1;
@@ -1473,6 +1475,25 @@ using LaneSortConfig = rocprim::radix_sort_config<rocprim::default_config, rocpr
 #define BH_LANE_LO_BIT 8
 #endif
 constexpr unsigned LANE_SORT_LO_BIT = BH_LANE_LO_BIT;
+
+// The pipelined step (engine.cpp): a build made while the previous evaluation still kicks the
+// velocities leaves them out (src.vx = null); they follow with the build's permutation.
+__global__ __launch_bounds__(TB) void k_permute_vel(int64_t n, const uint32_t *__restrict__ perm,
+                                                    const double *__restrict__ svx,
+                                                    const double *__restrict__ svy,
+                                                    double *__restrict__ dvx,
+                                                    double *__restrict__ dvy) {
+    const int64_t a = (int64_t)xcd_block() * TB + threadIdx.x;
+    if (a >= n) return;
+    const uint32_t i = perm[a];
+    dvx[a] = svx[i];
+    dvy[a] = svy[i];
+}
+
+void permute_velocities(int64_t n, const uint32_t *perm, const double *svx, const double *svy,
+                        double *dvx, double *dvy, hipStream_t s) {
+    if (n > 0) k_permute_vel<<<grid_for(n), TB, 0, s>>>(n, perm, svx, svy, dvx, dvy);
+}
 
 hipError_t lane_order(const TreeBuffers &b, int64_t n, int J, bool refresh, uint32_t *lanes,
                       hipStream_t s) {

@@ -41,6 +41,11 @@ sys.path.insert(0, os.path.join(ROOT, "barnes-hut-n-body_amd"))
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md, chip-level parameters)
 FP64_VEC_PEAK_TF = 78.6  # MI355X FP64 vector peak (FMA = 2 flop), AMD spec sheet (not in the guide)
 FP64_NOFMA_PEAK_TF = 39.3  # the same issue rate without FMA: -ffp-contract=off (bit-exactness)
+# k_direct's inner loop per interaction (gfx950 ISA of direct.hip, fast path): 33 fp64 VALU
+# instructions (11 mul, 7 add, 15 fma/fmac) + 1 v_rsq_f64; one wave64 fp64 instruction per CU
+# per clock (the 78.6 TF peak = 256 CU x 2.4 GHz x 64 lanes x 2)
+DIRECT_VALU_PER_INTERACTION = 34
+N_CU = 256
 FLOP_PER_INTERACTION = 20  # SURVEY §8d convention: one point force (BHA:250-259), sqrt/div = 1
 NODE_BYTES = 32        # one fp64 node record (comX, comY, mass, next/meta) — SURVEY §8d
 BODY_EVAL_BYTES = 40   # body read (x, y, m) + acceleration write (ax, ay) per evaluation
@@ -445,8 +450,16 @@ def main():
         bodies_per_launch = bodies / world
         flops_per_launch = FLOP_PER_INTERACTION * bodies_per_launch * (bodies - 1)
         kernel = "k_direct"
-        extra = {"interactions_per_s": round(flops_per_launch / FLOP_PER_INTERACTION /
-                                             (trav_ms * 1e-3)) if trav_ms > 0 else 0}
+        ips = flops_per_launch / FLOP_PER_INTERACTION / (trav_ms * 1e-3) if trav_ms > 0 else 0
+        extra = {"interactions_per_s": round(ips)}
+        if clock_stats and clock_stats.get("median_mhz"):
+            # the instruction-issue ceiling of this exact sequence at the measured clock
+            ceil = N_CU * clock_stats["median_mhz"] * 1e6 * 64 / DIRECT_VALU_PER_INTERACTION
+            extra["valu_issue_ceiling"] = {
+                "valu_per_interaction": DIRECT_VALU_PER_INTERACTION,
+                "clock_mhz": clock_stats["median_mhz"],
+                "interactions_per_s": round(ceil),
+                "frac": round(ips / ceil, 4)}
     else:
         kernel = "k_traverse" if world == 1 else "k_traverse (one rank's 4 rounds, 2 streams)"
         cs = [c for c in (cnt_start, cnt_end) if c]

@@ -1032,3 +1032,32 @@ def test_profiling_timings_do_not_change_results():
     b.step(4)
     for u, v in zip(a.get_bodies(), b.get_bodies()):
         assert bits_equal(u, v)
+
+
+def test_pipelined_call_equals_single_steps():
+    """One GPU, theta > 0: inside a bh_step(k) call every step but the last overlaps its second
+    traversal with the merge rule and the next step's first build (engine.cpp, the pipelined
+    step).  k = 20 in one call (two lane-map refreshes, merges mid-call) against 20 calls of one
+    step each (never pipelined): the same state bit for bit, the same last tree and removals,
+    and both equal to the oracle."""
+    arrs = scenes.two_disks(30000, 6000)
+    bx, by = np.array([900.0, 1500.0]), np.array([400.0, 420.0])
+    arrs = (np.concatenate([arrs[0], bx]), np.concatenate([arrs[1], by]),
+            np.concatenate([arrs[2], np.zeros(2)]), np.concatenate([arrs[3], np.zeros(2)]),
+            np.concatenate([arrs[4], np.array([6000.0, 8000.0])]))
+    p = bh_amd.default_params(theta=0.5)
+    one = bh_amd.Engine(p)
+    one.reset_bodies(*arrs)
+    one.step(20)
+    many = bh_amd.Engine(p)
+    many.reset_bodies(*arrs)
+    for _ in range(20):
+        many.step(1)
+    assert one.num_bodies() < len(arrs[0])  # the heavy bodies merged inside the call
+    for u, v in zip(one.get_bodies(), many.get_bodies()):
+        assert bits_equal(u, v)
+    for u, v in zip(one.get_quads(), many.get_quads()):
+        assert bits_equal(u, v)
+    ref = oracle.Oracle(*arrs, theta=0.5)
+    ref.step(20)
+    _assert_state_equal(one, ref)
