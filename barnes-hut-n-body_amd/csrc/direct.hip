@@ -103,12 +103,32 @@ __device__ __forceinline__ void sum_tile(const double4_t *s_rec, int cnt, double
 #ifndef BH_DIRECT_U
 #define BH_DIRECT_U 4
 #endif
+#ifndef BH_DIRECT_PF
+#define BH_DIRECT_PF 0
+#endif
     constexpr int U = BH_DIRECT_U;
     int j = 0;
+#if BH_DIRECT_PF
+    // the next batch's records are read while this batch computes (register double buffer)
+    double4_t nx[U];
+    if (U <= cnt) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) nx[u] = s_rec[u];
+    }
+#endif
     for (; j + U <= cnt; j += U) {
         double4_t r[U];
+#if BH_DIRECT_PF
+#pragma unroll
+        for (int u = 0; u < U; ++u) r[u] = nx[u];
+        if (j + 2 * U <= cnt) {
+#pragma unroll
+            for (int u = 0; u < U; ++u) nx[u] = s_rec[j + U + u];
+        }
+#else
 #pragma unroll
         for (int u = 0; u < U; ++u) r[u] = s_rec[j + u];  // broadcast reads, issued together
+#endif
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const bool other = (uint32_t)__double_as_longlong(r[u].w) != self;  // BHA:219

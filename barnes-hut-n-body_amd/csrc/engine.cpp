@@ -191,7 +191,7 @@ struct bh_engine {
     Node *s_nodes = nullptr;
     hipEvent_t table_ev = nullptr;
     bool inject_guard = false;  // bh_debug_inject(1): the next LET build trips k_let_guard
-    // pipelined step (one GPU): the next step's first build runs on stream2 while this step's
+    // pipelined step (one GPU): the next step's first build runs on pipe_stream while this step's
     // second traversal runs; it builds into nodes_alt / alt, and the traversal reads copies of
     // what that build and the merge rule overwrite (masses, flags, lane map, node count)
     Node *nodes_alt = nullptr;
@@ -201,6 +201,7 @@ struct bh_engine {
     int64_t trav_cap = 0;
     bool prebuilt = false;  // the current step's first build was made by the previous step
     hipEvent_t pipe_ev[2] = {nullptr, nullptr};
+    hipStream_t pipe_stream = nullptr;  // the overlapped work's stream (BH_PIPE_PRIORITY)
     // one GPU: the previous evaluation's wave durations and the longest-first run order
     // (slot 0: the one-GPU launch over all lanes; 1 + k: LET round k's piece)
     uint32_t *wave_cost = nullptr, *run_order = nullptr;
@@ -875,7 +876,7 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
 
 // Longest-first wave dispatch for a one-GPU traversal over all n lanes (traverse.hip).
 #ifndef BH_TRAV_LPT
-#define BH_TRAV_LPT 1
+#define BH_TRAV_LPT 0  // measured without gain; the wave durations stay recordable
 #endif
 // The order for the next launch is made right after each launch (wave_order_next), off the
 // traversal's timed interval; a launch over another lane count first makes its own.
@@ -1054,7 +1055,7 @@ int merge_bufs(bh_engine *e) {
     return BH_OK;
 }
 
-// s: the engine's stream, or stream2 in the pipelined step (no phase marks there)
+// s: the engine's stream, or pipe_stream in the pipelined step (no phase marks there)
 int merge(bh_engine *e, hipStream_t s = nullptr) {
     if (e->p.merge_min_dist <= 0.0 || e->n <= 1 || !e->heavy_possible) return BH_OK;  // BHA:465
     const bool marks = !s;
@@ -1087,8 +1088,11 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
     uint32_t *h = static_cast<uint32_t *>(e->pin);
     HIPCHK(e, hipMemcpyAsync(h, e->scalars, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipMemcpyAsync(h + 4, e->box, sizeof(MergeHeader), hipMemcpyDeviceToHost, e->stream));
+    HIPCHK(e, hipMemcpyAsync(h + 12, e->scalars + 8, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                             e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     const uint32_t nd = h[2];
+    const uint32_t nd_before_last = h[12];  // removals before the call's last merge rule
     const MergeHeader hdr = *reinterpret_cast<const MergeHeader *>(h + 4);
     if (h[3]) {
         *overflow = h[3];
@@ -1113,7 +1117,10 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
     e->n = n - (int64_t)nd;
     e->inv_valid = false;  // another n: another exchange layout
     e->removed.assign(dead.begin(), dead.end());
-    e->tree_valid = false;  // BHA:526
+    // BHA:526: lastTree = null only when the last step's merge rule removed a body.  Bodies
+    // removed by earlier steps were tombstones in the last build (sentinel keys: the tail of its
+    // order), so its first n - nd sorted keys still describe the whole tree.
+    if (nd != nd_before_last) e->tree_valid = false;
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return BH_OK;
 }
@@ -1194,7 +1201,7 @@ int agree_let_flags(bh_engine *e, uint32_t ls[2], uint32_t *own_sub) {
 // Step s's second traversal (a(t+dt), BHA:421-433) and step s+1's first build (BHA:359, over the
 // same positions after the merge rule, BHA:438) are independent: the kick writes only
 // velocities, the merge rule only masses and flags, and the build reads neither velocities nor
-// the traversal's output.  So the merge rule and the next build run on stream2 while the
+// the traversal's output.  So the merge rule and the next build run on a second stream while the
 // traversal runs -- the build kernels (single-workgroup span passes, scans, sorts: ~260 us of
 // mostly under-filled launches per build at C3) fill the chip next to the traversal's tail.
 // The traversal reads copies of what they overwrite (masses, flags, lane map, node count) and
@@ -1202,6 +1209,9 @@ int agree_let_flags(bh_engine *e, uint32_t ls[2], uint32_t *own_sub) {
 // the kick is done.  Every kernel sees the inputs of the sequential order: bit-identical.
 #ifndef BH_PIPELINE
 #define BH_PIPELINE 1
+#endif
+#ifndef BH_PIPE_PRIORITY
+#define BH_PIPE_PRIORITY 1  // the overlapped work's stream at the highest priority
 #endif
 bool pipelined(const bh_engine *e, bool last) {
     return BH_PIPELINE && BH_FUSE_KICK && !last && e->n > 0 && !e->comm && !e->group &&
@@ -1222,9 +1232,13 @@ int pipe_alloc(bh_engine *e) {
     }
     for (hipEvent_t &ev : e->pipe_ev)
         if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    if (!e->stream2) {
-        HIPCHK(e, hipStreamCreateWithFlags(&e->stream2, hipStreamNonBlocking));
-        HIPCHK(e, hipEventCreateWithFlags(&e->built_ev, hipEventDisableTiming));
+    if (!e->pipe_stream) {
+        // the traversal fills every wave slot with a queue of waiting workgroups: at the default
+        // priority the overlapped kernels would be dispatched only in its tail
+        int lo = 0, hi = 0;
+        HIPCHK(e, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(e, hipStreamCreateWithPriority(&e->pipe_stream, hipStreamNonBlocking,
+                                              BH_PIPE_PRIORITY ? hi : lo));
     }
     return BH_OK;
 }
@@ -1246,7 +1260,7 @@ int evaluate_pipelined(bh_engine *e) {
                                  hipMemcpyDeviceToDevice, s));
     HIPCHK(e, hipMemcpyAsync(e->T_trav, e->base + n, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
     HIPCHK(e, hipEventRecord(e->pipe_ev[0], s));
-    HIPCHK(e, hipStreamWaitEvent(e->stream2, e->pipe_ev[0], 0));
+    HIPCHK(e, hipStreamWaitEvent(e->pipe_stream, e->pipe_ev[0], 0));
     const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};  // BHA:378
     const KickArgs ka{KICK_ONLY, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
     WaveOrder wo;
@@ -1256,9 +1270,9 @@ int evaluate_pipelined(bh_engine *e) {
     HIPCHK(e, hipGetLastError());
     TRY(mark(e, 1));
     TRY(wave_order_next(e, 0, n, s));
-    TRY(merge(e, e->stream2));                      // BHA:438
-    TRY(build_into(e, e->stream2, true));           // step s+1's first tree (BHA:359)
-    HIPCHK(e, hipEventRecord(e->pipe_ev[1], e->stream2));
+    TRY(merge(e, e->pipe_stream));                  // BHA:438
+    TRY(build_into(e, e->pipe_stream, true));       // step s+1's first tree (BHA:359)
+    HIPCHK(e, hipEventRecord(e->pipe_ev[1], e->pipe_stream));
     HIPCHK(e, hipStreamWaitEvent(s, e->pipe_ev[1], 0));
     permute_velocities(n, e->perm, e->st.vx, e->st.vy, e->alt.vx, e->alt.vy, s);
     HIPCHK(e, hipGetLastError());
@@ -1308,6 +1322,9 @@ int step_once(bh_engine *e, bool last) {
         }
         e->tree_valid = true;  // lastTree = root (BHA:435)
     }
+    if (last)  // the call's removal count before its last merge rule (finish_merges, BHA:526)
+        HIPCHK(e, hipMemcpyAsync(e->scalars + 8, e->scalars + 2, sizeof(uint32_t),
+                                 hipMemcpyDeviceToDevice, e->stream));
     return merge(e);  // BHA:438
 }
 
@@ -1681,6 +1698,10 @@ void bh_destroy(bh_engine *e) {
     if (e->built_ev) (void)hipEventDestroy(e->built_ev);
     for (hipEvent_t ev : e->pipe_ev)
         if (ev) (void)hipEventDestroy(ev);
+    if (e->pipe_stream) {
+        (void)hipStreamSynchronize(e->pipe_stream);
+        (void)hipStreamDestroy(e->pipe_stream);
+    }
     free_state(e->st);
     free_state(e->alt);
     free_state(e->snap);

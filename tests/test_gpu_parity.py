@@ -1038,8 +1038,9 @@ def test_pipelined_call_equals_single_steps():
     """One GPU, theta > 0: inside a bh_step(k) call every step but the last overlaps its second
     traversal with the merge rule and the next step's first build (engine.cpp, the pipelined
     step).  k = 20 in one call (two lane-map refreshes, merges mid-call) against 20 calls of one
-    step each (never pipelined): the same state bit for bit, the same last tree and removals,
-    and both equal to the oracle."""
+    step each (never pipelined): the same state bit for bit and the same last tree, both equal
+    to the oracle's -- lastTree (BHA:435) is the last step's tree also when earlier steps of the
+    call merged bodies (BHA:526 clears it only for the last step's merge)."""
     arrs = scenes.two_disks(30000, 6000)
     bx, by = np.array([900.0, 1500.0]), np.array([400.0, 420.0])
     arrs = (np.concatenate([arrs[0], bx]), np.concatenate([arrs[1], by]),
@@ -1061,3 +1062,5 @@ def test_pipelined_call_equals_single_steps():
     ref = oracle.Oracle(*arrs, theta=0.5)
     ref.step(20)
     _assert_state_equal(one, ref)
+    for u, v in zip(one.get_quads(), ref.quads()):
+        assert bits_equal(u, v)

@@ -100,7 +100,7 @@ __global__ __launch_bounds__(TB) void k_pair(int iters, double soft2, double *ou
 int main() {
     int dev = 0, cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    const int blocks = cus * 4 * 8 * 64 / TB;  // 8 waves per SIMD
+    int blocks = cus * 4 * 8 * 64 / TB;  // 8 waves per SIMD (k_pair also at 4: k_direct's C5 grid)
     double *out = nullptr;
     Clocks *c = nullptr;
     CK(hipMalloc(&out, sizeof(double) * blocks * TB));
@@ -130,6 +130,9 @@ int main() {
     report("v_rsq_f64", CHAINS, it / 4, [&] { k_rsq<<<blocks, TB>>>(it / 4, out, c); });
     // per interaction: the 33 fp64 VALU ops + v_rsq_f64 of k_direct, + 1 add (px[u] += 1)
     report("point_force_interactions", 4, it / 16, [&] { k_pair<<<blocks, TB>>>(it / 16, 1.0, out, c); });
+    blocks = cus * 4 * 4 * 64 / TB;  // 4 waves per SIMD: 262 144 bodies, one lane each
+    report("point_force_interactions_4waves", 4, it / 16,
+           [&] { k_pair<<<blocks, TB>>>(it / 16, 1.0, out, c); });
     CK(hipDeviceSynchronize());
     return 0;
 }
