@@ -559,6 +559,17 @@ static void sim_drain(void) {
     g_sim_flushes += mx;
 }
 
+/* Resume-stack model (analysis helper): a node some active lanes accept while others open it
+ * ("mixed") parks the accepting lanes until the cursor leaves its subtree -- a stack entry of
+ * (next, lane mask).  Counts the pushes and the largest stack depth per group (histogram). */
+static int g_mix_sd, g_mix_max;
+static int64_t g_mix_pushes, g_mix_hist[65];
+
+void oracle_mixstack_stats(int64_t *pushes, int64_t *hist65) {
+    *pushes = g_mix_pushes;
+    for (int k = 0; k < 65; ++k) hist65[k] = g_mix_hist[k];
+}
+
 static int64_t union_walk(const Tree *t, const ForceCtx *c, int64_t node, const int64_t *bis,
                           uint64_t mask, int64_t *lane_visits) {
     const Node *nd = &t->nodes[node];
@@ -589,8 +600,14 @@ static int64_t union_walk(const Tree *t, const ForceCtx *c, int64_t node, const 
     g_contribs += __builtin_popcountll(acc);
     sim_push(acc);
     int64_t it = 1;
+    const int mixed = acc && open;
+    if (mixed) {
+        ++g_mix_pushes;
+        if (++g_mix_sd > g_mix_max) g_mix_max = g_mix_sd;
+    }
     if (open)
         for (int k = 0; k < 4; ++k) it += union_walk(t, c, nd->child + k, bis, open, lane_visits);
+    g_mix_sd -= mixed;
     return it;
 }
 
@@ -621,11 +638,15 @@ int64_t oracle_group_union(oracle_engine *e, const int64_t *order, int64_t count
     g_force_iters = g_contribs = 0;
     g_pm_blocks = g_pm_merges = 0;
     g_pm_pend = 0;
+    g_mix_pushes = 0;
+    for (int k = 0; k < 65; ++k) g_mix_hist[k] = 0;
     for (int64_t g0 = 0; g0 < count; g0 += group) {
+        g_mix_sd = g_mix_max = 0;
         const int nb = (int)((count - g0) < group ? (count - g0) : group);
         const uint64_t mask = nb == 64 ? ~0ull : ((1ull << nb) - 1);
         const int64_t it = union_walk(&e->tree, &c, 0, order + g0, mask, &lv);
         pm_drain();
+        g_mix_hist[g_mix_max < 64 ? g_mix_max : 64]++;
         if (g_sim_q) sim_drain();
         if (per_group) per_group[g0 / group] = it;
         iters += it;

@@ -14,11 +14,11 @@ import sys
 import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path[:0] = [ROOT, os.path.join(ROOT, "barnes-hut-n-body_amd"), os.path.join(ROOT, "tests")]
+sys.path[:0] = [ROOT, os.path.join(ROOT, "barnes-hut-n-body_amd"), os.path.join(ROOT, "tools")]
 
 import oracle  # noqa: E402
 from bh_amd import scenes  # noqa: E402
-from test_dist_gloo import morton_order  # noqa: E402
+from morton import morton_order  # noqa: E402
 
 
 def main():
