@@ -332,9 +332,7 @@ void let_unpack_vel(int64_t n, const uint32_t *lanes, const double *a2, GatherLa
 // ---- launchers (direct.hip): theta = 0 all-pairs ---------------------------------
 // Non-empty leaves of the last tree in pre-order (the reference's theta = 0 summation order).
 struct LeafList {
-    double *xy;      // interleaved (x, y)
-    double *m;
-    uint32_t *slot;  // body slot (self-skip)
+    double *rec;  // 32 B per leaf: x, y, m, body slot (low 32 bits; self-skip), in pre-order
 };
 size_t leaf_select_bytes(int64_t node_cap);
 // cover: 2 (node_cap + 1) int32 of scratch (leaves under a mass-0 node are never visited)

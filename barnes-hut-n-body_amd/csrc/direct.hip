@@ -20,6 +20,7 @@ namespace bh {
 namespace {
 
 constexpr int TB = 256;
+typedef double double4_t __attribute__((ext_vector_type(4)));
 #ifndef BH_DIRECT_TILE
 #define BH_DIRECT_TILE 1024
 #endif
@@ -64,10 +65,12 @@ __global__ __launch_bounds__(TB) void k_leaf_gather(const Node *__restrict__ nod
     const uint32_t i = blockIdx.x * TB + threadIdx.x;
     if (i >= *d_count) return;
     const Node nd = nodes[sel[i]];
-    L.xy[2 * i] = nd.comX;  // leaf: the body's own x, y, m (BHA:176-178)
-    L.xy[2 * i + 1] = nd.comY;
-    L.m[i] = nd.mass;
-    L.slot[i] = nd.meta & NODE_BODY_MASK;
+    double4_t r;  // leaf: the body's own x, y, m (BHA:176-178)
+    r.x = nd.comX;
+    r.y = nd.comY;
+    r.z = nd.mass;
+    r.w = __longlong_as_double((long long)(nd.meta & NODE_BODY_MASK));
+    reinterpret_cast<double4_t *>(L.rec)[i] = r;
 }
 
 typedef double double2_t __attribute__((ext_vector_type(2)));
@@ -92,8 +95,6 @@ __device__ __forceinline__ void pair_force(double px, double py, double pm, doub
     fx += f * dx * invR;
     fy += f * dy * invR;
 }
-
-typedef double double4_t __attribute__((ext_vector_type(4)));
 
 // One staged leaf: (x, y, m, slot bits).
 template <bool FAST>
@@ -174,15 +175,8 @@ __global__ __launch_bounds__(TB) void k_direct(LeafList L, const uint32_t *__res
     for (uint32_t t0 = 0; t0 < nl; t0 += TILE) {
         const int cnt = (int)min((uint32_t)TILE, nl - t0);
         __syncthreads();
-        for (int i = threadIdx.x; i < cnt; i += TB) {
-            const double2_t q = *reinterpret_cast<const double2_t *>(L.xy + 2 * (t0 + i));
-            double4_t r;
-            r.x = q.x;
-            r.y = q.y;
-            r.z = L.m[t0 + i];
-            r.w = __longlong_as_double((long long)L.slot[t0 + i]);
-            s_rec[i] = r;
-        }
+        for (int i = threadIdx.x; i < cnt; i += TB)
+            s_rec[i] = reinterpret_cast<const double4_t *>(L.rec)[t0 + i];
         __syncthreads();
         if (fast)
             sum_tile<true>(s_rec, cnt, bx, by, Gm, soft2, self, fx, fy);

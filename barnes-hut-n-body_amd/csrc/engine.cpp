@@ -145,7 +145,7 @@ struct bh_engine {
     uint8_t *leaf_flags = nullptr;
     uint32_t *leaf_sel = nullptr, *leaf_count = nullptr;
     int32_t *leaf_cover = nullptr;  // 2 (node_cap + 1): subtrees of massless nodes
-    LeafList leaves{nullptr, nullptr, nullptr};
+    LeafList leaves{nullptr};
     void *leaf_tmp = nullptr;
     size_t leaf_tmp_bytes = 0;
     size_t leaf_node_cap = 0;  // node capacity the flags were sized for
@@ -527,9 +527,7 @@ int ensure_direct(bh_engine *e) {
     TRY(dev_alloc(e, e->leaf_sel, (size_t)e->node_cap));
     TRY(dev_alloc(e, e->leaf_count, 1));
     TRY(dev_alloc(e, e->leaf_cover, 2 * ((size_t)e->node_cap + 1)));
-    TRY(dev_alloc(e, e->leaves.xy, 2 * (size_t)e->cap));
-    TRY(dev_alloc(e, e->leaves.m, (size_t)e->cap));
-    TRY(dev_alloc(e, e->leaves.slot, (size_t)e->cap));
+    TRY(dev_alloc(e, e->leaves.rec, 4 * (size_t)e->cap));  // (x, y, m, slot) per leaf
     const size_t tb = leaf_select_bytes((int64_t)e->node_cap);
     if (e->leaf_tmp) (void)hipFree(e->leaf_tmp);
     e->leaf_tmp = nullptr;
@@ -1720,8 +1718,8 @@ void bh_destroy(bh_engine *e) {
                     e->base, e->cell_start, e->nodes, e->span_list, e->super_list,
                     e->span_children, e->scalars, e->visits32, e->contrib32, e->lanes, e->wave_iters, e->wave_blocks, e->heavy, e->keep,
                     e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->mbits, e->mslot, e->scratch,
-                    e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaf_cover, e->leaves.xy, e->leaves.m,
-                    e->leaves.slot, e->leaf_tmp, e->spl, e->bcount, e->bstart, e->nodes_alt, e->wave_cost, e->run_order,
+                    e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaf_cover, e->leaves.rec,
+                    e->leaf_tmp, e->spl, e->bcount, e->bstart, e->nodes_alt, e->wave_cost, e->run_order,
                     e->m_trav, e->cidx_trav, e->lanes_trav, e->T_trav};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
