@@ -112,6 +112,19 @@ struct __attribute__((aligned(16))) SpanSlot {
     double v[4][3];
 };
 
+// Wave priority of the kernels that the pipelined one-GPU step runs next to the second traversal
+// (merge rule, next tree build; engine.cpp evaluate_pipelined): they are latency-bound chains on
+// the critical path once the traversal's last workgroups are placed, and at the default priority
+// a traversal wave sharing their SIMD wins half the issue slots (k_merge_replay, one workgroup:
+// 8-24 us alone, 170 us in the traversal's tail).  s_setprio only orders issue between the waves
+// of one SIMD; alone on the GPU it changes nothing.
+#ifndef BH_CHAIN_PRIO
+#define BH_CHAIN_PRIO 1
+#endif
+__device__ __forceinline__ void chain_prio() {
+    if (BH_CHAIN_PRIO) asm volatile("s_setprio 3");
+}
+
 // Workgroup i of a launch runs on XCD i % 8 (8 XCDs, each with its own 4 MB L2).  For gathers
 // whose neighbouring blocks read overlapping lines, xcd_block() remaps the hardware block index
 // so that every XCD takes runs of BH_XCD_RUN consecutive logical blocks (0: identity; 16 is
@@ -211,13 +224,21 @@ struct WaveOrder {
     const uint32_t *order = nullptr;
     uint32_t *cost = nullptr;
 };
+// Work-queue launch of a traversal (traverse.hip k_traverse_q): ctr = 9 zeroed counters (one per
+// XCD + a done count; the launch leaves them zeroed), at most `waves` waves resident by design,
+// the first `loop_waves` of them looping over tasks.
+struct TaskQueue {
+    uint32_t *ctr = nullptr;
+    uint32_t waves = 0;
+    uint32_t loop_waves = 0;
+};
 size_t wave_order_runs(int64_t n);  // runs of a launch over n lanes (0: too many to order)
 hipError_t wave_order(const uint32_t *cost, int64_t n, uint32_t *order, hipStream_t s);
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
               const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, const TraverseCounters *cnt,
               hipStream_t s, const KickArgs *kick = nullptr, const uint32_t *lanes = nullptr,
-              const WaveOrder *wo = nullptr);
+              const WaveOrder *wo = nullptr, const TaskQueue *tq = nullptr);
 // multi-GPU shard pieces (bh_shard_range): `rounds` x `world` pieces of whole wavefronts
 __host__ __device__ inline int64_t shard_sub(int64_t n, int world, int rounds) {
     const int64_t parts = (int64_t)world * rounds;
@@ -373,7 +394,7 @@ static_assert(sizeof(MergeHeader) == sizeof(MergePair), "mailbox header size");
 // heavy = live m > thr (BHA:474) -> slot list (any order); then the distance test (BHA:493-501)
 void merge_candidates(int64_t n, const double *x, const double *y, const double *m,
                       const uint32_t *cidx, double thr, double minD2, uint32_t *heavy,
-                      MergePair *box, uint32_t cap, hipStream_t s);
+                      MergePair *box, uint32_t cap, hipStream_t s, bool header_zeroed = false);
 // Sequential merge rule on the device (one workgroup): removals become tombstones
 // (cidx |= CIDX_DEAD) logged in dlog[scal[2]++]; scal[3] = pair count if the mailbox overflowed.
 // skeys/sidx: scratch of 2 x cap entries (long lists); bits: (n_cap >> 5) + 1 words and

@@ -205,6 +205,8 @@ struct bh_engine {
     // one GPU: the previous evaluation's wave durations and the longest-first run order
     // (slot 0: the one-GPU launch over all lanes; 1 + k: LET round k's piece)
     uint32_t *wave_cost = nullptr, *run_order = nullptr;
+    uint32_t *tq_ctr = nullptr;  // the pipelined step's work-queue traversal (9 counters)
+    uint32_t tq_cus = 0;
     int64_t cost_stride = 0, order_stride = 0;
     int64_t order_n[1 + BH_SHARD_ROUNDS] = {};  // run_order slot j: a permutation of the runs
                                                // of a launch over order_n[j] lanes (0: none)
@@ -1054,7 +1056,9 @@ int merge_bufs(bh_engine *e) {
 }
 
 // s: the engine's stream, or pipe_stream in the pipelined step (no phase marks there)
-int merge(bh_engine *e, hipStream_t s = nullptr) {
+// header_zeroed: the caller cleared the mailbox header on an earlier stream position (the
+// pipelined step does it before the second traversal, where a fill kernel is not starved)
+int merge(bh_engine *e, hipStream_t s = nullptr, bool header_zeroed = false) {
     if (e->p.merge_min_dist <= 0.0 || e->n <= 1 || !e->heavy_possible) return BH_OK;  // BHA:465
     const bool marks = !s;
     if (!s) s = e->stream;
@@ -1063,7 +1067,7 @@ int merge(bh_engine *e, hipStream_t s = nullptr) {
     TRY(merge_bufs(e));
     const double minD2 = e->p.merge_min_dist * e->p.merge_min_dist;  // BHA:468
     merge_candidates(e->n, e->st.x, e->st.y, e->st.m, e->st.cidx, e->p.merge_max_mass, minD2,
-                     e->heavy, e->box, e->box_cap, s);
+                     e->heavy, e->box, e->box_cap, s, header_zeroed);
     merge_replay(e->box, e->box_cap, e->st.m, e->st.cidx, e->scalars, e->dlog, e->rkeys, e->ridx,
                  e->mbits, e->mslot, e->n, s);
     HIPCHK(e, hipGetLastError());
@@ -1211,6 +1215,18 @@ int agree_let_flags(bh_engine *e, uint32_t ls[2], uint32_t *own_sub) {
 #ifndef BH_PIPE_PRIORITY
 #define BH_PIPE_PRIORITY 1  // the overlapped work's stream at the highest priority
 #endif
+// The second traversal as a work queue (traverse.hip k_traverse_q): at most BH_TRAV_QUEUE_WAVES
+// waves per SIMD, of which BH_TRAV_QUEUE_LOOP loop over tasks; the others take one task and free
+// their slot for the overlapped merge rule and build.
+#ifndef BH_TRAV_QUEUE
+#define BH_TRAV_QUEUE 0  // A/B pending (tools/r03_s3.sh)
+#endif
+#ifndef BH_TRAV_QUEUE_WAVES
+#define BH_TRAV_QUEUE_WAVES 8
+#endif
+#ifndef BH_TRAV_QUEUE_LOOP
+#define BH_TRAV_QUEUE_LOOP 6
+#endif
 bool pipelined(const bh_engine *e, bool last) {
     return BH_PIPELINE && BH_FUSE_KICK && !last && e->n > 0 && !e->comm && !e->group &&
            !e->solo && e->p.theta != 0.0;
@@ -1227,6 +1243,13 @@ int pipe_alloc(bh_engine *e) {
         TRY(dev_alloc(e, e->lanes_trav, (size_t)e->cap));
         if (!e->T_trav) TRY(dev_alloc(e, e->T_trav, 1));
         e->trav_cap = e->cap;
+    }
+    if (BH_TRAV_QUEUE && !e->tq_ctr) {
+        TRY(dev_alloc(e, e->tq_ctr, 16));
+        HIPCHK(e, hipMemset(e->tq_ctr, 0, 16 * sizeof(uint32_t)));
+        int cus = 0;
+        HIPCHK(e, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
+        e->tq_cus = (uint32_t)std::max(cus, 1);
     }
     for (hipEvent_t &ev : e->pipe_ev)
         if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -1257,18 +1280,31 @@ int evaluate_pipelined(bh_engine *e) {
         HIPCHK(e, hipMemcpyAsync(e->lanes_trav, e->lanes, sizeof(uint32_t) * n,
                                  hipMemcpyDeviceToDevice, s));
     HIPCHK(e, hipMemcpyAsync(e->T_trav, e->base + n, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    // the merge rule's mailbox header is cleared here, before the traversal: on the overlapped
+    // stream the fill kernel would wait until the traversal's last workgroups are placed
+    const bool merging = e->p.merge_min_dist > 0.0 && e->n > 1 && e->heavy_possible;
+    if (merging) {
+        TRY(merge_bufs(e));
+        HIPCHK(e, hipMemsetAsync(e->box, 0, sizeof(MergeHeader), s));
+    }
     HIPCHK(e, hipEventRecord(e->pipe_ev[0], s));
     HIPCHK(e, hipStreamWaitEvent(e->pipe_stream, e->pipe_ev[0], 0));
     const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};  // BHA:378
     const KickArgs ka{KICK_ONLY, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
     WaveOrder wo;
     TRY(wave_order_for(e, 0, n, s, wo));
+    TaskQueue tq;
+    if (BH_TRAV_QUEUE && e->tq_ctr && !wo.order) {
+        tq.ctr = e->tq_ctr;
+        tq.waves = e->tq_cus * 4u * BH_TRAV_QUEUE_WAVES;
+        tq.loop_waves = e->tq_cus * 4u * BH_TRAV_QUEUE_LOOP;
+    }
     traverse(e->nodes, e->node_cap, e->T_trav, e->st.x, e->st.y, e->m_trav, e->cidx_trav, 0, n,
-             e->geo, fp, e->a2, nullptr, s, &ka, lanes ? e->lanes_trav : nullptr, &wo);
+             e->geo, fp, e->a2, nullptr, s, &ka, lanes ? e->lanes_trav : nullptr, &wo, &tq);
     HIPCHK(e, hipGetLastError());
     TRY(mark(e, 1));
     TRY(wave_order_next(e, 0, n, s));
-    TRY(merge(e, e->pipe_stream));                  // BHA:438
+    TRY(merge(e, e->pipe_stream, merging));         // BHA:438
     TRY(build_into(e, e->pipe_stream, true));       // step s+1's first tree (BHA:359)
     HIPCHK(e, hipEventRecord(e->pipe_ev[1], e->pipe_stream));
     HIPCHK(e, hipStreamWaitEvent(s, e->pipe_ev[1], 0));
@@ -1720,7 +1756,7 @@ void bh_destroy(bh_engine *e) {
                     e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->mbits, e->mslot, e->scratch,
                     e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaf_cover, e->leaves.rec,
                     e->leaf_tmp, e->spl, e->bcount, e->bstart, e->nodes_alt, e->wave_cost, e->run_order,
-                    e->m_trav, e->cidx_trav, e->lanes_trav, e->T_trav};
+                    e->m_trav, e->cidx_trav, e->lanes_trav, e->T_trav, e->tq_ctr};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     for (hipEvent_t ev : e->ev) (void)hipEventDestroy(ev);

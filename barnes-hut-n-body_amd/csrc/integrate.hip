@@ -85,6 +85,7 @@ __global__ __launch_bounds__(TB) void k_scatter_acc(int64_t n, const uint32_t *_
 __global__ __launch_bounds__(TB) void k_heavy(int64_t n, const double *__restrict__ m,
                                               const uint32_t *__restrict__ cidx, double thr,
                                               uint32_t *__restrict__ heavy, MergeHeader *hdr) {
+    chain_prio();
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
     if (m[i] > thr && !(cidx[i] & CIDX_DEAD)) heavy[atomicAdd(&hdr->heavies, 1u)] = (uint32_t)i;
@@ -98,6 +99,7 @@ __global__ __launch_bounds__(TB) void k_candidates(int64_t n, const double *__re
                                                    const uint32_t *__restrict__ cidx,
                                                    const uint32_t *__restrict__ heavy,
                                                    double minD2, MergePair *box, uint32_t cap) {
+    chain_prio();
     int64_t j = (int64_t)blockIdx.x * TB + threadIdx.x;
     MergeHeader *hdr = reinterpret_cast<MergeHeader *>(box);
     const uint32_t H = __builtin_amdgcn_readfirstlane(
@@ -306,6 +308,7 @@ __global__ __launch_bounds__(REPLAY_TB) void k_merge_replay(const MergePair *__r
                                                             uint32_t *dlog, uint64_t *skeys,
                                                             uint32_t *sidx, uint32_t *bits,
                                                             uint32_t *slot_of, int key_bits) {
+    chain_prio();
     __shared__ uint64_t lk[REPLAY_LDS];
     __shared__ uint32_t li[REPLAY_LDS];
     __shared__ uint32_t hkey[REPLAY_HASH], hcidx[REPLAY_HASH];
@@ -571,8 +574,8 @@ void scatter_acc_to_caller(int64_t n, const uint32_t *cidx, const double *a2, do
 
 void merge_candidates(int64_t n, const double *x, const double *y, const double *m,
                       const uint32_t *cidx, double thr, double minD2, uint32_t *heavy,
-                      MergePair *box, uint32_t cap, hipStream_t s) {
-    (void)hipMemsetAsync(box, 0, sizeof(MergeHeader), s);
+                      MergePair *box, uint32_t cap, hipStream_t s, bool header_zeroed) {
+    if (!header_zeroed) (void)hipMemsetAsync(box, 0, sizeof(MergeHeader), s);
     if (n <= 0) return;
     MergeHeader *hdr = reinterpret_cast<MergeHeader *>(box);
     k_heavy<<<grid_for(n), TB, 0, s>>>(n, m, cidx, thr, heavy, hdr);

@@ -15,6 +15,8 @@
 // The kernel is bound by fp64 VALU issue (the IEEE sqrt and two IEEE divisions per
 // interaction), not by HBM: the node stream is shared by 64 lanes and served from the
 // scalar cache / L2.  See DESIGN.md for the roofline accounting.
+#include <algorithm>
+
 #include "bh_device.hpp"
 #include "fastmath.hpp"
 
@@ -164,24 +166,18 @@ __device__ uint64_t g_trav_times[4 * TRAV_TIMING_MAX];
 // KICK (KickMode): the integration step that follows the evaluation is applied by the lane
 // itself after its walk -- the body's x, y are only ever read by its own lane (other lanes see
 // it through the leaf records), so the update in place is race-free and a2 is not written.
+// One wave's 64 lanes [lo + 64 v, lo + 64 v + 64): walk, then the epilogue.
 template <bool COUNT, bool OFF32, int KICK>
-__global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
-                                                 const uint32_t *__restrict__ d_T, double *x,
-                                                 double *y, const double *__restrict__ m,
-                                                 const uint32_t *__restrict__ cidx,
-                                                 int64_t lo, int64_t hi, ForceParams fp,
-                                                 Geometry g, double *__restrict__ a2,
-                                                 TraverseCounters cnt, KickArgs kick,
-                                                 const uint32_t *__restrict__ lanes,
-                                                 WaveOrder wo) {
-#if defined(BH_TRAV_TIMING)
-    const uint64_t t_start = wall_clock64();
-#else
-    const uint64_t t_start = wo.cost ? wall_clock64() : 0;
-#endif
-    uint32_t v = xcd_block<BH_TRAV_XCD_RUN>();
-    if (wo.order)  // the v-th run to start is the order[v]-th run of waves (wave_order)
-        v = wo.order[v / BH_TRAV_XCD_RUN] * BH_TRAV_XCD_RUN + v % BH_TRAV_XCD_RUN;
+__device__ __forceinline__ void trav_wave(uint32_t v, uint64_t t_start,
+                                          const Node *__restrict__ nodes,
+                                          const uint32_t *__restrict__ d_T, double *x, double *y,
+                                          const double *__restrict__ m,
+                                          const uint32_t *__restrict__ cidx, int64_t lo,
+                                          int64_t hi, const ForceParams &fp, const Geometry &g,
+                                          double *__restrict__ a2, const TraverseCounters &cnt,
+                                          const KickArgs &kick,
+                                          const uint32_t *__restrict__ lanes,
+                                          const WaveOrder &wo) {
     const int64_t q = lo + (int64_t)v * TB + threadIdx.x;  // lane
     const uint32_t lp = lanes && q < hi ? lanes[q] : (uint32_t)q;
     const bool valid = q < hi && (!lanes || lp != LANE_IDLE);
@@ -267,6 +263,68 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
         cnt.visits[p] = nvis;
         cnt.contrib[p] = ncontrib;
     }
+}
+
+template <bool COUNT, bool OFF32, int KICK>
+__global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
+                                                 const uint32_t *__restrict__ d_T, double *x,
+                                                 double *y, const double *__restrict__ m,
+                                                 const uint32_t *__restrict__ cidx,
+                                                 int64_t lo, int64_t hi, ForceParams fp,
+                                                 Geometry g, double *__restrict__ a2,
+                                                 TraverseCounters cnt, KickArgs kick,
+                                                 const uint32_t *__restrict__ lanes,
+                                                 WaveOrder wo) {
+#if defined(BH_TRAV_TIMING)
+    const uint64_t t_start = wall_clock64();
+#else
+    const uint64_t t_start = wo.cost ? wall_clock64() : 0;
+#endif
+    uint32_t v = xcd_block<BH_TRAV_XCD_RUN>();
+    if (wo.order)  // the v-th run to start is the order[v]-th run of waves (wave_order)
+        v = wo.order[v / BH_TRAV_XCD_RUN] * BH_TRAV_XCD_RUN + v % BH_TRAV_XCD_RUN;
+    trav_wave<COUNT, OFF32, KICK>(v, t_start, nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, cnt,
+                                  kick, lanes, wo);
+}
+
+// Work-queue form for a traversal that shares the GPU with a chain of other kernels (the
+// pipelined step's merge rule and next build, engine.cpp): the launch holds at most
+// `pa.waves` waves; the first `pa.loop_waves` of them take wave tasks until none is left, the
+// others take one task each and leave, so that once the first generation of tasks is done the
+// chain finds free wave slots on every CU instead of waiting until the last of ~16 K one-wave
+// workgroups has been placed.  Tasks are handed out per XCD in the same runs of
+// BH_TRAV_XCD_RUN waves as xcd_block gives the plain launch (the run r = j * 8 + xcd), from an
+// agent-scope counter per XCD; every wave adds to a done counter when it leaves and the last one
+// clears all nine counters for the next launch.  Each task is exactly one wave of the plain
+// launch: same lanes, same walk, same epilogue.
+template <bool OFF32, int KICK>
+__global__ __launch_bounds__(TB) void k_traverse_q(const Node *__restrict__ nodes,
+                                                   const uint32_t *__restrict__ d_T, double *x,
+                                                   double *y, const double *__restrict__ m,
+                                                   const uint32_t *__restrict__ cidx,
+                                                   int64_t lo, int64_t hi, ForceParams fp,
+                                                   Geometry g, double *__restrict__ a2,
+                                                   KickArgs kick,
+                                                   const uint32_t *__restrict__ lanes,
+                                                   TaskQueue tq) {
+    constexpr uint32_t C = BH_TRAV_XCD_RUN;
+    const uint32_t xcd = blockIdx.x & 7u;  // blocks are dispatched to the XCDs round-robin
+    const uint32_t waves = (uint32_t)((hi - lo + TB - 1) / TB);
+    const bool loops = blockIdx.x < tq.loop_waves;
+    const TraverseCounters none{nullptr, nullptr, nullptr, nullptr};
+    const WaveOrder wo{};
+    while (true) {
+        uint32_t k = 0;
+        if (threadIdx.x == 0) k = atomicAdd(tq.ctr + xcd, 1u);
+        k = __builtin_amdgcn_readfirstlane(k);
+        const uint32_t v = ((k / C) * 8u + xcd) * C + k % C;  // increasing in k: the XCD is done
+        if (v >= waves) break;                                 // at its first task past the end
+        trav_wave<false, OFF32, KICK>(v, 0, nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, none,
+                                      kick, lanes, wo);
+        if (!loops) break;
+    }
+    if (threadIdx.x == 0 && atomicAdd(tq.ctr + 8, 1u) == gridDim.x - 1u)
+        for (int i = 0; i < 9; ++i) atomicExch(tq.ctr + i, 0u);  // the last wave out
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
@@ -380,8 +438,23 @@ hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_ba
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
               const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, const TraverseCounters *cnt,
-              hipStream_t s, const KickArgs *kick, const uint32_t *lanes, const WaveOrder *wo) {
+              hipStream_t s, const KickArgs *kick, const uint32_t *lanes, const WaveOrder *wo,
+              const TaskQueue *tq) {
     if (hi <= lo) return;
+    if (tq && tq->ctr && !cnt && kick && kick->mode == KICK_ONLY) {  // the pipelined step's a(t+dt)
+        const bool off32 = node_cap * sizeof(Node) < (size_t(1) << 32);
+        const uint32_t waves = (uint32_t)((hi - lo + TB - 1) / TB);
+        const unsigned grid = (unsigned)std::min<uint32_t>(waves, tq->waves) & ~7u;
+        if (grid >= 8) {
+            if (off32)
+                k_traverse_q<true, KICK_ONLY><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi,
+                                                                 fp, g, a2, *kick, lanes, *tq);
+            else
+                k_traverse_q<false, KICK_ONLY><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi,
+                                                                  fp, g, a2, *kick, lanes, *tq);
+            return;
+        }
+    }
     unsigned grid = (unsigned)((hi - lo + TB - 1) / TB);
     const WaveOrder w = wo && wave_order_runs(hi - lo) ? *wo : WaveOrder{};
     if (w.order)  // whole runs: every run index the order maps to exists in the grid

@@ -61,6 +61,7 @@ __global__ __launch_bounds__(TB) void k_morton(int64_t n, const double *__restri
                                                uint64_t *__restrict__ keys,
                                                uint32_t *__restrict__ keys32,
                                                uint32_t *__restrict__ idx) {
+    chain_prio();
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
     double px = x[i], py = y[i];
@@ -174,6 +175,7 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_count(int64_t n,
                                                           uint32_t nb, uint32_t *__restrict__ bkt,
                                                           uint32_t *__restrict__ off,
                                                           uint32_t *__restrict__ counts) {
+    chain_prio();
     const int64_t i = (int64_t)blockIdx.x * SORT_TB + threadIdx.x;
     const bool valid = i < n;
     uint32_t b = 0;
@@ -215,6 +217,7 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_scatter(int64_t n,
                                                             const uint32_t *__restrict__ off,
                                                             const uint32_t *__restrict__ starts,
                                                             uint64_t *__restrict__ comp) {
+    chain_prio();
     const int64_t i = (int64_t)blockIdx.x * SORT_TB + threadIdx.x;
     if (i >= n) return;
     comp[starts[bkt[i]] + off[i]] = ((uint64_t)keys32[i] << 32) | (uint64_t)i;
@@ -267,6 +270,7 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
                                                          uint32_t *__restrict__ keys32_s,
                                                          uint32_t *__restrict__ perm,
                                                          uint64_t *keys_s) {
+    chain_prio();
     __shared__ uint64_t L[SORT_CAP];
     __shared__ uint32_t s_cnt[RADIX_BINS], s_start[RADIX_BINS];
     __shared__ uint32_t s_min, s_max, s_maxbin;
@@ -373,6 +377,7 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
 __global__ __launch_bounds__(TB) void k_key_gather(int64_t n, const uint64_t *__restrict__ keys,
                                                    const uint32_t *__restrict__ perm,
                                                    uint64_t *__restrict__ keys_s) {
+    chain_prio();
     const int64_t a = (int64_t)xcd_block() * TB + threadIdx.x;
     if (a < n) keys_s[a] = keys[perm[a]];
 }
@@ -381,6 +386,7 @@ __global__ __launch_bounds__(TB) void k_key_fixup(int64_t n, int J,
                                                   const uint32_t *__restrict__ keys32_s,
                                                   uint64_t *__restrict__ keys_s,
                                                   uint32_t *__restrict__ perm) {
+    chain_prio();
     const int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (a + 1 >= n) return;
     const uint32_t k = keys32_s[a];
@@ -408,6 +414,7 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
                                              uint32_t *__restrict__ cnt,
                                              uint64_t *__restrict__ spl,
                                              uint32_t *__restrict__ inv) {
+    chain_prio();
     int64_t a = (int64_t)xcd_block() * TB + threadIdx.x;
     if (a > n) return;
     if (a == n) {
@@ -446,6 +453,7 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
 __global__ __launch_bounds__(TB) void k_cells(int64_t n, int J, int D0,
                                               const uint64_t *__restrict__ keys_s,
                                               uint32_t *__restrict__ cell_start) {
+    chain_prio();
     const int64_t bin = (int64_t)blockIdx.x * TB + threadIdx.x;
     const int64_t nbins = (int64_t)1 << (2 * D0);
     if (bin > nbins) return;
@@ -753,6 +761,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
                                                      uint32_t *err,
                                                      const uint32_t *__restrict__ inv,
                                                      uint32_t *__restrict__ lanes) {
+    chain_prio();
     __shared__ double s_m[COM_CAP + 1], s_x[COM_CAP + 1], s_y[COM_CAP + 1];  // [COM_CAP]: pad
     __shared__ uint32_t s_next[COM_CAP];
     __shared__ ushort4 s_ch[COM_CAP];
@@ -1174,6 +1183,7 @@ __global__ __launch_bounds__(TB) void k_span_find(int64_t n, int J, int D0,
                                                   uint32_t span_stride,
                                                   uint32_t *__restrict__ super_list,
                                                   uint32_t n_groups, Node *nodes) {
+    chain_prio();
     const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
     const int L = blockIdx.y;
     if (k >= (int64_t)span_stride) return;
@@ -1221,6 +1231,7 @@ __global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__r
                                                       uint32_t span_stride,
                                                       const Node *__restrict__ nodes,
                                                       SpanSlot *__restrict__ span_children) {
+    chain_prio();
     const uint32_t L = blockIdx.y;
     for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < span_stride; i += gridDim.x * TB) {
         const size_t slot = (size_t)L * span_stride + i;
@@ -1285,6 +1296,7 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span(int J, const uint32_t *__r
                                                       uint32_t span_stride,
                                                       const SpanSlot *__restrict__ span_children,
                                                       Node *nodes) {
+    chain_prio();
     __shared__ double r_m[2][SPAN_GROUP], r_x[2][SPAN_GROUP], r_y[2][SPAN_GROUP];
     const uint32_t g0 = blockIdx.x * SPAN_GROUP;
     const uint32_t kl = threadIdx.x, k = g0 + kl;
@@ -1364,6 +1376,7 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span_top(int J,
                                                           const SpanSlot *__restrict__ span_children,
                                                           const uint32_t *__restrict__ super_list,
                                                           uint32_t n_groups, Node *nodes) {
+    chain_prio();
     for (int L = J; L >= 0; --L) {
         for (uint32_t gi = threadIdx.x; gi < n_groups; gi += SPAN_TB) {
             const uint32_t ko = super_list[(size_t)L * n_groups + gi];
@@ -1453,6 +1466,7 @@ __device__ __forceinline__ uint32_t hilbert16(uint64_t key, int J) {
 __global__ __launch_bounds__(TB) void k_hilbert_keys(int64_t n, int J, const uint64_t *__restrict__ keys_s,
                                                      uint32_t *__restrict__ hkey,
                                                      uint32_t *__restrict__ slot) {
+    chain_prio();
     const int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (a >= n) return;
     const uint64_t k = keys_s[a];
@@ -1462,6 +1476,7 @@ __global__ __launch_bounds__(TB) void k_hilbert_keys(int64_t n, int J, const uin
 
 __global__ __launch_bounds__(TB) void k_lane_remap(int64_t n, const uint32_t *__restrict__ inv,
                                                    uint32_t *__restrict__ lanes) {
+    chain_prio();
     const int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (q < n) lanes[q] = inv[lanes[q]];
 }
