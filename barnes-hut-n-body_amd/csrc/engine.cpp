@@ -222,6 +222,8 @@ struct bh_engine {
     bool solo = false;
     LetCell *solo_table = nullptr;
     uint8_t *solo_all = nullptr;    // every cell marked
+    double *solo_xchg = nullptr;    // BH_SOLO_XCHG: receive buffer of the emulated exchange
+    int64_t solo_xchg_cap = 0;
     uint32_t *solo_cstart = nullptr;
 
     // profiling
@@ -676,6 +678,14 @@ int round_streams(bh_engine *e) {
 // Round k's in-place all-gather of W doubles per lane on the comm stream (RCCL), or the peers'
 // pieces copied in (in-process group: the caller has passed a barrier after every member
 // recorded round_ev[ev_round]; ev_round < 0: the peers' events were waited for already).
+bool solo_xchg_on() {
+    static const bool on = [] {
+        const char *v = std::getenv("BH_SOLO_XCHG");
+        return v && std::strcmp(v, "0") != 0;
+    }();
+    return on;
+}
+
 int gather_round(bh_engine *e, const GatherLayout &gl, int k, int W, int ev_round) {
     const int64_t size = gl.off[k + 1] - gl.off[k];
     double *piece = e->a2 + W * (int64_t)e->world * gl.off[k];  // round k, rank 0
@@ -683,6 +693,20 @@ int gather_round(bh_engine *e, const GatherLayout &gl, int k, int W, int ev_roun
     if (e->comm) {
         NCCLCHK(e, ncclAllGather(piece + W * e->rank * size, piece, (size_t)(W * size),
                                  ncclDouble, e->comm, e->comm_stream));
+    } else if (e->solo && e->world > 1 && solo_xchg_on()) {
+        // measurement only (tools/solo_rank.py): the bytes a rank receives per round, as one
+        // device copy of the own piece on the comm stream -- the copy kernel competes for wave
+        // slots with the traversal rounds the way the all-gather's kernel would; peers' positions
+        // stay where they are (the copy goes to a scratch buffer)
+        const int64_t need = (int64_t)W * size * (e->world - 1);
+        if (e->solo_xchg_cap < need) {
+            TRY(dev_alloc(e, e->solo_xchg, (size_t)need));
+            e->solo_xchg_cap = need;
+        }
+        for (int q = 1; q < e->world; ++q)
+            HIPCHK(e, hipMemcpyAsync(e->solo_xchg + (int64_t)W * size * (q - 1),
+                                     piece + W * e->rank * size, sizeof(double) * W * size,
+                                     hipMemcpyDeviceToDevice, e->comm_stream));
     } else if (e->group) {
         for (int q = 0; q < e->world; ++q) {
             if (q == e->rank) continue;
@@ -749,6 +773,25 @@ int sync_velocities(bh_engine *e) {
 // all positions from the exchange.
 int wave_order_for(bh_engine *e, int slot, int64_t lanes, hipStream_t s, WaveOrder &wo);
 int wave_order_next(bh_engine *e, int slot, int64_t lanes, hipStream_t s);
+
+// LET rounds as work queues too (each round's own counters): the one-shot waves leave wave
+// slots on every CU to the comm stream's all-gather kernels while the next round runs.
+#ifndef BH_LET_QUEUE
+#define BH_LET_QUEUE 0
+#endif
+#ifndef BH_LET_QUEUE_LOOP
+#define BH_LET_QUEUE_LOOP 6
+#endif
+// 16 counters per queue: slot 0 the pipelined step's second traversal, 1 + k LET round k
+int tq_alloc(bh_engine *e) {
+    if (e->tq_ctr) return BH_OK;
+    TRY(dev_alloc(e, e->tq_ctr, 16 * (1 + BH_SHARD_ROUNDS)));
+    HIPCHK(e, hipMemset(e->tq_ctr, 0, 16 * (1 + BH_SHARD_ROUNDS) * sizeof(uint32_t)));
+    int cus = 0;
+    HIPCHK(e, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
+    e->tq_cus = (uint32_t)std::max(cus, 1);
+    return BH_OK;
+}
 
 int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     *done = false;
@@ -849,9 +892,16 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         double *a2r = e->a2 + W * (gather_slot(gl, lo) - lo);
         WaveOrder wo;
         TRY(wave_order_for(e, 1 + k, hi - lo, rs, wo));
+        TaskQueue tq;
+        if (BH_LET_QUEUE && !wo.order) {
+            TRY(tq_alloc(e));
+            tq.ctr = e->tq_ctr + 16 * (1 + k);
+            tq.waves = e->tq_cus * 4u * 8u;
+            tq.loop_waves = e->tq_cus * 4u * BH_LET_QUEUE_LOOP;
+        }
         traverse(e->L.nodes, e->let_node_cap, e->L.posc + LET_CELLS, e->sub_dst.x, e->sub_dst.y,
                  e->sub_dst.m, e->sub_dst.cidx, lo, hi, e->geo, fp, a2r, nullptr, rs,
-                 &ka, e->L.lanes, &wo);
+                 &ka, e->L.lanes, &wo, &tq);
         HIPCHK(e, hipGetLastError());
         TRY(wave_order_next(e, 1 + k, hi - lo, rs));
         HIPCHK(e, hipEventRecord(e->round_ev[k], rs));
@@ -1244,13 +1294,7 @@ int pipe_alloc(bh_engine *e) {
         if (!e->T_trav) TRY(dev_alloc(e, e->T_trav, 1));
         e->trav_cap = e->cap;
     }
-    if (BH_TRAV_QUEUE && !e->tq_ctr) {
-        TRY(dev_alloc(e, e->tq_ctr, 16));
-        HIPCHK(e, hipMemset(e->tq_ctr, 0, 16 * sizeof(uint32_t)));
-        int cus = 0;
-        HIPCHK(e, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
-        e->tq_cus = (uint32_t)std::max(cus, 1);
-    }
+    if (BH_TRAV_QUEUE) TRY(tq_alloc(e));
     for (hipEvent_t &ev : e->pipe_ev)
         if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     if (!e->pipe_stream) {
@@ -1756,7 +1800,8 @@ void bh_destroy(bh_engine *e) {
                     e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->mbits, e->mslot, e->scratch,
                     e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaf_cover, e->leaves.rec,
                     e->leaf_tmp, e->spl, e->bcount, e->bstart, e->nodes_alt, e->wave_cost, e->run_order,
-                    e->m_trav, e->cidx_trav, e->lanes_trav, e->T_trav, e->tq_ctr};
+                    e->m_trav, e->cidx_trav, e->lanes_trav, e->T_trav, e->tq_ctr,
+                    e->solo_xchg};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     for (hipEvent_t ev : e->ev) (void)hipEventDestroy(ev);

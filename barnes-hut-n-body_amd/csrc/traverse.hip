@@ -441,17 +441,27 @@ void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x
               hipStream_t s, const KickArgs *kick, const uint32_t *lanes, const WaveOrder *wo,
               const TaskQueue *tq) {
     if (hi <= lo) return;
-    if (tq && tq->ctr && !cnt && kick && kick->mode == KICK_ONLY) {  // the pipelined step's a(t+dt)
+    // work-queue form: the pipelined step's a(t+dt) (KICK_ONLY) and the LET rounds (owner kicks)
+    if (tq && tq->ctr && !cnt && kick &&
+        (kick->mode == KICK_ONLY || kick->mode == KICK_OWN_DRIFT || kick->mode == KICK_OWN_ONLY)) {
         const bool off32 = node_cap * sizeof(Node) < (size_t(1) << 32);
         const uint32_t waves = (uint32_t)((hi - lo + TB - 1) / TB);
         const unsigned grid = (unsigned)std::min<uint32_t>(waves, tq->waves) & ~7u;
         if (grid >= 8) {
-            if (off32)
-                k_traverse_q<true, KICK_ONLY><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi,
-                                                                 fp, g, a2, *kick, lanes, *tq);
-            else
-                k_traverse_q<false, KICK_ONLY><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi,
-                                                                  fp, g, a2, *kick, lanes, *tq);
+#define BH_TRAVQ(O, K) \
+    k_traverse_q<O, K><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, *kick, \
+                                           lanes, *tq)
+            if (kick->mode == KICK_ONLY) {
+                if (off32) BH_TRAVQ(true, KICK_ONLY);
+                else BH_TRAVQ(false, KICK_ONLY);
+            } else if (kick->mode == KICK_OWN_DRIFT) {
+                if (off32) BH_TRAVQ(true, KICK_OWN_DRIFT);
+                else BH_TRAVQ(false, KICK_OWN_DRIFT);
+            } else {
+                if (off32) BH_TRAVQ(true, KICK_OWN_ONLY);
+                else BH_TRAVQ(false, KICK_OWN_ONLY);
+            }
+#undef BH_TRAVQ
             return;
         }
     }

@@ -1,11 +1,12 @@
 #!/usr/bin/env python3
 """Kernel timeline of one step from a rocprofv3 --kernel-trace CSV (measurement helper).
 
-Usage: python tools/timeline.py <run_kernel_trace.csv> [step_from_end=2] [out.txt]
+Usage: python tools/timeline.py <run_kernel_trace.csv> [step_from_end=2] [out.txt] [anchor]
 
 A one-GPU C3 step launches two fused traversals (`k_traverse<false, true, 1>` = kick + drift,
 `<..., 2>` = kick only).  The window is from the start of the n-th last kick+drift traversal to
-the start of the next one; every kernel in it is printed with its start / end offsets in us,
+the start of the next one (another anchor kernel: 4th argument, e.g. k_let_flags for one LET
+evaluation); every kernel in it is printed with its start / end offsets in us,
 its queue and stream, so the overlap of the pipelined build with the second traversal and the
 exposed gaps can be read off.  The summary line adds the union of busy time and the idle gaps.
 """
@@ -22,7 +23,8 @@ def main():
         ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
                    r.get("Queue_Id", "?"), r.get("Stream_Id", "?")))
     ks.sort()
-    starts = [k[0] for k in ks if "k_traverse<false, true, 1>" in k[2]]
+    anchor = sys.argv[4] if len(sys.argv) > 4 else "k_traverse<false, true, 1>"
+    starts = [k[0] for k in ks if anchor in k[2]]
     if len(starts) < back + 1:
         sys.exit("not enough steps in the trace")
     t0, t1 = starts[-back - 1], starts[-back]
@@ -51,7 +53,7 @@ def main():
             out.append(f"  gap of {g / 1e3:.1f} us at {at / 1e3:.1f}")
     text = "\n".join(out)
     print(text)
-    if len(sys.argv) > 3:
+    if len(sys.argv) > 3 and sys.argv[3] != "-":
         open(sys.argv[3], "w").write(text + "\n")
 
 
