@@ -370,6 +370,9 @@ void direct_forces(const LeafList &L, const uint32_t *d_count, const double *x, 
 void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
                 double dtHalf, double dt, hipStream_t s, const uint32_t *lanes = nullptr,
                 GatherLayout gl = GatherLayout{});
+void copy_trav_inputs(int64_t n, const double *m, double *m_t, const uint32_t *cidx,
+                      uint32_t *cidx_t, const uint32_t *lanes, uint32_t *lanes_t,
+                      const uint32_t *T, uint32_t *T_t, hipStream_t s);
 void kick(int64_t n, const double *a2, double *vx, double *vy, double dtHalf, hipStream_t s,
           const uint32_t *lanes = nullptr, GatherLayout gl = GatherLayout{});
 void iota_u32(uint32_t *p, int64_t n, hipStream_t s);

@@ -1317,13 +1317,9 @@ int evaluate_pipelined(bh_engine *e) {
     TRY(mark(e, 0));
     hipStream_t s = e->stream;
     const bool lanes = e->lanes_valid;
-    HIPCHK(e, hipMemcpyAsync(e->m_trav, e->st.m, sizeof(double) * n, hipMemcpyDeviceToDevice, s));
-    HIPCHK(e, hipMemcpyAsync(e->cidx_trav, e->st.cidx, sizeof(uint32_t) * n,
-                             hipMemcpyDeviceToDevice, s));
-    if (lanes)
-        HIPCHK(e, hipMemcpyAsync(e->lanes_trav, e->lanes, sizeof(uint32_t) * n,
-                                 hipMemcpyDeviceToDevice, s));
-    HIPCHK(e, hipMemcpyAsync(e->T_trav, e->base + n, sizeof(uint32_t), hipMemcpyDeviceToDevice, s));
+    copy_trav_inputs(n, e->st.m, e->m_trav, e->st.cidx, e->cidx_trav, lanes ? e->lanes : nullptr,
+                     e->lanes_trav, e->base + n, e->T_trav, s);
+    HIPCHK(e, hipGetLastError());
     // the merge rule's mailbox header is cleared here, before the traversal: on the overlapped
     // stream the fill kernel would wait until the traversal's last workgroups are placed
     const bool merging = e->p.merge_min_dist > 0.0 && e->n > 1 && e->heavy_possible;

@@ -46,6 +46,25 @@ __global__ __launch_bounds__(TB) void k_kick(int64_t n, const double *__restrict
     vy[p] = vy[p] + a.y * dtHalf;
 }
 
+// The pipelined step's copies of what the overlapped merge rule and build overwrite while the
+// second traversal reads it (masses, flags, lane map, node count): one launch instead of four
+// device copies.
+__global__ __launch_bounds__(TB) void k_trav_inputs(int64_t n, const double *__restrict__ m,
+                                                    double *__restrict__ m_t,
+                                                    const uint32_t *__restrict__ cidx,
+                                                    uint32_t *__restrict__ cidx_t,
+                                                    const uint32_t *__restrict__ lanes,
+                                                    uint32_t *__restrict__ lanes_t,
+                                                    const uint32_t *__restrict__ T,
+                                                    uint32_t *__restrict__ T_t) {
+    const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i == 0) *T_t = *T;
+    if (i >= n) return;
+    m_t[i] = m[i];
+    cidx_t[i] = cidx[i];
+    if (lanes) lanes_t[i] = lanes[i];
+}
+
 __global__ __launch_bounds__(TB) void k_iota(uint32_t *__restrict__ p, int64_t n) {
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i < n) p[i] = (uint32_t)i;
@@ -545,6 +564,13 @@ hipError_t compact_lanes(int64_t n, const uint32_t *lanes, const uint32_t *keep,
 void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
                 double dtHalf, double dt, hipStream_t s, const uint32_t *lanes, GatherLayout gl) {
     if (n > 0) k_kick_drift<<<grid_for(n), TB, 0, s>>>(n, a2, x, y, vx, vy, dtHalf, dt, lanes, gl);
+}
+
+void copy_trav_inputs(int64_t n, const double *m, double *m_t, const uint32_t *cidx,
+                      uint32_t *cidx_t, const uint32_t *lanes, uint32_t *lanes_t,
+                      const uint32_t *T, uint32_t *T_t, hipStream_t s) {
+    k_trav_inputs<<<grid_for(n > 0 ? n : 1), TB, 0, s>>>(n, m, m_t, cidx, cidx_t, lanes, lanes_t,
+                                                          T, T_t);
 }
 
 void kick(int64_t n, const double *a2, double *vx, double *vy, double dtHalf, hipStream_t s,
