@@ -224,21 +224,13 @@ struct WaveOrder {
     const uint32_t *order = nullptr;
     uint32_t *cost = nullptr;
 };
-// Work-queue launch of a traversal (traverse.hip k_traverse_q): ctr = 9 zeroed counters (one per
-// XCD + a done count; the launch leaves them zeroed), at most `waves` waves resident by design,
-// the first `loop_waves` of them looping over tasks.
-struct TaskQueue {
-    uint32_t *ctr = nullptr;
-    uint32_t waves = 0;
-    uint32_t loop_waves = 0;
-};
 size_t wave_order_runs(int64_t n);  // runs of a launch over n lanes (0: too many to order)
 hipError_t wave_order(const uint32_t *cost, int64_t n, uint32_t *order, hipStream_t s);
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
               const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, const TraverseCounters *cnt,
               hipStream_t s, const KickArgs *kick = nullptr, const uint32_t *lanes = nullptr,
-              const WaveOrder *wo = nullptr, const TaskQueue *tq = nullptr);
+              const WaveOrder *wo = nullptr);
 // multi-GPU shard pieces (bh_shard_range): `rounds` x `world` pieces of whole wavefronts
 __host__ __device__ inline int64_t shard_sub(int64_t n, int world, int rounds) {
     const int64_t parts = (int64_t)world * rounds;

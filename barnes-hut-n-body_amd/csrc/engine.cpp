@@ -205,8 +205,6 @@ struct bh_engine {
     // one GPU: the previous evaluation's wave durations and the longest-first run order
     // (slot 0: the one-GPU launch over all lanes; 1 + k: LET round k's piece)
     uint32_t *wave_cost = nullptr, *run_order = nullptr;
-    uint32_t *tq_ctr = nullptr;  // the pipelined step's work-queue traversal (9 counters)
-    uint32_t tq_cus = 0;
     int64_t cost_stride = 0, order_stride = 0;
     int64_t order_n[1 + BH_SHARD_ROUNDS] = {};  // run_order slot j: a permutation of the runs
                                                // of a launch over order_n[j] lanes (0: none)
@@ -774,25 +772,6 @@ int sync_velocities(bh_engine *e) {
 int wave_order_for(bh_engine *e, int slot, int64_t lanes, hipStream_t s, WaveOrder &wo);
 int wave_order_next(bh_engine *e, int slot, int64_t lanes, hipStream_t s);
 
-// LET rounds as work queues too (each round's own counters): the one-shot waves leave wave
-// slots on every CU to the comm stream's all-gather kernels while the next round runs.
-#ifndef BH_LET_QUEUE
-#define BH_LET_QUEUE 0
-#endif
-#ifndef BH_LET_QUEUE_LOOP
-#define BH_LET_QUEUE_LOOP 6
-#endif
-// 16 counters per queue: slot 0 the pipelined step's second traversal, 1 + k LET round k
-int tq_alloc(bh_engine *e) {
-    if (e->tq_ctr) return BH_OK;
-    TRY(dev_alloc(e, e->tq_ctr, 16 * (1 + BH_SHARD_ROUNDS)));
-    HIPCHK(e, hipMemset(e->tq_ctr, 0, 16 * (1 + BH_SHARD_ROUNDS) * sizeof(uint32_t)));
-    int cus = 0;
-    HIPCHK(e, hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, e->device));
-    e->tq_cus = (uint32_t)std::max(cus, 1);
-    return BH_OK;
-}
-
 int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     *done = false;
     if (kick != KICK_DRIFT && kick != KICK_ONLY) return BH_OK;
@@ -892,16 +871,9 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         double *a2r = e->a2 + W * (gather_slot(gl, lo) - lo);
         WaveOrder wo;
         TRY(wave_order_for(e, 1 + k, hi - lo, rs, wo));
-        TaskQueue tq;
-        if (BH_LET_QUEUE && !wo.order) {
-            TRY(tq_alloc(e));
-            tq.ctr = e->tq_ctr + 16 * (1 + k);
-            tq.waves = e->tq_cus * 4u * 8u;
-            tq.loop_waves = e->tq_cus * 4u * BH_LET_QUEUE_LOOP;
-        }
         traverse(e->L.nodes, e->let_node_cap, e->L.posc + LET_CELLS, e->sub_dst.x, e->sub_dst.y,
                  e->sub_dst.m, e->sub_dst.cidx, lo, hi, e->geo, fp, a2r, nullptr, rs,
-                 &ka, e->L.lanes, &wo, &tq);
+                 &ka, e->L.lanes, &wo);
         HIPCHK(e, hipGetLastError());
         TRY(wave_order_next(e, 1 + k, hi - lo, rs));
         HIPCHK(e, hipEventRecord(e->round_ev[k], rs));
@@ -1265,18 +1237,6 @@ int agree_let_flags(bh_engine *e, uint32_t ls[2], uint32_t *own_sub) {
 #ifndef BH_PIPE_PRIORITY
 #define BH_PIPE_PRIORITY 1  // the overlapped work's stream at the highest priority
 #endif
-// The second traversal as a work queue (traverse.hip k_traverse_q): at most BH_TRAV_QUEUE_WAVES
-// waves per SIMD, of which BH_TRAV_QUEUE_LOOP loop over tasks; the others take one task and free
-// their slot for the overlapped merge rule and build.
-#ifndef BH_TRAV_QUEUE
-#define BH_TRAV_QUEUE 0  // A/B pending (tools/r03_s3.sh)
-#endif
-#ifndef BH_TRAV_QUEUE_WAVES
-#define BH_TRAV_QUEUE_WAVES 8
-#endif
-#ifndef BH_TRAV_QUEUE_LOOP
-#define BH_TRAV_QUEUE_LOOP 6
-#endif
 bool pipelined(const bh_engine *e, bool last) {
     return BH_PIPELINE && BH_FUSE_KICK && !last && e->n > 0 && !e->comm && !e->group &&
            !e->solo && e->p.theta != 0.0;
@@ -1294,7 +1254,6 @@ int pipe_alloc(bh_engine *e) {
         if (!e->T_trav) TRY(dev_alloc(e, e->T_trav, 1));
         e->trav_cap = e->cap;
     }
-    if (BH_TRAV_QUEUE) TRY(tq_alloc(e));
     for (hipEvent_t &ev : e->pipe_ev)
         if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
     if (!e->pipe_stream) {
@@ -1333,14 +1292,8 @@ int evaluate_pipelined(bh_engine *e) {
     const KickArgs ka{KICK_ONLY, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
     WaveOrder wo;
     TRY(wave_order_for(e, 0, n, s, wo));
-    TaskQueue tq;
-    if (BH_TRAV_QUEUE && e->tq_ctr && !wo.order) {
-        tq.ctr = e->tq_ctr;
-        tq.waves = e->tq_cus * 4u * BH_TRAV_QUEUE_WAVES;
-        tq.loop_waves = e->tq_cus * 4u * BH_TRAV_QUEUE_LOOP;
-    }
     traverse(e->nodes, e->node_cap, e->T_trav, e->st.x, e->st.y, e->m_trav, e->cidx_trav, 0, n,
-             e->geo, fp, e->a2, nullptr, s, &ka, lanes ? e->lanes_trav : nullptr, &wo, &tq);
+             e->geo, fp, e->a2, nullptr, s, &ka, lanes ? e->lanes_trav : nullptr, &wo);
     HIPCHK(e, hipGetLastError());
     TRY(mark(e, 1));
     TRY(wave_order_next(e, 0, n, s));
@@ -1796,8 +1749,7 @@ void bh_destroy(bh_engine *e) {
                     e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->mbits, e->mslot, e->scratch,
                     e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaf_cover, e->leaves.rec,
                     e->leaf_tmp, e->spl, e->bcount, e->bstart, e->nodes_alt, e->wave_cost, e->run_order,
-                    e->m_trav, e->cidx_trav, e->lanes_trav, e->T_trav, e->tq_ctr,
-                    e->solo_xchg};
+                    e->m_trav, e->cidx_trav, e->lanes_trav, e->T_trav, e->solo_xchg};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     for (hipEvent_t ev : e->ev) (void)hipEventDestroy(ev);

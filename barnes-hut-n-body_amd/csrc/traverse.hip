@@ -15,8 +15,6 @@
 // The kernel is bound by fp64 VALU issue (the IEEE sqrt and two IEEE divisions per
 // interaction), not by HBM: the node stream is shared by 64 lanes and served from the
 // scalar cache / L2.  See DESIGN.md for the roofline accounting.
-#include <algorithm>
-
 #include "bh_device.hpp"
 #include "fastmath.hpp"
 
@@ -287,46 +285,6 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
                                   kick, lanes, wo);
 }
 
-// Work-queue form for a traversal that shares the GPU with a chain of other kernels (the
-// pipelined step's merge rule and next build, engine.cpp): the launch holds at most
-// `pa.waves` waves; the first `pa.loop_waves` of them take wave tasks until none is left, the
-// others take one task each and leave, so that once the first generation of tasks is done the
-// chain finds free wave slots on every CU instead of waiting until the last of ~16 K one-wave
-// workgroups has been placed.  Tasks are handed out per XCD in the same runs of
-// BH_TRAV_XCD_RUN waves as xcd_block gives the plain launch (the run r = j * 8 + xcd), from an
-// agent-scope counter per XCD; every wave adds to a done counter when it leaves and the last one
-// clears all nine counters for the next launch.  Each task is exactly one wave of the plain
-// launch: same lanes, same walk, same epilogue.
-template <bool OFF32, int KICK>
-__global__ __launch_bounds__(TB) void k_traverse_q(const Node *__restrict__ nodes,
-                                                   const uint32_t *__restrict__ d_T, double *x,
-                                                   double *y, const double *__restrict__ m,
-                                                   const uint32_t *__restrict__ cidx,
-                                                   int64_t lo, int64_t hi, ForceParams fp,
-                                                   Geometry g, double *__restrict__ a2,
-                                                   KickArgs kick,
-                                                   const uint32_t *__restrict__ lanes,
-                                                   TaskQueue tq) {
-    constexpr uint32_t C = BH_TRAV_XCD_RUN;
-    const uint32_t xcd = blockIdx.x & 7u;  // blocks are dispatched to the XCDs round-robin
-    const uint32_t waves = (uint32_t)((hi - lo + TB - 1) / TB);
-    const bool loops = blockIdx.x < tq.loop_waves;
-    const TraverseCounters none{nullptr, nullptr, nullptr, nullptr};
-    const WaveOrder wo{};
-    while (true) {
-        uint32_t k = 0;
-        if (threadIdx.x == 0) k = atomicAdd(tq.ctr + xcd, 1u);
-        k = __builtin_amdgcn_readfirstlane(k);
-        const uint32_t v = ((k / C) * 8u + xcd) * C + k % C;  // increasing in k: the XCD is done
-        if (v >= waves) break;                                 // at its first task past the end
-        trav_wave<false, OFF32, KICK>(v, 0, nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, none,
-                                      kick, lanes, wo);
-        if (!loops) break;
-    }
-    if (threadIdx.x == 0 && atomicAdd(tq.ctr + 8, 1u) == gridDim.x - 1u)
-        for (int i = 0; i < 9; ++i) atomicExch(tq.ctr + i, 0u);  // the last wave out
-}
-
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
     z += 0x9E3779B97F4A7C15ull;
     z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
@@ -438,33 +396,8 @@ hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_ba
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
               const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, const TraverseCounters *cnt,
-              hipStream_t s, const KickArgs *kick, const uint32_t *lanes, const WaveOrder *wo,
-              const TaskQueue *tq) {
+              hipStream_t s, const KickArgs *kick, const uint32_t *lanes, const WaveOrder *wo) {
     if (hi <= lo) return;
-    // work-queue form: the pipelined step's a(t+dt) (KICK_ONLY) and the LET rounds (owner kicks)
-    if (tq && tq->ctr && !cnt && kick &&
-        (kick->mode == KICK_ONLY || kick->mode == KICK_OWN_DRIFT || kick->mode == KICK_OWN_ONLY)) {
-        const bool off32 = node_cap * sizeof(Node) < (size_t(1) << 32);
-        const uint32_t waves = (uint32_t)((hi - lo + TB - 1) / TB);
-        const unsigned grid = (unsigned)std::min<uint32_t>(waves, tq->waves) & ~7u;
-        if (grid >= 8) {
-#define BH_TRAVQ(O, K) \
-    k_traverse_q<O, K><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, *kick, \
-                                           lanes, *tq)
-            if (kick->mode == KICK_ONLY) {
-                if (off32) BH_TRAVQ(true, KICK_ONLY);
-                else BH_TRAVQ(false, KICK_ONLY);
-            } else if (kick->mode == KICK_OWN_DRIFT) {
-                if (off32) BH_TRAVQ(true, KICK_OWN_DRIFT);
-                else BH_TRAVQ(false, KICK_OWN_DRIFT);
-            } else {
-                if (off32) BH_TRAVQ(true, KICK_OWN_ONLY);
-                else BH_TRAVQ(false, KICK_OWN_ONLY);
-            }
-#undef BH_TRAVQ
-            return;
-        }
-    }
     unsigned grid = (unsigned)((hi - lo + TB - 1) / TB);
     const WaveOrder w = wo && wave_order_runs(hi - lo) ? *wo : WaveOrder{};
     if (w.order)  // whole runs: every run index the order maps to exists in the grid
