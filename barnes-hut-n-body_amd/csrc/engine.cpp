@@ -1576,19 +1576,6 @@ int bh_create(const bh_params *p, int device, bh_engine **out) {
     return BH_OK;
 }
 
-// The all-gathers' stream at the highest priority (BH_COMM_PRIO): their kernels are queued while
-// the next traversal round is being placed and should take the wave slots it frees first.
-#ifndef BH_COMM_PRIO
-#define BH_COMM_PRIO 1
-#endif
-static hipError_t comm_stream_create(hipStream_t *s) {
-    if (!BH_COMM_PRIO) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
-    int lo = 0, hi = 0;
-    hipError_t hr = hipDeviceGetStreamPriorityRange(&lo, &hi);
-    if (hr != hipSuccess) return hr;
-    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, hi);
-}
-
 int bh_comm_unique_id(void *out128) {
     if (!out128) return BH_E_INVALID;
     ncclUniqueId id;
@@ -1615,7 +1602,7 @@ int bh_create_dist(const bh_params *p, int device, int rank, int world, const vo
             e->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(nr);
             rc = BH_E_COMM;
         }
-        hipError_t hr = comm_stream_create(&e->comm_stream);
+        hipError_t hr = hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking);
         for (int k = 0; k < BH_SHARD_ROUNDS && hr == hipSuccess; ++k)
             hr = hipEventCreateWithFlags(&e->round_ev[k], hipEventDisableTiming);
         if (hr == hipSuccess) hr = hipEventCreateWithFlags(&e->gathered_ev, hipEventDisableTiming);
@@ -1661,7 +1648,7 @@ int bh_create_local(const bh_params *p, int device, int rank, bh_local_group *gr
     e->world = group->world;
     int rc = engine_init(e, p, device);
     if (rc == BH_OK) {
-        hipError_t hr = comm_stream_create(&e->comm_stream);
+        hipError_t hr = hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking);
         for (int k = 0; k < BH_SHARD_ROUNDS && hr == hipSuccess; ++k)
             hr = hipEventCreateWithFlags(&e->round_ev[k], hipEventDisableTiming);
         if (hr == hipSuccess) hr = hipEventCreateWithFlags(&e->gathered_ev, hipEventDisableTiming);
@@ -1695,7 +1682,7 @@ int bh_create_solo(const bh_params *p, int device, int rank, int world, bh_engin
     e->world = world;
     int rc = engine_init(e, p, device);
     if (rc == BH_OK) {
-        hipError_t hr = comm_stream_create(&e->comm_stream);
+        hipError_t hr = hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking);
         for (int k = 0; k < BH_SHARD_ROUNDS && hr == hipSuccess; ++k)
             hr = hipEventCreateWithFlags(&e->round_ev[k], hipEventDisableTiming);
         if (hr == hipSuccess) hr = hipEventCreateWithFlags(&e->gathered_ev, hipEventDisableTiming);
