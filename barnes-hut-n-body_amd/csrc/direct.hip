@@ -96,62 +96,51 @@ __device__ __forceinline__ void pair_force(double px, double py, double pm, doub
     fy += f * dy * invR;
 }
 
-// One staged leaf: (x, y, m, slot bits).
+// One staged leaf: (x, y, m, slot bits).  NB bodies per lane (BH_DIRECT_NB): each broadcast
+// record serves NB independent interaction chains.
+#ifndef BH_DIRECT_NB
+#define BH_DIRECT_NB 1
+#endif
+constexpr int NB = BH_DIRECT_NB;
+
 template <bool FAST>
-__device__ __forceinline__ void sum_tile(const double4_t *s_rec, int cnt, double bx, double by,
-                                         double Gm, double soft2, uint32_t self, double &fx,
-                                         double &fy) {
+__device__ __forceinline__ void leaf_terms(const double4_t &r, const double (&bx)[NB],
+                                           const double (&by)[NB], const double (&Gm)[NB],
+                                           double soft2, const uint32_t (&self)[NB],
+                                           double (&fx)[NB], double (&fy)[NB]) {
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        const bool other = (uint32_t)__double_as_longlong(r.w) != self[b];  // BHA:219
+        if (FAST) {
+            // no self-skip at all: the own leaf has dx = dy = +0.0, so its term is an exact
+            // +-0.0 and fx, fy (never -0.0) are unchanged -- valid because the fast path
+            // guarantees a finite f for it (fastmath.hpp, lane_self_ok) and r2 >= soft2 > 0
+            (void)other;
+            pair_force<true>(r.x, r.y, r.z, bx[b], by[b], Gm[b], soft2, fx[b], fy[b]);
+        } else if (other) {
+            pair_force<false>(r.x, r.y, r.z, bx[b], by[b], Gm[b], soft2, fx[b], fy[b]);
+        }
+    }
+}
+
+template <bool FAST>
+__device__ __forceinline__ void sum_tile(const double4_t *s_rec, int cnt, const double (&bx)[NB],
+                                         const double (&by)[NB], const double (&Gm)[NB],
+                                         double soft2, const uint32_t (&self)[NB],
+                                         double (&fx)[NB], double (&fy)[NB]) {
 #ifndef BH_DIRECT_U
 #define BH_DIRECT_U 4
 #endif
-#ifndef BH_DIRECT_PF
-#define BH_DIRECT_PF 0
-#endif
     constexpr int U = BH_DIRECT_U;
     int j = 0;
-#if BH_DIRECT_PF
-    // the next batch's records are read while this batch computes (register double buffer)
-    double4_t nx[U];
-    if (U <= cnt) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) nx[u] = s_rec[u];
-    }
-#endif
     for (; j + U <= cnt; j += U) {
         double4_t r[U];
-#if BH_DIRECT_PF
-#pragma unroll
-        for (int u = 0; u < U; ++u) r[u] = nx[u];
-        if (j + 2 * U <= cnt) {
-#pragma unroll
-            for (int u = 0; u < U; ++u) nx[u] = s_rec[j + U + u];
-        }
-#else
 #pragma unroll
         for (int u = 0; u < U; ++u) r[u] = s_rec[j + u];  // broadcast reads, issued together
-#endif
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const bool other = (uint32_t)__double_as_longlong(r[u].w) != self;  // BHA:219
-            if (FAST) {
-                // no self-skip at all: the own leaf has dx = dy = +0.0, so its term is an exact
-                // +-0.0 and fx, fy (never -0.0) are unchanged -- valid because the fast path
-                // guarantees a finite f for it (fastmath.hpp, lane_self_ok) and r2 >= soft2 > 0
-                (void)other;
-                pair_force<true>(r[u].x, r[u].y, r[u].z, bx, by, Gm, soft2, fx, fy);
-            } else if (other) {
-                pair_force<false>(r[u].x, r[u].y, r[u].z, bx, by, Gm, soft2, fx, fy);
-            }
-        }
+        for (int u = 0; u < U; ++u) leaf_terms<FAST>(r[u], bx, by, Gm, soft2, self, fx, fy);
     }
-    for (; j < cnt; ++j) {
-        const double4_t r = s_rec[j];
-        const bool other = (uint32_t)__double_as_longlong(r.w) != self;
-        if (FAST)
-            pair_force<true>(r.x, r.y, r.z, bx, by, Gm, soft2, fx, fy);
-        else if (other)
-            pair_force<false>(r.x, r.y, r.z, bx, by, Gm, soft2, fx, fy);
-    }
+    for (; j < cnt; ++j) leaf_terms<FAST>(s_rec[j], bx, by, Gm, soft2, self, fx, fy);
 }
 
 __global__ __launch_bounds__(TB) void k_direct(LeafList L, const uint32_t *__restrict__ d_count,
@@ -161,17 +150,26 @@ __global__ __launch_bounds__(TB) void k_direct(LeafList L, const uint32_t *__res
                                                int64_t hi, double G, double soft2,
                                                double *__restrict__ a2) {
     __shared__ double4_t s_rec[TILE];
-    const int64_t p = lo + (int64_t)blockIdx.x * TB + threadIdx.x;
-    const bool valid = p < hi;
-    const double bx = valid ? x[p] : 0.0;
-    const double by = valid ? y[p] : 0.0;
-    const double bm = valid ? m[p] : 1.0;
-    const double Gm = G * bm;  // (Config.G * b.m) first (BHA:256)
-    const uint32_t self = valid ? (uint32_t)p : 0xFFFFFFFFu;
-    const bool fast =
-        __ballot(valid && !(lane_fast_ok(bx, by, soft2) && lane_self_ok(Gm, bm))) == 0ull;
+    int64_t p[NB];
+    bool valid[NB];
+    double bx[NB], by[NB], bm[NB], Gm[NB], fx[NB], fy[NB];
+    uint32_t self[NB];
+    bool slow = false;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        p[b] = lo + ((int64_t)blockIdx.x * NB + b) * TB + threadIdx.x;
+        valid[b] = p[b] < hi;
+        bx[b] = valid[b] ? x[p[b]] : 0.0;
+        by[b] = valid[b] ? y[p[b]] : 0.0;
+        bm[b] = valid[b] ? m[p[b]] : 1.0;
+        Gm[b] = G * bm[b];  // (Config.G * b.m) first (BHA:256)
+        self[b] = valid[b] ? (uint32_t)p[b] : 0xFFFFFFFFu;
+        slow |= valid[b] && !(lane_fast_ok(bx[b], by[b], soft2) && lane_self_ok(Gm[b], bm[b]));
+        fx[b] = 0.0;
+        fy[b] = 0.0;
+    }
+    const bool fast = __ballot(slow) == 0ull;
     const uint32_t nl = *d_count;
-    double fx = 0.0, fy = 0.0;
     for (uint32_t t0 = 0; t0 < nl; t0 += TILE) {
         const int cnt = (int)min((uint32_t)TILE, nl - t0);
         __syncthreads();
@@ -183,11 +181,14 @@ __global__ __launch_bounds__(TB) void k_direct(LeafList L, const uint32_t *__res
         else
             sum_tile<false>(s_rec, cnt, bx, by, Gm, soft2, self, fx, fy);
     }
-    if (!valid) return;
-    double2_t acc;
-    acc.x = fx / bm;  // BHA:390-391
-    acc.y = fy / bm;
-    *reinterpret_cast<double2_t *>(a2 + 2 * p) = acc;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        if (!valid[b]) continue;
+        double2_t acc;
+        acc.x = fx[b] / bm[b];  // BHA:390-391
+        acc.y = fy[b] / bm[b];
+        *reinterpret_cast<double2_t *>(a2 + 2 * p[b]) = acc;
+    }
 }
 
 }  // namespace
@@ -226,8 +227,8 @@ void direct_forces(const LeafList &L, const uint32_t *d_count, const double *x, 
                    const double *m, int64_t lo, int64_t hi, double G, double soft2, double *a2,
                    hipStream_t s) {
     if (hi <= lo) return;
-    k_direct<<<(unsigned)((hi - lo + TB - 1) / TB), TB, 0, s>>>(L, d_count, x, y, m, lo, hi, G,
-                                                              soft2, a2);
+    k_direct<<<(unsigned)((hi - lo + TB * NB - 1) / (TB * NB)), TB, 0, s>>>(L, d_count, x, y, m, lo,
+                                                                          hi, G, soft2, a2);
 }
 
 }  // namespace bh
