@@ -198,12 +198,33 @@ __global__ __launch_bounds__(64) void k_let_flags(LetPieces pc, PosSrc ps,
     }
 }
 
+// also pads subset slots [n_real, S) as dead bodies (sentinel keys: never in the tree, never
+// evaluated) and writes the status: overflow when n_real > S (the build then misses bodies: the
+// call is replayed); the grid covers n >= S threads
 __global__ __launch_bounds__(TB) void k_let_gather(int64_t n, PosSrc ps,
                                                    const uint8_t *__restrict__ flag8,
                                                    const uint32_t *__restrict__ bpos,
-                                                   BodyState st, BodyState sub) {
+                                                   BodyState st, BodyState sub, int64_t S,
+                                                   const uint32_t *__restrict__ count,
+                                                   LetCell *__restrict__ table,
+                                                   uint32_t *__restrict__ scal) {
     __shared__ uint32_t s_w[TB / 64];
     const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    {
+        const int64_t n_real = *count;
+        if (i == 0) {
+            table[LET_CELLS] = LetCell{0.0, 0.0, 0.0, n_real > S ? 1u : 0u, 0u};
+            atomicMax(scal + 5, (uint32_t)n_real);
+        }
+        if (i < S && i >= n_real) {
+            sub.x[i] = 0.0;
+            sub.y[i] = 0.0;
+            sub.vx[i] = __longlong_as_double(-1ll);  // no replicated slot
+            sub.vy[i] = 0.0;
+            sub.m[i] = 0.0;
+            sub.cidx[i] = CIDX_DEAD;
+        }
+    }
     const bool f = i < n && flag8[i];
     const uint64_t m = __ballot(f);
     const uint32_t w = threadIdx.x >> 6;
@@ -223,40 +244,16 @@ __global__ __launch_bounds__(TB) void k_let_gather(int64_t n, PosSrc ps,
     sub.cidx[j] = st.cidx[i];
 }
 
-// subset slots [n_real, S) as dead bodies (sentinel keys: never in the tree, never evaluated);
-// the status: overflow when n_real > S (the build then misses bodies: the call is replayed)
-__global__ __launch_bounds__(TB) void k_let_pad(int64_t S, const uint32_t *__restrict__ count,
-                                                BodyState sub, LetCell *__restrict__ table,
-                                                uint32_t *__restrict__ scal) {
-    const int64_t j = (int64_t)blockIdx.x * TB + threadIdx.x;
-    const int64_t n_real = *count;
-    if (j == 0) {
-        table[LET_CELLS] = LetCell{0.0, 0.0, 0.0, n_real > S ? 1u : 0u, 0u};
-        atomicMax(scal + 5, (uint32_t)n_real);
-    }
-    if (j >= S || j < n_real) return;
-    sub.x[j] = 0.0;
-    sub.y[j] = 0.0;
-    sub.vx[j] = __longlong_as_double(-1ll);  // no replicated slot
-    sub.vy[j] = 0.0;
-    sub.m[j] = 0.0;
-    sub.cidx[j] = CIDX_DEAD;
-}
-
-__global__ void k_let_overflow(int world, const LetCell *__restrict__ tables,
-                               uint32_t *__restrict__ scal) {
-    for (int q = 0; q < world; ++q)
-        if (tables[(int64_t)q * LET_TSTRIDE + LET_CELLS].cnt) scal[4] = 1u;
-}
-
-// a tree larger than its array can only come from a broken invariant: no walk, and the call is
-// replayed (bh_step) instead of reading past the array
-__global__ void k_let_guard(LetBufs L, uint32_t *__restrict__ scal) {
+// a tree larger than its array can only come from a broken invariant: no walk (node count 0), and
+// the call is replayed (bh_step) instead of reading past the array (the writers above check
+// every position against node_cap)
+__device__ __forceinline__ void let_guard(const LetBufs &L, uint32_t *__restrict__ scal) {
     if (L.posc[LET_CELLS] + 1u >= L.node_cap) {
         scal[4] = 1u;
         L.posc[LET_CELLS] = 0u;
     }
 }
+__global__ void k_let_guard(LetBufs L, uint32_t *__restrict__ scal) { let_guard(L, scal); }
 
 // ---- after the subset build ----------------------------------------------------------------
 __global__ __launch_bounds__(TB) void k_let_cells(int64_t n, int J,
@@ -338,9 +335,13 @@ __device__ LetCell let_parent(const LetCell *c, int d, uint32_t i, const Geometr
 static_assert(LET_P == 8, "k_let_top_hi assumes 256 depth-LET_P cells per depth-4 cell");
 __global__ __launch_bounds__(256) void k_let_top_hi(int world, Geometry g,
                                                     const LetCell *__restrict__ tables,
-                                                    LetCell *__restrict__ levels) {
+                                                    LetCell *__restrict__ levels,
+                                                    uint32_t *__restrict__ scal) {
     __shared__ LetCell sh[256];
     const uint32_t b = blockIdx.x, t = threadIdx.x;
+    if (b == 0 && t == 0)  // some rank's subset overflowed: every rank replays the call
+        for (int q = 0; q < world; ++q)
+            if (tables[(int64_t)q * LET_TSTRIDE + LET_CELLS].cnt) scal[4] = 1u;
     {
         const uint32_t c = b * 256u + t;
         LetCell r{0.0, 0.0, 0.0, 0u, 0u};
@@ -562,8 +563,10 @@ __global__ __launch_bounds__(TB) void k_let_copy_blocks(LetBufs L, const Node *_
 
 __global__ __launch_bounds__(TB) void k_let_subpos(int64_t n_sub, int64_t n,
                                                    const double *__restrict__ rep,
-                                                   uint32_t *__restrict__ subpos) {
+                                                   uint32_t *__restrict__ subpos, LetBufs L,
+                                                   uint32_t *__restrict__ scal) {
     const int64_t s = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (s == 0) let_guard(L, scal);  // before k_let_lanes reads scal[4]
     if (s >= n_sub) return;
     const int64_t i = (int64_t)__double_as_longlong(rep[s]);
     if (i >= 0 && i < n) subpos[i] = (uint32_t)s;
@@ -715,8 +718,8 @@ hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
     e = rocprim::exclusive_scan(L.scratch, bytes, L.sel, L.selpos, 0u, (size_t)(nb + 1),
                                 rocprim::plus<uint32_t>(), s);
     if (e != hipSuccess) return e;
-    k_let_gather<<<(unsigned)nb, TB, 0, s>>>(pc.n, ps, L.flag8, L.selpos, st, sub);
-    k_let_pad<<<grid_for(S > 0 ? S : 1), TB, 0, s>>>(S, L.selpos + nb, sub, L.table, scal);
+    k_let_gather<<<(unsigned)nb, TB, 0, s>>>(pc.n, ps, L.flag8, L.selpos, st, sub, S,
+                                             L.selpos + nb, L.table, scal);
     return hipGetLastError();
 }
 
@@ -729,8 +732,7 @@ hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const T
 
 hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, const LetBufs &L,
                         const TreeBuffers &tb, uint32_t *scal, hipStream_t s) {
-    k_let_overflow<<<1, 1, 0, s>>>(pc.world, L.tables, scal);
-    k_let_top_hi<<<256, 256, 0, s>>>(pc.world, g, L.tables, L.levels);
+    k_let_top_hi<<<256, 256, 0, s>>>(pc.world, g, L.tables, L.levels, scal);
     k_let_top_lo<<<1, 256, 0, s>>>(g, L.levels);
     k_let_w<<<grid_for(LET_CELLS + 1), TB, 0, s>>>(L, tb, scal);
     size_t bytes = L.scratch_bytes;
@@ -742,10 +744,12 @@ hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, c
                                 rocprim::plus<uint32_t>(), s);
     if (e != hipSuccess) return e;
     k_let_write_top<<<grid_for(level_off(LET_P)), TB, 0, s>>>(L);
-    k_let_guard<<<1, 1, 0, s>>>(L, scal);
     k_let_write_cells<<<grid_for(LET_CELLS), TB, 0, s>>>(L);
     k_let_copy_blocks<<<BH_LET_COPY_GRID, TB, 0, s>>>(L, tb.nodes);
-    if (n_sub > 0) k_let_subpos<<<grid_for(n_sub), TB, 0, s>>>(n_sub, pc.n, tb.dst.vx, L.subpos);
+    if (n_sub > 0)
+        k_let_subpos<<<grid_for(n_sub), TB, 0, s>>>(n_sub, pc.n, tb.dst.vx, L.subpos, L, scal);
+    else
+        k_let_guard<<<1, 1, 0, s>>>(L, scal);
     const int64_t own_lanes = (int64_t)pc.rounds * pc.sub;
     if (own_lanes > 0 && pc.n > 0)
         k_let_lanes<<<grid_for(own_lanes), TB, 0, s>>>(pc, (uint32_t)n_sub, L.subpos, scal,
