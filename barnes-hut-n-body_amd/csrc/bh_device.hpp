@@ -143,6 +143,107 @@ __device__ __forceinline__ uint32_t xcd_block() {
     }
     return b;
 }
+
+// Morton key of one body (BHA:126,153-154): the depth-J cell by exact grid-line compares, the
+// sentinel for a body outside the root or merged away (k_morton, the fused traversal epilogue).
+__device__ __forceinline__ uint64_t morton_key(const Geometry &g, double px, double py, bool dead) {
+    const double cx = g.root_cx, cy = g.root_cy, h = g.root_h;
+    if (!(px >= cx - h && px < cx + h && py >= cy - h && py < cy + h) || dead)
+        return sentinel_key(g.J);  // BHA:126 -- not inserted (or merged away this call)
+    // The descent (BHA:153-154 at every depth: digit = p >= cell centre) ends in the depth-J
+    // cell [x0 + i w, x0 + (i + 1) w) that holds p: every centre it compares against is a grid
+    // line x0 + k w, exact in binary64 (dyadic, < 40 significant bits), and p stays in the
+    // current cell, so i = floor((p - x0) / w) in exact arithmetic.  It is taken from the
+    // rounded quotient (off by at most one near a line) and settled by two exact compares
+    // against the grid lines, the same compares the descent makes.
+    const double w = 2.0 * g.h[g.J];
+    const double x0 = cx - h, y0 = cy - h;
+    const int64_t top = ((int64_t)1 << g.J) - 1;
+    auto cell = [&](double p, double o) __attribute__((always_inline)) {
+        int64_t c = (int64_t)((p - o) * (1.0 / w));
+        c = c < 0 ? 0 : (c > top ? top : c);
+        if (p < o + (double)c * w) --c;
+        else if (c < top && p >= o + (double)(c + 1) * w) ++c;
+        return (uint64_t)c;
+    };
+    auto spread = [](uint64_t v) __attribute__((always_inline)) {  // bit k -> bit 2k
+        v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
+        v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
+        v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
+        v = (v | (v << 2)) & 0x3333333333333333ull;
+        return (v | (v << 1)) & 0x5555555555555555ull;
+    };
+    return spread(cell(px, x0)) | (spread(cell(py, y0)) << 1);  // digit = ix | iy << 1
+}
+
+__device__ __forceinline__ bool spl_le(const uint64_t *__restrict__ spl, uint32_t t, uint64_t v) {
+    return t == 0 || spl[t] <= v;  // spl[0] acts as -infinity: bucket 0 takes everything below
+}
+
+// largest t in [0, nb) with spl[t] <= v, galloping from `guess`
+__device__ inline uint32_t find_bucket(const uint64_t *__restrict__ spl, uint32_t nb, uint64_t v,
+                                       uint32_t guess) {
+    uint32_t t = min(guess, nb - 1);
+    uint32_t lo, hi;  // spl_le(lo) holds; hi == nb or !spl_le(hi)
+    if (spl_le(spl, t, v)) {
+        lo = t;
+        uint32_t step = 1;
+        for (;;) {
+            const uint32_t j = lo + step;
+            if (j >= nb) {
+                hi = nb;
+                break;
+            }
+            if (!spl_le(spl, j, v)) {
+                hi = j;
+                break;
+            }
+            lo = j;
+            step <<= 1;
+        }
+    } else {  // t > 0
+        hi = t;
+        uint32_t step = 1;
+        for (;;) {
+            if (step >= hi) {
+                lo = 0;
+                break;
+            }
+            const uint32_t j = hi - step;
+            if (spl_le(spl, j, v)) {
+                lo = j;
+                break;
+            }
+            hi = j;
+            step <<= 1;
+        }
+    }
+    while (hi - lo > 1) {
+        const uint32_t mid = lo + ((hi - lo) >> 1);
+        if (spl_le(spl, mid, v)) lo = mid; else hi = mid;
+    }
+    return lo;
+}
+
+// One atomic per distinct bucket among the wave's active lanes: the lane's offset inside bucket b
+// (any order inside a bucket: each bucket is sorted whole by (key32, slot) afterwards).
+__device__ __forceinline__ uint32_t bucket_offset(uint32_t b, uint32_t *__restrict__ counts) {
+    uint64_t todo = __ballot(1);
+    uint32_t myoff = 0;
+    while (todo) {
+        const int leader = __builtin_ctzll(todo);
+        const uint32_t bl = __builtin_amdgcn_readlane(b, leader);
+        const uint64_t same = __ballot(b == bl);
+        uint32_t o = 0;
+        if ((int)__lane_id() == leader) o = atomicAdd(&counts[bl], (uint32_t)__popcll(same));
+        o = __builtin_amdgcn_readlane(o, leader);
+        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(same >> 32),
+                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)same, 0u));
+        if (b == bl) myoff = o + below;
+        todo &= ~same;
+    }
+    return myoff;
+}
 #endif
 
 // ---- launchers (tree_build.hip) --------------------------------------------------
@@ -169,6 +270,7 @@ struct TreeBuffers {
     uint64_t *spl;
     uint32_t spl_nb;
     uint32_t *bcount, *bstart;
+    bool keys_ready = false;  // keys, keys32 and the bucket counts were written by the traversal
 };
 
 int cell_table_depth(int J, int64_t n);
@@ -196,11 +298,22 @@ hipError_t lane_order(const TreeBuffers &b, int64_t n, int J, bool refresh, uint
 enum KickMode {
     KICK_NONE = 0, KICK_DRIFT = 1, KICK_ONLY = 2, KICK_OWN_DRIFT = 3, KICK_OWN_ONLY = 4
 };
+// The next build's first two passes done by the drifting traversal (KICK_DRIFT of the pipelined
+// one-GPU step): every lane writes its body's Morton key (k_morton) and bucket / in-bucket offset
+// of the adaptive sort (k_bucket_count) right after the drift; the build then starts at the scan.
+struct MortonFuse {
+    uint64_t *keys = nullptr;  // null: off
+    uint32_t *keys32 = nullptr;
+    const uint64_t *spl = nullptr;  // the previous build's splitters (spl_nb > 0)
+    uint32_t spl_nb = 0;
+    uint32_t *bkt = nullptr, *off = nullptr, *counts = nullptr;
+};
 struct KickArgs {
     KickMode mode;
     double *vx, *vy;  // x, y are the traversal's own position arrays (KICK_OWN_*: replicated v)
     double dtHalf, dt;
     const uint32_t *rep = nullptr;  // KICK_OWN_*: lane -> replicated slot (null: the lane)
+    MortonFuse mf{};
 };
 // Diagnostic counters of the counting walk (all per evaluation): per body, the non-empty
 // nodes visited (BHA:216 passed) and the point-force contributions (accepted internal nodes

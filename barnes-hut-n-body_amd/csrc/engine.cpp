@@ -200,6 +200,8 @@ struct bh_engine {
     uint32_t *cidx_trav = nullptr, *lanes_trav = nullptr, *T_trav = nullptr;
     int64_t trav_cap = 0;
     bool prebuilt = false;  // the current step's first build was made by the previous step
+    bool fuse_keys = false;   // the next KICK_DRIFT traversal writes the next build's keys / buckets
+    bool keys_ready = false;  // ... and it did: the next full build skips k_morton, k_bucket_count
     hipEvent_t pipe_ev[2] = {nullptr, nullptr};
     hipStream_t pipe_stream = nullptr;  // the overlapped work's stream (BH_PIPE_PRIORITY)
     // one GPU: the previous evaluation's wave durations and the longest-first run order
@@ -368,6 +370,7 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(dev_alloc(e, e->bstart, (size_t)sort_buckets(cap) + 2));
         HIPCHK(e, hipMemset(e->bcount, 0, sizeof(uint32_t) * ((size_t)sort_buckets(cap) + 2)));
         e->spl_nb = 0;
+        e->keys_ready = false;
         e->cap = cap;
     }
     size_t ncap = node_capacity(e->cap, J);
@@ -468,6 +471,12 @@ int collect_timings(bh_engine *e) {
     return BH_OK;
 }
 
+// The pipelined step's first traversal also computes the second build's Morton keys and
+// bucket counts (KICK_DRIFT epilogue, bh_device.hpp MortonFuse).
+#ifndef BH_FUSE_KEYS
+#define BH_FUSE_KEYS 1
+#endif
+
 // ---- buildTree() (BHA:359-366): sort + build; the state moves to the new Morton order ----
 #ifndef BH_LANE_REFRESH
 #define BH_LANE_REFRESH 16  // builds between Hilbert re-sorts of the lane map (0: Morton lanes)
@@ -486,6 +495,8 @@ int build_into(bh_engine *e, hipStream_t s, bool overlap) {
     const bool use_lanes = BH_LANE_REFRESH > 0 && n > 0 && e->p.theta != 0.0;
     const bool refresh = use_lanes && (!e->lanes_valid || e->lanes_age >= BH_LANE_REFRESH);
     tb.lanes_remap = use_lanes && !refresh ? e->lanes : nullptr;
+    tb.keys_ready = e->keys_ready && !overlap;
+    e->keys_ready = false;
     HIPCHK(e, tree_build(tb, n, e->geo, s));
     ++e->full_builds;
     e->inv_valid = false;  // the map follows this build's permutation
@@ -980,7 +991,13 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
     };
     if ((!e->comm && !e->group && !e->solo) || visits) {
         if (BH_FUSE_KICK && kick != KICK_NONE && !direct && !visits && fused) {
-            const KickArgs ka{kick, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
+            KickArgs ka{kick, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
+            if (BH_FUSE_KEYS && e->fuse_keys && kick == KICK_DRIFT && e->spl_nb > 0 && n > 0) {
+                ka.mf = MortonFuse{e->keys, e->keys32, e->spl, e->spl_nb, e->cnt, e->base,
+                                   e->bcount};
+                e->keys_ready = true;
+            }
+            e->fuse_keys = false;
             WaveOrder wo;
             TRY(wave_order_for(e, 0, n, e->stream, wo));
             traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, e->st.cidx, 0, n, e->geo, fp,
@@ -1179,6 +1196,7 @@ int restore(bh_engine *e) {
     TRY(copy_state(e, e->snap, e->st, e->snap_n));
     e->n = e->snap_n;
     e->spl_nb = 0;  // the splitters describe the discarded builds' order
+    e->keys_ready = false;
     e->lanes_valid = false;
     e->inv_valid = false;
     e->pos_pending = false;  // the snapshot holds every position
@@ -1320,6 +1338,7 @@ int step_once(bh_engine *e, bool last) {
     if (pipelined(e, last)) {
         TRY(pipe_alloc(e));
         bool fused = false;
+        e->fuse_keys = true;  // and the second build's keys and bucket counts
         TRY(evaluate(e, nullptr, KICK_DRIFT, &fused, true));  // a(t), kick + drift fused
         if (!fused) {
             e->err = "pipelined step: the first evaluation did not fuse its kick";
@@ -1774,6 +1793,7 @@ int bh_set_params(bh_engine *e, const bh_params *p) {
         e->geo = g;
         e->tree_valid = false;
         e->spl_nb = 0;  // keys change meaning
+        e->keys_ready = false;
         e->lanes_valid = false;
         e->inv_valid = false;
         if (g.J != e->J_alloc) {  // tree workspace sized for another depth; the state stays
@@ -1815,6 +1835,7 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     e->removed.clear();
     e->tree_valid = false;  // BHA:348
     e->spl_nb = 0;          // other bodies: the first build sorts from scratch
+    e->keys_ready = false;
     e->lanes_valid = false;
     e->st_morton = false;
     e->vel_stale = false;

@@ -253,8 +253,20 @@ __device__ __forceinline__ void trav_wave(uint32_t v, uint64_t t_start,
         kick.vx[p] = vxi;
         kick.vy[p] = vyi;
         if (KICK == KICK_DRIFT) {
-            x[p] = bx + vxi * kick.dt;
-            y[p] = by + vyi * kick.dt;
+            const double nx = bx + vxi * kick.dt, ny = by + vyi * kick.dt;
+            x[p] = nx;
+            y[p] = ny;
+            if (kick.mf.keys) {  // the next build's k_morton and k_bucket_count for this body
+                const uint64_t key = morton_key(g, nx, ny, (cidx[p] & CIDX_DEAD) != 0u);
+                const uint32_t k32 = (uint32_t)(key >> key32_shift(g.J));
+                kick.mf.keys[p] = key;
+                kick.mf.keys32[p] = k32;
+                const uint32_t b = find_bucket(kick.mf.spl, kick.mf.spl_nb,
+                                               ((uint64_t)k32 << 32) | (uint64_t)p,
+                                               (uint32_t)(p / SORT_B));
+                kick.mf.bkt[p] = b;
+                kick.mf.off[p] = bucket_offset(b, kick.mf.counts);
+            }
         }
     }
     if (COUNT) {

@@ -64,37 +64,7 @@ __global__ __launch_bounds__(TB) void k_morton(int64_t n, const double *__restri
     chain_prio();
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i >= n) return;
-    double px = x[i], py = y[i];
-    double cx = g.root_cx, cy = g.root_cy;
-    uint64_t key;
-    if (!quad_contains(cx, cy, g.root_h, px, py) || (cidx[i] & CIDX_DEAD)) {
-        key = sentinel_key(g.J);  // BHA:126 — not inserted (or merged away this call)
-    } else {
-        // The descent (BHA:153-154 at every depth: digit = p >= cell centre) ends in the depth-J
-        // cell [x0 + i w, x0 + (i + 1) w) that holds p: every centre it compares against is a
-        // grid line x0 + k w, exact in binary64 (dyadic, < 40 significant bits), and p stays in
-        // the current cell, so i = floor((p - x0) / w) in exact arithmetic.  It is taken from
-        // the rounded quotient (off by at most one near a line) and settled by two exact
-        // compares against the grid lines, the same compares the descent makes.
-        const double w = 2.0 * g.h[g.J];
-        const double x0 = cx - g.root_h, y0 = cy - g.root_h;
-        const int64_t top = ((int64_t)1 << g.J) - 1;
-        auto cell = [&](double p, double o) __attribute__((always_inline)) {
-            int64_t c = (int64_t)((p - o) * (1.0 / w));
-            c = c < 0 ? 0 : (c > top ? top : c);
-            if (p < o + (double)c * w) --c;
-            else if (c < top && p >= o + (double)(c + 1) * w) ++c;
-            return (uint64_t)c;
-        };
-        auto spread = [](uint64_t v) __attribute__((always_inline)) {  // bit k -> bit 2k
-            v = (v | (v << 16)) & 0x0000FFFF0000FFFFull;
-            v = (v | (v << 8)) & 0x00FF00FF00FF00FFull;
-            v = (v | (v << 4)) & 0x0F0F0F0F0F0F0F0Full;
-            v = (v | (v << 2)) & 0x3333333333333333ull;
-            return (v | (v << 1)) & 0x5555555555555555ull;
-        };
-        key = spread(cell(px, x0)) | (spread(cell(py, y0)) << 1);  // digit = ix | iy << 1
-    }
+    const uint64_t key = morton_key(g, x[i], y[i], (cidx[i] & CIDX_DEAD) != 0u);
     keys[i] = key;
     keys32[i] = (uint32_t)(key >> key32_shift(g.J));  // the sort key: top 32 of 2J+1 bits
     if (idx) idx[i] = (uint32_t)i;  // rocprim path only (the bucket sort uses the slot itself)
@@ -120,55 +90,6 @@ __global__ __launch_bounds__(TB) void k_morton(int64_t n, const double *__restri
 constexpr int SORT_TB = 256;
 constexpr int SORT_CAP = 4096;  // LDS bucket capacity (32 KB of composites)
 
-__device__ __forceinline__ bool spl_le(const uint64_t *__restrict__ spl, uint32_t t, uint64_t v) {
-    return t == 0 || spl[t] <= v;  // spl[0] acts as -infinity: bucket 0 takes everything below
-}
-
-// largest t in [0, nb) with spl[t] <= v, galloping from `guess`
-__device__ uint32_t find_bucket(const uint64_t *__restrict__ spl, uint32_t nb, uint64_t v,
-                                uint32_t guess) {
-    uint32_t t = min(guess, nb - 1);
-    uint32_t lo, hi;  // spl_le(lo) holds; hi == nb or !spl_le(hi)
-    if (spl_le(spl, t, v)) {
-        lo = t;
-        uint32_t step = 1;
-        for (;;) {
-            const uint32_t j = lo + step;
-            if (j >= nb) {
-                hi = nb;
-                break;
-            }
-            if (!spl_le(spl, j, v)) {
-                hi = j;
-                break;
-            }
-            lo = j;
-            step <<= 1;
-        }
-    } else {  // t > 0
-        hi = t;
-        uint32_t step = 1;
-        for (;;) {
-            if (step >= hi) {
-                lo = 0;
-                break;
-            }
-            const uint32_t j = hi - step;
-            if (spl_le(spl, j, v)) {
-                lo = j;
-                break;
-            }
-            hi = j;
-            step <<= 1;
-        }
-    }
-    while (hi - lo > 1) {
-        const uint32_t mid = lo + ((hi - lo) >> 1);
-        if (spl_le(spl, mid, v)) lo = mid; else hi = mid;
-    }
-    return lo;
-}
-
 __global__ __launch_bounds__(SORT_TB) void k_bucket_count(int64_t n,
                                                           const uint32_t *__restrict__ keys32,
                                                           const uint64_t *__restrict__ spl,
@@ -191,24 +112,10 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_count(int64_t n,
         else b = find_bucket(spl, nb, v, (uint32_t)(i / SORT_B));
     }
     // one atomic per distinct bucket of the wave (usually one): offsets in lane order
-    uint64_t todo = __ballot(valid);
-    uint32_t myoff = 0;
-    while (todo) {
-        const int leader = __builtin_ctzll(todo);
-        const uint32_t bl = __builtin_amdgcn_readlane(b, leader);
-        const uint64_t same = __ballot(valid && b == bl);
-        uint32_t o = 0;
-        if ((int)__lane_id() == leader) o = atomicAdd(&counts[bl], (uint32_t)__popcll(same));
-        o = __builtin_amdgcn_readlane(o, leader);
-        const uint32_t below = __builtin_amdgcn_mbcnt_hi((uint32_t)(same >> 32),
-                                                         __builtin_amdgcn_mbcnt_lo((uint32_t)same, 0u));
-        if (valid && b == bl) myoff = o + below;
-        todo &= ~same;
-    }
-    if (valid) {
-        bkt[i] = b;
-        off[i] = myoff;
-    }
+    if (!valid) return;
+    const uint32_t myoff = bucket_offset(b, counts);
+    bkt[i] = b;
+    off[i] = myoff;
 }
 
 __global__ __launch_bounds__(SORT_TB) void k_bucket_scatter(int64_t n,
@@ -1550,13 +1457,16 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     hipError_t st;
     const int D0 = cell_table_depth(g.J, n);
     const bool bucket = b.spl_nb > 0;
-    k_morton<<<grid_for(n), TB, 0, s>>>(n, b.src.x, b.src.y, b.src.cidx, g, b.keys, b.keys32,
-                                        bucket ? nullptr : b.idx);
+    const bool ready = bucket && b.keys_ready;  // the drifting traversal did both passes
+    if (!ready)
+        k_morton<<<grid_for(n), TB, 0, s>>>(n, b.src.x, b.src.y, b.src.cidx, g, b.keys, b.keys32,
+                                            bucket ? nullptr : b.idx);
     size_t bytes = b.scratch_bytes;
     if (bucket) {  // bucket ids / offsets live in cnt / base until k_prep needs them
         const unsigned sg = (unsigned)((n + SORT_TB - 1) / SORT_TB);
-        k_bucket_count<<<sg, SORT_TB, 0, s>>>(n, b.keys32, b.spl, b.spl_nb, b.cnt, b.base,
-                                              b.bcount);
+        if (!ready)
+            k_bucket_count<<<sg, SORT_TB, 0, s>>>(n, b.keys32, b.spl, b.spl_nb, b.cnt, b.base,
+                                                  b.bcount);
         st = rocprim::exclusive_scan(b.scratch, bytes, b.bcount, b.bstart, 0u,
                                      (size_t)b.spl_nb + 1, rocprim::plus<uint32_t>(), s);
         if (st != hipSuccess) return st;
