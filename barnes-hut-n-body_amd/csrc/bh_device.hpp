@@ -519,6 +519,8 @@ size_t compact_scratch_bytes(int64_t n);
 hipError_t compact_lanes(int64_t n, const uint32_t *lanes, const uint32_t *keep,
                          const uint32_t *pos, uint32_t *flag, uint32_t *qpos, uint32_t *out,
                          void *tmp, size_t tmp_bytes, hipStream_t s);
+void compact_pair(int64_t n, const uint32_t *keep, const uint32_t *pos, const double *sx,
+                  const double *sy, double *dx, double *dy, hipStream_t s);
 hipError_t compact_state(int64_t n, uint32_t *keep, const BodyState &src, const BodyState &dst,
                          const uint32_t *dead_cidx, uint32_t n_dead, uint32_t *pos, void *tmp,
                          size_t tmp_bytes, hipStream_t s);

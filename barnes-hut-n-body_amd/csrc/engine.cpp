@@ -152,6 +152,11 @@ struct bh_engine {
     int64_t leaf_cap = 0;
 
     bool tree_valid = false;  // lastTree (BHA:304): keys_s / cpl / base / nodes are current
+    // Multi-rank engines end a call with a LET build too; lastTree is then built on demand by
+    // bh_get_quads from the positions that build saw (lt_x, lt_y), without touching the state
+    bool lazy_tree = false;
+    double *lt_x = nullptr, *lt_y = nullptr;
+    int64_t lt_cap = 0;
 
     // Hilbert lane map of the single-GPU traversal (tree_build.hip lane_order): lane -> slot
     uint32_t *lanes = nullptr;
@@ -1161,7 +1166,15 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
     // BHA:526: lastTree = null only when the last step's merge rule removed a body.  Bodies
     // removed by earlier steps were tombstones in the last build (sentinel keys: the tail of its
     // order), so its first n - nd sorted keys still describe the whole tree.
-    if (nd != nd_before_last) e->tree_valid = false;
+    if (nd != nd_before_last) {
+        e->tree_valid = false;
+        e->lazy_tree = false;
+    } else if (e->lazy_tree) {  // the snapshot follows the compaction (its tombstones were not built)
+        compact_pair(n, e->keep, e->pos, e->lt_x, e->lt_y, e->alt.x, e->alt.y, e->stream);
+        HIPCHK(e, hipGetLastError());
+        std::swap(e->lt_x, e->alt.x);
+        std::swap(e->lt_y, e->alt.y);
+    }
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return BH_OK;
 }
@@ -1329,6 +1342,28 @@ int evaluate_pipelined(bh_engine *e) {
     return BH_OK;
 }
 
+#ifndef BH_LAZY_LASTTREE
+#define BH_LAZY_LASTTREE 1
+#endif
+// The positions the call's last build starts from (its jitter moves some of them): kept for the
+// lazy lastTree of bh_get_quads (16 B per body, device copies).
+int snapshot_positions(bh_engine *e) {
+    const int64_t n = e->n;
+    TRY(materialize_positions(e));
+    if (e->lt_cap < e->cap) {
+        TRY(dev_alloc(e, e->lt_x, (size_t)e->cap));
+        TRY(dev_alloc(e, e->lt_y, (size_t)e->cap));
+        e->lt_cap = e->cap;
+    }
+    if (n > 0) {
+        HIPCHK(e, hipMemcpyAsync(e->lt_x, e->st.x, sizeof(double) * n, hipMemcpyDeviceToDevice,
+                                 e->stream));
+        HIPCHK(e, hipMemcpyAsync(e->lt_y, e->st.y, sizeof(double) * n, hipMemcpyDeviceToDevice,
+                                 e->stream));
+    }
+    return BH_OK;
+}
+
 // ---- one PhysicsEngine.step() (BHA:405-439) ------------------------------------------
 // last: the final step of a bh_step call -- its second build is the full tree (lastTree,
 // BHA:435, for getTreeForDebug) also on a multi-rank engine that shards its builds.
@@ -1359,14 +1394,21 @@ int step_once(bh_engine *e, bool last) {
             HIPCHK(e, hipGetLastError());
             TRY(mark(e, 2));
         }
-        TRY(evaluate(e, nullptr, KICK_ONLY, &fused, !last));  // a(t+dt)
+        // the call's last build: a full tree for getTreeForDebug (lastTree, BHA:435) -- or, on a
+        // multi-rank engine, a LET build like the others, its input positions kept for a lazy
+        // full build in bh_get_quads
+        const bool lazy = last && BH_LAZY_LASTTREE && (e->comm || e->group || e->solo);
+        if (lazy) TRY(snapshot_positions(e));
+        bool let2 = false;
+        TRY(evaluate(e, nullptr, KICK_ONLY, &fused, !last || lazy, &let2));  // a(t+dt)
         if (!fused) {
             TRY(mark(e, -1));
             kick(n, e->a2, e->st.vx, e->st.vy, dtHalf, e->stream, e->a2_lanes, e->a2_layout);
             HIPCHK(e, hipGetLastError());
             TRY(mark(e, 2));
         }
-        e->tree_valid = true;  // lastTree = root (BHA:435)
+        e->tree_valid = !let2;  // lastTree = root (BHA:435)
+        e->lazy_tree = lazy && let2;
     }
     if (last)  // the call's removal count before its last merge rule (finish_merges, BHA:526)
         HIPCHK(e, hipMemcpyAsync(e->scalars + 8, e->scalars + 2, sizeof(uint32_t),
@@ -1768,7 +1810,8 @@ void bh_destroy(bh_engine *e) {
                     e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->mbits, e->mslot, e->scratch,
                     e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaf_cover, e->leaves.rec,
                     e->leaf_tmp, e->spl, e->bcount, e->bstart, e->nodes_alt, e->wave_cost, e->run_order,
-                    e->m_trav, e->cidx_trav, e->lanes_trav, e->T_trav, e->solo_xchg};
+                    e->m_trav, e->cidx_trav, e->lanes_trav, e->T_trav, e->solo_xchg,
+                    e->lt_x, e->lt_y};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     for (hipEvent_t ev : e->ev) (void)hipEventDestroy(ev);
@@ -1792,6 +1835,7 @@ int bh_set_params(bh_engine *e, const bh_params *p) {
         TRY(materialize_positions(e));
         e->geo = g;
         e->tree_valid = false;
+        e->lazy_tree = false;
         e->spl_nb = 0;  // keys change meaning
         e->keys_ready = false;
         e->lanes_valid = false;
@@ -1834,6 +1878,7 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     e->heavy_possible = true;
     e->removed.clear();
     e->tree_valid = false;  // BHA:348
+    e->lazy_tree = false;
     e->spl_nb = 0;          // other bodies: the first build sorts from scratch
     e->keys_ready = false;
     e->lanes_valid = false;
@@ -1863,6 +1908,7 @@ int bh_step(bh_engine *e, int32_t k) {
         e->removed.clear();
         e->merge_ran = false;
         e->prebuilt = false;
+        e->lazy_tree = false;
         for (int32_t s = 0; s < k; ++s) TRY(step_once(e, s + 1 == k));
         HIPCHK(e, hipStreamSynchronize(e->stream));
         if (may_let) {  // LET subset sizes of this call: [4] some rank overflowed, [5] largest
@@ -1886,6 +1932,13 @@ int bh_step(bh_engine *e, int32_t k) {
                 TRY(restore(e));
                 continue;
             }
+        }
+        // every replica complete at the API boundary: after a call that ended with a LET
+        // evaluation the positions are in the exchange buffer and the peers' velocities with
+        // their owners (every rank runs this: the velocity all-gather is collective)
+        if (e->vel_stale && k > 0) {
+            TRY(materialize_positions(e));
+            TRY(sync_velocities(e));
         }
         // the merge bookkeeping first, so that an error below leaves a compacted state
         const int tree_rc = (e->n > 0 && k > 0) ? check_tree_flags(e) : BH_OK;
@@ -1986,7 +2039,28 @@ int bh_get_quads(bh_engine *e, double *cx, double *cy, double *h, int64_t cap, i
     HIPCHK(e, hipSetDevice(e->device));
     const int64_t n = e->n;
     TRY(materialize_positions(e));
-    if (!e->tree_valid) {  // getTreeForDebug builds a fresh tree (BHA:329-332)
+    if (!e->tree_valid && (e->comm || e->group || e->solo)) {
+        // multi-rank: the tree is built into the workspace from the positions of the call's last
+        // build (the lazy lastTree) or the current ones (getTreeForDebug's fresh tree), and the
+        // state stays as it is -- a rank's slot order and lane map must not change on its own
+        HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
+        if (n > 0) {
+            TreeBuffers tb = tree_buffers(e);
+            if (e->lazy_tree) {
+                tb.src.x = e->lt_x;
+                tb.src.y = e->lt_y;
+            }
+            tb.src.vx = tb.src.vy = nullptr;  // positions, masses and flags are all it reads
+            tb.spl_nb = 0;                    // the caller's splitters describe another order
+            tb.lanes_remap = nullptr;
+            HIPCHK(e, tree_build(tb, n, e->geo, e->stream));
+            e->spl_nb = 0;  // k_prep wrote splitters of this order
+            e->keys_ready = false;
+            TRY(check_tree_flags(e));
+        } else {
+            HIPCHK(e, hipMemsetAsync(e->base, 0, sizeof(uint32_t), e->stream));
+        }
+    } else if (!e->tree_valid) {  // getTreeForDebug builds a fresh tree (BHA:329-332)
         HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
         TRY(build(e));
         if (n > 0) TRY(check_tree_flags(e));

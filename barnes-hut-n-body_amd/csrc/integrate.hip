@@ -508,6 +508,18 @@ __global__ __launch_bounds__(TB) void k_keep(int64_t n, const uint32_t *__restri
 }
 
 // compaction (BHA:519 removeAt), order preserved; list indices shift past removed ones
+// The same compaction for two extra arrays (the lazy lastTree's position snapshot).
+__global__ __launch_bounds__(TB) void k_compact_pair(int64_t n, const uint32_t *__restrict__ keep,
+                                                     const uint32_t *__restrict__ pos,
+                                                     const double *__restrict__ sx,
+                                                     const double *__restrict__ sy,
+                                                     double *__restrict__ dx,
+                                                     double *__restrict__ dy) {
+    const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= n || !keep[i]) return;
+    dx[pos[i]] = sx[i];
+    dy[pos[i]] = sy[i];
+}
 __global__ __launch_bounds__(TB) void k_compact(int64_t n, const uint32_t *__restrict__ keep,
                                                 const uint32_t *__restrict__ pos, BodyState src,
                                                 BodyState dst, const uint32_t *__restrict__ dead_cidx,
@@ -622,6 +634,11 @@ size_t compact_scratch_bytes(int64_t n) {
     (void)rocprim::exclusive_scan(nullptr, b, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u,
                                   (size_t)n, rocprim::plus<uint32_t>());
     return b;
+}
+
+void compact_pair(int64_t n, const uint32_t *keep, const uint32_t *pos, const double *sx,
+                  const double *sy, double *dx, double *dy, hipStream_t s) {
+    if (n > 0) k_compact_pair<<<grid_for(n), TB, 0, s>>>(n, keep, pos, sx, sy, dx, dy);
 }
 
 hipError_t compact_state(int64_t n, uint32_t *keep, const BodyState &src, const BodyState &dst,

@@ -68,9 +68,11 @@ int bh_create(const bh_params *p, int device, bh_engine **out);
  *     positions -- 16 B per body -- are all-gathered over RCCL in BH_SHARD_ROUNDS rounds into
  *     every replica; velocities stay with their owners and are all-gathered before the next
  *     full build; or
- *   - builds the full tree (the first build after a reset, every 32 builds, the last build of a
- *     bh_step call): it evaluates its range and the accelerations are all-gathered, after which
- *     every rank integrates every body.
+ *   - builds the full tree (the first build after a reset, every 32 builds): it evaluates its
+ *     range and the accelerations are all-gathered, after which every rank integrates every body.
+ * At the end of every bh_step call the positions and velocities are complete on every rank
+ * (velocities all-gathered if the call ended with a LET build); bh_get_quads then builds the
+ * last build's full tree on demand (lastTree) without changing the rank's state.
  * The merge rule is replicated (identical inputs).  world == 1 with a non-NULL id runs the same
  * RCCL path on one rank (used to test it on one GPU).  BH_LET and BH_ROUND_FRACS must be equal
  * on every rank (checked at creation: BH_E_INVALID on every rank otherwise). */

@@ -674,12 +674,14 @@ def test_multi_rank_decomposition_in_process(world):
         ref.close()
 
 
-def _run_group(world, params, arrs, calls):
-    """Every rank of an in-process group: reset, then bh_step(k) for k in calls; states."""
+def _run_group(world, params, arrs, calls, quads=None):
+    """Every rank of an in-process group: reset, then bh_step(k) for k in calls; states (and,
+    with a list `quads`, every rank's getTreeForDebug quads appended to it)."""
     import threading
     group = bh_amd.LocalGroup(world)
     engines = [bh_amd.Engine(params, device=0, rank=r, local_group=group) for r in range(world)]
     results, stats, errors = [None] * world, [None] * world, []
+    rank_quads = [None] * world
 
     def run(r):
         try:
@@ -688,6 +690,12 @@ def _run_group(world, params, arrs, calls):
                 engines[r].step(k)
             results[r] = engines[r].get_bodies()
             stats[r] = engines[r].let_stats()
+            if quads is not None:
+                rank_quads[r] = engines[r].get_quads()
+                # the lazy lastTree leaves the state alone: still the same bodies after it
+                again = engines[r].get_bodies()
+                for a, b in zip(again, results[r]):
+                    assert np.array_equal(a.view(np.int64), b.view(np.int64))
         except Exception as exc:  # surfaced below
             errors.append(exc)
 
@@ -701,6 +709,8 @@ def _run_group(world, params, arrs, calls):
     for e in engines:
         e.close()
     group.close()
+    if quads is not None:
+        quads.extend(rank_quads)
     return results, stats
 
 
@@ -746,13 +756,19 @@ def test_let_build_multi_rank_vs_single(world, scene, theta, monkeypatch):
     for k in (4, 3):
         single.step(k)
     want = single.get_bodies()
-    single.close()
-    got, stats = _run_group(world, params, arrs, (4, 3))
+    want_quads = single.get_quads()  # lastTree (BHA:435): test_pipelined_call_equals_single_steps
+    single.close()                   # ties it to the oracle's
+    rank_quads = []
+    got, stats = _run_group(world, params, arrs, (4, 3), quads=rank_quads)
     n = len(arrs[0])
     for r in range(world):
-        # 8 + 6 builds: the first (caller order after the reset) and the last of each call
-        # are full, the other 11 are LET builds
-        assert stats[r]["let_builds"] == 11 and stats[r]["full_builds"] == 3, stats[r]
+        # 8 + 6 builds: the first (caller order after the reset) is full, the other 13 are LET
+        # builds (a call's last build too: lastTree is built on demand)
+        assert stats[r]["let_builds"] == 13 and stats[r]["full_builds"] == 1, stats[r]
+        assert len(rank_quads[r]) == len(want_quads), f"rank {r}: quads"
+        for u, v in zip(rank_quads[r], want_quads):
+            assert np.array_equal(np.asarray(u).view(np.int64), np.asarray(v).view(np.int64)), \
+                f"rank {r}: lastTree quads"
         assert 0 < stats[r]["subset"] <= n and stats[r]["let_nodes"] > 0, stats[r]
         if scene == "cloud" and world == 8:  # the shard: a fraction of the bodies is built
             assert stats[r]["subset"] < n // 2, stats[r]
@@ -762,8 +778,8 @@ def test_let_build_multi_rank_vs_single(world, scene, theta, monkeypatch):
 
 def test_let_refresh_full_build_inside_a_call():
     """20 steps in one call = 40 builds: a full build sorts the caller's order, 32 LET builds,
-    the refresh full build (the replicas' slot order), 5 more LET builds, the call's last build
-    full -- every rank's state equals the single-GPU engine's bit for bit."""
+    the refresh full build (the replicas' slot order), 6 more LET builds -- every rank's state
+    equals the single-GPU engine's bit for bit."""
     arrs = scenes.uniform(120_000, 0.5, seed=41)
     params = bh_amd.default_params(theta=0.5)
     single = bh_amd.Engine(params, device=0)
@@ -773,7 +789,7 @@ def test_let_refresh_full_build_inside_a_call():
     single.close()
     got, stats = _run_group(4, params, arrs, (20,))
     for r in range(4):
-        assert stats[r]["let_builds"] == 37 and stats[r]["full_builds"] == 3, stats[r]
+        assert stats[r]["let_builds"] == 38 and stats[r]["full_builds"] == 2, stats[r]
         for k, name in enumerate(FIELDS):
             assert bits_equal(got[r][k], want[k]), f"rank {r}: {name}"
 
@@ -899,7 +915,7 @@ def test_let_nonpositive_masses(world, kind, monkeypatch):
     got, stats = _run_group(world, params, arrs, (4, 3))
     assert len(want[0]) < len(arrs[0])  # the heavy bodies merged
     for r in range(world):
-        assert stats[r]["let_builds"] == 11 and stats[r]["full_builds"] == 3, stats[r]
+        assert stats[r]["let_builds"] == 13 and stats[r]["full_builds"] == 1, stats[r]
         if kind == "negative":  # sharded: the halo rule ran, not the select-everything fallback
             assert stats[r]["subset"] < 0.75 * len(want[0]), stats[r]
         for k, name in enumerate(FIELDS):
