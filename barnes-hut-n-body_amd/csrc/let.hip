@@ -256,20 +256,6 @@ __device__ __forceinline__ void let_guard(const LetBufs &L, uint32_t *__restrict
 __global__ void k_let_guard(LetBufs L, uint32_t *__restrict__ scal) { let_guard(L, scal); }
 
 // ---- after the subset build ----------------------------------------------------------------
-__global__ __launch_bounds__(TB) void k_let_cells(int64_t n, int J,
-                                                  const uint64_t *__restrict__ keys_s,
-                                                  uint32_t *__restrict__ cstart) {
-    const int64_t bin = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (bin > LET_CELLS) return;
-    const int shift = 2 * (J - LET_P);
-    int64_t lo = 0, hi = n;  // first sorted index with (key >> shift) >= bin (sentinel: 4^P)
-    while (lo < hi) {
-        const int64_t mid = (lo + hi) >> 1;
-        if ((int64_t)(keys_s[mid] >> shift) < bin) lo = mid + 1; else hi = mid;
-    }
-    cstart[bin] = (uint32_t)lo;
-}
-
 // depth-P node of a cell with >= 2 subset bodies starting at sorted a: the internal nodes whose
 // first body is a are depths c(a-1)+1 .. c(a) at base[a] + (depth - c(a-1) - 1) (k_prep)
 __device__ __forceinline__ uint32_t cell_node(const TreeBuffers &tb, uint32_t a) {
@@ -277,12 +263,30 @@ __device__ __forceinline__ uint32_t cell_node(const TreeBuffers &tb, uint32_t a)
     return tb.base[a] + (uint32_t)(LET_P - cp - 1);
 }
 
-__global__ __launch_bounds__(TB) void k_let_table(LetBufs L, TreeBuffers tb) {
+// first sorted subset index with (key >> shift) >= bin (sentinel: 4^P)
+__device__ __forceinline__ uint32_t let_cell_start(int64_t n, int shift,
+                                                   const uint64_t *__restrict__ keys_s,
+                                                   int64_t bin) {
+    int64_t lo = 0, hi = n;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi) >> 1;
+        if ((int64_t)(keys_s[mid] >> shift) < bin) lo = mid + 1; else hi = mid;
+    }
+    return (uint32_t)lo;
+}
+
+// cstart (first subset body of every depth-P cell) and this rank's cell table in one launch:
+// each cell's thread finds its own start and the next cell's
+__global__ __launch_bounds__(TB) void k_let_table(int64_t n_sub, int J, LetBufs L, TreeBuffers tb) {
     const int64_t c = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (c >= LET_CELLS) return;
+    if (c > LET_CELLS) return;
+    const int shift = 2 * (J - LET_P);
+    const uint32_t a = let_cell_start(n_sub, shift, tb.keys_s, c);
+    L.cstart[c] = a;
+    if (c == LET_CELLS) return;
     LetCell r{0.0, 0.0, 0.0, 0u, 0u};
     if (L.ecell[c]) {
-        const uint32_t a = L.cstart[c], cn = L.cstart[c + 1] - a;
+        const uint32_t cn = let_cell_start(n_sub, shift, tb.keys_s, c + 1) - a;
         r.tag = 1u;
         if (cn == 1) {
             r.comX = tb.dst.x[a];
@@ -333,6 +337,9 @@ __device__ LetCell let_parent(const LetCell *c, int d, uint32_t i, const Geometr
 // Depths LET_P .. 4 of one depth-4 cell per workgroup (256 depth-8 cells): the exchanged values
 // (first rank that provided the cell), then the levels up, in LDS.
 static_assert(LET_P == 8, "k_let_top_hi assumes 256 depth-LET_P cells per depth-4 cell");
+#ifndef BH_LET_TOP_BATCH
+#define BH_LET_TOP_BATCH 8  // one round of loads for up to 8 ranks
+#endif
 __global__ __launch_bounds__(256) void k_let_top_hi(int world, Geometry g,
                                                     const LetCell *__restrict__ tables,
                                                     LetCell *__restrict__ levels,
@@ -345,15 +352,16 @@ __global__ __launch_bounds__(256) void k_let_top_hi(int world, Geometry g,
     {
         const uint32_t c = b * 256u + t;
         LetCell r{0.0, 0.0, 0.0, 0u, 0u};
-        // the ranks' entries four at a time: independent loads in flight, the first tagged wins
+        // the ranks' entries BH_LET_TOP_BATCH at a time: independent loads in flight, the first
+        // tagged wins
         bool found = false;
-        for (int q0 = 0; q0 < world && !found; q0 += 4) {
-            LetCell v[4];
+        for (int q0 = 0; q0 < world && !found; q0 += BH_LET_TOP_BATCH) {
+            LetCell v[BH_LET_TOP_BATCH];
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < BH_LET_TOP_BATCH; ++j)
                 if (q0 + j < world) v[j] = tables[(int64_t)(q0 + j) * LET_TSTRIDE + c];
 #pragma unroll
-            for (int j = 0; j < 4; ++j)
+            for (int j = 0; j < BH_LET_TOP_BATCH; ++j)
                 if (!found && q0 + j < world && v[j].tag) {
                     r = v[j];
                     found = true;
@@ -448,9 +456,7 @@ __device__ __forceinline__ uint32_t leaf_slot(const LetBufs &L, uint32_t bc) {
     return L.hcell[bc] ? L.cstart[bc] : NODE_BODY_MASK;
 }
 
-__global__ __launch_bounds__(TB) void k_let_write_top(LetBufs L) {
-    int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (t >= level_off(LET_P)) return;
+__device__ __forceinline__ void let_write_top(const LetBufs &L, int64_t t) {
     int d = 0;
     while (t >= ((int64_t)1 << (2 * d))) {
         t -= (int64_t)1 << (2 * d);
@@ -481,9 +487,7 @@ __global__ __launch_bounds__(TB) void k_let_write_top(LetBufs L) {
 
 // one record per depth-P cell that is not copied: a remote internal cell (accepted by every local
 // body: never opened) or a one-body leaf
-__global__ __launch_bounds__(TB) void k_let_write_cells(LetBufs L) {
-    const int64_t c = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (c >= LET_CELLS) return;
+__device__ __forceinline__ void let_write_cell(const LetBufs &L, int64_t c) {
     const uint32_t bs = L.bsz[c];
     if (bs != 1u || L.ccnt[c] != 0u) return;
     const uint32_t pos = L.posc[c + 1] - 1u;
@@ -498,6 +502,14 @@ __global__ __launch_bounds__(TB) void k_let_write_cells(LetBufs L) {
     else
         nd.meta = NODE_LEAF | leaf_slot(L, (uint32_t)c) | (v.mass == 0.0 ? NODE_SKIP : 0u);
     if (pos < L.node_cap) L.nodes[pos] = nd;
+}
+
+// the top records (threads [0, level_off(P))) and the per-cell records (the next LET_CELLS
+// threads) in one launch: disjoint node slots, the same inputs
+__global__ __launch_bounds__(TB) void k_let_write_top_cells(LetBufs L) {
+    const int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (t < level_off(LET_P)) let_write_top(L, t);
+    else if (t < level_off(LET_P) + LET_CELLS) let_write_cell(L, t - level_off(LET_P));
 }
 
 // the locally built subtrees, one thread per node (grid-stride over cpos[LET_CELLS] nodes): node t
@@ -725,8 +737,7 @@ hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
 
 hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const TreeBuffers &tb,
                      hipStream_t s) {
-    k_let_cells<<<grid_for(LET_CELLS + 1), TB, 0, s>>>(n_sub, g.J, tb.keys_s, L.cstart);
-    k_let_table<<<grid_for(LET_CELLS), TB, 0, s>>>(L, tb);
+    k_let_table<<<grid_for(LET_CELLS + 1), TB, 0, s>>>(n_sub, g.J, L, tb);
     return hipGetLastError();
 }
 
@@ -743,8 +754,7 @@ hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, c
     e = rocprim::exclusive_scan(L.scratch, bytes, L.ccnt, L.cpos, 0u, (size_t)(LET_CELLS + 1),
                                 rocprim::plus<uint32_t>(), s);
     if (e != hipSuccess) return e;
-    k_let_write_top<<<grid_for(level_off(LET_P)), TB, 0, s>>>(L);
-    k_let_write_cells<<<grid_for(LET_CELLS), TB, 0, s>>>(L);
+    k_let_write_top_cells<<<grid_for(level_off(LET_P) + LET_CELLS), TB, 0, s>>>(L);
     k_let_copy_blocks<<<BH_LET_COPY_GRID, TB, 0, s>>>(L, tb.nodes);
     if (n_sub > 0)
         k_let_subpos<<<grid_for(n_sub), TB, 0, s>>>(n_sub, pc.n, tb.dst.vx, L.subpos, L, scal);
