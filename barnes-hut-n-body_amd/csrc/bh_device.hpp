@@ -430,9 +430,11 @@ struct PosSrc {
     GatherLayout gl;
     const uint32_t *gslot;
 };
+// mf.keys non-null: the gather also writes the subset build's Morton keys and bucket
+// assignment (k_morton + k_bucket_count of tree_build, which then sets keys_ready)
 hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
                       const LetPieces &pc, double gap2, const LetBufs &L, const BodyState &sub,
-                      int64_t S, uint32_t *scal, hipStream_t s);
+                      int64_t S, uint32_t *scal, hipStream_t s, const MortonFuse &mf = {});
 // gslot[lanes[q]] = gather_slot(gl, q) (lanes null: the identity map)
 void let_gather_slots(int64_t n, const uint32_t *lanes, GatherLayout gl, uint32_t *gslot,
                       hipStream_t s);

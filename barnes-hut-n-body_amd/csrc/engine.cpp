@@ -578,6 +578,9 @@ int ensure_direct(bh_engine *e) {
 
 // ---- multi-rank: the build as a locally essential tree (let.hip) ----------------------
 int pinned_reserve(bh_engine *e, size_t bytes);
+#ifndef BH_LET_FUSE_KEYS
+#define BH_LET_FUSE_KEYS 1  // the subset gather writes the LET build's keys and buckets
+#endif
 #ifndef BH_LET_REFRESH
 #define BH_LET_REFRESH 32  // LET builds between full builds (the replicated Morton order)
 #endif
@@ -822,8 +825,17 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         }
         ps = PosSrc{e->a2, e->pos_layout, e->inv_lanes};
     }
+    // the subset build's keys and buckets from the gather when its buffers and splitters are
+    // those of the previous LET build (same S capacity and J; not the first build, which sorts
+    // with rocprim and sizes the subset afterwards)
+    MortonFuse mf{};
+    const bool fuse = BH_LET_FUSE_KEYS && e->let_known > 0 && e->s_spl_nb > 0 &&
+                      S <= e->let_sub_cap && e->geo.J == e->let_J && e->s_keys;
+    if (fuse)
+        mf = MortonFuse{e->s_keys, e->s_keys32, e->s_spl, e->s_spl_nb, e->s_cnt, e->s_base,
+                        e->s_bcount};
     HIPCHK(e, let_select(e->st, ps, e->geo, pc, gap2, e->L, e->sub_src, S, e->scalars,
-                         e->stream));
+                         e->stream, mf));
     if (e->let_known <= 0) {
         TRY(pinned_reserve(e, 64));
         uint32_t *h = static_cast<uint32_t *>(e->pin);
@@ -836,7 +848,8 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     TRY(let_alloc(e, S));
     const int64_t n_sub = S;  // padded: bodies past the real subset are dead
     ++e->let_builds;
-    const TreeBuffers sb = let_tree_buffers(e);
+    TreeBuffers sb = let_tree_buffers(e);
+    sb.keys_ready = fuse && e->s_spl_nb > 0;  // (let_alloc above kept the buffers: S fitted)
     HIPCHK(e, tree_build(sb, n_sub, e->geo, e->stream));
     e->s_spl_nb = sort_buckets(n_sub);  // k_prep wrote this build's splitters
     HIPCHK(e, let_table(n_sub, e->geo, e->L, sb, e->stream));

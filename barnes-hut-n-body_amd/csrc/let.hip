@@ -198,6 +198,18 @@ __global__ __launch_bounds__(64) void k_let_flags(LetPieces pc, PosSrc ps,
     }
 }
 
+// k_morton and k_bucket_count of the subset build for subset body j with Morton key `key`
+__device__ __forceinline__ void let_fuse_key(const Geometry &g, const MortonFuse &mf, int64_t j,
+                                             uint64_t key) {
+    const uint32_t k32 = (uint32_t)(key >> key32_shift(g.J));
+    mf.keys[j] = key;
+    mf.keys32[j] = k32;
+    const uint32_t b = find_bucket(mf.spl, mf.spl_nb, ((uint64_t)k32 << 32) | (uint64_t)j,
+                                   (uint32_t)(j / SORT_B));
+    mf.bkt[j] = b;
+    mf.off[j] = bucket_offset(b, mf.counts);
+}
+
 // also pads subset slots [n_real, S) as dead bodies (sentinel keys: never in the tree, never
 // evaluated) and writes the status: overflow when n_real > S (the build then misses bodies: the
 // call is replayed); the grid covers n >= S threads
@@ -207,7 +219,8 @@ __global__ __launch_bounds__(TB) void k_let_gather(int64_t n, PosSrc ps,
                                                    BodyState st, BodyState sub, int64_t S,
                                                    const uint32_t *__restrict__ count,
                                                    LetCell *__restrict__ table,
-                                                   uint32_t *__restrict__ scal) {
+                                                   uint32_t *__restrict__ scal, Geometry g,
+                                                   MortonFuse mf) {
     __shared__ uint32_t s_w[TB / 64];
     const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     {
@@ -223,6 +236,7 @@ __global__ __launch_bounds__(TB) void k_let_gather(int64_t n, PosSrc ps,
             sub.vy[i] = 0.0;
             sub.m[i] = 0.0;
             sub.cidx[i] = CIDX_DEAD;
+            if (mf.keys) let_fuse_key(g, mf, i, sentinel_key(g.J));
         }
     }
     const bool f = i < n && flag8[i];
@@ -241,7 +255,10 @@ __global__ __launch_bounds__(TB) void k_let_gather(int64_t n, PosSrc ps,
     sub.vx[j] = __longlong_as_double((long long)i);  // payload: the replicated slot
     sub.vy[j] = 0.0;
     sub.m[j] = st.m[i];
-    sub.cidx[j] = st.cidx[i];
+    const uint32_t ci = st.cidx[i];
+    sub.cidx[j] = ci;
+    if (mf.keys && (int64_t)j < S)  // (an overflowing subset is replayed: keys only below S)
+        let_fuse_key(g, mf, j, morton_key(g, px, py, (ci & CIDX_DEAD) != 0u));
 }
 
 // a tree larger than its array can only come from a broken invariant: no walk (node count 0), and
@@ -709,7 +726,7 @@ __global__ __launch_bounds__(TB) void k_let_clear(int64_t n, uint8_t *__restrict
 
 hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
                       const LetPieces &pc, double gap2, const LetBufs &L, const BodyState &sub,
-                      int64_t S, uint32_t *scal, hipStream_t s) {
+                      int64_t S, uint32_t *scal, hipStream_t s, const MortonFuse &mf) {
     if (pc.n <= 0) {
         hipError_t e = hipMemsetAsync(L.ecell, 0, LET_CELLS, s);
         return e == hipSuccess ? hipMemsetAsync(L.flag_all, 0, sizeof(uint32_t), s) : e;
@@ -731,7 +748,7 @@ hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
                                 rocprim::plus<uint32_t>(), s);
     if (e != hipSuccess) return e;
     k_let_gather<<<(unsigned)nb, TB, 0, s>>>(pc.n, ps, L.flag8, L.selpos, st, sub, S,
-                                             L.selpos + nb, L.table, scal);
+                                             L.selpos + nb, L.table, scal, g, mf);
     return hipGetLastError();
 }
 
