@@ -598,6 +598,8 @@ int let_alloc(bh_engine *e, int64_t n_sub) {
         TRY(dev_alloc(e, L.cstart, LET_CELLS + 1));
         TRY(dev_alloc(e, L.table, LET_TSTRIDE));
         TRY(dev_alloc(e, L.tables, (size_t)e->world * LET_TSTRIDE));
+        // (solo: the tables of ranks 2 .. world-1 stay zero -- nothing tagged -- for good)
+        HIPCHK(e, hipMemset(L.tables, 0, sizeof(LetCell) * (size_t)e->world * LET_TSTRIDE));
         TRY(dev_alloc(e, L.levels, ((size_t)1 << (2 * LET_P + 2)) / 3 + 1));
         TRY(dev_alloc(e, L.w, LET_CELLS + 1));
         TRY(dev_alloc(e, L.posc, LET_CELLS + 1));
@@ -857,7 +859,6 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     if (e->comm) {
         NCCLCHK(e, ncclAllGather(e->L.table, e->L.tables, tbytes, ncclUint8, e->comm, e->stream));
     } else if (e->solo) {  // own values first, the rest from the last full build
-        HIPCHK(e, hipMemsetAsync(e->L.tables, 0, tbytes * (size_t)e->world, e->stream));
         HIPCHK(e, hipMemcpyAsync(e->L.tables, e->L.table, tbytes, hipMemcpyDeviceToDevice,
                                  e->stream));
         if (e->world > 1 && e->solo_table)

@@ -357,11 +357,15 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
 
 // First sorted body of every depth-D0 cell (bins 0 .. 4^D0; the sentinel's prefix is 4^D0,
 // so bin 4^D0 starts at the first out-of-root body, i.e. at the in-root count).
+// Also fills the span super list [0, n_super) with 0xFF bytes for k_span_find (in place of a
+// memset launch; nothing reads it before k_span_find).
 __global__ __launch_bounds__(TB) void k_cells(int64_t n, int J, int D0,
                                               const uint64_t *__restrict__ keys_s,
-                                              uint32_t *__restrict__ cell_start) {
+                                              uint32_t *__restrict__ cell_start,
+                                              uint32_t *__restrict__ super_list, int64_t n_super) {
     chain_prio();
     const int64_t bin = (int64_t)blockIdx.x * TB + threadIdx.x;
+    for (int64_t k = bin; k < n_super; k += (int64_t)gridDim.x * TB) super_list[k] = 0xFFFFFFFFu;
     const int64_t nbins = (int64_t)1 << (2 * D0);
     if (bin > nbins) return;
     const int shift = 2 * (J - D0);
@@ -1486,17 +1490,15 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     st = rocprim::exclusive_scan(b.scratch, bytes, b.cnt, b.base, 0u, (size_t)(n + 1),
                                  rocprim::plus<uint32_t>(), s);
     if (st != hipSuccess) return st;
+    const uint32_t n_groups = span_groups(b.span_stride);
+    const int64_t n_super = n_groups > 1 ? (int64_t)(g.J + 1) * n_groups : 0;
     k_cells<<<grid_for(((int64_t)1 << (2 * D0)) + 1), TB, 0, s>>>(n, g.J, D0, b.keys_s,
-                                                                  b.cell_start);
+                                                                  b.cell_start, b.super_list,
+                                                                  n_super);
     k_emit_com<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), EC_TB, 0, s>>>(
         n, g, D0, b.keys_s, b.cpl, b.base, b.cell_start, b.dst.x, b.dst.y, b.dst.m, b.dst.cidx,
         b.idx, b.nodes, b.scalars + 1, b.keys32, b.lanes_remap);
     const dim3 span_grid((b.span_stride + TB - 1) / TB, g.J + 1);
-    const uint32_t n_groups = span_groups(b.span_stride);
-    if (n_groups > 1) {
-        st = hipMemsetAsync(b.super_list, 0xFF, sizeof(uint32_t) * (size_t)(g.J + 1) * n_groups, s);
-        if (st != hipSuccess) return st;
-    }
     k_span_find<<<span_grid, TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cpl, b.base, b.cell_start,
                                          b.span_list, b.span_stride, b.super_list, n_groups,
                                          b.nodes);
