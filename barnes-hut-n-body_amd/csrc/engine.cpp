@@ -207,7 +207,7 @@ struct bh_engine {
     bool prebuilt = false;  // the current step's first build was made by the previous step
     bool fuse_keys = false;   // the next KICK_DRIFT traversal writes the next build's keys / buckets
     bool keys_ready = false;  // ... and it did: the next full build skips k_morton, k_bucket_count
-    hipEvent_t pipe_ev[2] = {nullptr, nullptr};
+    hipEvent_t pipe_ev[3] = {nullptr, nullptr, nullptr};
     hipStream_t pipe_stream = nullptr;  // the overlapped work's stream (BH_PIPE_PRIORITY)
     // one GPU: the previous evaluation's wave durations and the longest-first run order
     // (slot 0: the one-GPU launch over all lanes; 1 + k: LET round k's piece)
@@ -1316,21 +1316,25 @@ int pipe_alloc(bh_engine *e) {
 // next step's first build; e->prebuilt tells the next evaluation its tree is there.
 int evaluate_pipelined(bh_engine *e) {
     const int64_t n = e->n;
+    hipStream_t s = e->stream;
+    // the merge rule's mailbox header is cleared on the overlapped stream while this build runs
+    // (after everything queued so far on the engine's stream, the last merge rule included): on
+    // the engine's stream it would sit between the build and the traversal, on the overlapped
+    // stream after the traversal's start it would wait until its last workgroups are placed
+    const bool merging = e->p.merge_min_dist > 0.0 && e->n > 1 && e->heavy_possible;
+    if (merging) {
+        TRY(merge_bufs(e));
+        HIPCHK(e, hipEventRecord(e->pipe_ev[2], s));
+        HIPCHK(e, hipStreamWaitEvent(e->pipe_stream, e->pipe_ev[2], 0));
+        HIPCHK(e, hipMemsetAsync(e->box, 0, sizeof(MergeHeader), e->pipe_stream));
+    }
     TRY(mark(e, -1));
     TRY(build(e));
     TRY(mark(e, 0));
-    hipStream_t s = e->stream;
     const bool lanes = e->lanes_valid;
     copy_trav_inputs(n, e->st.m, e->m_trav, e->st.cidx, e->cidx_trav, lanes ? e->lanes : nullptr,
                      e->lanes_trav, e->base + n, e->T_trav, s);
     HIPCHK(e, hipGetLastError());
-    // the merge rule's mailbox header is cleared here, before the traversal: on the overlapped
-    // stream the fill kernel would wait until the traversal's last workgroups are placed
-    const bool merging = e->p.merge_min_dist > 0.0 && e->n > 1 && e->heavy_possible;
-    if (merging) {
-        TRY(merge_bufs(e));
-        HIPCHK(e, hipMemsetAsync(e->box, 0, sizeof(MergeHeader), s));
-    }
     HIPCHK(e, hipEventRecord(e->pipe_ev[0], s));
     HIPCHK(e, hipStreamWaitEvent(e->pipe_stream, e->pipe_ev[0], 0));
     const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};  // BHA:378
