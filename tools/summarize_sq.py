@@ -34,7 +34,7 @@ def main():
     avg = {c: sum(v) / len(v) for c, v in acc.items()}
     waves = avg.get("SQ_WAVES", 0.0)
     out = [f"## {KERNEL.strip(', ')}...> SQ counters (C3, average per dispatch; rocprofv3 --pmc, "
-           f"{len(glob.glob(os.path.join(src, 'p*')))} passes)", "",
+           f"{len([d for d in glob.glob(os.path.join(src, 'p*')) if os.path.isdir(d)])} passes)", "",
            "| counter | per dispatch | per wave |", "|---|---|---|"]
     for c in sorted(avg):
         pw = avg[c] / waves if waves else 0.0
