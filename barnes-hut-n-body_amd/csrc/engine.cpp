@@ -166,9 +166,9 @@ struct bh_engine {
     GatherLayout a2_layout{};            // ... at the lane's gather slot (multi-rank rounds)
 
     // multi-rank locally essential tree (let.hip): subset state and tree workspace
-    // BH_LET unset: LET builds from 4 ranks up (at 2 ranks the subset is over half the bodies
-    // and the selection / exchange / copy outweigh the smaller build: solo C4 step 10.45 ms
-    // with LET against 10.15 replicated; 4 ranks 6.07 vs 6.82, 8 ranks 4.03 vs 5.15);
+    // BH_LET unset: LET builds from BH_LET_MIN_WORLD ranks up (round 3, solo C4 rank 0, ms per
+    // step LET / replicated: 2 ranks 9.80 / 10.21, 3 ranks 7.00 / 7.98, 4 ranks 5.53 / 6.80,
+    // 8 ranks 3.43 / 5.19; round 2 had 10.45 / 10.15 at 2 ranks, hence 4 then);
     // BH_LET=1 at any world size, BH_LET=0 never
     bool let_on = true;
     bool let_forced = false;
@@ -681,7 +681,12 @@ TreeBuffers let_tree_buffers(bh_engine *e) {
     return b;
 }
 
-bool let_active(const bh_engine *e) { return e->let_on && (e->let_forced || e->world >= 4); }
+#ifndef BH_LET_MIN_WORLD
+#define BH_LET_MIN_WORLD 2
+#endif
+bool let_active(const bh_engine *e) {
+    return e->let_on && (e->let_forced || e->world >= BH_LET_MIN_WORLD);
+}
 
 // Stream of round k (even: the engine's stream; odd: stream2, started after the build).
 int round_streams(bh_engine *e) {

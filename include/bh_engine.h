@@ -62,7 +62,7 @@ int bh_create(const bh_params *p, int device, bh_engine **out);
  * Replaces computeAccelerations' fan-out over worker threads (BHA:374-395) by a fan-out over
  * GPUs.  Every rank holds a replica of the state and owns one contiguous range of the Hilbert
  * wave order (bh_shard_range).  Per force evaluation a rank either
- *   - builds a locally essential tree (from 4 ranks up, or BH_LET=1): only the depth-8 cells its
+ *   - builds a locally essential tree (from 2 ranks up, or BH_LET=1): only the depth-8 cells its
  *     bodies can open, plus the top computed from every rank's cell values (one all-gather of
  *     2 MB cell tables); it evaluates its range, kicks (and drifts) its own bodies, and the new
  *     positions -- 16 B per body -- are all-gathered over RCCL in BH_SHARD_ROUNDS rounds into
@@ -192,8 +192,8 @@ int bh_traversal_counters(const bh_engine *e, int64_t *out5);
  * bh_step call (the cells this rank's bodies can open), out5[3] node records of the last LET
  * tree, out5[4] bh_step calls replayed because a subset outgrew its capacity (the capacity
  * follows the previous call's subsets, so the build needs no host round trip).  LET builds run
- * from 4 ranks up; BH_LET=1 in the environment before creating an engine enables them at any
- * world size, BH_LET=0 keeps every build full. */
+ * on every multi-rank engine (2 ranks up); BH_LET=1 in the environment before creating an engine
+ * enables them also on one rank, BH_LET=0 keeps every build full. */
 int bh_let_stats(const bh_engine *e, int64_t *out5);
 
 /* Enable/disable per-phase event timing (default off: no events in the hot loop). */

@@ -633,13 +633,20 @@ def test_c5_fp32_vs_fp64_tolerance_study():
     eng.close()
 
 
+@pytest.mark.parametrize("let", ["default", "0"])
 @pytest.mark.parametrize("world", [2, 3])
-def test_multi_rank_decomposition_in_process(world):
+def test_multi_rank_decomposition_in_process(world, let, monkeypatch):
     """The multi-GPU step with `world` ranks on one GPU (bh_create_local: one host thread per
     rank, the in-place all-gather of every round emulated with device-to-device copies, RCCL
     being unable to host several ranks per device): every rank's state after 3 steps of a
-    merge-active scene, and one theta = 0 evaluation, bit-identical to the oracle."""
+    merge-active scene, and one theta = 0 evaluation, bit-identical to the oracle -- with the
+    default builds (locally essential trees on every multi-rank engine) and with BH_LET=0
+    (every build full and replicated, the accelerations all-gathered)."""
     import threading
+    if let == "0":
+        monkeypatch.setenv("BH_LET", "0")
+    else:
+        monkeypatch.delenv("BH_LET", raising=False)
     for theta in (0.5, 0.0):
         arrs = scenes.config_scene("c1_code")
         group = bh_amd.LocalGroup(world)
@@ -748,7 +755,7 @@ def test_let_build_multi_rank_vs_single(world, scene, theta, monkeypatch):
     top from the exchanged cell values, and its forces -- hence every rank's state -- equal the
     single-GPU engine's bit for bit.  Two bh_step calls (the LET builds run in the middle of a
     call; the last build of a call is the full tree)."""
-    monkeypatch.setenv("BH_LET", "1")  # LET builds at every world size (default: from 4 ranks)
+    monkeypatch.setenv("BH_LET", "1")  # LET builds at every world size (default: from 2 ranks)
     arrs = _let_scene(scene)
     params = bh_amd.default_params(theta=theta, merge_min_dist=0.0 if scene == "jitter" else 8.0)
     single = bh_amd.Engine(params, device=0)

@@ -14,4 +14,4 @@ for w in 2 4 8; do
     grep '^{' gpurun_out/solo_w$w$let.log | tail -1 | tee -a gpurun_out/solo_curve.jsonl
   done
 done
-LET_TESTS=0 bash tools/let_gpu.sh
+if [ "${PROFILE:-1}" = 1 ]; then LET_TESTS=0 bash tools/let_gpu.sh; fi
