@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = (
     "bh_nbody3d_step", "bh_nbody3d_accelerations", "bh_nbody3d_get", "bh_nbody3d_last_ms",
     "bh_local_group_create", "bh_local_group_destroy", "bh_create_local",
     "bh_save_state", "bh_load_state", "bh_let_stats", "bh_create_solo", "bh_comm_ranks",
-    "bh_debug_inject",
+    "bh_debug_inject", "bh_set_mirror", "bh_map_bodies",
 )
 
 
@@ -110,6 +110,9 @@ def load_library(path: str | None = None):
     lib.bh_num_bodies.argtypes = [_VP]
     lib.bh_num_bodies.restype = ctypes.c_int64
     lib.bh_get_bodies.argtypes = [_VP, _D, _D, _D, _D, _D, ctypes.c_int64, _I64P]
+    lib.bh_set_mirror.argtypes = [_VP, ctypes.c_int]
+    _DPP = ctypes.POINTER(_D)
+    lib.bh_map_bodies.argtypes = [_VP, _DPP, _DPP, _DPP, _DPP, _DPP, _I64P]
     lib.bh_compute_accelerations.argtypes = [_VP, _D, _D, _I64P]
     lib.bh_get_quads.argtypes = [_VP, _D, _D, _D, ctypes.c_int64, _I64P]
     lib.bh_last_timings.argtypes = [_VP, _D]
@@ -363,6 +366,24 @@ class Engine:
         got = ctypes.c_int64(0)
         self._check(self._lib.bh_get_bodies(self._h, *[_dp(a) for a in out], n, ctypes.byref(got)))
         return tuple(a[: got.value] for a in out)
+
+    def set_mirror(self, on: bool):
+        """bh_set_mirror: every step() call writes the pinned caller-order mirror itself."""
+        self._check(self._lib.bh_set_mirror(self._h, 1 if on else 0))
+
+    def map_bodies(self):
+        """bh_map_bodies: read-only numpy views of the pinned mirror (x, y, vx, vy, m), valid
+        until the next call that changes the bodies -- copy them to keep them."""
+        ptrs = [_D() for _ in range(5)]
+        n = ctypes.c_int64(0)
+        self._check(self._lib.bh_map_bodies(self._h, *[ctypes.byref(p) for p in ptrs],
+                                            ctypes.byref(n)))
+        out = []
+        for p in ptrs:
+            a = np.ctypeslib.as_array(p, shape=(n.value,)) if n.value else np.empty(0)
+            a.flags.writeable = False
+            out.append(a)
+        return tuple(out)
 
     def compute_accelerations(self, visits: bool = False):
         n = self.num_bodies()

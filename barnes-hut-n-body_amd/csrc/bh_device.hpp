@@ -489,6 +489,17 @@ void scatter_to_caller(int64_t n, const uint32_t *cidx, int k, const double *con
 void scatter_acc_to_caller(int64_t n, const uint32_t *cidx, const double *a2, double *ax,
                            double *ay, hipStream_t s, const uint32_t *lanes = nullptr,
                            GatherLayout gl = GatherLayout{});
+// The pinned caller-order mirror: keep[c] / pos[c] over the caller indices of a state whose
+// tombstones still hold theirs (keep, pos: n entries; tmp: compact_scratch_bytes(n)), then
+// dst_j[pos[c]] = src_j[slot] for the live bodies -- the list after the call's removals.
+hipError_t mirror_index(int64_t n, const uint32_t *cidx, uint32_t *keep, uint32_t *pos, void *tmp,
+                        size_t tmp_bytes, hipStream_t s);
+void mirror_scatter(int64_t n, const uint32_t *cidx, const uint32_t *pos, int k,
+                    const double *const *src, double *const *dst, hipStream_t s);
+// dst[perm[a]] = src[a] for x and y: positions of a sorted build (jitter included) back into the
+// state's own slot order (multi-rank getTreeForDebug, engine.cpp bh_get_quads)
+void unpermute_positions(int64_t n, const uint32_t *perm, const double *sx, const double *sy,
+                         double *dx, double *dy, hipStream_t s);
 
 struct MergePair {
     uint32_t h_cidx, v_cidx;  // heavy body and candidate victim, caller indices

@@ -196,6 +196,7 @@ struct bh_engine {
     Node *s_nodes = nullptr;
     hipEvent_t table_ev = nullptr;
     bool inject_guard = false;  // bh_debug_inject(1): the next LET build trips k_let_guard
+    bool agree_failed = false;  // in-process group: this member could not read a peer's flags
     // pipelined step (one GPU): the next step's first build runs on pipe_stream while this step's
     // second traversal runs; it builds into nodes_alt / alt, and the traversal reads copies of
     // what that build and the merge rule overwrite (masses, flags, lane map, node count)
@@ -209,6 +210,37 @@ struct bh_engine {
     bool keys_ready = false;  // ... and it did: the next full build skips k_morton, k_bucket_count
     hipEvent_t pipe_ev[3] = {nullptr, nullptr, nullptr};
     hipStream_t pipe_stream = nullptr;  // the overlapped work's stream (BH_PIPE_PRIORITY)
+    // A call's last step is pipelined too (the front-end calls bh_step(1) once per frame): the
+    // call then ends with the next step's first tree already built (prebuilt: st in its order,
+    // jitter applied, nodes).  What the caller sees -- the reference's bodies after step(), before
+    // the next buildTree's jitter (BHA:146-151) -- is `view` (the previous slot order); lastTree
+    // (BHA:435) is nodes_alt with its walk structures copied aside (lt_keys, lt_cpl, lt_base).
+    // The next bh_step consumes the prebuilt tree; bh_set_params (geometry), bh_reset_bodies and
+    // a replay drop it.
+    BodyState view{};
+    int64_t view_cap = 0;
+    bool view_pending = false;
+    uint64_t *lt_keys = nullptr;
+    int8_t *lt_cpl = nullptr;
+    uint32_t *lt_base = nullptr;
+    int64_t lt_walk_cap = 0;
+    bool lt_aside = false;  // lastTree is (nodes_alt, lt_keys, lt_cpl, lt_base)
+    // Pinned caller-order mirror of the bodies (bh_set_mirror / bh_map_bodies): x, y, vx, vy, m
+    // at stride mir_cap, filled by the step itself on mir_stream
+    bool mirror_on = false;
+    double *mir = nullptr;        // pinned host, 5 * mir_cap
+    double *mir_stage = nullptr;  // device, 5 * mir_cap (caller order, compacted)
+    uint32_t *mir_keep = nullptr, *mir_pos = nullptr;  // device, caller order
+    int64_t mir_cap = 0;
+    void *mir_tmp = nullptr;      // the mirror's scan scratch (the overlapped build uses `scratch`)
+    size_t mir_tmp_bytes = 0;
+    bool mir_fresh = false;       // the mirror (after mir_ev) holds the current caller state
+    bool mir_launched = false;    // ... launched by the running call's last step
+    int64_t mir_n = 0;
+    hipStream_t mir_stream = nullptr;
+    hipEvent_t mir_ev = nullptr;   // copy-out complete
+    hipEvent_t mir_ev2 = nullptr;  // the mirror's kernels are done reading the state
+    hipEvent_t mir_in[2] = {nullptr, nullptr};
     // one GPU: the previous evaluation's wave durations and the longest-first run order
     // (slot 0: the one-GPU launch over all lanes; 1 + k: LET round k's piece)
     uint32_t *wave_cost = nullptr, *run_order = nullptr;
@@ -502,6 +534,7 @@ int build_into(bh_engine *e, hipStream_t s, bool overlap) {
     tb.lanes_remap = use_lanes && !refresh ? e->lanes : nullptr;
     tb.keys_ready = e->keys_ready && !overlap;
     e->keys_ready = false;
+    if (!overlap) e->mir_fresh = false;  // the jitter may move bodies
     HIPCHK(e, tree_build(tb, n, e->geo, s));
     ++e->full_builds;
     e->inv_valid = false;  // the map follows this build's permutation
@@ -985,6 +1018,8 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
     const int64_t n = e->n;
     if (e->prebuilt) {  // the pipelined step built this tree (single GPU: nothing deferred)
         e->prebuilt = false;
+        e->view_pending = false;  // its jitter is now part of the state (BHA:146-151)
+        e->mir_fresh = false;
     } else {
         TRY(materialize_positions(e));  // the replica's x, y; a2 is free again
         TRY(sync_velocities(e));        // before the full build permutes the state
@@ -1170,6 +1205,14 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
     std::sort(dead.begin(), dead.end());
     HIPCHK(e, hipMemcpy(e->dead_sorted, dead.data(), 4 * (size_t)nd, hipMemcpyHostToDevice));
     const int64_t n = e->n;
+    if (e->view_pending) {  // the caller-visible state (the previous order) loses the same bodies
+        HIPCHK(e, compact_state(n, e->keep, e->view, e->alt, e->dead_sorted, nd, e->pos,
+                                e->scratch, e->scratch_bytes, e->stream));
+        std::swap(e->view, e->alt);
+    }
+    // (a prebuilt tree stays valid: the removed bodies were tombstones in its build, sentinel keys
+    // at the tail of its order, so the compaction moves no slot the tree refers to, and its node
+    // count base[n'] is the same for every n' at or past the last body in the tree)
     HIPCHK(e, compact_state(n, e->keep, e->st, e->alt, e->dead_sorted, nd, e->pos, e->scratch,
                             e->scratch_bytes, e->stream));
     std::swap(e->st, e->alt);
@@ -1188,6 +1231,7 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
     if (nd != nd_before_last) {
         e->tree_valid = false;
         e->lazy_tree = false;
+        e->lt_aside = false;
     } else if (e->lazy_tree) {  // the snapshot follows the compaction (its tombstones were not built)
         compact_pair(n, e->keep, e->pos, e->lt_x, e->lt_y, e->alt.x, e->alt.y, e->stream);
         HIPCHK(e, hipGetLastError());
@@ -1221,12 +1265,18 @@ int snapshot(bh_engine *e) {
         e->snap_cap = e->cap;
     }
     e->snap_n = e->n;
-    return copy_state(e, e->st, e->snap, e->n);
+    // after a pipelined call the caller's state is the view (the prebuilt tree's jitter is not
+    // applied yet): a replay starts from it and builds its own first tree
+    return copy_state(e, e->view_pending ? e->view : e->st, e->snap, e->n);
 }
 
 int restore(bh_engine *e) {
     TRY(copy_state(e, e->snap, e->st, e->snap_n));
     e->n = e->snap_n;
+    e->prebuilt = false;
+    e->view_pending = false;
+    e->lt_aside = false;
+    e->mir_fresh = false;
     e->spl_nb = 0;  // the splitters describe the discarded builds' order
     e->keys_ready = false;
     e->lanes_valid = false;
@@ -1254,20 +1304,29 @@ int agree_let_flags(bh_engine *e, uint32_t ls[2], uint32_t *own_sub) {
         return BH_OK;
     }
     if (!e->group) return BH_OK;  // solo: no peers
-    e->group->barrier();          // every member's call is complete on the device
+    // a member that cannot read a peer's flags must not decide alone: every member sees its
+    // failure after the second barrier and all return an error together (none replays)
+    e->agree_failed = false;  // (its previous value was read before this call's LET barriers)
+    e->group->barrier();      // every member's call is complete on the device
     for (bh_engine *peer : e->group->members) {
         if (peer == e) continue;
         uint32_t q[2] = {0, 0};
         const hipError_t rc = hipMemcpy(q, peer->scalars + 4, sizeof(q), hipMemcpyDeviceToHost);
-        if (rc != hipSuccess) {  // still pass the second barrier: the peers wait for it
-            e->group->barrier();
+        if (rc != hipSuccess) {
+            e->agree_failed = true;
             e->err = std::string("agree_let_flags: ") + hipGetErrorString(rc);
-            return BH_E_DEVICE;
+            break;
         }
         ls[0] = std::max(ls[0], q[0]);
         ls[1] = std::max(ls[1], q[1]);
     }
     e->group->barrier();  // nobody clears its flags (a replay) before every member has read them
+    bool failed = false;
+    for (bh_engine *peer : e->group->members) failed = failed || peer->agree_failed;
+    if (failed) {
+        if (!e->agree_failed) e->err = "agree_let_flags: a peer could not read the LET flags";
+        return BH_E_DEVICE;
+    }
     return BH_OK;
 }
 
@@ -1287,15 +1346,28 @@ int agree_let_flags(bh_engine *e, uint32_t ls[2], uint32_t *own_sub) {
 #ifndef BH_PIPE_PRIORITY
 #define BH_PIPE_PRIORITY 1  // the overlapped work's stream at the highest priority
 #endif
+#ifndef BH_PIPE_LAST
+#define BH_PIPE_LAST 1  // pipeline a call's last step too (the next call starts on its tree)
+#endif
 bool pipelined(const bh_engine *e, bool last) {
-    return BH_PIPELINE && BH_FUSE_KICK && !last && e->n > 0 && !e->comm && !e->group &&
-           !e->solo && e->p.theta != 0.0;
+    return BH_PIPELINE && BH_FUSE_KICK && (!last || BH_PIPE_LAST) && e->n > 0 && !e->comm &&
+           !e->group && !e->solo && e->p.theta != 0.0;
 }
 
-int pipe_alloc(bh_engine *e) {
+int pipe_alloc(bh_engine *e, bool last) {
     if (e->nodes_alt_cap < e->node_cap) {
         TRY(dev_alloc(e, e->nodes_alt, e->node_cap));
         e->nodes_alt_cap = e->node_cap;
+    }
+    if (last && e->view_cap < e->cap) {
+        TRY(alloc_state(e, e->view, (size_t)e->cap));
+        e->view_cap = e->cap;
+    }
+    if (last && e->lt_walk_cap < e->cap) {
+        TRY(dev_alloc(e, e->lt_keys, (size_t)e->cap));
+        TRY(dev_alloc(e, e->lt_cpl, (size_t)e->cap));
+        TRY(dev_alloc(e, e->lt_base, (size_t)e->cap + 1));
+        e->lt_walk_cap = e->cap;
     }
     if (e->trav_cap < e->cap) {
         TRY(dev_alloc(e, e->m_trav, (size_t)e->cap));
@@ -1317,9 +1389,87 @@ int pipe_alloc(bh_engine *e) {
     return BH_OK;
 }
 
+// ---- the pinned caller-order mirror (bh_set_mirror / bh_map_bodies) -------------------
+// The front-end reads every body after every step (PNL:302-306).  With the mirror on, a call's
+// last step writes the bodies in the caller's order (after the call's removals, BHA:519) into
+// pinned host memory itself: positions and masses as soon as the merge rule is done, velocities
+// when the last traversal's kick is -- the device-to-host copies run on the DMA engines while the
+// overlapped next build (and the traversal's tail) still run.
+int mirror_alloc(bh_engine *e) {
+    if (e->mir_cap < e->cap) {
+        if (e->mir) (void)hipHostFree(e->mir);
+        e->mir = nullptr;
+        e->mir_cap = 0;
+        HIPCHK(e, hipHostMalloc((void **)&e->mir, sizeof(double) * 5 * (size_t)e->cap,
+                                hipHostMallocDefault));
+        TRY(dev_alloc(e, e->mir_stage, 5 * (size_t)e->cap));
+        TRY(dev_alloc(e, e->mir_keep, (size_t)e->cap));
+        TRY(dev_alloc(e, e->mir_pos, (size_t)e->cap));
+        const size_t tb = compact_scratch_bytes(e->cap);
+        if (e->mir_tmp) (void)hipFree(e->mir_tmp);
+        e->mir_tmp = nullptr;
+        HIPCHK(e, hipMalloc(&e->mir_tmp, tb));
+        e->mir_tmp_bytes = tb;
+        e->mir_cap = e->cap;
+        e->mir_fresh = false;
+    }
+    if (!e->mir_stream) {
+        int lo = 0, hi = 0;
+        HIPCHK(e, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(e, hipStreamCreateWithPriority(&e->mir_stream, hipStreamNonBlocking, hi));
+        for (hipEvent_t *ev : {&e->mir_ev, &e->mir_ev2, &e->mir_in[0], &e->mir_in[1]})
+            HIPCHK(e, hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    }
+    return BH_OK;
+}
+
+// src: the state the caller sees (tombstones of the running call still in it); its positions,
+// masses and caller indices are final once after_pos's queued work is, its velocities once
+// after_vel's is.  e->n bodies (before the call's compaction).
+int mirror_launch(bh_engine *e, const BodyState &src, hipStream_t after_pos, hipStream_t after_vel) {
+    TRY(mirror_alloc(e));
+    const int64_t n = e->n;
+    const int64_t c = e->mir_cap;
+    hipStream_t ms = e->mir_stream;
+    HIPCHK(e, hipEventRecord(e->mir_in[0], after_pos));
+    HIPCHK(e, hipEventRecord(e->mir_in[1], after_vel));
+    HIPCHK(e, hipStreamWaitEvent(ms, e->mir_in[0], 0));
+    if (n > 0) {
+        double *st = e->mir_stage;
+        HIPCHK(e, mirror_index(n, src.cidx, e->mir_keep, e->mir_pos, e->mir_tmp, e->mir_tmp_bytes,
+                               ms));
+        const double *s3[3] = {src.x, src.y, src.m};
+        double *d3[3] = {st, st + c, st + 4 * c};
+        mirror_scatter(n, src.cidx, e->mir_pos, 3, s3, d3, ms);
+        HIPCHK(e, hipGetLastError());
+        for (int j : {0, 1, 4})  // (the survivors are a prefix of each array)
+            HIPCHK(e, hipMemcpyAsync(e->mir + j * c, st + j * c, sizeof(double) * n,
+                                     hipMemcpyDeviceToHost, ms));
+        HIPCHK(e, hipStreamWaitEvent(ms, e->mir_in[1], 0));
+        const double *s2[2] = {src.vx, src.vy};
+        double *d2[2] = {st + 2 * c, st + 3 * c};
+        mirror_scatter(n, src.cidx, e->mir_pos, 2, s2, d2, ms);
+        HIPCHK(e, hipGetLastError());
+        HIPCHK(e, hipEventRecord(e->mir_ev2, ms));
+        for (int j : {2, 3})
+            HIPCHK(e, hipMemcpyAsync(e->mir + j * c, st + j * c, sizeof(double) * n,
+                                     hipMemcpyDeviceToHost, ms));
+    } else {
+        HIPCHK(e, hipStreamWaitEvent(ms, e->mir_in[1], 0));
+        HIPCHK(e, hipEventRecord(e->mir_ev2, ms));
+    }
+    HIPCHK(e, hipEventRecord(e->mir_ev, ms));
+    e->mir_launched = true;
+    return BH_OK;
+}
+
 // The second evaluation of a pipelined step: build, second traversal with the fused kick, and
 // next step's first build; e->prebuilt tells the next evaluation its tree is there.
-int evaluate_pipelined(bh_engine *e) {
+// last: the call's last step -- this step's tree is lastTree (BHA:435): its walk structures are
+// copied aside before the overlapped build reuses them, and the state before that build's jitter
+// (the previous slot order) becomes the caller-visible `view`.
+
+int evaluate_pipelined(bh_engine *e, bool last) {
     const int64_t n = e->n;
     hipStream_t s = e->stream;
     // the merge rule's mailbox header is cleared on the overlapped stream while this build runs
@@ -1351,7 +1501,21 @@ int evaluate_pipelined(bh_engine *e) {
     HIPCHK(e, hipGetLastError());
     TRY(mark(e, 1));
     TRY(wave_order_next(e, 0, n, s));
+    if (last) {
+        hipStream_t ps = e->pipe_stream;
+        // lastTree's walk (bh_get_quads): sorted keys, prefix lengths, node offsets
+        HIPCHK(e, hipMemcpyAsync(e->lt_keys, e->keys_s, sizeof(uint64_t) * n,
+                                 hipMemcpyDeviceToDevice, ps));
+        HIPCHK(e, hipMemcpyAsync(e->lt_cpl, e->cpl, (size_t)n, hipMemcpyDeviceToDevice, ps));
+        HIPCHK(e, hipMemcpyAsync(e->lt_base, e->base, sizeof(uint32_t) * (n + 1),
+                                 hipMemcpyDeviceToDevice, ps));
+        // the call's removal count before its last merge rule (finish_merges, BHA:526)
+        HIPCHK(e, hipMemcpyAsync(e->scalars + 8, e->scalars + 2, sizeof(uint32_t),
+                                 hipMemcpyDeviceToDevice, ps));
+    }
     TRY(merge(e, e->pipe_stream, merging));         // BHA:438
+    if (last && e->mirror_on)  // positions and masses are final: the caller-order copy-out starts
+        TRY(mirror_launch(e, e->st, e->pipe_stream, s));
     TRY(build_into(e, e->pipe_stream, true));       // step s+1's first tree (BHA:359)
     HIPCHK(e, hipEventRecord(e->pipe_ev[1], e->pipe_stream));
     HIPCHK(e, hipStreamWaitEvent(s, e->pipe_ev[1], 0));
@@ -1362,6 +1526,11 @@ int evaluate_pipelined(bh_engine *e) {
     std::swap(e->nodes, e->nodes_alt);
     std::swap(e->node_cap, e->nodes_alt_cap);
     e->prebuilt = true;
+    if (last) {  // the previous order's state (kicked, merged, not yet jittered) is what the caller sees
+        std::swap(e->view, e->alt);
+        e->view_pending = true;
+        e->lt_aside = true;
+    }
     return BH_OK;
 }
 
@@ -1394,7 +1563,7 @@ int step_once(bh_engine *e, bool last) {
     const int64_t n = e->n;
     const double dtHalf = e->p.dt * 0.5;  // BHA:412
     if (pipelined(e, last)) {
-        TRY(pipe_alloc(e));
+        TRY(pipe_alloc(e, last));
         bool fused = false;
         e->fuse_keys = true;  // and the second build's keys and bucket counts
         TRY(evaluate(e, nullptr, KICK_DRIFT, &fused, true));  // a(t), kick + drift fused
@@ -1402,7 +1571,7 @@ int step_once(bh_engine *e, bool last) {
             e->err = "pipelined step: the first evaluation did not fuse its kick";
             return BH_E_STATE;
         }
-        TRY(evaluate_pipelined(e));  // a(t+dt), the kick, the merge rule and the next tree
+        TRY(evaluate_pipelined(e, last));  // a(t+dt), the kick, the merge rule and the next tree
         e->tree_valid = true;
         return BH_OK;
     }
@@ -1445,7 +1614,7 @@ struct QuadWalker {
     const std::vector<uint64_t> &keys;
     const std::vector<int8_t> &cpl;
     const std::vector<uint32_t> &base;
-    bh_engine *e;
+    const Node *nodes;  // device
     double *cx, *cy, *h;
     int64_t cap, k = 0;
     int rc = BH_OK;
@@ -1479,7 +1648,7 @@ struct QuadWalker {
             int cp = lo > 0 ? (int)cpl[lo - 1] : -1;
             uint32_t ni = base[lo] + (uint32_t)(L - cp - 1);
             Node nd;
-            if (hipMemcpy(&nd, e->nodes + ni, sizeof(Node), hipMemcpyDeviceToHost) != hipSuccess) {
+            if (hipMemcpy(&nd, nodes + ni, sizeof(Node), hipMemcpyDeviceToHost) != hipSuccess) {
                 rc = BH_E_DEVICE;
                 return;
             }
@@ -1605,23 +1774,26 @@ static int agree_settings(bh_engine *e) {
     v[1] = e->let_forced ? 1.0 : 0.0;
     const double *cum = round_cum();
     for (int j = 0; j <= BH_SHARD_ROUNDS; ++j) v[2 + j] = cum[j];
-    double *d = nullptr;
-    if (hipMalloc((void **)&d, sizeof(double) * 3 * K) != hipSuccess) {
-        e->err = "agree_settings: hipMalloc";
-        return BH_E_DEVICE;
-    }
+    // device scratch from the engine's own buffers (allocated by ensure_capacity: no allocation
+    // that could fail on one rank only), and every rank takes part in both all-reduces whatever
+    // happened locally, so a local failure cannot leave the peers waiting in a collective
+    double *d = static_cast<double *>(e->scratch);
     double lo[K], hi[K];
     ncclResult_t nr = ncclSuccess;
+    if (!d || e->scratch_bytes < sizeof(double) * 3 * K) {
+        e->err = "agree_settings: no device scratch";
+        return BH_E_STATE;  // (every rank: the buffers are sized alike)
+    }
     hipError_t hr = hipMemcpyAsync(d, v, sizeof(v), hipMemcpyHostToDevice, e->stream);
-    if (hr == hipSuccess) nr = ncclAllReduce(d, d + K, K, ncclFloat64, ncclMin, e->comm, e->stream);
-    if (hr == hipSuccess && nr == ncclSuccess)
-        nr = ncclAllReduce(d, d + 2 * K, K, ncclFloat64, ncclMax, e->comm, e->stream);
-    if (hr == hipSuccess && nr == ncclSuccess)
-        hr = hipMemcpyAsync(lo, d + K, sizeof(lo), hipMemcpyDeviceToHost, e->stream);
-    if (hr == hipSuccess && nr == ncclSuccess)
-        hr = hipMemcpyAsync(hi, d + 2 * K, sizeof(hi), hipMemcpyDeviceToHost, e->stream);
-    if (hr == hipSuccess) hr = hipStreamSynchronize(e->stream);
-    (void)hipFree(d);
+    if (hr != hipSuccess)  // NaN bit patterns (if the device still takes a fill): no match
+        (void)hipMemsetAsync(d, 0xFF, sizeof(v), e->stream);
+    ncclResult_t n1 = ncclAllReduce(d, d + K, K, ncclFloat64, ncclMin, e->comm, e->stream);
+    ncclResult_t n2 = ncclAllReduce(d, d + 2 * K, K, ncclFloat64, ncclMax, e->comm, e->stream);
+    nr = n1 != ncclSuccess ? n1 : n2;
+    hipError_t h2 = hipMemcpyAsync(lo, d + K, sizeof(lo), hipMemcpyDeviceToHost, e->stream);
+    if (h2 == hipSuccess) h2 = hipMemcpyAsync(hi, d + 2 * K, sizeof(hi), hipMemcpyDeviceToHost, e->stream);
+    if (h2 == hipSuccess) h2 = hipStreamSynchronize(e->stream);
+    if (hr == hipSuccess) hr = h2;
     if (nr != ncclSuccess) {
         e->err = std::string("agree_settings: ") + ncclGetErrorString(nr);
         return BH_E_COMM;
@@ -1813,6 +1985,14 @@ void bh_destroy(bh_engine *e) {
         (void)hipStreamSynchronize(e->pipe_stream);
         (void)hipStreamDestroy(e->pipe_stream);
     }
+    if (e->mir_stream) {
+        (void)hipStreamSynchronize(e->mir_stream);
+        (void)hipStreamDestroy(e->mir_stream);
+    }
+    for (hipEvent_t ev : {e->mir_ev, e->mir_ev2, e->mir_in[0], e->mir_in[1]})
+        if (ev) (void)hipEventDestroy(ev);
+    if (e->mir) (void)hipHostFree(e->mir);
+    free_state(e->view);
     free_state(e->st);
     free_state(e->alt);
     free_state(e->snap);
@@ -1834,7 +2014,8 @@ void bh_destroy(bh_engine *e) {
                     e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaf_cover, e->leaves.rec,
                     e->leaf_tmp, e->spl, e->bcount, e->bstart, e->nodes_alt, e->wave_cost, e->run_order,
                     e->m_trav, e->cidx_trav, e->lanes_trav, e->T_trav, e->solo_xchg,
-                    e->lt_x, e->lt_y};
+                    e->lt_x, e->lt_y, e->lt_keys, e->lt_cpl, e->lt_base, e->mir_stage,
+                    e->mir_keep, e->mir_pos, e->mir_tmp};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     for (hipEvent_t ev : e->ev) (void)hipEventDestroy(ev);
@@ -1856,6 +2037,15 @@ int bh_set_params(bh_engine *e, const bh_params *p) {
     e->p = *p;
     if (geo_changed) {
         TRY(materialize_positions(e));
+        if (e->view_pending) {
+            // the prebuilt tree (and its jitter) belong to the old root cell: back to the state the
+            // caller sees, in its own slot order (the lane map described the prebuilt order)
+            std::swap(e->st, e->view);
+            e->view_pending = false;
+            e->lanes_valid = false;
+        }
+        e->prebuilt = false;
+        e->lt_aside = false;
         e->geo = g;
         e->tree_valid = false;
         e->lazy_tree = false;
@@ -1902,6 +2092,10 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     e->removed.clear();
     e->tree_valid = false;  // BHA:348
     e->lazy_tree = false;
+    e->prebuilt = false;    // other bodies: the pipelined call's next tree is void
+    e->view_pending = false;
+    e->lt_aside = false;
+    e->mir_fresh = false;
     e->spl_nb = 0;          // other bodies: the first build sorts from scratch
     e->keys_ready = false;
     e->lanes_valid = false;
@@ -1920,8 +2114,15 @@ int bh_step(bh_engine *e, int32_t k) {
     const bool may_let = k > 0 && e->n > 0 && (e->comm || e->group || e->solo) && let_active(e) &&
                          e->p.theta != 0.0;
     if (may_merge || may_let) TRY(snapshot(e));
+    // the previous call's pipelined last step built this call's first tree (a replay does not
+    // use it: restore() starts from the caller-visible state)
+    const bool carried = k > 0 && e->prebuilt;
+    if (k > 0) {
+        e->mir_fresh = false;
+        e->lt_aside = false;  // lastTree will be this call's (nodes_alt is rebuilt below)
+    }
     int let_replays = 0;
-    for (;;) {
+    for (bool first = true;; first = false) {
         e->ev_used = 0;
         e->timings_pending = false;
         // the subset splitters are trusted only within a call (another scene after a reset
@@ -1930,8 +2131,9 @@ int bh_step(bh_engine *e, int32_t k) {
         HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, 5 * sizeof(uint32_t), e->stream));
         e->removed.clear();
         e->merge_ran = false;
-        e->prebuilt = false;
+        if (k > 0) e->prebuilt = first && carried;
         e->lazy_tree = false;
+        e->mir_launched = false;
         for (int32_t s = 0; s < k; ++s) TRY(step_once(e, s + 1 == k));
         HIPCHK(e, hipStreamSynchronize(e->stream));
         if (may_let) {  // LET subset sizes of this call: [4] some rank overflowed, [5] largest
@@ -1980,6 +2182,14 @@ int bh_step(bh_engine *e, int32_t k) {
         if (tree_rc != BH_OK) return tree_rc;
         break;
     }
+    if (k > 0 && e->mirror_on) {
+        if (!e->mir_launched)  // the call's last step was not pipelined: copy out now
+            TRY(mirror_launch(e, e->view_pending ? e->view : e->st, e->stream, e->stream));
+        // the next call reuses the buffers the mirror's kernels read (not its host copies)
+        HIPCHK(e, hipStreamWaitEvent(e->stream, e->mir_ev2, 0));
+        e->mir_fresh = true;
+        e->mir_n = e->n;
+    }
     if (e->profiling) TRY(collect_timings(e));
     return BH_OK;
 }
@@ -1995,9 +2205,10 @@ int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, do
     TRY(materialize_positions(e));
     const int64_t n = e->n;
     if (n > 0) {  // back to caller (list) order, staged in the second state buffer
-        const double *src[5] = {e->st.x, e->st.y, e->st.vx, e->st.vy, e->st.m};
+        const BodyState &s = e->view_pending ? e->view : e->st;  // (not the prebuilt tree's jitter)
+        const double *src[5] = {s.x, s.y, s.vx, s.vy, s.m};
         double *stage[5] = {e->alt.x, e->alt.y, e->alt.vx, e->alt.vy, e->alt.m};
-        scatter_to_caller(n, e->st.cidx, 5, src, stage, e->stream);
+        scatter_to_caller(n, s.cidx, 5, src, stage, e->stream);
         HIPCHK(e, hipGetLastError());
         double *dst[5] = {x, y, vx, vy, m};
         for (int k = 0; k < 5; ++k)
@@ -2006,6 +2217,38 @@ int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, do
                                          hipMemcpyDeviceToHost, e->stream));
     }
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    return BH_OK;
+}
+
+int bh_set_mirror(bh_engine *e, int enabled) {
+    if (!e) return BH_E_INVALID;
+    HIPCHK(e, hipSetDevice(e->device));
+    e->mirror_on = enabled != 0;
+    if (e->mirror_on) TRY(mirror_alloc(e));
+    return BH_OK;
+}
+
+int bh_map_bodies(bh_engine *e, const double **x, const double **y, const double **vx,
+                  const double **vy, const double **m, int64_t *n_out) {
+    if (!e) return BH_E_INVALID;
+    HIPCHK(e, hipSetDevice(e->device));
+    if (!e->mir_fresh || e->mir_cap < e->n) {  // not written by the last call: copy out now
+        TRY(materialize_positions(e));
+        e->mir_launched = false;
+        TRY(mirror_launch(e, e->view_pending ? e->view : e->st, e->stream, e->stream));
+        HIPCHK(e, hipStreamWaitEvent(e->stream, e->mir_ev2, 0));
+        e->mir_fresh = true;
+        e->mir_n = e->n;
+    }
+    HIPCHK(e, hipEventSynchronize(e->mir_ev));
+    const int64_t c = e->mir_cap;
+    const double *b = e->mir;
+    if (x) *x = b;
+    if (y) *y = b + c;
+    if (vx) *vx = b + 2 * c;
+    if (vy) *vy = b + 3 * c;
+    if (m) *m = b + 4 * c;
+    if (n_out) *n_out = e->mir_n;
     return BH_OK;
 }
 
@@ -2018,6 +2261,7 @@ int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visi
     HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
     if (n > 0) {
         TRY(evaluate(e, visits ? e->visits32 : nullptr));
+        e->mir_fresh = false;
         scatter_acc_to_caller(n, e->st.cidx, e->a2, e->ax, e->ay, e->stream, e->a2_lanes,
                               e->a2_layout);
         HIPCHK(e, hipGetLastError());
@@ -2077,12 +2321,29 @@ int bh_get_quads(bh_engine *e, double *cx, double *cy, double *h, int64_t cap, i
             tb.spl_nb = 0;                    // the caller's splitters describe another order
             tb.lanes_remap = nullptr;
             HIPCHK(e, tree_build(tb, n, e->geo, e->stream));
+            if (!e->lazy_tree) {
+                // getTreeForDebug's fresh buildTree moves the bodies it jitters (BHA:146-151,
+                // 329-331): the moved positions go back into the replica in its own slot order
+                // (every rank makes the same calls, so the replicas stay equal)
+                unpermute_positions(n, e->perm, tb.dst.x, tb.dst.y, e->st.x, e->st.y, e->stream);
+                HIPCHK(e, hipGetLastError());
+                e->mir_fresh = false;
+            }
             e->spl_nb = 0;  // k_prep wrote splitters of this order
             e->keys_ready = false;
             TRY(check_tree_flags(e));
         } else {
             HIPCHK(e, hipMemsetAsync(e->base, 0, sizeof(uint32_t), e->stream));
         }
+        e->tree_valid = true;  // until the next step (a second call walks the same tree)
+    } else if (!e->tree_valid && e->view_pending) {
+        // getTreeForDebug's fresh tree (BHA:329-332) is the one the pipelined call already built
+        // from the caller's bodies after its merge rule: its jitter becomes part of the state, and
+        // the next step builds its own first tree from these positions (BHA:407)
+        e->view_pending = false;
+        e->prebuilt = false;
+        e->mir_fresh = false;
+        e->tree_valid = true;
     } else if (!e->tree_valid) {  // getTreeForDebug builds a fresh tree (BHA:329-332)
         HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
         TRY(build(e));
@@ -2092,15 +2353,19 @@ int bh_get_quads(bh_engine *e, double *cx, double *cy, double *h, int64_t cap, i
     std::vector<int8_t> cpl((size_t)n);
     std::vector<uint32_t> base((size_t)n + 1);
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    // lastTree kept aside by a pipelined last step, or the tree in the build buffers
+    const bool aside = e->tree_valid && e->lt_aside;
     if (n > 0) {
-        HIPCHK(e, hipMemcpy(keys.data(), e->keys_s, sizeof(uint64_t) * n, hipMemcpyDeviceToHost));
-        HIPCHK(e, hipMemcpy(cpl.data(), e->cpl, n, hipMemcpyDeviceToHost));
-        HIPCHK(e, hipMemcpy(base.data(), e->base, sizeof(uint32_t) * (n + 1), hipMemcpyDeviceToHost));
+        HIPCHK(e, hipMemcpy(keys.data(), aside ? e->lt_keys : e->keys_s, sizeof(uint64_t) * n,
+                            hipMemcpyDeviceToHost));
+        HIPCHK(e, hipMemcpy(cpl.data(), aside ? e->lt_cpl : e->cpl, n, hipMemcpyDeviceToHost));
+        HIPCHK(e, hipMemcpy(base.data(), aside ? e->lt_base : e->base, sizeof(uint32_t) * (n + 1),
+                            hipMemcpyDeviceToHost));
     }
     int64_t M = 0;
     const uint64_t SENT = sentinel_key(e->geo.J);
     while (M < n && keys[(size_t)M] != SENT) ++M;
-    QuadWalker w{e->geo, keys, cpl, base, e, cx, cy, h, cap};
+    QuadWalker w{e->geo, keys, cpl, base, aside ? e->nodes_alt : e->nodes, cx, cy, h, cap};
     w.rec(0, 0, M, e->geo.root_cx, e->geo.root_cy, e->geo.root_h);
     if (w.rc != BH_OK) return w.rc;
     if (n_out) *n_out = w.k;
@@ -2126,7 +2391,8 @@ int bh_last_timings(const bh_engine *e, double *out5) {
 int64_t bh_last_tree_nodes(const bh_engine *e) {
     if (!e || e->n <= 0) return 0;
     uint32_t T = 0;
-    if (hipMemcpy(&T, e->base + e->n, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+    const uint32_t *base = e->lt_aside ? e->lt_base : e->base;
+    if (hipMemcpy(&T, base + e->n, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
         return -1;
     return T;
 }

@@ -84,6 +84,32 @@ __global__ __launch_bounds__(TB) void k_scatter_caller(int64_t n, const uint32_t
     for (int j = 0; j < k; ++j) p.dst[j][o] = p.src[j][i];
 }
 
+// Caller-order mirror (engine.cpp bh_map_bodies): at the end of a bh_step call, before its
+// compaction, the state holds every caller index of the list the call started from exactly once
+// (tombstones keep theirs), so keep[c] = "c survives" over caller indices, its exclusive scan
+// pos[c] = c's index in the list after the removals (BHA:519), and the live bodies scatter there.
+// These kernels run next to the last traversal (wave priority, like the overlapped build).
+__global__ __launch_bounds__(TB) void k_mirror_keep(int64_t n, const uint32_t *__restrict__ cidx,
+                                                    uint32_t *__restrict__ keep) {
+    chain_prio();
+    const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = cidx[i];
+    keep[c & ~CIDX_DEAD] = (c & CIDX_DEAD) ? 0u : 1u;
+}
+
+__global__ __launch_bounds__(TB) void k_mirror_scatter(int64_t n, const uint32_t *__restrict__ cidx,
+                                                       const uint32_t *__restrict__ pos, int k,
+                                                       Ptrs5 p) {
+    chain_prio();
+    const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t c = cidx[i];
+    if (c & CIDX_DEAD) return;
+    const uint32_t o = pos[c];
+    for (int j = 0; j < k; ++j) p.dst[j][o] = p.src[j][i];
+}
+
 __global__ __launch_bounds__(TB) void k_scatter_acc(int64_t n, const uint32_t *__restrict__ cidx,
                                                     const double *__restrict__ a2,
                                                     double *__restrict__ ax,
@@ -603,6 +629,27 @@ void scatter_to_caller(int64_t n, const uint32_t *cidx, int k, const double *con
         p.dst[j] = dst[j];
     }
     k_scatter_caller<<<grid_for(n), TB, 0, s>>>(n, cidx, k < 5 ? k : 5, p);
+}
+
+hipError_t mirror_index(int64_t n, const uint32_t *cidx, uint32_t *keep, uint32_t *pos, void *tmp,
+                        size_t tmp_bytes, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    k_mirror_keep<<<grid_for(n), TB, 0, s>>>(n, cidx, keep);
+    hipError_t st = rocprim::exclusive_scan(tmp, tmp_bytes, keep, pos, 0u, (size_t)n,
+                                            rocprim::plus<uint32_t>(), s);
+    if (st != hipSuccess) return st;
+    return hipGetLastError();
+}
+
+void mirror_scatter(int64_t n, const uint32_t *cidx, const uint32_t *pos, int k,
+                    const double *const *src, double *const *dst, hipStream_t s) {
+    if (n <= 0) return;
+    Ptrs5 p{};
+    for (int j = 0; j < k && j < 5; ++j) {
+        p.src[j] = src[j];
+        p.dst[j] = dst[j];
+    }
+    k_mirror_scatter<<<grid_for(n), TB, 0, s>>>(n, cidx, pos, k < 5 ? k : 5, p);
 }
 
 void scatter_acc_to_caller(int64_t n, const uint32_t *cidx, const double *a2, double *ax,

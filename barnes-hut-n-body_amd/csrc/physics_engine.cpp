@@ -28,6 +28,7 @@ PhysicsEngine::PhysicsEngine(std::vector<Body> &initialBodies, int device)
     bh_default_params(&p);
     int rc = bh_create(&p, device, &eng_);
     if (rc != BH_OK) throw std::runtime_error("bh_create failed (rc=" + std::to_string(rc) + ")");
+    check(bh_set_mirror(eng_, 1));  // every step writes the caller-order bodies to pinned memory
     pushParams();
     pushBodies();
 }
@@ -76,10 +77,9 @@ void PhysicsEngine::pullBodies(bool afterStep) {
         check(bh_last_removed(eng_, rem.data(), cnt, &cnt));
         for (auto it = rem.rbegin(); it != rem.rend(); ++it) bodies_->erase(bodies_->begin() + *it);
     }
-    const int64_t n = bh_num_bodies(eng_);
-    std::vector<double> x(n), y(n), vx(n), vy(n), m(n);
+    const double *x, *y, *vx, *vy, *m;  // the engine's pinned mirror, filled by the step itself
     int64_t got = 0;
-    check(bh_get_bodies(eng_, x.data(), y.data(), vx.data(), vy.data(), m.data(), n, &got));
+    check(bh_map_bodies(eng_, &x, &y, &vx, &vy, &m, &got));
     if ((int64_t)bodies_->size() != got) throw std::runtime_error("engine and caller lists diverged");
     for (int64_t i = 0; i < got; ++i) (*bodies_)[(size_t)i] = Body{x[i], y[i], vx[i], vy[i], m[i]};
     shadow_ = *bodies_;

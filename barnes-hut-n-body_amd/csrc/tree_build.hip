@@ -1421,6 +1421,23 @@ void permute_velocities(int64_t n, const uint32_t *perm, const double *svx, cons
     if (n > 0) k_permute_vel<<<grid_for(n), TB, 0, s>>>(n, perm, svx, svy, dvx, dvy);
 }
 
+__global__ __launch_bounds__(TB) void k_unpermute_pos(int64_t n, const uint32_t *__restrict__ perm,
+                                                      const double *__restrict__ sx,
+                                                      const double *__restrict__ sy,
+                                                      double *__restrict__ dx,
+                                                      double *__restrict__ dy) {
+    const int64_t a = (int64_t)xcd_block() * TB + threadIdx.x;
+    if (a >= n) return;
+    const uint32_t i = perm[a];
+    dx[i] = sx[a];
+    dy[i] = sy[a];
+}
+
+void unpermute_positions(int64_t n, const uint32_t *perm, const double *sx, const double *sy,
+                         double *dx, double *dy, hipStream_t s) {
+    if (n > 0) k_unpermute_pos<<<grid_for(n), TB, 0, s>>>(n, perm, sx, sy, dx, dy);
+}
+
 hipError_t lane_order(const TreeBuffers &b, int64_t n, int J, bool refresh, uint32_t *lanes,
                       hipStream_t s) {
     if (n <= 0) return hipSuccess;

@@ -42,18 +42,25 @@ JNIEXPORT void JNICALL Java_Native_setParams(JNIEnv *env, jobject self, jlong h,
         throw_rt(env, e, "setParams");
 }
 
-/* external fun reset(h: Long, n: Int, soa: DoubleArray) */
+/* external fun reset(h: Long, n: Int, soa: DoubleArray)
+ * The Java array is copied into a native buffer first (GetDoubleArrayRegion): no device work runs
+ * while the JVM holds an array pinned, and the GC is never stalled by the upload. */
 JNIEXPORT void JNICALL Java_Native_reset(JNIEnv *env, jobject self, jlong h, jint n,
                                          jdoubleArray soa) {
     (void)self;
     bh_engine *e = (bh_engine *)(intptr_t)h;
-    if (n < 0 || (*env)->GetArrayLength(env, soa) < 5 * (jsize)n) {
-        throw_rt(env, NULL, "reset: the SoA array must hold 5 n doubles");
+    if (n < 0 || n > INT32_MAX / 5 || !soa || (*env)->GetArrayLength(env, soa) < 5 * (jsize)n) {
+        throw_rt(env, NULL, "reset: the SoA array must hold 5 n doubles (n < 2^31 / 5)");
         return;
     }
-    jdouble *a = (*env)->GetPrimitiveArrayCritical(env, soa, NULL);
+    double *a = (double *)malloc(sizeof(double) * (5 * (size_t)n + 1));
+    if (!a) {
+        throw_rt(env, NULL, "reset: out of memory");
+        return;
+    }
+    if (n > 0) (*env)->GetDoubleArrayRegion(env, soa, 0, 5 * (jsize)n, a);
     const int rc = bh_shim_reset(e, (int64_t)n, a);
-    (*env)->ReleasePrimitiveArrayCritical(env, soa, a, JNI_ABORT); /* read only */
+    free(a);
     if (rc != BH_OK) throw_rt(env, e, "reset");
 }
 
@@ -64,22 +71,26 @@ JNIEXPORT void JNICALL Java_Native_step(JNIEnv *env, jobject self, jlong h, jint
     if (bh_shim_step(e, (int32_t)k) != BH_OK) throw_rt(env, e, "step");
 }
 
-/* external fun get(h: Long): DoubleArray  (SoA, length 5 N) */
+/* external fun get(h: Long): DoubleArray  (SoA, length 5 N)
+ * Filled from the engine's pinned caller-order mirror (bh_map_bodies), which the step wrote
+ * itself: five SetDoubleArrayRegion copies, no device call while a Java array is held. */
 JNIEXPORT jdoubleArray JNICALL Java_Native_get(JNIEnv *env, jobject self, jlong h) {
     (void)self;
     bh_engine *e = (bh_engine *)(intptr_t)h;
+    const double *f[5] = {NULL, NULL, NULL, NULL, NULL};
     int64_t n = 0;
-    int rc = bh_shim_get(e, NULL, 0, &n);
-    if (rc != BH_OK && rc != BH_E_CAPACITY) {
+    if (bh_shim_map(e, f, &n) != BH_OK) {
         throw_rt(env, e, "get");
         return NULL;
     }
+    if (n > INT32_MAX / 5) {
+        throw_rt(env, NULL, "get: more bodies than a Java array holds (5 n >= 2^31)");
+        return NULL;
+    }
     jdoubleArray out = (*env)->NewDoubleArray(env, (jsize)(5 * n));
-    if (!out || n == 0) return out;
-    jdouble *a = (*env)->GetPrimitiveArrayCritical(env, out, NULL);
-    rc = bh_shim_get(e, a, n, &n);
-    (*env)->ReleasePrimitiveArrayCritical(env, out, a, 0);
-    if (rc != BH_OK) throw_rt(env, e, "get");
+    if (!out || n == 0) return out; /* NULL: OutOfMemoryError is pending */
+    for (int k = 0; k < 5; ++k)
+        (*env)->SetDoubleArrayRegion(env, out, (jsize)(k * n), (jsize)n, f[k]);
     return out;
 }
 
@@ -91,6 +102,10 @@ JNIEXPORT jdoubleArray JNICALL Java_Native_quads(JNIEnv *env, jobject self, jlon
     int rc = bh_shim_quads(e, NULL, 0, &nq); /* builds the tree if the cache was dropped */
     if (rc != BH_OK && rc != BH_E_CAPACITY) {
         throw_rt(env, e, "quads");
+        return NULL;
+    }
+    if (nq > INT32_MAX / 3) {
+        throw_rt(env, NULL, "quads: more cells than a Java array holds");
         return NULL;
     }
     double *q = (double *)malloc(sizeof(double) * (size_t)(3 * nq + 1));
@@ -118,6 +133,10 @@ JNIEXPORT jintArray JNICALL Java_Native_lastRemoved(JNIEnv *env, jobject self, j
     int rc = bh_shim_last_removed(e, NULL, 0, &cnt);
     if (rc != BH_OK && rc != BH_E_CAPACITY) {
         throw_rt(env, e, "lastRemoved");
+        return NULL;
+    }
+    if (cnt > INT32_MAX) {
+        throw_rt(env, NULL, "lastRemoved: more removals than a Java array holds");
         return NULL;
     }
     int32_t *idx = (int32_t *)malloc(sizeof(int32_t) * (size_t)(cnt + 1));

@@ -6,7 +6,13 @@
 int bh_shim_create(int device, bh_engine **out) {
     bh_params p;
     bh_default_params(&p); /* Config.kt defaults (CFG:5-23); setParams follows before any step */
-    return bh_create(&p, device, out);
+    int rc = bh_create(&p, device, out);
+    if (rc == BH_OK) rc = bh_set_mirror(*out, 1); /* getBodies after every frame (PNL:302) */
+    if (rc != BH_OK && *out) {
+        bh_destroy(*out);
+        *out = NULL;
+    }
+    return rc;
 }
 
 int bh_shim_set_params(bh_engine *e, double G, double dt, double theta, double soft2,
@@ -41,6 +47,11 @@ int bh_shim_get(bh_engine *e, double *soa, int64_t cap, int64_t *n) {
     return bh_get_bodies(e, soa, soa + cnt, soa + 2 * cnt, soa + 3 * cnt, soa + 4 * cnt, cnt, &got);
 }
 
+int bh_shim_map(bh_engine *e, const double *soa[5], int64_t *n) {
+    if (!soa || !n) return BH_E_INVALID;
+    return bh_map_bodies(e, &soa[0], &soa[1], &soa[2], &soa[3], &soa[4], n);
+}
+
 int bh_shim_quads(bh_engine *e, double *q, int64_t cap, int64_t *nq) {
     int64_t need = 0;
     int rc = bh_get_quads(e, NULL, NULL, NULL, 0, &need);
@@ -53,7 +64,7 @@ int bh_shim_quads(bh_engine *e, double *q, int64_t cap, int64_t *nq) {
     int64_t got = 0;
     rc = bh_get_quads(e, tmp, tmp + need, tmp + 2 * need, need, &got);
     if (rc == BH_OK) {
-        for (int64_t i = 0; i < got; ++i) { /* BHTree.fromQuads reads triples */
+        for (int64_t i = 0; i < got; ++i) { /* QuadList reads triples */
             q[3 * i] = tmp[i];
             q[3 * i + 1] = tmp[need + i];
             q[3 * i + 2] = tmp[2 * need + i];

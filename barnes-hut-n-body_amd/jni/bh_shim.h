@@ -3,7 +3,7 @@
  * over the C-ABI (include/bh_engine.h): no JNI types, so tests/c/abi_harness.c drives exactly
  * this code against the oracle, and bh_jni.c only moves Java arrays in and out.
  *
- * Array layouts are the Kotlin shim's (PhysicsEngine.soa() / pull() / BHTree.fromQuads):
+ * Array layouts are the Kotlin shim's (PhysicsEngine.soa() / pull() / QuadList (kotlin/PhysicsEngine.kt)):
  *   bodies  SoA, 5 n doubles: x[0..n) y[0..n) vx[0..n) vy[0..n) m[0..n)   (BHA:21-25)
  *   quads   interleaved triples cx, cy, h in visitQuads pre-order          (BHA:265-274)
  *   removed int32 list indices, ascending, relative to the list before the last step (BHA:519)
@@ -20,7 +20,8 @@
 extern "C" {
 #endif
 
-/* Native.create(device): PhysicsEngine's engine (BHA:287) on HIP device `device`. */
+/* Native.create(device): PhysicsEngine's engine (BHA:287) on HIP device `device`, with the
+ * pinned body mirror on (every step writes the caller-order bodies to host memory itself). */
 int bh_shim_create(int device, bh_engine **out);
 
 /* Native.setParams: Config.G / DT / theta / SOFT2 / WIDTH_PX / HEIGHT_PX (CFG:5-23) and
@@ -38,6 +39,10 @@ int bh_shim_step(bh_engine *e, int32_t k);
 /* Native.get: getBodies() (BHA:335) into a 5 cap SoA array; *n = body count.  cap < n:
  * BH_E_CAPACITY with *n set (size query with soa = NULL, cap = 0). */
 int bh_shim_get(bh_engine *e, double *soa, int64_t cap, int64_t *n);
+
+/* Native.get's source: the engine's pinned caller-order mirror (bh_map_bodies) -- soa[0..5)
+ * point at x, y, vx, vy, m of *n bodies, valid until the next call that changes the bodies. */
+int bh_shim_map(bh_engine *e, const double *soa[5], int64_t *n);
 
 /* Native.quads: getTreeForDebug().visitQuads{} (BHA:265-274, 329-332) as 3 cap interleaved
  * doubles; *nq = quad count.  cap < nq: BH_E_CAPACITY with *nq set (size query). */

@@ -1,0 +1,36 @@
+// Native.kt -- the JNI natives of the drop-in PhysicsEngine (PhysicsEngine.kt), implemented by
+// barnes-hut-n-body_amd/jni/bh_jni.c (Java_Native_*) over the C-ABI include/bh_engine.h.
+// Build the library where a JDK exists:
+//     make -C barnes-hut-n-body_amd jni JAVA_HOME=/path/to/jdk      -> lib/libbh_jni.so
+// and run with -Djava.library.path=barnes-hut-n-body_amd/lib.
+// tests/test_kotlin_dropin.py checks these declarations against bh_jni.c's exports.
+
+object Native {
+    init {
+        System.loadLibrary("bh_jni")
+    }
+
+    /** bh_create on HIP device `device`; the engine fills its pinned body mirror every step. */
+    external fun create(device: Int): Long
+
+    /** bh_set_params: Config.G/DT/theta/SOFT2/WIDTH_PX/HEIGHT_PX (CFG:5-23) + merge knobs. */
+    external fun setParams(
+        h: Long, G: Double, dt: Double, theta: Double, soft2: Double,
+        w: Int, hgt: Int, mergeMaxMass: Double, mergeMinDist: Double
+    )
+
+    /** bh_reset_bodies from SoA [x..., y..., vx..., vy..., m...] of n bodies. */
+    external fun reset(h: Long, n: Int, soa: DoubleArray)
+
+    /** bh_step(k). */
+    external fun step(h: Long, k: Int)
+
+    /** The bodies as SoA (length 5 N), caller order (bh_map_bodies: the pinned mirror). */
+    external fun get(h: Long): DoubleArray
+
+    /** bh_get_quads as interleaved (cx, cy, h) triples in visitQuads order. */
+    external fun quads(h: Long): DoubleArray
+
+    /** bh_last_removed: list indices the last step() removed (BHA:519). */
+    external fun lastRemoved(h: Long): IntArray
+}

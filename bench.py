@@ -75,6 +75,9 @@ def parse():
     ap.add_argument("--no-verify", dest="verify", action="store_false")
     ap.add_argument("--no-single-gpu", action="store_true",
                     help="N > 1: skip rank 0's one-GPU run of the same workload")
+    ap.add_argument("--no-drop-in", action="store_true",
+                    help="skip the one-step-per-call leg (the front-end's call pattern)")
+    ap.add_argument("--drop-in-calls", type=int, default=20)
     ap.add_argument("--dry-run", action="store_true",
                     help="print the launch plan (the torchrun child command for N > 1) and exit")
     return ap.parse_args()
@@ -252,13 +255,47 @@ def verify_leg(bh_amd, eng, case, arrs, dist, rank, world):
             "source": "tests/golden/digests.json (SHA-256 of the CPU oracle's final state)"}
 
 
+def available_processors():
+    """The reference's worker count, Runtime.getRuntime().availableProcessors() (BHA:292, used
+    at BHA:377 and 470): the CPUs this process may run on, bounded by the cgroup CPU quota the
+    way a container-aware JVM bounds it.  Returns (count, details)."""
+    import math
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        affinity = os.cpu_count() or 1
+    quota = None
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as fh:
+                q, period = fh.read().split()[:2]
+            if q != "max":
+                quota = max(1, math.ceil(int(q) / int(period)))
+        except (OSError, ValueError):
+            pass
+    count = min(affinity, quota) if quota else affinity
+    return count, {"os_cpu_count": os.cpu_count(), "sched_affinity": affinity,
+                   "cgroup_cpu_quota": quota}
+
+
 def cpu_baseline_leg(args, arrs, scene_name, direct):
     """The reference CPU path, restated in C (oracle/bh_oracle.c: serial pointer-tree build,
     `threads` workers on an atomic body queue, BHA:359-395), on a bounded sample of the same
-    workload, timed on this host's cores."""
+    workload, timed on this host's cores with the reference's own thread policy
+    (availableProcessors(), BHA:292)."""
+    res = _cpu_baseline(args, arrs, scene_name, direct)
+    res["host"] = args._cpu_host
+    res["thread_policy"] = ("availableProcessors() (BHA:292): sched affinity bounded by the "
+                            "cgroup CPU quota" if not args.cpu_threads else "--cpu-threads")
+    return res
+
+
+def _cpu_baseline(args, arrs, scene_name, direct):
     import numpy as np
     import oracle
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    avail, host = available_processors()
+    args._cpu_host = host
+    threads = args.cpu_threads or avail
     n0 = len(arrs[0])
     if direct:
         # theta = 0: one evaluation of a body subsample through the oracle's tree walk (every
@@ -328,6 +365,57 @@ def single_gpu_leg(bh_amd, params, device, arrs, steps, warmup):
     return {"value": round(0.5 * (n0 + n1) * steps / el, 1), "unit": "body-steps/s",
             "ms_per_step": round(1e3 * el / max(steps, 1), 4), "n_gpus": 1,
             "note": "rank 0's GPU alone, single-GPU engine, same scene / steps / warmup"}
+
+
+def drop_in_leg(eng, steps, warmup=2):
+    """The front-end's own call pattern (NBodyPanel.kt:290-293 tick() -> engine.step(), then
+    paintComponent reads every body, NBodyPanel.kt:302-306): one bh_step(1) call per frame.
+    Timed on the engine's current state (after the batched timed region), three ways:
+    step only; step + bh_get_bodies into pageable numpy arrays (the plain copying ABI);
+    step + bh_map_bodies (the engine's pinned caller-order mirror, written by the step itself
+    while its last build overlaps -- what the JNI shim reads)."""
+    import numpy as np
+    out = {"calls": steps, "steps_per_call": 1}
+
+    def timed(fn):
+        for _ in range(warmup):
+            fn()
+        eng.synchronize()
+        n0 = eng.num_bodies()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            fn()
+        eng.synchronize()
+        el = time.perf_counter() - t0
+        return 1e3 * el / steps, 0.5 * (n0 + eng.num_bodies()) * steps / el
+
+    def step_only():
+        eng.step(1)
+
+    def step_copy():
+        eng.step(1)
+        eng.get_bodies()
+
+    ms, v = timed(step_only)
+    out.update(ms_per_step=round(ms, 4), value=round(v, 1))
+    ms, v = timed(step_copy)
+    out.update(ms_per_step_with_get_bodies=round(ms, 4), value_with_get_bodies=round(v, 1))
+    if hasattr(eng, "set_mirror"):
+        eng.set_mirror(True)
+        sink = np.zeros(1)
+
+        def step_map():
+            eng.step(1)
+            x, y, vx, vy, m = eng.map_bodies()
+            sink[0] += x[-1] + m[0]  # touch the mapped arrays (the caller reads them)
+
+        ms, v = timed(step_map)
+        eng.set_mirror(False)
+        out.update(ms_per_step_with_mirror=round(ms, 4), value_with_mirror=round(v, 1))
+    out["note"] = ("one bh_step(1) call per frame as the Swing front-end does; 'with_get_bodies' "
+                   "adds the 40 B/body caller-order copy-out to pageable host memory; "
+                   "'with_mirror' reads the pinned mirror the step fills asynchronously")
+    return out
 
 
 def main():
@@ -508,6 +596,10 @@ def main():
     roofline.update(extra)
 
     # rank 0's extra legs; the other ranks wait at the next collective
+    drop_in = None
+    if world == 1 and not args.no_drop_in:
+        drop_in = drop_in_leg(eng, args.drop_in_calls)
+        drop_in["ms_per_step_batched"] = round(ms_per_step, 4)
     single = None
     if rank == 0 and world > 1 and not args.no_single_gpu:
         single = single_gpu_leg(bh_amd, params, local_rank, arrs, args.steps, args.warmup)
@@ -558,6 +650,8 @@ def main():
             "cpu_baseline": cpu_baseline,
             "verify": verify,
         }
+        if drop_in is not None:
+            line["drop_in"] = drop_in
         if rccl is not None:
             line["rccl"] = rccl
         if single is not None:

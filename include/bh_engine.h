@@ -141,6 +141,19 @@ int64_t bh_num_bodies(const bh_engine *e);
 int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, double *m,
                   int64_t cap, int64_t *n_out);
 
+/* getBodies() without a copy (BHA:335; NBodyPanel reads every body after every step,
+ * PNL:302-306): a pinned host mirror of the bodies in the caller's list order.
+ * bh_set_mirror(e, 1) makes every bh_step call write it itself -- positions and masses while
+ * its last traversal still runs, velocities right after -- so the device-to-host copy overlaps
+ * the call's last tree build.  bh_map_bodies waits for that copy (or makes one if the state
+ * changed since) and returns pointers to x[N], y[N], vx[N], vy[N], m[N] (any pointer may be
+ * NULL).  They stay valid -- and the data unchanged -- until the next call on this engine that
+ * changes or moves the bodies (bh_step, bh_reset_bodies, bh_get_quads, bh_compute_accelerations,
+ * bh_load_state, bh_set_mirror, bh_destroy). */
+int bh_set_mirror(bh_engine *e, int enabled);
+int bh_map_bodies(bh_engine *e, const double **x, const double **y, const double **vx,
+                  const double **vy, const double **m, int64_t *n_out);
+
 /* buildTree() + computeAccelerations() (BHA:359-395) on the current state, exactly as
  * the first half of step() does it (including the jitter's position mutation).  ax/ay
  * (length N, caller order) receive F/m.  visits (nullable, length N) receives the number

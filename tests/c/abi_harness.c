@@ -174,7 +174,7 @@ static void shim_step(Shim *s) {
     shim_pull(s, 1);
 }
 
-/* getTreeForDebug(): Native.quads (BHTree.fromQuads: interleaved triples), then pull(false);
+/* getTreeForDebug(): Native.quads (QuadList: interleaved triples), then pull(false);
  * returned de-interleaved (cx[], cy[], h[]) for the comparison with the oracle */
 static double *shim_tree(Shim *s, int64_t *nq) {
     shim_params(s);

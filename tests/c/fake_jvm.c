@@ -39,17 +39,6 @@ static jsize get_length(JNIEnv *env, jarray a) {
     (void)env;
     return a->len;
 }
-static void *get_critical(JNIEnv *env, jarray a, jboolean *is_copy) {
-    (void)env;
-    if (is_copy) *is_copy = 0;
-    return a->data;
-}
-static void release_critical(JNIEnv *env, jarray a, void *c, jint mode) {
-    (void)env;
-    (void)a;
-    (void)c;
-    (void)mode;
-}
 static jdoubleArray new_double_array(JNIEnv *env, jsize len) {
     (void)env;
     return new_array(len, sizeof(jdouble));
@@ -58,6 +47,16 @@ static void set_double_region(JNIEnv *env, jdoubleArray a, jsize start, jsize le
                               const jdouble *buf) {
     (void)env;
     memcpy(a->data + sizeof(jdouble) * (size_t)start, buf, sizeof(jdouble) * (size_t)len);
+}
+static void get_double_region(JNIEnv *env, jdoubleArray a, jsize start, jsize len,
+                              jdouble *buf) {
+    (void)env;
+    if (start < 0 || len < 0 || start + len > a->len) { /* ArrayIndexOutOfBoundsException */
+        snprintf(pending, sizeof(pending), "GetDoubleArrayRegion out of bounds");
+        has_pending = 1;
+        return;
+    }
+    memcpy(buf, a->data + sizeof(jdouble) * (size_t)start, sizeof(jdouble) * (size_t)len);
 }
 static jintArray new_int_array(JNIEnv *env, jsize len) {
     (void)env;
@@ -69,8 +68,14 @@ static void set_int_region(JNIEnv *env, jintArray a, jsize start, jsize len, con
 }
 
 static const struct JNINativeInterface_ table = {
-    find_class,       throw_new,        get_length,     get_critical, release_critical,
-    new_double_array, set_double_region, new_int_array, set_int_region,
+    .FindClass = find_class,
+    .ThrowNew = throw_new,
+    .GetArrayLength = get_length,
+    .NewDoubleArray = new_double_array,
+    .SetDoubleArrayRegion = set_double_region,
+    .GetDoubleArrayRegion = get_double_region,
+    .NewIntArray = new_int_array,
+    .SetIntArrayRegion = set_int_region,
 };
 static JNIEnv env_ptr = &table;
 

@@ -11,7 +11,6 @@
 
 #define JNIEXPORT __attribute__((visibility("default")))
 #define JNICALL
-#define JNI_ABORT 2
 
 typedef int32_t jint;
 typedef int64_t jlong;
@@ -32,11 +31,11 @@ struct JNINativeInterface_ {
     jclass (*FindClass)(JNIEnv *env, const char *name);
     jint (*ThrowNew)(JNIEnv *env, jclass clazz, const char *msg);
     jsize (*GetArrayLength)(JNIEnv *env, jarray array);
-    void *(*GetPrimitiveArrayCritical)(JNIEnv *env, jarray array, jboolean *isCopy);
-    void (*ReleasePrimitiveArrayCritical)(JNIEnv *env, jarray array, void *carray, jint mode);
     jdoubleArray (*NewDoubleArray)(JNIEnv *env, jsize len);
     void (*SetDoubleArrayRegion)(JNIEnv *env, jdoubleArray array, jsize start, jsize len,
                                  const jdouble *buf);
+    void (*GetDoubleArrayRegion)(JNIEnv *env, jdoubleArray array, jsize start, jsize len,
+                                 jdouble *buf);
     jintArray (*NewIntArray)(JNIEnv *env, jsize len);
     void (*SetIntArrayRegion)(JNIEnv *env, jintArray array, jsize start, jsize len,
                               const jint *buf);

@@ -1,6 +1,7 @@
 #!/usr/bin/env python3
 """Full-state digests at the SURVEY §8d parity horizons of the large configurations
-(committed as tests/golden/digests.json; re-run only on purpose, ~30 min on 8 cores).
+(committed as tests/golden/digests.json; re-run only on purpose: ~30 min on 8 cores for the
+10-step cases, ~3.5 h more for the 100-step ones).
 
 For each case the C restatement (oracle/bh_oracle.c) runs the reference step (BHA:405-439)
 K times from the seeded scene and the SHA-256 of every final SoA field (little-endian fp64,
@@ -36,6 +37,8 @@ OUT = os.path.join(HERE, "digests.json")
 # name: (scene, theta, steps K; 0 = one evaluation of the accelerations)
 CASES = {
     "c3_k10": ("c3", 0.5, 10),
+    "c3_k100": ("c3", 0.5, 100),   # the north star's 100-step horizon at the headline size
+    "c4_k100": ("c4", 0.5, 100),   # ... and at the north-star size (~3 h on 8 cores)
     "c4_k10": ("c4", 0.5, 10),
     "c3x8_k2": ("c3x8", 0.5, 2),
     "c5_eval": ("c5", 0.0, 0),

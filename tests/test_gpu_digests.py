@@ -36,13 +36,38 @@ def _check_state(state, want, tag):
     assert not bad, f"{tag}: fields {bad} differ from the oracle's digest"
 
 
-@pytest.mark.parametrize("case", ["c3_k10", "c4_k10", "c3x8_k2"])
+def _want(case):
+    if case not in DIGESTS:
+        pytest.skip(f"{case}: no digest committed (tests/golden/make_digests.py {case})")
+    return DIGESTS[case]
+
+
+@pytest.mark.parametrize("case", ["c3_k10", "c4_k10", "c3x8_k2", "c3_k100", "c4_k100"])
 def test_full_state_digest(case):
-    want = DIGESTS[case]
+    """One bh_step(K) call; c3_k100 / c4_k100 are the north star's 100-step horizon at the
+    headline and the north-star sizes (BHA:405-439 x 100)."""
+    want = _want(case)
     eng = bh_amd.Engine(bh_amd.default_params(theta=want["theta"]), device=0)
     eng.reset_bodies(*scenes.config_scene(want["scene"]))
     eng.step(want["steps"])
     _check_state(eng.get_bodies(), want, case)
+    eng.close()
+
+
+def test_c3_100_one_step_calls_digest():
+    """The north star's horizon through the front-end's own call pattern (PNL:290-306): 100
+    calls of bh_step(1), the bodies read back after each one from the pinned mirror (every call
+    pipelined: it ends with the next step's tree built) -- the oracle's C3 x 100 state."""
+    want = _want("c3_k100")
+    eng = bh_amd.Engine(bh_amd.default_params(theta=want["theta"]), device=0)
+    eng.reset_bodies(*scenes.config_scene(want["scene"]))
+    eng.set_mirror(True)
+    for _ in range(want["steps"]):
+        eng.step(1)
+        x = eng.map_bodies()[0]
+        assert len(x) == eng.num_bodies()
+    _check_state(tuple(np.array(a) for a in eng.map_bodies()), want, "mirror")
+    _check_state(eng.get_bodies(), want, "get_bodies")
     eng.close()
 
 
@@ -58,12 +83,13 @@ def test_c5_all_accelerations_digest():
     eng.close()
 
 
-def test_c4_eight_rank_group_digest():
+@pytest.mark.parametrize("case", ["c4_k10", "c4_k100"])
+def test_c4_eight_rank_group_digest(case):
     """The north-star configuration's decomposition: C4 (1e7 bodies) on 8 in-process ranks
     (bh_create_local; each rank builds the locally essential tree of its 4 Morton pieces and
-    evaluates them, the pieces are gathered in place), 10 steps: every rank's full state has
-    the oracle's digest."""
-    want = DIGESTS["c4_k10"]
+    evaluates them, the pieces are gathered in place), 10 and 100 steps in one call: every
+    rank's full state has the oracle's digest."""
+    want = _want(case)
     world = 8
     arrs = scenes.config_scene(want["scene"])
     group = bh_amd.LocalGroup(world)
@@ -84,14 +110,17 @@ def test_c4_eight_rank_group_digest():
     for t in threads:
         t.start()
     for t in threads:
-        t.join(timeout=100)
+        t.join(timeout=100 + 3 * want["steps"])
     assert not errors, errors
     assert not any(t.is_alive() for t in threads), "rank thread hung"
     for r in range(world):
         _check_state(results[r], want, f"rank {r}")
-        # the sharded build ran: 19 of the 20 builds are locally essential trees over a part of
-        # the cloud (the first build sorts the caller's order; lastTree is built on demand)
-        assert stats[r]["let_builds"] == 19 and stats[r]["full_builds"] == 1, stats[r]
+        # the sharded build ran: all builds but the first (which sorts the caller's order) and
+        # one in every BH_LET_REFRESH + 1 are locally essential trees over a part of the cloud
+        # (lastTree is built on demand)
+        builds = stats[r]["let_builds"] + stats[r]["full_builds"]
+        assert builds == 2 * want["steps"], stats[r]
+        assert stats[r]["full_builds"] == 1 + (builds - 1) // 33, stats[r]
         assert stats[r]["subset"] < want["n"] // 3, stats[r]
     for e in engines:
         e.close()

@@ -1087,3 +1087,114 @@ def test_pipelined_call_equals_single_steps():
     _assert_state_equal(one, ref)
     for u, v in zip(one.get_quads(), ref.quads()):
         assert bits_equal(u, v)
+
+
+def _frames_scene():
+    """Two disks with two merging heavies, a 6-fold and a 4-fold stack of coincident bodies and
+    20 bodies 3.6e-4 from a disk body: the jitter (BHA:146-151) moves bodies in most builds."""
+    arrs = scenes.two_disks(30000, 6000)
+    ex = np.concatenate([[900.0, 1500.0], np.full(6, 1234.5678), np.full(4, 700.25),
+                         arrs[0][:20] + 3e-4])
+    ey = np.concatenate([[400.0, 420.0], np.full(6, 321.0123), np.full(4, 500.5),
+                         arrs[1][:20] - 2e-4])
+    em = np.concatenate([[6000.0, 8000.0], np.ones(30)])
+    z = np.zeros(len(ex))
+    return tuple(np.concatenate([a, b]) for a, b in zip(arrs, (ex, ey, z, z, em)))
+
+
+def _assert_arrays_equal(got, want, what):
+    assert len(got[0]) == len(want[0]), f"{what}: N {len(got[0])} vs {len(want[0])}"
+    for k, name in enumerate(FIELDS):
+        bad = np.flatnonzero(np.asarray(got[k]).view(np.int64) != want[k].view(np.int64))
+        assert bad.size == 0, f"{what} {name}: {bad.size} words differ, first at {bad[:5]}"
+
+
+def test_one_step_calls_match_the_oracle_frame_by_frame():
+    """The front-end's own pattern: one step() per frame (PNL:290-293), every body read after
+    it (PNL:302-306), getTreeForDebug().visitQuads every few frames (PNL:333-340).  Every call's
+    last step is pipelined: the call ends with the next step's first tree built (its jitter
+    applied to the engine's copy of the state), while the caller sees the bodies as the reference
+    holds them after step() -- through bh_get_bodies and through the pinned mirror the step fills
+    itself (bh_map_bodies) -- and lastTree is the step's own tree (BHA:435), or, after a merge
+    removed a body in the last step, the fresh tree of BHA:329-332.  Frame by frame bit-identical
+    to the oracle, with merges and jitter along the way."""
+    arrs = _frames_scene()
+    p = bh_amd.default_params(theta=0.5)
+    eng = bh_amd.Engine(p)
+    eng.reset_bodies(*arrs)
+    mir = bh_amd.Engine(p)
+    mir.reset_bodies(*arrs)
+    mir.set_mirror(True)
+    ref = oracle.Oracle(*arrs, theta=0.5)
+    quad_frames = {1, 2, 5, 9, 10, 14, 19, 23}
+    for f in range(24):
+        eng.step(1)
+        mir.step(1)
+        ref.step(1)
+        want = ref.get_bodies()
+        _assert_arrays_equal(mir.map_bodies(), want, f"frame {f} mirror")
+        _assert_arrays_equal(eng.get_bodies(), want, f"frame {f}")
+        if f in quad_frames:
+            wq = ref.quads()
+            for e in (eng, mir):
+                for _ in range(2):  # the shim sizes, then fetches: the same tree twice
+                    for u, v in zip(e.get_quads(), wq):
+                        assert bits_equal(u, v), f"frame {f} quads"
+            want = ref.get_bodies()  # a fresh tree jitters the bodies (BHA:146-151)
+            _assert_arrays_equal(mir.map_bodies(), want, f"frame {f} mirror after quads")
+            _assert_arrays_equal(eng.get_bodies(), want, f"frame {f} after quads")
+    assert eng.num_bodies() < len(arrs[0])  # the heavies merged along the way
+
+
+def test_one_step_calls_then_reconfigure_checkpoint_and_evaluate(tmp_path):
+    """What the caller may do between two pipelined calls, each against the oracle: a root-cell
+    change (the prebuilt tree and its jitter belong to the old root and are dropped), a
+    checkpoint (the caller-visible state, not the prebuilt one), buildTree + computeAccelerations
+    (consumes the prebuilt tree), resetBodies, and a call that must be replayed from its snapshot
+    (merge mailbox overflow) right after a pipelined one."""
+    arrs = _frames_scene()
+    eng, ref = _pair(arrs, theta=0.5)
+    for _ in range(3):
+        eng.step(1)
+        ref.step(1)
+    eng.set_params(bh_amd.default_params(theta=0.5, width_px=1920, height_px=1080))
+    ref.set_params(oracle.params(theta=0.5, width_px=1920, height_px=1080))
+    eng.step(1)
+    ref.step(1)
+    _assert_state_equal(eng, ref)
+    eng.save_state(str(tmp_path / "s.bhs"))
+    back = bh_amd.Engine(bh_amd.default_params())
+    back.load_state(str(tmp_path / "s.bhs"))
+    _assert_state_equal(back, ref)
+    back.close()
+    eng.step(1)
+    ref.step(1)
+    ax, ay = eng.compute_accelerations()
+    rax, ray = ref.accelerations()
+    assert bits_equal(ax, rax) and bits_equal(ay, ray)
+    _assert_state_equal(eng, ref)
+    eng.step(2)
+    ref.step(2)
+    _assert_state_equal(eng, ref)
+    # a merge-free pipelined call, then the rule switched on: the next call overflows the
+    # mailbox and is replayed from the caller-visible state
+    rng = np.random.default_rng(77)
+    nh = 520
+    hx, hy = 1000.0 + 20.0 * rng.random(nh), 400.0 + 20.0 * rng.random(nh)
+    field = scenes.uniform(3000, 0.5, seed=17)
+    x, y = np.concatenate([hx, field[0]]), np.concatenate([hy, field[1]])
+    m = np.concatenate([rng.uniform(4001.0, 6000.0, nh), field[4]])
+    crowd = (x, y, np.zeros(len(x)), np.zeros(len(x)), m)
+    off = dict(theta=0.5, merge_min_dist=0.0)
+    eng.set_params(bh_amd.default_params(**off))
+    ref.set_params(oracle.params(**off))
+    eng.reset_bodies(*crowd)
+    ref.reset_bodies(*crowd)
+    eng.step(1)
+    ref.step(1)
+    eng.set_params(bh_amd.default_params(theta=0.5))
+    ref.set_params(oracle.params(theta=0.5))
+    eng.step(1)
+    ref.step(1)
+    _assert_state_equal(eng, ref)
+    assert eng.num_bodies() < len(x) - nh // 2

@@ -1,0 +1,61 @@
+#!/usr/bin/env bash
+# The GPU session runner: every measurement and test step of a gpurun call, by name, in order.
+#
+#   TAG=r04b bash tools/session.sh STEP [STEP ...]
+#
+# Steps (outputs under gpurun_out/, prefixed with $TAG):
+#   tests          python -m pytest tests -m gpu (PYTEST_K="expr" narrows it)  -> ${TAG}_pytest.log
+#   smoke          __graft_entry__.smoke()                                     -> ${TAG}_smoke.log
+#   bench          the driver's command: bench.py --steps 20 --warmup 5        -> ${TAG}_bench_lines.jsonl
+#   configs        one bench line per BASELINE configuration (c1_baseline, c1_code, c2, c4, c5)
+#   profile        rocprofv3 kernel trace + stats and FETCH_SIZE / WRITE_SIZE passes of C3
+#                  (tools/profile.sh; CONFIG=c5 etc. for another workload) -> prof_<CONFIG>/
+#   sq             SQ counters of the traversal (tools/profile_sq.sh)
+#   timeline       one C3 bench under a kernel trace, summarised per step (tools/timeline.py)
+#   solo           one rank's share of the 8-GPU C4 step, alone (tools/solo_rank.py, ranks 0, 5)
+#   ab             A/B of in-tree library builds (tools/ab.sh; LIBS="A B", AB_ARGS=...)
+# Every GPU step runs under its own time limit; a failing step (any rc but 0) ends the session, so
+# nothing else touches the GPU after a fault, an abort or a timeout.
+# (Round 3's one-off session scripts are kept in tools/archive/: committed profiles cite them.)
+set -u
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+TAG=${TAG:-s}
+O=gpurun_out/$TAG
+run() {  # $1 = seconds, $2 = log, rest = command
+  local t=$1 log=$2
+  shift 2
+  timeout -k 10 "$t" "$@" > "$log" 2>&1
+  local rc=$?
+  echo "[$TAG] $* -> rc=$rc"
+  tail -3 "$log" | cut -c1-600
+  [ $rc -eq 0 ] || { echo "[$TAG] STOP (rc=$rc)"; exit $rc; }
+}
+bench_line() {  # bench.py args... -> one JSON line appended to ${O}_bench_lines.jsonl
+  run 600 ${O}_bench.log python -u bench.py "$@"
+  grep '^{' ${O}_bench.log | tail -1 >> ${O}_bench_lines.jsonl
+}
+for step in "$@"; do
+  case $step in
+    tests)
+      run ${PYTEST_TIMEOUT:-1200} ${O}_pytest.log python -u -m pytest tests -m gpu -x -v \
+        --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} ;;
+    smoke) run 300 ${O}_smoke.log python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench) bench_line --steps 20 --warmup 5 ;;
+    configs)
+      for c in c1_baseline c1_code c2 c4; do bench_line --config $c --steps 10 --warmup 2; done
+      bench_line --config c5 --steps 2 --warmup 1 ;;
+    profile) run 1800 ${O}_profile.log bash tools/profile.sh ;;
+    sq) run 900 ${O}_sq.log bash tools/profile_sq.sh ;;
+    timeline)
+      run 600 ${O}_timeline.log rocprofv3 --kernel-trace -d ${O}_tl -o run --output-format csv \
+        -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-counters --no-drop-in ;;
+    solo)
+      for r in 0 5; do
+        run 600 ${O}_solo$r.log python -u tools/solo_rank.py --config c4 --world 8 --rank $r
+        grep '^{' ${O}_solo$r.log | tail -1 >> ${O}_solo.jsonl
+      done ;;
+    ab) run 1800 ${O}_ab.log bash tools/ab.sh ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
