@@ -480,6 +480,11 @@ void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, d
 void copy_trav_inputs(int64_t n, const double *m, double *m_t, const uint32_t *cidx,
                       uint32_t *cidx_t, const uint32_t *lanes, uint32_t *lanes_t,
                       const uint32_t *T, uint32_t *T_t, hipStream_t s);
+// k_kick_drift of a2 written by lane (lanes: lane -> slot, or null) plus, when mf.keys is set, the
+// next build's keys and bucket assignment -- the drifting traversal's epilogue as its own pass
+void kick_drift_keys(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
+                     const uint32_t *cidx, double dtHalf, double dt, const uint32_t *lanes,
+                     const Geometry &g, const MortonFuse &mf, hipStream_t s);
 void kick(int64_t n, const double *a2, double *vx, double *vy, double dtHalf, hipStream_t s,
           const uint32_t *lanes = nullptr, GatherLayout gl = GatherLayout{});
 void iota_u32(uint32_t *p, int64_t n, hipStream_t s);

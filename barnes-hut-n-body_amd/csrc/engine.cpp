@@ -206,6 +206,10 @@ struct bh_engine {
     uint32_t *cidx_trav = nullptr, *lanes_trav = nullptr, *T_trav = nullptr;
     int64_t trav_cap = 0;
     bool prebuilt = false;  // the current step's first build was made by the previous step
+    // deep pipeline: the previous step also evaluated a(t) on that tree (beside its own second
+    // traversal), by lane of the current map, with these force parameters
+    bool forces_ready = false;
+    ForceParams fp_ready{0.0, 0.0, 0.0};
     bool fuse_keys = false;   // the next KICK_DRIFT traversal writes the next build's keys / buckets
     bool keys_ready = false;  // ... and it did: the next full build skips k_morton, k_bucket_count
     hipEvent_t pipe_ev[3] = {nullptr, nullptr, nullptr};
@@ -267,6 +271,7 @@ struct bh_engine {
     bool profiling = false;
     std::vector<hipEvent_t> ev;
     std::vector<int> ev_phase;
+    std::vector<int> ev_weight;  // traversal intervals: evaluations they contain
     size_t ev_used = 0;
     double phase_ms[kPhases] = {0, 0, 0, 0, 0};
     double trav_ms_sum = 0.0;
@@ -463,7 +468,8 @@ TreeBuffers tree_buffers(bh_engine *e) {
 }
 
 // ---- profiling events ----------------------------------------------------------------
-int mark(bh_engine *e, int phase) {  // close the interval of `phase` that began at the last mark
+// weight: force evaluations inside a traversal interval (the deep pipeline's holds two)
+int mark(bh_engine *e, int phase, int weight = 1) {  // close the interval of `phase` begun at the last mark
     if (!e->profiling) return BH_OK;
     // phases are contiguous on the stream: the previous phase's end mark starts the next one
     if (phase < 0 && e->ev_used > 0) return BH_OK;
@@ -477,9 +483,11 @@ int mark(bh_engine *e, int phase) {  // close the interval of `phase` that began
         }
         e->ev.push_back(ev);
         e->ev_phase.push_back(-1);
+        e->ev_weight.push_back(1);
     }
     HIPCHK(e, hipEventRecord(e->ev[e->ev_used], e->stream));
     e->ev_phase[e->ev_used] = phase;  // phase of the interval ending here (-1: start marker)
+    e->ev_weight[e->ev_used] = weight;
     ++e->ev_used;
     e->timings_pending = true;
     return BH_OK;
@@ -498,10 +506,11 @@ int collect_timings(bh_engine *e) {
         float ms = 0.f;
         HIPCHK(e, hipEventElapsedTime(&ms, e->ev[i - 1], e->ev[i]));
         e->phase_ms[ph] += ms;
-        if (ph == 1) {
+        if (ph == 1) {  // per evaluation: an interval holding w evaluations counts w times
+            const int w = e->ev_weight[i];
             e->trav_ms_sum += ms;
-            e->trav_launches += 1;
-            e->trav_samples.push_back(ms);
+            e->trav_launches += w;
+            for (int j = 0; j < w; ++j) e->trav_samples.push_back(ms / w);
         }
     }
     e->timings_pending = false;
@@ -1016,10 +1025,12 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
     }
     e->let_age = 0;
     const int64_t n = e->n;
+    bool have_forces = false;  // a(t) on this tree, evaluated ahead by the previous step
     if (e->prebuilt) {  // the pipelined step built this tree (single GPU: nothing deferred)
         e->prebuilt = false;
         e->view_pending = false;  // its jitter is now part of the state (BHA:146-151)
         e->mir_fresh = false;
+        have_forces = e->forces_ready;
     } else {
         TRY(materialize_positions(e));  // the replica's x, y; a2 is free again
         TRY(sync_velocities(e));        // before the full build permutes the state
@@ -1027,7 +1038,10 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
         TRY(build(e));
         TRY(mark(e, 0));
     }
+    e->forces_ready = false;
     ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};  // BHA:378
+    have_forces = have_forces && fp.G == e->fp_ready.G && fp.soft2 == e->fp_ready.soft2 &&
+                  fp.theta2 == e->fp_ready.theta2;
     const uint32_t *d_T = e->base + n;
     const bool direct = fp.theta2 == 0.0 && !visits;
     if (direct) {
@@ -1057,6 +1071,16 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
                 e->keys_ready = true;
             }
             e->fuse_keys = false;
+            if (have_forces && kick == KICK_DRIFT) {
+                // a(t) is in a2 by lane (the previous step's deep pipeline): the epilogue alone
+                TRY(mark(e, -1));
+                kick_drift_keys(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, e->st.cidx,
+                                ka.dtHalf, ka.dt, lanes, e->geo, ka.mf, e->stream);
+                HIPCHK(e, hipGetLastError());
+                *fused = true;
+                TRY(mark(e, 2));
+                return BH_OK;
+            }
             WaveOrder wo;
             TRY(wave_order_for(e, 0, n, e->stream, wo));
             traverse(e->nodes, e->node_cap, d_T, e->st.x, e->st.y, e->st.m, e->st.cidx, 0, n, e->geo, fp,
@@ -1184,11 +1208,18 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
     if (!e->merge_ran) return BH_OK;
     e->merge_ran = false;
     TRY(materialize_positions(e));
-    TRY(pinned_reserve(e, 64));
+    // one round trip: the counts, the mailbox header and the first DLOG_AHEAD removals (a step
+    // removes tens of bodies at C3) come back together
+    constexpr uint32_t DLOG_AHEAD = 4096;
+    TRY(pinned_reserve(e, 64 + 2 * sizeof(uint32_t) * DLOG_AHEAD));
     uint32_t *h = static_cast<uint32_t *>(e->pin);
+    uint32_t *hlog = h + 16, *hsorted = h + 16 + DLOG_AHEAD;
     HIPCHK(e, hipMemcpyAsync(h, e->scalars, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipMemcpyAsync(h + 4, e->box, sizeof(MergeHeader), hipMemcpyDeviceToHost, e->stream));
     HIPCHK(e, hipMemcpyAsync(h + 12, e->scalars + 8, sizeof(uint32_t), hipMemcpyDeviceToHost,
+                             e->stream));
+    const uint32_t ahead = (uint32_t)std::min<int64_t>(DLOG_AHEAD, e->dlog_cap);
+    HIPCHK(e, hipMemcpyAsync(hlog, e->dlog, sizeof(uint32_t) * ahead, hipMemcpyDeviceToHost,
                              e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     const uint32_t nd = h[2];
@@ -1201,9 +1232,19 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
     if (hdr.heavies == 0) e->heavy_possible = false;
     if (nd == 0) return BH_OK;
     std::vector<uint32_t> dead(nd);
-    HIPCHK(e, hipMemcpy(dead.data(), e->dlog, 4 * (size_t)nd, hipMemcpyDeviceToHost));
+    if (nd <= ahead) {
+        std::memcpy(dead.data(), hlog, 4 * (size_t)nd);
+    } else {
+        HIPCHK(e, hipMemcpy(dead.data(), e->dlog, 4 * (size_t)nd, hipMemcpyDeviceToHost));
+    }
     std::sort(dead.begin(), dead.end());
-    HIPCHK(e, hipMemcpy(e->dead_sorted, dead.data(), 4 * (size_t)nd, hipMemcpyHostToDevice));
+    if (nd <= DLOG_AHEAD) {  // from pinned memory, in stream order: no wait
+        std::memcpy(hsorted, dead.data(), 4 * (size_t)nd);
+        HIPCHK(e, hipMemcpyAsync(e->dead_sorted, hsorted, 4 * (size_t)nd, hipMemcpyHostToDevice,
+                                 e->stream));
+    } else {
+        HIPCHK(e, hipMemcpy(e->dead_sorted, dead.data(), 4 * (size_t)nd, hipMemcpyHostToDevice));
+    }
     const int64_t n = e->n;
     if (e->view_pending) {  // the caller-visible state (the previous order) loses the same bodies
         HIPCHK(e, compact_state(n, e->keep, e->view, e->alt, e->dead_sorted, nd, e->pos,
@@ -1266,7 +1307,13 @@ int snapshot(bh_engine *e) {
     }
     e->snap_n = e->n;
     // after a pipelined call the caller's state is the view (the prebuilt tree's jitter is not
-    // applied yet): a replay starts from it and builds its own first tree
+    // applied yet): a replay starts from it and builds its own first tree.  The call never writes
+    // the view's buffers (its own last step makes a new view from `alt`), so the snapshot takes
+    // them over instead of copying 44 B per body
+    if (e->view_pending && e->view_cap == e->snap_cap) {
+        std::swap(e->snap, e->view);
+        return BH_OK;
+    }
     return copy_state(e, e->view_pending ? e->view : e->st, e->snap, e->n);
 }
 
@@ -1345,6 +1392,9 @@ int agree_let_flags(bh_engine *e, uint32_t ls[2], uint32_t *own_sub) {
 #endif
 #ifndef BH_PIPE_PRIORITY
 #define BH_PIPE_PRIORITY 1  // the overlapped work's stream at the highest priority
+#endif
+#ifndef BH_DEEP_PIPE
+#define BH_DEEP_PIPE 1  // the next step's a(t) evaluated beside this step's second traversal
 #endif
 #ifndef BH_PIPE_LAST
 #define BH_PIPE_LAST 1  // pipeline a call's last step too (the next call starts on its tree)
@@ -1499,7 +1549,7 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     traverse(e->nodes, e->node_cap, e->T_trav, e->st.x, e->st.y, e->m_trav, e->cidx_trav, 0, n,
              e->geo, fp, e->a2, nullptr, s, &ka, lanes ? e->lanes_trav : nullptr, &wo);
     HIPCHK(e, hipGetLastError());
-    TRY(mark(e, 1));
+    if (!BH_DEEP_PIPE) TRY(mark(e, 1));
     TRY(wave_order_next(e, 0, n, s));
     if (last) {
         hipStream_t ps = e->pipe_stream;
@@ -1517,8 +1567,18 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     if (last && e->mirror_on)  // positions and masses are final: the caller-order copy-out starts
         TRY(mirror_launch(e, e->st, e->pipe_stream, s));
     TRY(build_into(e, e->pipe_stream, true));       // step s+1's first tree (BHA:359)
+    if (BH_DEEP_PIPE) {
+        // ... and a(t) of step s+1 on it (BHA:407-408): a force evaluation reads positions and
+        // masses only, so it runs beside this traversal, whose tail it fills; the next step's
+        // kick and drift need this traversal's velocities and run after both (kick_drift_keys)
+        traverse(e->nodes_alt, e->nodes_alt_cap, e->base + n, e->alt.x, e->alt.y, e->alt.m,
+                 e->alt.cidx, 0, n, e->geo, fp, e->a2, nullptr, e->pipe_stream, nullptr,
+                 e->lanes_valid ? e->lanes : nullptr, nullptr);
+        HIPCHK(e, hipGetLastError());
+    }
     HIPCHK(e, hipEventRecord(e->pipe_ev[1], e->pipe_stream));
     HIPCHK(e, hipStreamWaitEvent(s, e->pipe_ev[1], 0));
+    if (BH_DEEP_PIPE) TRY(mark(e, 1, 2));  // this traversal, the overlapped chain, the next a(t)
     permute_velocities(n, e->perm, e->st.vx, e->st.vy, e->alt.vx, e->alt.vy, s);
     HIPCHK(e, hipGetLastError());
     TRY(mark(e, 0));  // the wait for the overlapped build and the velocity permutation
@@ -1526,6 +1586,8 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     std::swap(e->nodes, e->nodes_alt);
     std::swap(e->node_cap, e->nodes_alt_cap);
     e->prebuilt = true;
+    e->forces_ready = BH_DEEP_PIPE != 0;
+    e->fp_ready = fp;
     if (last) {  // the previous order's state (kicked, merged, not yet jittered) is what the caller sees
         std::swap(e->view, e->alt);
         e->view_pending = true;

@@ -33,6 +33,42 @@ __global__ __launch_bounds__(TB) void k_kick_drift(int64_t n, const double *__re
     y[p] = y[p] + vyi * dt;
 }
 
+// The same kick + drift by lane of the traversal's lane map, after an evaluation that was made
+// ahead (the deep pipeline, engine.cpp evaluate_pipelined), with the next build's first two passes
+// (k_morton, k_bucket_count) for the moved body -- what the drifting traversal's epilogue does
+// (traverse.hip trav_wave), operation for operation.
+__global__ __launch_bounds__(TB) void k_kick_drift_keys(int64_t n, const double *__restrict__ a2,
+                                                        double *__restrict__ x,
+                                                        double *__restrict__ y,
+                                                        double *__restrict__ vx,
+                                                        double *__restrict__ vy,
+                                                        const uint32_t *__restrict__ cidx,
+                                                        double dtHalf, double dt,
+                                                        const uint32_t *__restrict__ lanes,
+                                                        Geometry g, MortonFuse mf) {
+    const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (i >= n) return;
+    const double2_t a = *reinterpret_cast<const double2_t *>(a2 + 2 * i);
+    const int64_t p = lanes ? (int64_t)lanes[i] : i;
+    const double vxi = vx[p] + a.x * dtHalf;
+    const double vyi = vy[p] + a.y * dtHalf;
+    vx[p] = vxi;
+    vy[p] = vyi;
+    const double nx = x[p] + vxi * dt, ny = y[p] + vyi * dt;
+    x[p] = nx;
+    y[p] = ny;
+    if (mf.keys) {
+        const uint64_t key = morton_key(g, nx, ny, (cidx[p] & CIDX_DEAD) != 0u);
+        const uint32_t k32 = (uint32_t)(key >> key32_shift(g.J));
+        mf.keys[p] = key;
+        mf.keys32[p] = k32;
+        const uint32_t b = find_bucket(mf.spl, mf.spl_nb, ((uint64_t)k32 << 32) | (uint64_t)p,
+                                       (uint32_t)(p / SORT_B));
+        mf.bkt[p] = b;
+        mf.off[p] = bucket_offset(b, mf.counts);
+    }
+}
+
 // BHA:429-432
 __global__ __launch_bounds__(TB) void k_kick(int64_t n, const double *__restrict__ a2,
                                              double *__restrict__ vx, double *__restrict__ vy,
@@ -602,6 +638,14 @@ hipError_t compact_lanes(int64_t n, const uint32_t *lanes, const uint32_t *keep,
 void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
                 double dtHalf, double dt, hipStream_t s, const uint32_t *lanes, GatherLayout gl) {
     if (n > 0) k_kick_drift<<<grid_for(n), TB, 0, s>>>(n, a2, x, y, vx, vy, dtHalf, dt, lanes, gl);
+}
+
+void kick_drift_keys(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
+                     const uint32_t *cidx, double dtHalf, double dt, const uint32_t *lanes,
+                     const Geometry &g, const MortonFuse &mf, hipStream_t s) {
+    if (n > 0)
+        k_kick_drift_keys<<<grid_for(n), TB, 0, s>>>(n, a2, x, y, vx, vy, cidx, dtHalf, dt, lanes,
+                                                     g, mf);
 }
 
 void copy_trav_inputs(int64_t n, const double *m, double *m_t, const uint32_t *cidx,

@@ -16,7 +16,10 @@ for r in $(seq 1 $ROUNDS); do
 import json, sys
 line = [l for l in open(sys.argv[2]) if l.startswith("{")][-1]
 d = json.loads(line)
-r = d["roofline"]; print(sys.argv[1], d["ms_per_step"], r.get("kernel_ms", {}).get("avg"), r.get("kernel_ms", {}).get("max"), d["phase_ms"])
+r = d["roofline"]; di = d.get("drop_in") or {}
+print(sys.argv[1], d["ms_per_step"], r.get("kernel_ms", {}).get("avg"), r.get("kernel_ms", {}).get("max"), d["phase_ms"],
+      "drop_in", di.get("ms_per_step"), di.get("ms_per_step_with_get_bodies"), di.get("ms_per_step_with_mirror"),
+      "verify", (d.get("verify") or {}).get("digest_match"))
 PY
   done
 done
