@@ -360,9 +360,12 @@ class Engine:
     def num_bodies(self) -> int:
         return int(self._lib.bh_num_bodies(self._h))
 
-    def get_bodies(self):
+    def get_bodies(self, out=None):
+        """bh_get_bodies: (x, y, vx, vy, m) in caller order; `out` = five float64 arrays of at
+        least N entries to fill (a caller that reuses its buffers), else new arrays."""
         n = self.num_bodies()
-        out = [np.empty(n, dtype=np.float64) for _ in range(5)]
+        if out is None or any(len(a) < n or a.dtype != np.float64 for a in out):
+            out = [np.empty(n, dtype=np.float64) for _ in range(5)]
         got = ctypes.c_int64(0)
         self._check(self._lib.bh_get_bodies(self._h, *[_dp(a) for a in out], n, ctypes.byref(got)))
         return tuple(a[: got.value] for a in out)

@@ -477,9 +477,11 @@ void direct_forces(const LeafList &L, const uint32_t *d_count, const double *x, 
 void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
                 double dtHalf, double dt, hipStream_t s, const uint32_t *lanes = nullptr,
                 GatherLayout gl = GatherLayout{});
+struct MergePair;
+// (box: the merge mailbox, whose header it clears for the overlapped merge rule, or null)
 void copy_trav_inputs(int64_t n, const double *m, double *m_t, const uint32_t *cidx,
                       uint32_t *cidx_t, const uint32_t *lanes, uint32_t *lanes_t,
-                      const uint32_t *T, uint32_t *T_t, hipStream_t s);
+                      const uint32_t *T, uint32_t *T_t, hipStream_t s, MergePair *box = nullptr);
 // k_kick_drift of a2 written by lane (lanes: lane -> slot, or null) plus, when mf.keys is set, the
 // next build's keys and bucket assignment -- the drifting traversal's epilogue as its own pass
 void kick_drift_keys(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
@@ -537,6 +539,9 @@ size_t compact_scratch_bytes(int64_t n);
 hipError_t compact_lanes(int64_t n, const uint32_t *lanes, const uint32_t *keep,
                          const uint32_t *pos, uint32_t *flag, uint32_t *qpos, uint32_t *out,
                          void *tmp, size_t tmp_bytes, hipStream_t s);
+// (flag, qpos of that compact_lanes call) interleaved pairs by lane: out[2 qpos[q]..] = a2[2 q..]
+void compact_lane_pairs(int64_t n, const uint32_t *flag, const uint32_t *qpos, const double *a2,
+                        double *out, hipStream_t s);
 void compact_pair(int64_t n, const uint32_t *keep, const uint32_t *pos, const double *sx,
                   const double *sy, double *dx, double *dy, hipStream_t s);
 hipError_t compact_state(int64_t n, uint32_t *keep, const BodyState &src, const BodyState &dst,

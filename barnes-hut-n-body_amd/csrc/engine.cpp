@@ -210,6 +210,8 @@ struct bh_engine {
     // traversal), by lane of the current map, with these force parameters
     bool forces_ready = false;
     ForceParams fp_ready{0.0, 0.0, 0.0};
+    double *a2_alt = nullptr;  // a2's compaction target (the carried forces over removals)
+    int64_t a2_alt_cap = 0;
     bool fuse_keys = false;   // the next KICK_DRIFT traversal writes the next build's keys / buckets
     bool keys_ready = false;  // ... and it did: the next full build skips k_morton, k_bucket_count
     hipEvent_t pipe_ev[3] = {nullptr, nullptr, nullptr};
@@ -1262,6 +1264,18 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
                                 e->scratch, e->scratch_bytes, e->stream));
         std::swap(e->lanes, e->keys32_s);
         e->inv_valid = false;
+        if (e->prebuilt && e->forces_ready) {
+            // the next step's a(t), already evaluated by lane, follows its lanes (flag, qpos)
+            if (e->a2_alt_cap < e->cap) {
+                TRY(dev_alloc(e, e->a2_alt, 2 * (size_t)e->cap));
+                e->a2_alt_cap = e->cap;
+            }
+            compact_lane_pairs(n, e->idx, e->keys32, e->a2, e->a2_alt, e->stream);
+            HIPCHK(e, hipGetLastError());
+            std::swap(e->a2, e->a2_alt);  // (one GPU: both hold 2 cap doubles)
+        }
+    } else {
+        e->forces_ready = false;
     }
     e->n = n - (int64_t)nd;
     e->inv_valid = false;  // another n: another exchange layout
@@ -1394,7 +1408,11 @@ int agree_let_flags(bh_engine *e, uint32_t ls[2], uint32_t *own_sub) {
 #define BH_PIPE_PRIORITY 1  // the overlapped work's stream at the highest priority
 #endif
 #ifndef BH_DEEP_PIPE
-#define BH_DEEP_PIPE 1  // the next step's a(t) evaluated beside this step's second traversal
+// 1: the next step's a(t) evaluated beside this step's second traversal (kick + drift + keys as
+// their own pass).  Measured slower (C3 1.925 against 1.884 ms per step, round 4):
+// the next tree is ready only after the traversal's last waves are placed, so the two
+// evaluations barely overlap and share the caches when they do.
+#define BH_DEEP_PIPE 0
 #endif
 #ifndef BH_PIPE_LAST
 #define BH_PIPE_LAST 1  // pipeline a call's last step too (the next call starts on its tree)
@@ -1522,23 +1540,17 @@ int mirror_launch(bh_engine *e, const BodyState &src, hipStream_t after_pos, hip
 int evaluate_pipelined(bh_engine *e, bool last) {
     const int64_t n = e->n;
     hipStream_t s = e->stream;
-    // the merge rule's mailbox header is cleared on the overlapped stream while this build runs
-    // (after everything queued so far on the engine's stream, the last merge rule included): on
-    // the engine's stream it would sit between the build and the traversal, on the overlapped
-    // stream after the traversal's start it would wait until its last workgroups are placed
+    // the merge rule's mailbox header is cleared by k_trav_inputs below (after the previous merge
+    // rule, which the engine's stream waited for, and before the overlapped one): a fill of its
+    // own sat on the engine's hardware queue between the build and the traversal
     const bool merging = e->p.merge_min_dist > 0.0 && e->n > 1 && e->heavy_possible;
-    if (merging) {
-        TRY(merge_bufs(e));
-        HIPCHK(e, hipEventRecord(e->pipe_ev[2], s));
-        HIPCHK(e, hipStreamWaitEvent(e->pipe_stream, e->pipe_ev[2], 0));
-        HIPCHK(e, hipMemsetAsync(e->box, 0, sizeof(MergeHeader), e->pipe_stream));
-    }
+    if (merging) TRY(merge_bufs(e));
     TRY(mark(e, -1));
     TRY(build(e));
     TRY(mark(e, 0));
     const bool lanes = e->lanes_valid;
     copy_trav_inputs(n, e->st.m, e->m_trav, e->st.cidx, e->cidx_trav, lanes ? e->lanes : nullptr,
-                     e->lanes_trav, e->base + n, e->T_trav, s);
+                     e->lanes_trav, e->base + n, e->T_trav, s, merging ? e->box : nullptr);
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->pipe_ev[0], s));
     HIPCHK(e, hipStreamWaitEvent(e->pipe_stream, e->pipe_ev[0], 0));
@@ -2076,7 +2088,7 @@ void bh_destroy(bh_engine *e) {
                     e->leaf_flags, e->leaf_sel, e->leaf_count, e->leaf_cover, e->leaves.rec,
                     e->leaf_tmp, e->spl, e->bcount, e->bstart, e->nodes_alt, e->wave_cost, e->run_order,
                     e->m_trav, e->cidx_trav, e->lanes_trav, e->T_trav, e->solo_xchg,
-                    e->lt_x, e->lt_y, e->lt_keys, e->lt_cpl, e->lt_base, e->mir_stage,
+                    e->lt_x, e->lt_y, e->a2_alt, e->lt_keys, e->lt_cpl, e->lt_base, e->mir_stage,
                     e->mir_keep, e->mir_pos, e->mir_tmp};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);

@@ -92,9 +92,11 @@ __global__ __launch_bounds__(TB) void k_trav_inputs(int64_t n, const double *__r
                                                     const uint32_t *__restrict__ lanes,
                                                     uint32_t *__restrict__ lanes_t,
                                                     const uint32_t *__restrict__ T,
-                                                    uint32_t *__restrict__ T_t) {
+                                                    uint32_t *__restrict__ T_t,
+                                                    uint32_t *__restrict__ box_header) {
     const int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (i == 0) *T_t = *T;
+    if (box_header && i < (int64_t)(sizeof(MergeHeader) / sizeof(uint32_t))) box_header[i] = 0u;
     if (i >= n) return;
     m_t[i] = m[i];
     cidx_t[i] = cidx[i];
@@ -621,7 +623,23 @@ __global__ __launch_bounds__(TB) void k_lane_compact(int64_t n, const uint32_t *
     if (q < n && flag[q]) out[qpos[q]] = pos[lanes[q]];
 }
 
+// The deep pipeline's forces (by lane) through the same lane compaction: out[qpos[q]] = a2[q].
+__global__ __launch_bounds__(TB) void k_lane_pairs(int64_t n, const uint32_t *__restrict__ flag,
+                                                   const uint32_t *__restrict__ qpos,
+                                                   const double *__restrict__ a2,
+                                                   double *__restrict__ out) {
+    int64_t q = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (q < n && flag[q])
+        *reinterpret_cast<double2_t *>(out + 2 * (int64_t)qpos[q]) =
+            *reinterpret_cast<const double2_t *>(a2 + 2 * q);
+}
+
 }  // namespace
+
+void compact_lane_pairs(int64_t n, const uint32_t *flag, const uint32_t *qpos, const double *a2,
+                        double *out, hipStream_t s) {
+    if (n > 0) k_lane_pairs<<<grid_for(n), TB, 0, s>>>(n, flag, qpos, a2, out);
+}
 
 hipError_t compact_lanes(int64_t n, const uint32_t *lanes, const uint32_t *keep,
                          const uint32_t *pos, uint32_t *flag, uint32_t *qpos, uint32_t *out,
@@ -650,9 +668,10 @@ void kick_drift_keys(int64_t n, const double *a2, double *x, double *y, double *
 
 void copy_trav_inputs(int64_t n, const double *m, double *m_t, const uint32_t *cidx,
                       uint32_t *cidx_t, const uint32_t *lanes, uint32_t *lanes_t,
-                      const uint32_t *T, uint32_t *T_t, hipStream_t s) {
+                      const uint32_t *T, uint32_t *T_t, hipStream_t s, MergePair *box) {
     k_trav_inputs<<<grid_for(n > 0 ? n : 1), TB, 0, s>>>(n, m, m_t, cidx, cidx_t, lanes, lanes_t,
-                                                          T, T_t);
+                                                          T, T_t,
+                                                          reinterpret_cast<uint32_t *>(box));
 }
 
 void kick(int64_t n, const double *a2, double *vx, double *vy, double dtHalf, hipStream_t s,
