@@ -44,7 +44,7 @@ EXPORTED_SYMBOLS = (
     "bh_nbody3d_step", "bh_nbody3d_accelerations", "bh_nbody3d_get", "bh_nbody3d_last_ms",
     "bh_local_group_create", "bh_local_group_destroy", "bh_create_local",
     "bh_save_state", "bh_load_state", "bh_let_stats", "bh_create_solo", "bh_comm_ranks",
-    "bh_debug_inject", "bh_set_mirror", "bh_map_bodies",
+    "bh_debug_inject", "bh_set_mirror", "bh_map_bodies", "bh_let_spec_stats",
 )
 
 
@@ -125,6 +125,7 @@ def load_library(path: str | None = None):
     lib.bh_traversal_stats.argtypes = [_VP, _I64P, _I64P, _I64P]
     lib.bh_traversal_counters.argtypes = [_VP, _I64P]
     lib.bh_let_stats.argtypes = [_VP, _I64P]
+    lib.bh_let_spec_stats.argtypes = [_VP, _I64P]
     lib.bh_comm_ranks.argtypes = [_VP, ctypes.POINTER(ctypes.c_int32),
                                   ctypes.POINTER(ctypes.c_int32)]
     lib.bh_debug_inject.argtypes = [_VP, ctypes.c_int]
@@ -422,8 +423,12 @@ class Engine:
         """Multi-rank build sharding: LET builds, full builds, last subset size, last LET nodes."""
         out = np.zeros(5, dtype=np.int64)
         self._check(self._lib.bh_let_stats(self._h, out.ctypes.data_as(_I64P)))
-        return dict(zip(("let_builds", "full_builds", "subset", "let_nodes", "overflows"),
-                        out.tolist()))
+        d = dict(zip(("let_builds", "full_builds", "subset", "let_nodes", "overflows"),
+                     out.tolist()))
+        sp = np.zeros(2, dtype=np.int64)
+        self._check(self._lib.bh_let_spec_stats(self._h, sp.ctypes.data_as(_I64P)))
+        d["spec_builds"], d["spec_fallbacks"] = int(sp[0]), int(sp[1])
+        return d
 
     def comm_ranks(self):
         """(ncclCommCount, ncclCommUserRank) of the engine's RCCL communicator; (0, rank) for

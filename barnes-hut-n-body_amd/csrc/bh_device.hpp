@@ -438,13 +438,16 @@ hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
 // gslot[lanes[q]] = gather_slot(gl, q) (lanes null: the identity map)
 void let_gather_slots(int64_t n, const uint32_t *lanes, GatherLayout gl, uint32_t *gslot,
                       hipStream_t s);
-// after tree_build over the subset: the own cells' exchange table
+// after tree_build over the subset: the own cells' exchange table; detect_cross: flag (status
+// record's tag) a body the build's jitter moved into another depth-LET_P cell (tb.src / tb.dst)
 hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const TreeBuffers &tb,
-                     hipStream_t s);
+                     hipStream_t s, bool detect_cross = false);
 // after the exchange (L.tables, LET_TSTRIDE per rank): any rank's overflow -> scal[4]; top
-// levels, layout, node array, lane map; tree size posc[LET_CELLS]
+// levels, layout, node array, lane map; tree size posc[LET_CELLS]; cross (nullable) <- whether
+// any rank flagged a jitter move across a depth-LET_P cell
 hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, const LetBufs &L,
-                        const TreeBuffers &tb, uint32_t *scal, hipStream_t s);
+                        const TreeBuffers &tb, uint32_t *scal, hipStream_t s,
+                        uint32_t *cross = nullptr);
 // owner integration: a2 (gather slots) holds every lane's (x, y) -> the replicated state; the
 // solo fill writes the current positions of all lanes first
 void let_set_pos(int64_t n, const uint32_t *lanes, const double *a2, GatherLayout gl, double *x,

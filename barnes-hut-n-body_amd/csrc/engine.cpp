@@ -69,6 +69,32 @@ struct bh_local_group {
     }
 };
 
+// The buffers a locally essential tree build writes (everything but the selection's), once more:
+// a step's first LET build is made speculatively beside the previous evaluation's rounds, which
+// still read the other set (engine.cpp spec_let_build; swap_let_sets exchanges the two).
+struct LetAlt {
+    BodyState sub_dst{};
+    uint64_t *s_keys = nullptr, *s_keys_s = nullptr, *s_spl = nullptr;
+    uint32_t *s_keys32 = nullptr, *s_keys32_s = nullptr, *s_idx = nullptr, *s_perm = nullptr;
+    int8_t *s_cpl = nullptr;
+    uint32_t *s_cnt = nullptr, *s_base = nullptr, *s_cell_start = nullptr;
+    uint32_t *s_span_list = nullptr, *s_super_list = nullptr, *s_bcount = nullptr,
+             *s_bstart = nullptr;
+    bh::SpanSlot *s_span_children = nullptr;
+    Node *s_nodes = nullptr;
+    uint32_t s_spl_nb = 0;
+    int64_t let_sub_cap = 0;
+    int let_J = -1;
+    size_t let_node_cap = 0;
+    hipEvent_t table_ev = nullptr;
+    int64_t set_cap = 0;
+    uint32_t *cstart = nullptr, *w = nullptr, *posc = nullptr, *bsz = nullptr, *csrc = nullptr,
+             *ccnt = nullptr, *cpos = nullptr, *lanes = nullptr, *subpos = nullptr;
+    LetCell *table = nullptr, *tables = nullptr, *levels = nullptr;
+    Node *nodes = nullptr;
+    uint32_t node_cap = 0;
+};
+
 struct bh_engine {
     bh_params p{};
     Geometry geo{};
@@ -195,6 +221,19 @@ struct bh_engine {
     bh::SpanSlot *s_span_children = nullptr;
     Node *s_nodes = nullptr;
     hipEvent_t table_ev = nullptr;
+    int64_t set_cap = 0;        // n capacity of this set's per-body arrays (L.lanes, L.subpos)
+    LetAlt la{};                // the other set (the speculative build's)
+    // the LET pipeline: step s+1's first build made beside step s's second evaluation
+    bool spec_allowed = false;  // set by step_once: the running evaluation is not the call's last
+    bool spec_ready = false;    // la holds the next evaluation's tree (spec_ev on spec_stream)
+    int64_t spec_n_sub = 0;
+    hipStream_t spec_stream = nullptr;
+    hipEvent_t spec_src_ev = nullptr, spec_ev = nullptr, spec_tab_ev = nullptr,
+               spec_flag_ev = nullptr;
+    uint32_t *spec_flag_h = nullptr;  // pinned: the crossing flag of the last LET build
+    LetCell *pub_table = nullptr;     // in-process group: the table this member exchanges now
+    hipEvent_t pub_table_ev = nullptr;
+    int64_t spec_builds = 0, spec_fallbacks = 0;
     bool inject_guard = false;  // bh_debug_inject(1): the next LET build trips k_let_guard
     bool agree_failed = false;  // in-process group: this member could not read a peer's flags
     // pipelined step (one GPU): the next step's first build runs on pipe_stream while this step's
@@ -630,7 +669,7 @@ int pinned_reserve(bh_engine *e, size_t bytes);
 #endif
 int let_alloc(bh_engine *e, int64_t n_sub) {
     const int J = e->geo.J;
-    if (e->let_cap < e->cap || !e->L.ecell) {  // per-body and per-cell arrays
+    if (e->let_cap < e->cap || !e->L.ecell) {  // the selection's per-body and per-cell arrays
         const int64_t cap = e->cap;
         LetBufs &L = e->L;
         TRY(dev_alloc(e, L.ecell, LET_CELLS));
@@ -639,6 +678,15 @@ int let_alloc(bh_engine *e, int64_t n_sub) {
         TRY(dev_alloc(e, L.flag8, cap));
         TRY(dev_alloc(e, L.sel, let_sel_blocks(cap) + 2));
         TRY(dev_alloc(e, L.selpos, let_sel_blocks(cap) + 2));
+        TRY(dev_alloc(e, e->inv_lanes, cap));
+        e->inv_valid = false;
+        TRY(dev_alloc(e, L.own, cap));
+        TRY(alloc_state(e, e->sub_src, cap));
+        e->let_cap = cap;
+    }
+    if (e->set_cap < e->cap || !e->L.cstart) {  // this set's per-cell and per-body arrays
+        const int64_t cap = e->cap;
+        LetBufs &L = e->L;
         TRY(dev_alloc(e, L.cstart, LET_CELLS + 1));
         TRY(dev_alloc(e, L.table, LET_TSTRIDE));
         TRY(dev_alloc(e, L.tables, (size_t)e->world * LET_TSTRIDE));
@@ -652,13 +700,9 @@ int let_alloc(bh_engine *e, int64_t n_sub) {
         TRY(dev_alloc(e, L.ccnt, LET_CELLS + 1));
         TRY(dev_alloc(e, L.cpos, LET_CELLS + 1));
         TRY(dev_alloc(e, L.lanes, cap));
-        TRY(dev_alloc(e, e->inv_lanes, cap));
-        e->inv_valid = false;
-        TRY(dev_alloc(e, L.own, cap));
         TRY(dev_alloc(e, L.subpos, cap));
-        TRY(alloc_state(e, e->sub_src, cap));
         if (!e->table_ev) HIPCHK(e, hipEventCreateWithFlags(&e->table_ev, hipEventDisableTiming));
-        e->let_cap = cap;
+        e->set_cap = cap;
     }
     e->L.scratch = e->scratch;
     e->L.scratch_bytes = e->scratch_bytes;
@@ -692,6 +736,50 @@ int let_alloc(bh_engine *e, int64_t n_sub) {
     e->let_sub_cap = sc;
     e->let_J = J;
     return BH_OK;
+}
+
+// Exchange the current LET build's buffers with the other set (LetAlt).
+void swap_let_sets(bh_engine *e) {
+    LetAlt &a = e->la;
+    LetBufs &L = e->L;
+    std::swap(e->sub_dst, a.sub_dst);
+    std::swap(e->s_keys, a.s_keys);
+    std::swap(e->s_keys_s, a.s_keys_s);
+    std::swap(e->s_spl, a.s_spl);
+    std::swap(e->s_keys32, a.s_keys32);
+    std::swap(e->s_keys32_s, a.s_keys32_s);
+    std::swap(e->s_idx, a.s_idx);
+    std::swap(e->s_perm, a.s_perm);
+    std::swap(e->s_cpl, a.s_cpl);
+    std::swap(e->s_cnt, a.s_cnt);
+    std::swap(e->s_base, a.s_base);
+    std::swap(e->s_cell_start, a.s_cell_start);
+    std::swap(e->s_span_list, a.s_span_list);
+    std::swap(e->s_super_list, a.s_super_list);
+    std::swap(e->s_bcount, a.s_bcount);
+    std::swap(e->s_bstart, a.s_bstart);
+    std::swap(e->s_span_children, a.s_span_children);
+    std::swap(e->s_nodes, a.s_nodes);
+    std::swap(e->s_spl_nb, a.s_spl_nb);
+    std::swap(e->let_sub_cap, a.let_sub_cap);
+    std::swap(e->let_J, a.let_J);
+    std::swap(e->let_node_cap, a.let_node_cap);
+    std::swap(e->table_ev, a.table_ev);
+    std::swap(e->set_cap, a.set_cap);
+    std::swap(L.cstart, a.cstart);
+    std::swap(L.w, a.w);
+    std::swap(L.posc, a.posc);
+    std::swap(L.bsz, a.bsz);
+    std::swap(L.csrc, a.csrc);
+    std::swap(L.ccnt, a.ccnt);
+    std::swap(L.cpos, a.cpos);
+    std::swap(L.lanes, a.lanes);
+    std::swap(L.subpos, a.subpos);
+    std::swap(L.table, a.table);
+    std::swap(L.tables, a.tables);
+    std::swap(L.levels, a.levels);
+    std::swap(L.nodes, a.nodes);
+    std::swap(L.node_cap, a.node_cap);
 }
 
 TreeBuffers let_tree_buffers(bh_engine *e) {
@@ -842,6 +930,100 @@ int sync_velocities(bh_engine *e) {
 int wave_order_for(bh_engine *e, int slot, int64_t lanes, hipStream_t s, WaveOrder &wo);
 int wave_order_next(bh_engine *e, int slot, int64_t lanes, hipStream_t s);
 
+#ifndef BH_LET_SPEC
+#define BH_LET_SPEC 1  // the LET pipeline: a step's first build beside the previous evaluation
+#endif
+int spec_events(bh_engine *e) {
+    if (e->spec_stream) return BH_OK;
+    int lo = 0, hi = 0;
+    HIPCHK(e, hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIPCHK(e, hipStreamCreateWithPriority(&e->spec_stream, hipStreamNonBlocking, hi));
+    for (hipEvent_t *ev : {&e->spec_src_ev, &e->spec_ev, &e->spec_tab_ev, &e->spec_flag_ev})
+        HIPCHK(e, hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    HIPCHK(e, hipHostMalloc((void **)&e->spec_flag_h, 64, hipHostMallocDefault));
+    return BH_OK;
+}
+
+// Every rank's LET cell table into L.tables, on stream s.  RCCL: one all-gather -- on the engine's
+// stream for the evaluation's own build, on the comm stream behind the rounds' gathers already
+// queued there for the speculative one (collectives keep one order on every rank).  In-process
+// group: each member publishes its table and event, then copies every member's.
+int exchange_tables(bh_engine *e, hipStream_t s, bool spec) {
+    const size_t tbytes = sizeof(LetCell) * (size_t)LET_TSTRIDE;
+    if (e->comm) {
+        if (!spec) {
+            NCCLCHK(e, ncclAllGather(e->L.table, e->L.tables, tbytes, ncclUint8, e->comm, s));
+        } else {
+            HIPCHK(e, hipEventRecord(e->spec_tab_ev, s));
+            HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->spec_tab_ev, 0));
+            NCCLCHK(e, ncclAllGather(e->L.table, e->L.tables, tbytes, ncclUint8, e->comm,
+                                     e->comm_stream));
+            HIPCHK(e, hipEventRecord(e->spec_tab_ev, e->comm_stream));
+            HIPCHK(e, hipStreamWaitEvent(s, e->spec_tab_ev, 0));
+        }
+    } else if (e->solo) {  // own values first, the rest from the last full build
+        HIPCHK(e, hipMemcpyAsync(e->L.tables, e->L.table, tbytes, hipMemcpyDeviceToDevice, s));
+        if (e->world > 1 && e->solo_table)
+            HIPCHK(e, hipMemcpyAsync(e->L.tables + LET_TSTRIDE, e->solo_table, tbytes,
+                                     hipMemcpyDeviceToDevice, s));
+    } else {
+        // (a member reads the published pointers after the barrier; it publishes again only
+        // after the round barriers that follow, which every member passes first)
+        e->pub_table = e->L.table;
+        e->pub_table_ev = e->table_ev;
+        HIPCHK(e, hipEventRecord(e->table_ev, s));
+        e->group->barrier();
+        for (int q = 0; q < e->world; ++q) {
+            bh_engine *peer = e->group->members[q];
+            if (peer != e) HIPCHK(e, hipStreamWaitEvent(s, peer->pub_table_ev, 0));
+            HIPCHK(e, hipMemcpyAsync(e->L.tables + (size_t)q * LET_TSTRIDE, peer->pub_table, tbytes,
+                                     hipMemcpyDeviceToDevice, s));
+        }
+    }
+    return BH_OK;
+}
+
+// The next evaluation's LET build, made now on spec_stream beside this evaluation's rounds: the
+// same subset (no body changed cells: checked), with the positions this evaluation's build left
+// (sub_dst, its jitter applied), built into the other buffer set; the next evaluation takes it
+// over (evaluate_let, spec_ready) instead of selecting and building.
+int spec_let_build(bh_engine *e, int64_t n_sub, const LetPieces &pc) {
+    hipStream_t ss = e->spec_stream;
+    HIPCHK(e, hipStreamWaitEvent(ss, e->spec_src_ev, 0));
+    const BodyState src = e->sub_dst;  // this evaluation's subset, as its build left it
+    swap_let_sets(e);
+    int rc = let_alloc(e, n_sub);
+    if (rc == BH_OK) {
+        TreeBuffers sb = let_tree_buffers(e);
+        sb.src = src;
+        sb.keys_ready = false;
+        hipError_t hr = tree_build(sb, n_sub, e->geo, ss);
+        if (hr == hipSuccess) {
+            e->s_spl_nb = sort_buckets(n_sub);
+            hr = hipMemsetAsync(e->L.table + LET_CELLS, 0, sizeof(LetCell), ss);  // status: none
+        }
+        if (hr == hipSuccess) hr = let_table(n_sub, e->geo, e->L, sb, ss);
+        if (hr != hipSuccess) {
+            e->err = std::string("spec_let_build: ") + hipGetErrorString(hr);
+            rc = BH_E_DEVICE;
+        }
+        if (rc == BH_OK) rc = exchange_tables(e, ss, true);
+        if (rc == BH_OK) {
+            hr = let_assemble(n_sub, e->geo, pc, e->L, sb, e->scalars, ss);
+            if (hr == hipSuccess) hr = hipEventRecord(e->spec_ev, ss);
+            if (hr != hipSuccess) {
+                e->err = std::string("spec_let_build: ") + hipGetErrorString(hr);
+                rc = BH_E_DEVICE;
+            }
+        }
+    }
+    swap_let_sets(e);  // the current set stays this evaluation's until the next one takes over
+    if (rc != BH_OK) return rc;
+    e->spec_ready = true;
+    e->spec_n_sub = n_sub;
+    return BH_OK;
+}
+
 int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     *done = false;
     if (kick != KICK_DRIFT && kick != KICK_ONLY) return BH_OK;
@@ -860,78 +1042,93 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         for (bh_engine *peer : e->group->members)
             if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->gathered_ev, 0));
     }
-    TRY(let_alloc(e, 0));
-    // subset capacity: the largest subset of the previous call + headroom, no host round trip;
-    // a subset beyond it is an overflow every rank sees after the exchange, and bh_step replays
-    // the call with the observed size (the first LET build of an engine reads its size once)
-    // (the selection writes sub_src, sized for the whole state; padding up to S = n is harmless)
-    int64_t S = e->let_known > 0 ? std::min<int64_t>(n, e->let_known + e->let_known / 8 + 4096) : n;
-    PosSrc ps{nullptr, GatherLayout{}, nullptr};
-    if (e->pos_pending && lanes != e->pos_lanes) TRY(materialize_positions(e));  // map changed
-    if (e->pos_pending) {  // the previous LET evaluation's positions, straight from a2
-        if (!e->inv_valid) {  // per lane map: each slot's position in the exchange buffer
-            let_gather_slots(n, lanes, e->pos_layout, e->inv_lanes, e->stream);
-            HIPCHK(e, hipGetLastError());
-            e->inv_valid = true;
-        }
-        ps = PosSrc{e->a2, e->pos_layout, e->inv_lanes};
-    }
-    // the subset build's keys and buckets from the gather when its buffers and splitters are
-    // those of the previous LET build (same S capacity and J; not the first build, which sorts
-    // with rocprim and sizes the subset afterwards)
-    MortonFuse mf{};
-    const bool fuse = BH_LET_FUSE_KEYS && e->let_known > 0 && e->s_spl_nb > 0 &&
-                      S <= e->let_sub_cap && e->geo.J == e->let_J && e->s_keys;
-    if (fuse)
-        mf = MortonFuse{e->s_keys, e->s_keys32, e->s_spl, e->s_spl_nb, e->s_cnt, e->s_base,
-                        e->s_bcount};
-    HIPCHK(e, let_select(e->st, ps, e->geo, pc, gap2, e->L, e->sub_src, S, e->scalars,
-                         e->stream, mf));
-    if (e->let_known <= 0) {
-        TRY(pinned_reserve(e, 64));
-        uint32_t *h = static_cast<uint32_t *>(e->pin);
-        HIPCHK(e, hipMemcpyAsync(h, e->L.selpos + let_sel_blocks(n), sizeof(uint32_t), hipMemcpyDeviceToHost,
-                                 e->stream));
-        HIPCHK(e, hipStreamSynchronize(e->stream));
-        e->let_known = std::max<int64_t>(h[0], 1);
-        S = std::min<int64_t>(n, e->let_known + e->let_known / 8 + 4096);  // padded above
-    }
-    TRY(let_alloc(e, S));
-    const int64_t n_sub = S;  // padded: bodies past the real subset are dead
-    ++e->let_builds;
-    TreeBuffers sb = let_tree_buffers(e);
-    sb.keys_ready = fuse && e->s_spl_nb > 0;  // (let_alloc above kept the buffers: S fitted)
-    HIPCHK(e, tree_build(sb, n_sub, e->geo, e->stream));
-    e->s_spl_nb = sort_buckets(n_sub);  // k_prep wrote this build's splitters
-    HIPCHK(e, let_table(n_sub, e->geo, e->L, sb, e->stream));
-    const size_t tbytes = sizeof(LetCell) * (size_t)LET_TSTRIDE;
-    if (e->comm) {
-        NCCLCHK(e, ncclAllGather(e->L.table, e->L.tables, tbytes, ncclUint8, e->comm, e->stream));
-    } else if (e->solo) {  // own values first, the rest from the last full build
-        HIPCHK(e, hipMemcpyAsync(e->L.tables, e->L.table, tbytes, hipMemcpyDeviceToDevice,
-                                 e->stream));
-        if (e->world > 1 && e->solo_table)
-            HIPCHK(e, hipMemcpyAsync(e->L.tables + LET_TSTRIDE, e->solo_table, tbytes,
-                                     hipMemcpyDeviceToDevice, e->stream));
-    } else {
-        HIPCHK(e, hipEventRecord(e->table_ev, e->stream));
-        e->group->barrier();
-        for (int q = 0; q < e->world; ++q) {
-            bh_engine *peer = e->group->members[q];
-            if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->table_ev, 0));
-            HIPCHK(e, hipMemcpyAsync(e->L.tables + (size_t)q * LET_TSTRIDE, peer->L.table, tbytes,
-                                     hipMemcpyDeviceToDevice, e->stream));
+    int64_t n_sub = 0;
+    bool spec_used = false;
+    if (e->spec_ready) {
+        e->spec_ready = false;
+        if (kick == KICK_DRIFT && e->spec_n_sub > 0) {
+            // this tree was built beside the previous evaluation's rounds (spec_let_build)
+            HIPCHK(e, hipStreamWaitEvent(e->stream, e->spec_ev, 0));
+            swap_let_sets(e);
+            n_sub = e->spec_n_sub;
+            ++e->let_builds;
+            ++e->spec_builds;
+            spec_used = true;
         }
     }
-    {
-        // bh_debug_inject: a node array of one record makes k_let_guard fire on this rank only,
-        // exactly as a broken invariant would (empty tree, idle lanes, replay flag set)
-        const uint32_t node_cap = e->L.node_cap;
-        if (e->inject_guard) e->L.node_cap = 1u;
-        e->inject_guard = false;
-        const hipError_t rc = let_assemble(n_sub, e->geo, pc, e->L, sb, e->scalars, e->stream);
-        e->L.node_cap = node_cap;
-        HIPCHK(e, rc);
+    // may the next evaluation's first build be made speculatively beside this one's rounds?  Only
+    // where nothing but this build's jitter moves a body in between: the second evaluation of a
+    // step that is not the call's last, no merge rule that can act (BHA:438), the next build a
+    // LET build too.  Whether the jitter moved a body across a depth-8 cell is known after the
+    // table exchange (every rank alike).
+    const bool spec_want = BH_LET_SPEC && !spec_used && kick == KICK_ONLY && e->spec_allowed &&
+                           (e->p.merge_min_dist <= 0.0 || !e->heavy_possible) &&
+                           e->let_age + 1 < BH_LET_REFRESH;
+    if (!spec_used) {
+        TRY(let_alloc(e, 0));
+        // subset capacity: the largest subset of the previous call + headroom, no host round trip;
+        // a subset beyond it is an overflow every rank sees after the exchange, and bh_step replays
+        // the call with the observed size (the first LET build of an engine reads its size once)
+        // (the selection writes sub_src, sized for the whole state; padding up to S = n is harmless)
+        int64_t S = e->let_known > 0 ? std::min<int64_t>(n, e->let_known + e->let_known / 8 + 4096) : n;
+        PosSrc ps{nullptr, GatherLayout{}, nullptr};
+        if (e->pos_pending && lanes != e->pos_lanes) TRY(materialize_positions(e));  // map changed
+        if (e->pos_pending) {  // the previous LET evaluation's positions, straight from a2
+            if (!e->inv_valid) {  // per lane map: each slot's position in the exchange buffer
+                let_gather_slots(n, lanes, e->pos_layout, e->inv_lanes, e->stream);
+                HIPCHK(e, hipGetLastError());
+                e->inv_valid = true;
+            }
+            ps = PosSrc{e->a2, e->pos_layout, e->inv_lanes};
+        }
+        // the subset build's keys and buckets from the gather when its buffers and splitters are
+        // those of the previous LET build (same S capacity and J; not the first build, which sorts
+        // with rocprim and sizes the subset afterwards)
+        MortonFuse mf{};
+        const bool fuse = BH_LET_FUSE_KEYS && e->let_known > 0 && e->s_spl_nb > 0 &&
+                          S <= e->let_sub_cap && e->geo.J == e->let_J && e->s_keys;
+        if (fuse)
+            mf = MortonFuse{e->s_keys, e->s_keys32, e->s_spl, e->s_spl_nb, e->s_cnt, e->s_base,
+                            e->s_bcount};
+        HIPCHK(e, let_select(e->st, ps, e->geo, pc, gap2, e->L, e->sub_src, S, e->scalars,
+                             e->stream, mf));
+        if (e->let_known <= 0) {
+            TRY(pinned_reserve(e, 64));
+            uint32_t *h = static_cast<uint32_t *>(e->pin);
+            HIPCHK(e, hipMemcpyAsync(h, e->L.selpos + let_sel_blocks(n), sizeof(uint32_t), hipMemcpyDeviceToHost,
+                                     e->stream));
+            HIPCHK(e, hipStreamSynchronize(e->stream));
+            e->let_known = std::max<int64_t>(h[0], 1);
+            S = std::min<int64_t>(n, e->let_known + e->let_known / 8 + 4096);  // padded above
+        }
+        TRY(let_alloc(e, S));
+        n_sub = S;  // padded: bodies past the real subset are dead
+        ++e->let_builds;
+        TreeBuffers sb = let_tree_buffers(e);
+        sb.keys_ready = fuse && e->s_spl_nb > 0;  // (let_alloc above kept the buffers: S fitted)
+        HIPCHK(e, tree_build(sb, n_sub, e->geo, e->stream));
+        e->s_spl_nb = sort_buckets(n_sub);  // k_prep wrote this build's splitters
+        HIPCHK(e, let_table(n_sub, e->geo, e->L, sb, e->stream, spec_want));
+        if (spec_want) TRY(spec_events(e));
+        TRY(exchange_tables(e, e->stream, false));
+        {
+            // bh_debug_inject: a node array of one record makes k_let_guard fire on this rank only,
+            // exactly as a broken invariant would (empty tree, idle lanes, replay flag set)
+            const uint32_t node_cap = e->L.node_cap;
+            if (e->inject_guard) e->L.node_cap = 1u;
+            e->inject_guard = false;
+            const hipError_t rc = let_assemble(n_sub, e->geo, pc, e->L, sb, e->scalars, e->stream,
+                                               spec_want ? e->scalars + 10 : nullptr);
+            e->L.node_cap = node_cap;
+            HIPCHK(e, rc);
+        }
+        if (spec_want) {  // the crossing flag, read while the rounds below run
+            HIPCHK(e, hipMemcpyAsync(e->spec_flag_h, e->scalars + 10, sizeof(uint32_t),
+                                     hipMemcpyDeviceToHost, e->stream));
+            HIPCHK(e, hipEventRecord(e->spec_flag_ev, e->stream));
+            // sub_dst is final, and the assembly's scans are done with the shared scratch
+            HIPCHK(e, hipEventRecord(e->spec_src_ev, e->stream));
+        }
     }
     TRY(mark(e, 0));
     const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};
@@ -959,6 +1156,11 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
         if (e->group) e->group->barrier();
         TRY(gather_round(e, gl, k, W, k));
+    }
+    if (spec_want) {
+        HIPCHK(e, hipEventSynchronize(e->spec_flag_ev));
+        if (*e->spec_flag_h == 0u) TRY(spec_let_build(e, n_sub, pc));
+        else ++e->spec_fallbacks;  // a body changed cells: the next evaluation selects anew
     }
     TRY(mark(e, 1));
     HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
@@ -1026,6 +1228,7 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
         }
     }
     e->let_age = 0;
+    e->spec_ready = false;  // (a speculative LET build is only ever taken by a LET evaluation)
     const int64_t n = e->n;
     bool have_forces = false;  // a(t) on this tree, evaluated ahead by the previous step
     if (e->prebuilt) {  // the pipelined step built this tree (single GPU: nothing deferred)
@@ -1338,6 +1541,7 @@ int restore(bh_engine *e) {
     e->view_pending = false;
     e->lt_aside = false;
     e->mir_fresh = false;
+    e->spec_ready = false;
     e->spl_nb = 0;  // the splitters describe the discarded builds' order
     e->keys_ready = false;
     e->lanes_valid = false;
@@ -1666,7 +1870,10 @@ int step_once(bh_engine *e, bool last) {
         const bool lazy = last && BH_LAZY_LASTTREE && (e->comm || e->group || e->solo);
         if (lazy) TRY(snapshot_positions(e));
         bool let2 = false;
-        TRY(evaluate(e, nullptr, KICK_ONLY, &fused, !last || lazy, &let2));  // a(t+dt)
+        e->spec_allowed = !last;  // the next step's first build may be made beside this evaluation
+        const int rc2 = evaluate(e, nullptr, KICK_ONLY, &fused, !last || lazy, &let2);  // a(t+dt)
+        e->spec_allowed = false;
+        TRY(rc2);
         if (!fused) {
             TRY(mark(e, -1));
             kick(n, e->a2, e->st.vx, e->st.vy, dtHalf, e->stream, e->a2_lanes, e->a2_layout);
@@ -2041,6 +2248,7 @@ void bh_destroy(bh_engine *e) {
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
+    if (e->spec_stream) (void)hipStreamSynchronize(e->spec_stream);
     if (e->comm) (void)ncclCommDestroy(e->comm);
     if (e->group && e->rank < (int)e->group->members.size() && e->group->members[e->rank] == e)
         e->group->members[e->rank] = nullptr;
@@ -2072,6 +2280,22 @@ void bh_destroy(bh_engine *e) {
     free_state(e->snap);
     free_state(e->sub_src);
     free_state(e->sub_dst);
+    {
+        LetAlt &a = e->la;
+        free_state(a.sub_dst);
+        void *alts[] = {a.s_keys, a.s_keys_s, a.s_spl, a.s_keys32, a.s_keys32_s, a.s_idx,
+                        a.s_perm, a.s_cpl, a.s_cnt, a.s_base, a.s_cell_start, a.s_span_list,
+                        a.s_super_list, a.s_bcount, a.s_bstart, a.s_span_children, a.s_nodes,
+                        a.cstart, a.w, a.posc, a.bsz, a.csrc, a.ccnt, a.cpos, a.lanes, a.subpos,
+                        a.table, a.tables, a.levels, a.nodes};
+        for (void *q : alts)
+            if (q) (void)hipFree(q);
+        if (a.table_ev) (void)hipEventDestroy(a.table_ev);
+    }
+    if (e->spec_stream) (void)hipStreamDestroy(e->spec_stream);
+    for (hipEvent_t ev : {e->spec_src_ev, e->spec_ev, e->spec_tab_ev, e->spec_flag_ev})
+        if (ev) (void)hipEventDestroy(ev);
+    if (e->spec_flag_h) (void)hipHostFree(e->spec_flag_h);
     if (e->table_ev) (void)hipEventDestroy(e->table_ev);
     void *lets[] = {e->inv_lanes, e->L.csrc, e->L.ccnt, e->L.cpos, e->solo_table, e->solo_all, e->solo_cstart, e->L.ecell, e->L.hcell, e->L.own, e->L.subpos, e->L.flag_all, e->L.flag8, e->L.sel, e->L.selpos, e->L.cstart,
                     e->L.table, e->L.tables, e->L.levels, e->L.w, e->L.posc, e->L.bsz,
@@ -2167,6 +2391,7 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     e->tree_valid = false;  // BHA:348
     e->lazy_tree = false;
     e->prebuilt = false;    // other bodies: the pipelined call's next tree is void
+    e->spec_ready = false;
     e->view_pending = false;
     e->lt_aside = false;
     e->mir_fresh = false;
@@ -2208,6 +2433,7 @@ int bh_step(bh_engine *e, int32_t k) {
         if (k > 0) e->prebuilt = first && carried;
         e->lazy_tree = false;
         e->mir_launched = false;
+        e->spec_ready = false;
         for (int32_t s = 0; s < k; ++s) TRY(step_once(e, s + 1 == k));
         HIPCHK(e, hipStreamSynchronize(e->stream));
         if (may_let) {  // LET subset sizes of this call: [4] some rank overflowed, [5] largest
@@ -2517,6 +2743,13 @@ int bh_let_stats(const bh_engine *e, int64_t *out4) {
         hipMemcpy(&T, e->L.posc + LET_CELLS, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
         return BH_E_DEVICE;
     out4[3] = T;
+    return BH_OK;
+}
+
+int bh_let_spec_stats(const bh_engine *e, int64_t *out2) {
+    if (!e || !out2) return BH_E_INVALID;
+    out2[0] = e->spec_builds;
+    out2[1] = e->spec_fallbacks;
     return BH_OK;
 }
 

@@ -209,6 +209,12 @@ int bh_traversal_counters(const bh_engine *e, int64_t *out5);
  * enables them also on one rank, BH_LET=0 keeps every build full. */
 int bh_let_stats(const bh_engine *e, int64_t *out5);
 
+/* The LET pipeline of multi-rank engines: out2[0] LET builds made speculatively beside the
+ * previous evaluation's rounds (a step's first build, reusing the second build's subset with the
+ * positions it left) and taken over, out2[1] evaluations whose speculation was called off because
+ * the build's jitter (BHA:146-151) moved a body into another depth-8 cell on some rank. */
+int bh_let_spec_stats(const bh_engine *e, int64_t *out2);
+
 /* Enable/disable per-phase event timing (default off: no events in the hot loop). */
 int bh_set_profiling(bh_engine *e, int enabled);
 

@@ -12,6 +12,8 @@
 #                  (tools/profile.sh; CONFIG=c5 etc. for another workload) -> prof_<CONFIG>/
 #   sq             SQ counters of the traversal (tools/profile_sq.sh)
 #   timeline       one C3 bench under a kernel trace, summarised per step (tools/timeline.py)
+#   dropin         the front-end's one-step calls under a kernel + copy trace (tools/dropin_calls.py,
+#                  summarised by tools/timeline.py)                             -> ${TAG}_dropin_*
 #   solo           one rank's share of the 8-GPU C4 step, alone (tools/solo_rank.py, ranks 0, 5)
 #   ab             A/B of in-tree library builds (tools/ab.sh; LIBS="A B", AB_ARGS=...)
 # Every GPU step runs under its own time limit; a failing step (any rc but 0) ends the session, so
@@ -50,6 +52,13 @@ for step in "$@"; do
     timeline)
       run 600 ${O}_timeline.log rocprofv3 --kernel-trace -d ${O}_tl -o run --output-format csv \
         -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-counters --no-drop-in ;;
+    dropin)
+      export TMPDIR=/tmp
+      run 600 ${O}_dropin.log rocprofv3 --kernel-trace --memory-copy-trace -d ${O}_dropin_trace \
+        -o run --output-format csv -- python3 tools/dropin_calls.py
+      kt=$(find ${O}_dropin_trace -name '*kernel_trace.csv' | head -1)
+      python3 tools/timeline.py "$kt" 2 ${O}_dropin_timeline.txt > /dev/null
+      tail -4 ${O}_dropin_timeline.txt ;;
     solo)
       for r in 0 5; do
         run 600 ${O}_solo$r.log python -u tools/solo_rank.py --config c4 --world 8 --rank $r
