@@ -50,7 +50,7 @@ def scene():
             np.concatenate([vy, np.zeros(k)]), np.concatenate([m, em]))
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, params=None):
     import sys
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     sys.path[:0] = [root, os.path.join(root, "barnes-hut-n-body_amd"), os.path.dirname(__file__)]
@@ -58,7 +58,7 @@ def _worker(rank, world, port, out_dir):
 
     dist.init_process_group("gloo", init_method=f"tcp://127.0.0.1:{port}", rank=rank,
                             world_size=world)
-    mr = MirrorRank(PARAMS, rank, world, dist)
+    mr = MirrorRank(params or PARAMS, rank, world, dist)
     mr.reset_bodies(*scene())
     for k in CALLS:
         mr.step(k)
@@ -69,18 +69,23 @@ def _worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_exchange_protocol_matches_the_reference_step(tmp_path, world):
+@pytest.mark.parametrize("world,merge", [(2, True), (3, True), (2, False), (3, False)])
+def test_exchange_protocol_matches_the_reference_step(tmp_path, world, merge):
+    """merge=False: no merge rule, so the LET pipeline runs -- a step's first LET build reuses
+    the previous evaluation's subset with the positions its build left (engine.cpp
+    spec_let_build)."""
     import bh_amd  # noqa: F401  (the engine library's host-only shard layout must load)
     import oracle
 
-    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    params = dict(PARAMS, merge_min_dist=8.0 if merge else 0.0)
+    mp.spawn(_worker, args=(world, _free_port(), str(tmp_path), params), nprocs=world, join=True)
     arrs = scene()
-    ref = oracle.Oracle(*arrs, threads=1, **PARAMS)
+    ref = oracle.Oracle(*arrs, threads=1, **params)
     for k in CALLS:
         ref.step(k)
     want = ref.get_bodies()
-    assert len(want[0]) < len(arrs[0])  # the merge rule removed bodies
+    if merge:
+        assert len(want[0]) < len(arrs[0])  # the merge rule removed bodies
     for r in range(world):
         got = np.load(tmp_path / f"rank{r}.npz")
         stats = json.load(open(tmp_path / f"stats{r}.json"))
@@ -89,6 +94,10 @@ def test_exchange_protocol_matches_the_reference_step(tmp_path, world):
         assert stats["let"] == 2 * sum(CALLS) - len(CALLS) - 1 and stats["full"] == len(CALLS) + 1
         assert stats["vel_syncs"] == len(CALLS)
         assert stats["merged"] == len(arrs[0]) - len(want[0])
+        # speculative builds: the first build of every step after the first of each call
+        assert stats["spec"] + stats["spec_off"] == (0 if merge else sum(CALLS) - len(CALLS)), stats
+        if not merge:
+            assert stats["spec"] >= 1, stats
         # every rank owns bodies; at world 3 a rank builds a part of the scene only
         assert 0 < stats["max_subset"] <= len(arrs[0])
         if world == 3:

@@ -15,6 +15,8 @@
 #   dropin         the front-end's one-step calls under a kernel + copy trace (tools/dropin_calls.py,
 #                  summarised by tools/timeline.py)                             -> ${TAG}_dropin_*
 #   solo           one rank's share of the 8-GPU C4 step, alone (tools/solo_rank.py, ranks 0, 5)
+#   soloab         the solo step of rank 0 (C4 / 8) alternately with lib/libA.so and the default
+#                  build, 2 rounds                                             -> ${TAG}_soloab.jsonl
 #   ab             A/B of in-tree library builds (tools/ab.sh; LIBS="A B", AB_ARGS=...)
 # Every GPU step runs under its own time limit; a failing step (any rc but 0) ends the session, so
 # nothing else touches the GPU after a fault, an abort or a timeout.
@@ -63,6 +65,17 @@ for step in "$@"; do
       for r in 0 5; do
         run 600 ${O}_solo$r.log python -u tools/solo_rank.py --config c4 --world 8 --rank $r
         grep '^{' ${O}_solo$r.log | tail -1 >> ${O}_solo.jsonl
+      done ;;
+    soloab)
+      for rr in 1 2; do
+        for L in A default; do
+          lib=$PWD/barnes-hut-n-body_amd/lib/libbh_engine.so
+          [ $L = A ] && lib=$PWD/barnes-hut-n-body_amd/lib/libA.so
+          export BH_ENGINE_LIB=$lib
+          run 600 ${O}_soloab_$L$rr.log python -u tools/solo_rank.py --config c4 --world 8 --rank 0
+          unset BH_ENGINE_LIB
+          echo "{\"lib\": \"$L\", \"line\": $(grep '^{' ${O}_soloab_$L$rr.log | tail -1)}" >> ${O}_soloab.jsonl
+        done
       done ;;
     ab) run 1800 ${O}_ab.log bash tools/ab.sh ;;
     *) echo "unknown step $step"; exit 2 ;;
