@@ -1407,7 +1407,10 @@ int merge(bh_engine *e, hipStream_t s = nullptr, bool header_zeroed = false) {
 // renumber caller indices; record the removals for bh_last_removed.  *overflow receives the
 // candidate count of a step whose pairs did not fit the mailbox (nothing is compacted then:
 // the call is replayed from its snapshot with a larger mailbox, see bh_step).
-int finish_merges(bh_engine *e, uint32_t *overflow) {
+// *tree_flags receives scalars[1] (the builds' error flags) when the merge rule ran (the same
+// read-back), else *have_flags stays false.
+int finish_merges(bh_engine *e, uint32_t *overflow, uint32_t *tree_flags = nullptr,
+                  bool *have_flags = nullptr) {
     *overflow = 0;
     e->removed.clear();
     if (!e->merge_ran) return BH_OK;
@@ -1427,6 +1430,8 @@ int finish_merges(bh_engine *e, uint32_t *overflow) {
     HIPCHK(e, hipMemcpyAsync(hlog, e->dlog, sizeof(uint32_t) * ahead, hipMemcpyDeviceToHost,
                              e->stream));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (tree_flags) *tree_flags = h[1];
+    if (have_flags) *have_flags = true;
     const uint32_t nd = h[2];
     const uint32_t nd_before_last = h[12];  // removals before the call's last merge rule
     const MergeHeader hdr = *reinterpret_cast<const MergeHeader *>(h + 4);
@@ -2466,9 +2471,19 @@ int bh_step(bh_engine *e, int32_t k) {
             TRY(sync_velocities(e));
         }
         // the merge bookkeeping first, so that an error below leaves a compacted state
-        const int tree_rc = (e->n > 0 && k > 0) ? check_tree_flags(e) : BH_OK;
-        uint32_t overflow = 0;
-        TRY(finish_merges(e, &overflow));
+        uint32_t overflow = 0, tflags = 0;
+        bool have_flags = false;
+        TRY(finish_merges(e, &overflow, &tflags, &have_flags));  // (reads the flags too)
+        int tree_rc = BH_OK;
+        if (e->n > 0 && k > 0) {
+            if (!have_flags) {
+                tree_rc = check_tree_flags(e);
+            } else if (tflags) {
+                e->err = "jitter replay reached an unsupported geometry (body stayed inside a "
+                         "depth J+1 cell)";
+                tree_rc = BH_E_STATE;
+            }
+        }
         if (overflow) {  // a step's candidate pairs exceeded the mailbox: replay the call
             if (!may_merge) {
                 e->err = "merge rule: candidate mailbox overflow without a snapshot";
