@@ -1085,6 +1085,24 @@ constexpr uint32_t SPAN_REF = 1u << 31;  // child list entry: owner slot of a sp
 constexpr uint32_t SPAN_SUPER = 1u << 31;
 constexpr int SPAN_GROUP = 1024;
 
+// Experiment (BH_SPAN_XCD): the span passes' producers and their consumer on one XCD, so that the
+// level-by-level pass (k_com_span) reads span_list / span_children from its own L2.  Every
+// logical block is launched 8 times; the copy that runs on the group's XCD (g % 8, read from
+// HW_REG_XCC_ID) does the work.  (Relies on 8 consecutive blocks landing on 8 XCDs.)
+#ifndef BH_SPAN_XCD
+#define BH_SPAN_XCD 0
+#endif
+__device__ __forceinline__ uint32_t xcc_id() {
+    return __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;
+}
+// logical block of this physical block, or -1 when another copy does it
+__device__ __forceinline__ int span_block(uint32_t per_group_blocks) {
+    if (!BH_SPAN_XCD) return (int)blockIdx.x;
+    const uint32_t lb = blockIdx.x >> 3;
+    const uint32_t g = lb / per_group_blocks;
+    return xcc_id() == (g & 7u) ? (int)lb : -1;
+}
+
 __global__ __launch_bounds__(TB) void k_span_find(int64_t n, int J, int D0,
                                                   const uint64_t *__restrict__ keys_s,
                                                   const int8_t *__restrict__ cpl,
@@ -1095,7 +1113,9 @@ __global__ __launch_bounds__(TB) void k_span_find(int64_t n, int J, int D0,
                                                   uint32_t *__restrict__ super_list,
                                                   uint32_t n_groups, Node *nodes) {
     chain_prio();
-    const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
+    const int lb = span_block(SPAN_GROUP / TB);
+    if (lb < 0) return;
+    const int64_t k = (int64_t)lb * TB + threadIdx.x;
     const int L = blockIdx.y;
     if (k >= (int64_t)span_stride) return;
     const int64_t chunk0 = k << COM_CHUNK_SHIFT;
@@ -1144,7 +1164,10 @@ __global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__r
                                                       SpanSlot *__restrict__ span_children) {
     chain_prio();
     const uint32_t L = blockIdx.y;
-    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < span_stride; i += gridDim.x * TB) {
+    const int lb = span_block(SPAN_GROUP / TB);
+    if (lb < 0) return;
+    const uint32_t nlb = BH_SPAN_XCD ? gridDim.x >> 3 : gridDim.x;
+    for (uint32_t i = (uint32_t)lb * TB + threadIdx.x; i < span_stride; i += nlb * TB) {
         const size_t slot = (size_t)L * span_stride + i;
         const uint32_t e = span_list[slot];
         if (e == NO_SPAN) continue;  // empty slot: never read
@@ -1209,7 +1232,9 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span(int J, const uint32_t *__r
                                                       Node *nodes) {
     chain_prio();
     __shared__ double r_m[2][SPAN_GROUP], r_x[2][SPAN_GROUP], r_y[2][SPAN_GROUP];
-    const uint32_t g0 = blockIdx.x * SPAN_GROUP;
+    const int gb = span_block(1);
+    if (gb < 0) return;
+    const uint32_t g0 = (uint32_t)gb * SPAN_GROUP;
     const uint32_t kl = threadIdx.x, k = g0 + kl;
     const bool valid = k < span_stride;
     // levels (bit L) at which this boundary owns a node finished here (not group-crossing)
@@ -1255,10 +1280,14 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span(int J, const uint32_t *__r
             r_x[cur][kl] = ox;
             r_y[cur][kl] = oy;
             Node *dst = nodes + C.ni;
+#ifndef BH_SPAN_NOSTORE  // (timing experiment only: results wrong)
             dst->mass = mSum;
             dst->comX = ox;  // massless: never visited (the cell centre is not recorded)
             dst->comY = oy;
             if (!(mSum > 0.0)) dst->meta |= NODE_SKIP | NODE_LEAF;  // a skip-leaf
+#else
+            (void)dst;
+#endif
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): LDS results visible; stores fly on
         __builtin_amdgcn_s_barrier();
@@ -1515,13 +1544,13 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     k_emit_com<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), EC_TB, 0, s>>>(
         n, g, D0, b.keys_s, b.cpl, b.base, b.cell_start, b.dst.x, b.dst.y, b.dst.m, b.dst.cidx,
         b.idx, b.nodes, b.scalars + 1, b.keys32, b.lanes_remap);
-    const dim3 span_grid((b.span_stride + TB - 1) / TB, g.J + 1);
+    const dim3 span_grid(((b.span_stride + TB - 1) / TB) * (BH_SPAN_XCD ? 8 : 1), g.J + 1);
     k_span_find<<<span_grid, TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cpl, b.base, b.cell_start,
                                          b.span_list, b.span_stride, b.super_list, n_groups,
                                          b.nodes);
     k_span_children<<<span_grid, TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.nodes,
                                              b.span_children);
-    k_com_span<<<n_groups, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
+    k_com_span<<<n_groups * (BH_SPAN_XCD ? 8 : 1), SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
                                             b.nodes);
     if (n_groups > 1)
         k_com_span_top<<<1, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,

@@ -78,6 +78,22 @@ for step in "$@"; do
         done
       done ;;
     ab) run 1800 ${O}_ab.log bash tools/ab.sh ;;
+    span)  # kernel-trace stats of C3 with the default build and the lib/libX.so / libN.so variants
+      export TMPDIR=/tmp
+      for L in default X N; do
+        lib=$PWD/barnes-hut-n-body_amd/lib/libbh_engine.so
+        [ $L = default ] || lib=$PWD/barnes-hut-n-body_amd/lib/lib$L.so
+        extra=""
+        [ $L = N ] && extra=--no-verify
+        export BH_ENGINE_LIB=$lib
+        run 600 ${O}_span_$L.log rocprofv3 --kernel-trace --stats -d ${O}_span_$L -o run \
+          --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline \
+          --no-counters --no-drop-in $extra
+        unset BH_ENGINE_LIB
+        st=$(find ${O}_span_$L -name '*kernel_stats.csv' | head -1)
+        grep -E 'k_com_span|k_span_|k_emit|k_build' "$st" | cut -d, -f1-5 > ${O}_span_$L.txt || true
+        cat ${O}_span_$L.txt
+      done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done
