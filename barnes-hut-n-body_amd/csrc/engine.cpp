@@ -229,8 +229,10 @@ struct bh_engine {
     int64_t spec_n_sub = 0;
     hipStream_t spec_stream = nullptr;
     hipEvent_t spec_src_ev = nullptr, spec_ev = nullptr, spec_tab_ev = nullptr,
-               spec_flag_ev = nullptr;
-    uint32_t *spec_flag_h = nullptr;  // pinned: the crossing flag of the last LET build
+               spec_flag_ev = nullptr, sub_cnt_ev = nullptr;
+    uint32_t *spec_flag_h = nullptr;  // pinned: [0] the crossing flag of the last LET build,
+                                      // [4] the last selection's subset size (sub_cnt_ev)
+    bool sub_cnt_pending = false;
     LetCell *pub_table = nullptr;     // in-process group: the table this member exchanges now
     hipEvent_t pub_table_ev = nullptr;
     int64_t spec_builds = 0, spec_fallbacks = 0;
@@ -441,8 +443,9 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         e->cost_stride = cap / 64 + 2;
         e->order_stride = (int64_t)wave_order_runs(cap) + 1;
         TRY(dev_alloc(e, e->wave_cost, (size_t)(e->cost_stride * (1 + BH_SHARD_ROUNDS))));
-        HIPCHK(e, hipMemset(e->wave_cost, 0,
-                            sizeof(uint32_t) * (size_t)(e->cost_stride * (1 + BH_SHARD_ROUNDS))));
+        HIPCHK(e, hipMemsetAsync(e->wave_cost, 0,
+                                 sizeof(uint32_t) * (size_t)(e->cost_stride * (1 + BH_SHARD_ROUNDS)),
+                                 e->stream));
         TRY(dev_alloc(e, e->run_order, (size_t)(e->order_stride * (1 + BH_SHARD_ROUNDS))));
         for (int64_t &o : e->order_n) o = 0;
         TRY(dev_alloc(e, e->heavy, cap));
@@ -451,7 +454,8 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(dev_alloc(e, e->spl, (size_t)sort_buckets(cap) + 2));
         TRY(dev_alloc(e, e->bcount, (size_t)sort_buckets(cap) + 2));
         TRY(dev_alloc(e, e->bstart, (size_t)sort_buckets(cap) + 2));
-        HIPCHK(e, hipMemset(e->bcount, 0, sizeof(uint32_t) * ((size_t)sort_buckets(cap) + 2)));
+        HIPCHK(e, hipMemsetAsync(e->bcount, 0, sizeof(uint32_t) * ((size_t)sort_buckets(cap) + 2),
+                                 e->stream));
         e->spl_nb = 0;
         e->keys_ready = false;
         e->cap = cap;
@@ -602,10 +606,10 @@ int build_into(bh_engine *e, hipStream_t s, bool overlap) {
     if (e->solo && n > 0 && e->p.theta != 0.0) {  // the peers' cell values for later LET builds
         if (!e->solo_table) {
             TRY(dev_alloc(e, e->solo_table, LET_TSTRIDE));
-            HIPCHK(e, hipMemset(e->solo_table, 0, sizeof(LetCell) * LET_TSTRIDE));
+            HIPCHK(e, hipMemsetAsync(e->solo_table, 0, sizeof(LetCell) * LET_TSTRIDE, e->stream));
             TRY(dev_alloc(e, e->solo_all, LET_CELLS));
             TRY(dev_alloc(e, e->solo_cstart, LET_CELLS + 1));
-            HIPCHK(e, hipMemset(e->solo_all, 1, LET_CELLS));
+            HIPCHK(e, hipMemsetAsync(e->solo_all, 1, LET_CELLS, e->stream));
         }
         LetBufs Ls{};
         Ls.ecell = e->solo_all;
@@ -667,7 +671,10 @@ int pinned_reserve(bh_engine *e, size_t bytes);
 #ifndef BH_LET_REFRESH
 #define BH_LET_REFRESH 32  // LET builds between full builds (the replicated Morton order)
 #endif
-int let_alloc(bh_engine *e, int64_t n_sub) {
+// s: the stream the set is built on next (the fills of fresh buffers are ordered before it: a
+// plain hipMemset is not ordered with the engine's non-blocking streams)
+int let_alloc(bh_engine *e, int64_t n_sub, hipStream_t s = nullptr) {
+    if (!s) s = e->stream;
     const int J = e->geo.J;
     if (e->let_cap < e->cap || !e->L.ecell) {  // the selection's per-body and per-cell arrays
         const int64_t cap = e->cap;
@@ -691,7 +698,7 @@ int let_alloc(bh_engine *e, int64_t n_sub) {
         TRY(dev_alloc(e, L.table, LET_TSTRIDE));
         TRY(dev_alloc(e, L.tables, (size_t)e->world * LET_TSTRIDE));
         // (solo: the tables of ranks 2 .. world-1 stay zero -- nothing tagged -- for good)
-        HIPCHK(e, hipMemset(L.tables, 0, sizeof(LetCell) * (size_t)e->world * LET_TSTRIDE));
+        HIPCHK(e, hipMemsetAsync(L.tables, 0, sizeof(LetCell) * (size_t)e->world * LET_TSTRIDE, s));
         TRY(dev_alloc(e, L.levels, ((size_t)1 << (2 * LET_P + 2)) / 3 + 1));
         TRY(dev_alloc(e, L.w, LET_CELLS + 1));
         TRY(dev_alloc(e, L.posc, LET_CELLS + 1));
@@ -731,7 +738,7 @@ int let_alloc(bh_engine *e, int64_t n_sub) {
     TRY(dev_alloc(e, e->s_spl, (size_t)sort_buckets(sc) + 2));
     TRY(dev_alloc(e, e->s_bcount, (size_t)sort_buckets(sc) + 2));
     TRY(dev_alloc(e, e->s_bstart, (size_t)sort_buckets(sc) + 2));
-    HIPCHK(e, hipMemset(e->s_bcount, 0, sizeof(uint32_t) * ((size_t)sort_buckets(sc) + 2)));
+    HIPCHK(e, hipMemsetAsync(e->s_bcount, 0, sizeof(uint32_t) * ((size_t)sort_buckets(sc) + 2), s));
     e->s_spl_nb = 0;
     e->let_sub_cap = sc;
     e->let_J = J;
@@ -938,7 +945,8 @@ int spec_events(bh_engine *e) {
     int lo = 0, hi = 0;
     HIPCHK(e, hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIPCHK(e, hipStreamCreateWithPriority(&e->spec_stream, hipStreamNonBlocking, hi));
-    for (hipEvent_t *ev : {&e->spec_src_ev, &e->spec_ev, &e->spec_tab_ev, &e->spec_flag_ev})
+    for (hipEvent_t *ev :
+         {&e->spec_src_ev, &e->spec_ev, &e->spec_tab_ev, &e->spec_flag_ev, &e->sub_cnt_ev})
         HIPCHK(e, hipEventCreateWithFlags(ev, hipEventDisableTiming));
     HIPCHK(e, hipHostMalloc((void **)&e->spec_flag_h, 64, hipHostMallocDefault));
     return BH_OK;
@@ -992,7 +1000,7 @@ int spec_let_build(bh_engine *e, int64_t n_sub, const LetPieces &pc) {
     HIPCHK(e, hipStreamWaitEvent(ss, e->spec_src_ev, 0));
     const BodyState src = e->sub_dst;  // this evaluation's subset, as its build left it
     swap_let_sets(e);
-    int rc = let_alloc(e, n_sub);
+    int rc = let_alloc(e, n_sub, ss);
     if (rc == BH_OK) {
         TreeBuffers sb = let_tree_buffers(e);
         sb.src = src;
@@ -1024,6 +1032,65 @@ int spec_let_build(bh_engine *e, int64_t n_sub, const LetPieces &pc) {
     return BH_OK;
 }
 
+// BH_SPEC_CHECK=1 (diagnostic): a speculative build is not taken over; the evaluation selects and
+// builds as usual and the two trees are compared on the host (mismatch counts on stderr).
+bool spec_check_on() {
+    static const bool on = [] {
+        const char *v = std::getenv("BH_SPEC_CHECK");
+        return v && std::strcmp(v, "0") != 0;
+    }();
+    return on;
+}
+
+template <typename T>
+int64_t count_diff(bh_engine *e, const T *a, const T *b, int64_t n, int64_t *first) {
+    std::vector<T> ha((size_t)n), hb((size_t)n);
+    *first = -1;
+    if (n <= 0) return 0;
+    if (hipMemcpy(ha.data(), a, sizeof(T) * n, hipMemcpyDeviceToHost) != hipSuccess ||
+        hipMemcpy(hb.data(), b, sizeof(T) * n, hipMemcpyDeviceToHost) != hipSuccess)
+        return -1;
+    int64_t d = 0;
+    for (int64_t i = 0; i < n; ++i)
+        if (std::memcmp(&ha[i], &hb[i], sizeof(T)) != 0) {
+            if (*first < 0) *first = i;
+            ++d;
+        }
+    (void)e;
+    return d;
+}
+
+int spec_compare(bh_engine *e, int64_t n_sub, const LetPieces &pc) {
+    HIPCHK(e, hipStreamSynchronize(e->stream));
+    HIPCHK(e, hipStreamSynchronize(e->spec_stream));
+    const LetAlt &a = e->la;
+    uint32_t cnt[2] = {0, 0};
+    HIPCHK(e, hipMemcpy(cnt, e->L.posc + LET_CELLS, 4, hipMemcpyDeviceToHost));
+    HIPCHK(e, hipMemcpy(cnt + 1, a.posc + LET_CELLS, 4, hipMemcpyDeviceToHost));
+    int64_t f[8];
+    const int64_t nn = std::min<int64_t>(cnt[0], cnt[1]);
+    const int64_t m = std::min<int64_t>(n_sub, e->spec_n_sub);
+    const int64_t dn = count_diff(e, e->L.nodes, a.nodes, nn, f + 0);
+    const int64_t dx = count_diff(e, e->sub_dst.x, a.sub_dst.x, m, f + 1);
+    const int64_t dy = count_diff(e, e->sub_dst.y, a.sub_dst.y, m, f + 2);
+    const int64_t dm = count_diff(e, e->sub_dst.m, a.sub_dst.m, m, f + 3);
+    const int64_t dc = count_diff(e, e->sub_dst.cidx, a.sub_dst.cidx, m, f + 4);
+    const int64_t dv = count_diff(e, e->sub_dst.vx, a.sub_dst.vx, m, f + 5);
+    const int64_t lo = (int64_t)pc.rank * pc.rounds * pc.sub;
+    const int64_t nl = std::max<int64_t>(0, std::min<int64_t>(pc.n, lo + (int64_t)pc.rounds * pc.sub) - lo);
+    const int64_t dl = count_diff(e, e->L.lanes + lo, a.lanes + lo, nl, f + 6);
+    const int64_t dt = count_diff(e, e->L.tables, a.tables, (int64_t)e->world * LET_TSTRIDE, f + 7);
+    std::fprintf(stderr,
+                 "SPEC_CHECK rank %d: n_sub %lld/%lld nodes %u/%u diff nodes %lld@%lld x %lld@%lld "
+                 "y %lld@%lld m %lld@%lld cidx %lld@%lld vx %lld@%lld lanes %lld@%lld tables "
+                 "%lld@%lld\n",
+                 e->rank, (long long)n_sub, (long long)e->spec_n_sub, cnt[0], cnt[1], (long long)dn,
+                 (long long)f[0], (long long)dx, (long long)f[1], (long long)dy, (long long)f[2],
+                 (long long)dm, (long long)f[3], (long long)dc, (long long)f[4], (long long)dv,
+                 (long long)f[5], (long long)dl, (long long)f[6], (long long)dt, (long long)f[7]);
+    return BH_OK;
+}
+
 int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     *done = false;
     if (kick != KICK_DRIFT && kick != KICK_ONLY) return BH_OK;
@@ -1043,10 +1110,13 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
             if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->gathered_ev, 0));
     }
     int64_t n_sub = 0;
-    bool spec_used = false;
+    bool spec_used = false, spec_check = false;
     if (e->spec_ready) {
         e->spec_ready = false;
-        if (kick == KICK_DRIFT && e->spec_n_sub > 0) {
+        if (kick == KICK_DRIFT && e->spec_n_sub > 0 && spec_check_on()) {
+            HIPCHK(e, hipStreamWaitEvent(e->stream, e->spec_ev, 0));
+            spec_check = true;  // select and build as usual, then compare the two trees
+        } else if (kick == KICK_DRIFT && e->spec_n_sub > 0) {
             // this tree was built beside the previous evaluation's rounds (spec_let_build)
             HIPCHK(e, hipStreamWaitEvent(e->stream, e->spec_ev, 0));
             swap_let_sets(e);
@@ -1066,10 +1136,20 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
                            e->let_age + 1 < BH_LET_REFRESH;
     if (!spec_used) {
         TRY(let_alloc(e, 0));
+        TRY(spec_events(e));
         // subset capacity: the largest subset of the previous call + headroom, no host round trip;
         // a subset beyond it is an overflow every rank sees after the exchange, and bh_step replays
         // the call with the observed size (the first LET build of an engine reads its size once)
-        // (the selection writes sub_src, sized for the whole state; padding up to S = n is harmless)
+        // (the selection writes sub_src, sized for the whole state; padding up to S = n is harmless).
+        // Within a call the size follows the previous selection's (a contracting cloud's subsets
+        // grow by more than the headroom over a 100-step call: round 4 saw one replay of the C4 / 8
+        // call).  The wait costs the GPU nothing: that selection ran before the previous
+        // evaluation's build and rounds, which are still queued behind it.
+        if (e->let_known > 0 && e->sub_cnt_pending) {
+            HIPCHK(e, hipEventSynchronize(e->sub_cnt_ev));
+            e->sub_cnt_pending = false;
+            e->let_known = std::max<int64_t>(e->let_known, e->spec_flag_h[4]);
+        }
         int64_t S = e->let_known > 0 ? std::min<int64_t>(n, e->let_known + e->let_known / 8 + 4096) : n;
         PosSrc ps{nullptr, GatherLayout{}, nullptr};
         if (e->pos_pending && lanes != e->pos_lanes) TRY(materialize_positions(e));  // map changed
@@ -1092,6 +1172,12 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
                             e->s_bcount};
         HIPCHK(e, let_select(e->st, ps, e->geo, pc, gap2, e->L, e->sub_src, S, e->scalars,
                              e->stream, mf));
+        if (e->let_known > 0) {
+            HIPCHK(e, hipMemcpyAsync(e->spec_flag_h + 4, e->L.selpos + let_sel_blocks(n),
+                                     sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
+            HIPCHK(e, hipEventRecord(e->sub_cnt_ev, e->stream));
+            e->sub_cnt_pending = true;
+        }
         if (e->let_known <= 0) {
             TRY(pinned_reserve(e, 64));
             uint32_t *h = static_cast<uint32_t *>(e->pin);
@@ -1109,7 +1195,6 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         HIPCHK(e, tree_build(sb, n_sub, e->geo, e->stream));
         e->s_spl_nb = sort_buckets(n_sub);  // k_prep wrote this build's splitters
         HIPCHK(e, let_table(n_sub, e->geo, e->L, sb, e->stream, spec_want));
-        if (spec_want) TRY(spec_events(e));
         TRY(exchange_tables(e, e->stream, false));
         {
             // bh_debug_inject: a node array of one record makes k_let_guard fire on this rank only,
@@ -1122,6 +1207,7 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
             e->L.node_cap = node_cap;
             HIPCHK(e, rc);
         }
+        if (spec_check) TRY(spec_compare(e, n_sub, pc));
         if (spec_want) {  // the crossing flag, read while the rounds below run
             HIPCHK(e, hipMemcpyAsync(e->spec_flag_h, e->scalars + 10, sizeof(uint32_t),
                                      hipMemcpyDeviceToHost, e->stream));
@@ -1986,7 +2072,7 @@ int engine_init(bh_engine *e, const bh_params *p, int device) {
     HIPCHK(e, hipSetDevice(device));
     HIPCHK(e, hipStreamCreateWithFlags(&e->stream, hipStreamNonBlocking));
     TRY(dev_alloc(e, e->scalars, 16));
-    HIPCHK(e, hipMemset(e->scalars, 0, 16 * sizeof(uint32_t)));
+    HIPCHK(e, hipMemsetAsync(e->scalars, 0, 16 * sizeof(uint32_t), e->stream));
     TRY(ensure_capacity(e, 1));
     return BH_OK;
 }
@@ -2298,7 +2384,7 @@ void bh_destroy(bh_engine *e) {
         if (a.table_ev) (void)hipEventDestroy(a.table_ev);
     }
     if (e->spec_stream) (void)hipStreamDestroy(e->spec_stream);
-    for (hipEvent_t ev : {e->spec_src_ev, e->spec_ev, e->spec_tab_ev, e->spec_flag_ev})
+    for (hipEvent_t ev : {e->spec_src_ev, e->spec_ev, e->spec_tab_ev, e->spec_flag_ev, e->sub_cnt_ev})
         if (ev) (void)hipEventDestroy(ev);
     if (e->spec_flag_h) (void)hipHostFree(e->spec_flag_h);
     if (e->table_ev) (void)hipEventDestroy(e->table_ev);
@@ -2440,6 +2526,9 @@ int bh_step(bh_engine *e, int32_t k) {
         e->mir_launched = false;
         e->spec_ready = false;
         for (int32_t s = 0; s < k; ++s) TRY(step_once(e, s + 1 == k));
+        // a copy-out launched by the last pipelined step reads the state the compaction (or a
+        // replay's restore) below rewrites
+        if (e->mir_launched) HIPCHK(e, hipStreamWaitEvent(e->stream, e->mir_ev2, 0));
         HIPCHK(e, hipStreamSynchronize(e->stream));
         if (may_let) {  // LET subset sizes of this call: [4] some rank overflowed, [5] largest
             uint32_t ls[2] = {0, 0};
