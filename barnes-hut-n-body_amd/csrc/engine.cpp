@@ -230,8 +230,8 @@ struct bh_engine {
     hipStream_t spec_stream = nullptr;
     hipEvent_t spec_src_ev = nullptr, spec_ev = nullptr, spec_tab_ev = nullptr,
                spec_flag_ev = nullptr, sub_cnt_ev = nullptr;
-    uint32_t *spec_flag_h = nullptr;  // pinned: [0] the crossing flag of the last LET build,
-                                      // [4] the last selection's subset size (sub_cnt_ev)
+    uint32_t *spec_flag_h = nullptr;  // pinned: the crossing flag of the last LET build
+    uint32_t *sub_cnt_h = nullptr;    // pinned: the last selection's subset size (sub_cnt_ev)
     bool sub_cnt_pending = false;
     LetCell *pub_table = nullptr;     // in-process group: the table this member exchanges now
     hipEvent_t pub_table_ev = nullptr;
@@ -940,13 +940,19 @@ int wave_order_next(bh_engine *e, int slot, int64_t lanes, hipStream_t s);
 #ifndef BH_LET_SPEC
 #define BH_LET_SPEC 1  // the LET pipeline: a step's first build beside the previous evaluation
 #endif
+#ifndef BH_SPEC_HIPRIO
+#define BH_SPEC_HIPRIO 1  // the speculative build's stream at the highest priority
+#endif
+#ifndef BH_SUB_TRACK
+#define BH_SUB_TRACK 1  // the subset capacity follows the previous selection within a call
+#endif
 int spec_events(bh_engine *e) {
     if (e->spec_stream) return BH_OK;
     int lo = 0, hi = 0;
     HIPCHK(e, hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIPCHK(e, hipStreamCreateWithPriority(&e->spec_stream, hipStreamNonBlocking, hi));
-    for (hipEvent_t *ev :
-         {&e->spec_src_ev, &e->spec_ev, &e->spec_tab_ev, &e->spec_flag_ev, &e->sub_cnt_ev})
+    HIPCHK(e, hipStreamCreateWithPriority(&e->spec_stream, hipStreamNonBlocking,
+                                          BH_SPEC_HIPRIO ? hi : lo));
+    for (hipEvent_t *ev : {&e->spec_src_ev, &e->spec_ev, &e->spec_tab_ev, &e->spec_flag_ev})
         HIPCHK(e, hipEventCreateWithFlags(ev, hipEventDisableTiming));
     HIPCHK(e, hipHostMalloc((void **)&e->spec_flag_h, 64, hipHostMallocDefault));
     return BH_OK;
@@ -1136,7 +1142,6 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
                            e->let_age + 1 < BH_LET_REFRESH;
     if (!spec_used) {
         TRY(let_alloc(e, 0));
-        TRY(spec_events(e));
         // subset capacity: the largest subset of the previous call + headroom, no host round trip;
         // a subset beyond it is an overflow every rank sees after the exchange, and bh_step replays
         // the call with the observed size (the first LET build of an engine reads its size once)
@@ -1145,10 +1150,10 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         // grow by more than the headroom over a 100-step call: round 4 saw one replay of the C4 / 8
         // call).  The wait costs the GPU nothing: that selection ran before the previous
         // evaluation's build and rounds, which are still queued behind it.
-        if (e->let_known > 0 && e->sub_cnt_pending) {
+        if (BH_SUB_TRACK && e->let_known > 0 && e->sub_cnt_pending) {
             HIPCHK(e, hipEventSynchronize(e->sub_cnt_ev));
             e->sub_cnt_pending = false;
-            e->let_known = std::max<int64_t>(e->let_known, e->spec_flag_h[4]);
+            e->let_known = std::max<int64_t>(e->let_known, *e->sub_cnt_h);
         }
         int64_t S = e->let_known > 0 ? std::min<int64_t>(n, e->let_known + e->let_known / 8 + 4096) : n;
         PosSrc ps{nullptr, GatherLayout{}, nullptr};
@@ -1172,8 +1177,12 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
                             e->s_bcount};
         HIPCHK(e, let_select(e->st, ps, e->geo, pc, gap2, e->L, e->sub_src, S, e->scalars,
                              e->stream, mf));
-        if (e->let_known > 0) {
-            HIPCHK(e, hipMemcpyAsync(e->spec_flag_h + 4, e->L.selpos + let_sel_blocks(n),
+        if (BH_SUB_TRACK && e->let_known > 0) {
+            if (!e->sub_cnt_h) {
+                HIPCHK(e, hipHostMalloc((void **)&e->sub_cnt_h, 64, hipHostMallocDefault));
+                HIPCHK(e, hipEventCreateWithFlags(&e->sub_cnt_ev, hipEventDisableTiming));
+            }
+            HIPCHK(e, hipMemcpyAsync(e->sub_cnt_h, e->L.selpos + let_sel_blocks(n),
                                      sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
             HIPCHK(e, hipEventRecord(e->sub_cnt_ev, e->stream));
             e->sub_cnt_pending = true;
@@ -1194,6 +1203,7 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         sb.keys_ready = fuse && e->s_spl_nb > 0;  // (let_alloc above kept the buffers: S fitted)
         HIPCHK(e, tree_build(sb, n_sub, e->geo, e->stream));
         e->s_spl_nb = sort_buckets(n_sub);  // k_prep wrote this build's splitters
+        if (spec_want) TRY(spec_events(e));
         HIPCHK(e, let_table(n_sub, e->geo, e->L, sb, e->stream, spec_want));
         TRY(exchange_tables(e, e->stream, false));
         {
@@ -2387,6 +2397,7 @@ void bh_destroy(bh_engine *e) {
     for (hipEvent_t ev : {e->spec_src_ev, e->spec_ev, e->spec_tab_ev, e->spec_flag_ev, e->sub_cnt_ev})
         if (ev) (void)hipEventDestroy(ev);
     if (e->spec_flag_h) (void)hipHostFree(e->spec_flag_h);
+    if (e->sub_cnt_h) (void)hipHostFree(e->sub_cnt_h);
     if (e->table_ev) (void)hipEventDestroy(e->table_ev);
     void *lets[] = {e->inv_lanes, e->L.csrc, e->L.ccnt, e->L.cpos, e->solo_table, e->solo_all, e->solo_cstart, e->L.ecell, e->L.hcell, e->L.own, e->L.subpos, e->L.flag_all, e->L.flag8, e->L.sel, e->L.selpos, e->L.cstart,
                     e->L.table, e->L.tables, e->L.levels, e->L.w, e->L.posc, e->L.bsz,

@@ -1085,24 +1085,6 @@ constexpr uint32_t SPAN_REF = 1u << 31;  // child list entry: owner slot of a sp
 constexpr uint32_t SPAN_SUPER = 1u << 31;
 constexpr int SPAN_GROUP = 1024;
 
-// Experiment (BH_SPAN_XCD): the span passes' producers and their consumer on one XCD, so that the
-// level-by-level pass (k_com_span) reads span_list / span_children from its own L2.  Every
-// logical block is launched 8 times; the copy that runs on the group's XCD (g % 8, read from
-// HW_REG_XCC_ID) does the work.  (Relies on 8 consecutive blocks landing on 8 XCDs.)
-#ifndef BH_SPAN_XCD
-#define BH_SPAN_XCD 0
-#endif
-__device__ __forceinline__ uint32_t xcc_id() {
-    return __builtin_amdgcn_s_getreg((31 << 11) | 20) & 7u;
-}
-// logical block of this physical block, or -1 when another copy does it
-__device__ __forceinline__ int span_block(uint32_t per_group_blocks) {
-    if (!BH_SPAN_XCD) return (int)blockIdx.x;
-    const uint32_t lb = blockIdx.x >> 3;
-    const uint32_t g = lb / per_group_blocks;
-    return xcc_id() == (g & 7u) ? (int)lb : -1;
-}
-
 __global__ __launch_bounds__(TB) void k_span_find(int64_t n, int J, int D0,
                                                   const uint64_t *__restrict__ keys_s,
                                                   const int8_t *__restrict__ cpl,
@@ -1113,9 +1095,7 @@ __global__ __launch_bounds__(TB) void k_span_find(int64_t n, int J, int D0,
                                                   uint32_t *__restrict__ super_list,
                                                   uint32_t n_groups, Node *nodes) {
     chain_prio();
-    const int lb = span_block(SPAN_GROUP / TB);
-    if (lb < 0) return;
-    const int64_t k = (int64_t)lb * TB + threadIdx.x;
+    const int64_t k = (int64_t)blockIdx.x * TB + threadIdx.x;
     const int L = blockIdx.y;
     if (k >= (int64_t)span_stride) return;
     const int64_t chunk0 = k << COM_CHUNK_SHIFT;
@@ -1164,10 +1144,7 @@ __global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__r
                                                       SpanSlot *__restrict__ span_children) {
     chain_prio();
     const uint32_t L = blockIdx.y;
-    const int lb = span_block(SPAN_GROUP / TB);
-    if (lb < 0) return;
-    const uint32_t nlb = BH_SPAN_XCD ? gridDim.x >> 3 : gridDim.x;
-    for (uint32_t i = (uint32_t)lb * TB + threadIdx.x; i < span_stride; i += nlb * TB) {
+    for (uint32_t i = blockIdx.x * TB + threadIdx.x; i < span_stride; i += gridDim.x * TB) {
         const size_t slot = (size_t)L * span_stride + i;
         const uint32_t e = span_list[slot];
         if (e == NO_SPAN) continue;  // empty slot: never read
@@ -1194,7 +1171,7 @@ __global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__r
             }
             c = max(cn.next, c + 1);
         }
-        span_children[slot] = out;
+        span_put(span_children, (size_t)(J + 1) * span_stride, slot, out);
     }
 }
 
@@ -1207,6 +1184,12 @@ __global__ __launch_bounds__(TB) void k_span_children(int J, const uint32_t *__r
 // stores to global stay in flight across the LDS-only barriers.
 constexpr int SPAN_TB = SPAN_GROUP;
 
+#ifdef BH_SPAN_TIMING  // diagnostic build: per-level wall-clock stamps of k_com_span's group 0
+constexpr int SPAN_T_REC = 64, SPAN_T_W = 32;  // launches kept (ring), stamps per launch
+__device__ uint64_t g_span_times[SPAN_T_REC * SPAN_T_W];
+__device__ uint32_t g_span_launch;
+#endif
+
 struct SpanRegs {
     uint32_t ni;
     uint32_t ch[4];
@@ -1214,9 +1197,9 @@ struct SpanRegs {
 };
 
 __device__ __forceinline__ void load_span(SpanRegs &r, const uint32_t *span_list,
-                                          const SpanSlot *span_children, size_t slot) {
+                                          const SpanSlot *span_children, size_t P, size_t slot) {
     r.ni = span_list[slot];
-    const SpanSlot q = span_children[slot];
+    const SpanSlot q = span_get(span_children, P, slot);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
         r.ch[k] = q.ch[k];
@@ -1232,11 +1215,22 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span(int J, const uint32_t *__r
                                                       Node *nodes) {
     chain_prio();
     __shared__ double r_m[2][SPAN_GROUP], r_x[2][SPAN_GROUP], r_y[2][SPAN_GROUP];
-    const int gb = span_block(1);
-    if (gb < 0) return;
-    const uint32_t g0 = (uint32_t)gb * SPAN_GROUP;
+    const uint32_t g0 = blockIdx.x * SPAN_GROUP;
     const uint32_t kl = threadIdx.x, k = g0 + kl;
     const bool valid = k < span_stride;
+#ifdef BH_SPAN_TIMING
+    __shared__ uint64_t t_st[SPAN_T_W];
+    int t_n = 0;  // (uniform)
+    if (threadIdx.x == 0) t_st[0] = wall_clock64();
+    t_n = 1;
+#define SPAN_STAMP()                                                          \
+    do {                                                                      \
+        if (t_n < SPAN_T_W && threadIdx.x == 0) t_st[t_n] = wall_clock64();   \
+        ++t_n;                                                                \
+    } while (0)
+#else
+#define SPAN_STAMP() (void)0
+#endif
     // levels (bit L) at which this boundary owns a node finished here (not group-crossing)
     uint64_t own = 0;
     if (valid) {
@@ -1246,10 +1240,26 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span(int J, const uint32_t *__r
             if (e != NO_SPAN && !(e & SPAN_SUPER)) own |= 1ull << L;
         }
     }
+#ifdef BH_SPAN_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    SPAN_STAMP();
+#endif
     auto fetch = [&](SpanRegs &r, int L) __attribute__((always_inline)) {
         r.ni = NO_SPAN;
+#ifdef BH_SPAN_NOLOAD  // (timing experiment only: results wrong)
+        if (L >= 0 && ((own >> L) & 1ull)) {
+            r.ni = 0u;
+            for (int c = 0; c < 4; ++c) {
+                r.ch[c] = 0xFFFFFFFFu;
+                r.v[c][0] = r.v[c][1] = r.v[c][2] = 1.0;
+            }
+        }
+#else
         if (L >= 0 && ((own >> L) & 1ull))
-            load_span(r, span_list, span_children, (size_t)L * span_stride + k);
+            load_span(r, span_list, span_children, (size_t)(J + 1) * span_stride,
+                      (size_t)L * span_stride + k);
+#endif
     };
     auto level = [&](const SpanRegs &C, int L) __attribute__((always_inline)) {
         const int cur = L & 1, prev = cur ^ 1;
@@ -1280,30 +1290,44 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span(int J, const uint32_t *__r
             r_x[cur][kl] = ox;
             r_y[cur][kl] = oy;
             Node *dst = nodes + C.ni;
-#ifndef BH_SPAN_NOSTORE  // (timing experiment only: results wrong)
             dst->mass = mSum;
             dst->comX = ox;  // massless: never visited (the cell centre is not recorded)
             dst->comY = oy;
             if (!(mSum > 0.0)) dst->meta |= NODE_SKIP | NODE_LEAF;  // a skip-leaf
-#else
-            (void)dst;
-#endif
         }
         __builtin_amdgcn_s_waitcnt(0xC07F);  // lgkmcnt(0): LDS results visible; stores fly on
         __builtin_amdgcn_s_barrier();
+        SPAN_STAMP();
     };
     // a span child always sits one level below its parent and is owned by a boundary of the
     // same group, so the level pass needs no other synchronisation
-    SpanRegs P, Q;
-    fetch(P, J);
-    fetch(Q, J - 1);
-    for (int L = J; L >= 0; L -= 2) {
-        level(P, L);
-        fetch(P, L - 2);
-        if (L == 0) break;
-        level(Q, L - 1);
-        fetch(Q, L - 3);
+#ifndef BH_SPAN_AHEAD
+#define BH_SPAN_AHEAD 2  // levels whose records are in flight
+#endif
+    SpanRegs R[BH_SPAN_AHEAD];
+#pragma unroll
+    for (int j = 0; j < BH_SPAN_AHEAD; ++j) fetch(R[j], J - j);
+    for (int L = J; L >= 0; L -= BH_SPAN_AHEAD) {
+#pragma unroll
+        for (int j = 0; j < BH_SPAN_AHEAD; ++j) {
+            if (L - j >= 0) {
+                level(R[j], L - j);
+                fetch(R[j], L - j - BH_SPAN_AHEAD);
+            }
+        }
     }
+#ifdef BH_SPAN_TIMING
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    SPAN_STAMP();
+    if (blockIdx.x == 0 && threadIdx.x == 0) {
+        const uint32_t rec = atomicAdd(&g_span_launch, 1u) % SPAN_T_REC;
+        uint64_t *o = g_span_times + (size_t)rec * SPAN_T_W;
+        for (int q = 0; q < SPAN_T_W; ++q) o[q] = q < t_n ? t_st[q] : 0ull;
+        o[SPAN_T_W - 1] = (uint64_t)t_n;
+    }
+#endif
+#undef SPAN_STAMP
 }
 
 // The nodes that cross a group boundary (few: at most one per group boundary and level),
@@ -1323,7 +1347,7 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span_top(int J,
             if (ko == NO_SPAN) continue;
             const size_t slot = (size_t)L * span_stride + ko;
             const uint32_t ni = span_list[slot] & ~SPAN_SUPER;
-            const SpanSlot q = span_children[slot];
+            const SpanSlot q = span_get(span_children, (size_t)(J + 1) * span_stride, slot);
             double mSum = 0.0, cx = 0.0, cy = 0.0;
             for (int c = 0; c < 4; ++c) {
                 if (q.ch[c] != 0xFFFFFFFFu && (q.ch[c] & SPAN_REF)) {
@@ -1544,19 +1568,28 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     k_emit_com<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), EC_TB, 0, s>>>(
         n, g, D0, b.keys_s, b.cpl, b.base, b.cell_start, b.dst.x, b.dst.y, b.dst.m, b.dst.cidx,
         b.idx, b.nodes, b.scalars + 1, b.keys32, b.lanes_remap);
-    const dim3 span_grid(((b.span_stride + TB - 1) / TB) * (BH_SPAN_XCD ? 8 : 1), g.J + 1);
+    const dim3 span_grid((b.span_stride + TB - 1) / TB, g.J + 1);
     k_span_find<<<span_grid, TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cpl, b.base, b.cell_start,
                                          b.span_list, b.span_stride, b.super_list, n_groups,
                                          b.nodes);
     k_span_children<<<span_grid, TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.nodes,
                                              b.span_children);
-    k_com_span<<<n_groups * (BH_SPAN_XCD ? 8 : 1), SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
+    k_com_span<<<n_groups, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
                                             b.nodes);
     if (n_groups > 1)
         k_com_span_top<<<1, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
                                              b.super_list, n_groups, b.nodes);
     return hipGetLastError();
 }
+
+#ifdef BH_SPAN_TIMING
+extern "C" int bh_debug_span_times(uint64_t *out, uint32_t *launches) {
+    hipError_t e = hipMemcpyFromSymbol(out, HIP_SYMBOL(g_span_times),
+                                       sizeof(uint64_t) * SPAN_T_REC * SPAN_T_W);
+    if (e == hipSuccess) e = hipMemcpyFromSymbol(launches, HIP_SYMBOL(g_span_launch), 4);
+    return (int)e;
+}
+#endif
 
 #ifdef BH_EC_TIMING
 extern "C" int bh_debug_ec_times(uint64_t *out, int n) {

@@ -16,8 +16,9 @@
 #                  summarised by tools/timeline.py)                             -> ${TAG}_dropin_*
 #   solo           one rank's share of the 8-GPU C4 step, alone (tools/solo_rank.py, ranks 0, 5)
 #   soloab         the solo step of rank 0 (C4 / 8) alternately with lib/libA.so and the default
-#                  build, 2 rounds                                             -> ${TAG}_soloab.jsonl
+#                  build (SOLO_LIBS="A default" to change), 2 rounds          -> ${TAG}_soloab.jsonl
 #   ab             A/B of in-tree library builds (tools/ab.sh; LIBS="A B", AB_ARGS=...)
+#   kstats         C3 bench under rocprofv3 --kernel-trace --stats per library (KSTATS_LIBS)
 # Every GPU step runs under its own time limit; a failing step (any rc but 0) ends the session, so
 # nothing else touches the GPU after a fault, an abort or a timeout.
 # (Round 3's one-off session scripts are kept in tools/archive/: committed profiles cite them.)
@@ -66,11 +67,11 @@ for step in "$@"; do
         run 600 ${O}_solo$r.log python -u tools/solo_rank.py --config c4 --world 8 --rank $r
         grep '^{' ${O}_solo$r.log | tail -1 >> ${O}_solo.jsonl
       done ;;
-    soloab)
+    soloab)  # SOLO_LIBS="A B ..." (lib/lib<X>.so; "default" = the in-tree build)
       for rr in 1 2; do
-        for L in A default; do
+        for L in ${SOLO_LIBS:-A default}; do
           lib=$PWD/barnes-hut-n-body_amd/lib/libbh_engine.so
-          [ $L = A ] && lib=$PWD/barnes-hut-n-body_amd/lib/libA.so
+          [ $L = default ] || lib=$PWD/barnes-hut-n-body_amd/lib/lib$L.so
           export BH_ENGINE_LIB=$lib
           run 600 ${O}_soloab_$L$rr.log python -u tools/solo_rank.py --config c4 --world 8 --rank 0
           unset BH_ENGINE_LIB
@@ -78,21 +79,16 @@ for step in "$@"; do
         done
       done ;;
     ab) run 1800 ${O}_ab.log bash tools/ab.sh ;;
-    span)  # kernel-trace stats of C3 with the default build and the lib/libX.so / libN.so variants
+    kstats)  # kernel-trace stats of C3 per library (KSTATS_LIBS="default X ..."; lib/lib<X>.so)
       export TMPDIR=/tmp
-      for L in default X N; do
+      for L in ${KSTATS_LIBS:-default}; do
         lib=$PWD/barnes-hut-n-body_amd/lib/libbh_engine.so
         [ $L = default ] || lib=$PWD/barnes-hut-n-body_amd/lib/lib$L.so
-        extra=""
-        [ $L = N ] && extra=--no-verify
         export BH_ENGINE_LIB=$lib
-        run 600 ${O}_span_$L.log rocprofv3 --kernel-trace --stats -d ${O}_span_$L -o run \
+        run 600 ${O}_kstats_$L.log rocprofv3 --kernel-trace --stats -d ${O}_kstats_$L -o run \
           --output-format csv -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline \
-          --no-counters --no-drop-in $extra
+          --no-counters --no-drop-in
         unset BH_ENGINE_LIB
-        st=$(find ${O}_span_$L -name '*kernel_stats.csv' | head -1)
-        grep -E 'k_com_span|k_span_|k_emit|k_build' "$st" | cut -d, -f1-5 > ${O}_span_$L.txt || true
-        cat ${O}_span_$L.txt
       done ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
