@@ -111,29 +111,13 @@ struct __attribute__((aligned(16))) SpanSlot {
     uint32_t ch[4];
     double v[4][3];
 };
-// Stored as planes of P = (J + 1) * span_stride entries (the child references as one uint4
-// plane, then one plane per value) inside the (J + 2) * span_stride records allocated: a wave's
-// load of one field is contiguous (the one-workgroup level pass reads every record through one
-// CU; 112-byte records cost ~4 us per level in address processing, round 4).
-__device__ __forceinline__ void span_put(SpanSlot *base, size_t P, size_t slot, const SpanSlot &s) {
-    uint4 *ch = reinterpret_cast<uint4 *>(base);
-    ch[slot] = make_uint4(s.ch[0], s.ch[1], s.ch[2], s.ch[3]);
-    double *v = reinterpret_cast<double *>(ch + P);
-#pragma unroll
-    for (int q = 0; q < 12; ++q) v[(size_t)q * P + slot] = s.v[q / 3][q % 3];
+// (accessors: the records were also tried as field planes -- coalesced per field -- with no
+// gain: the level pass is bound by the line requests one CU can keep in flight, round 4)
+__device__ __forceinline__ void span_put(SpanSlot *base, size_t, size_t slot, const SpanSlot &s) {
+    base[slot] = s;
 }
-__device__ __forceinline__ SpanSlot span_get(const SpanSlot *base, size_t P, size_t slot) {
-    const uint4 *ch = reinterpret_cast<const uint4 *>(base);
-    const uint4 c = ch[slot];
-    SpanSlot s;
-    s.ch[0] = c.x;
-    s.ch[1] = c.y;
-    s.ch[2] = c.z;
-    s.ch[3] = c.w;
-    const double *v = reinterpret_cast<const double *>(ch + P);
-#pragma unroll
-    for (int q = 0; q < 12; ++q) s.v[q / 3][q % 3] = v[(size_t)q * P + slot];
-    return s;
+__device__ __forceinline__ SpanSlot span_get(const SpanSlot *base, size_t, size_t slot) {
+    return base[slot];
 }
 
 // Wave priority of the kernels that the pipelined one-GPU step runs next to the second traversal
@@ -338,6 +322,10 @@ struct KickArgs {
     double dtHalf, dt;
     const uint32_t *rep = nullptr;  // KICK_OWN_*: lane -> replicated slot (null: the lane)
     MortonFuse mf{};
+    // KICK_ONLY after a build that left the velocities in the previous slot order: v[p] =
+    // sv[perm[p]] + a dt/2 (the build's permutation of v, fused; null: in place)
+    const double *svx = nullptr, *svy = nullptr;
+    const uint32_t *perm = nullptr;
 };
 // Diagnostic counters of the counting walk (all per evaluation): per body, the non-empty
 // nodes visited (BHA:216 passed) and the point-force contributions (accepted internal nodes

@@ -123,6 +123,7 @@ struct bh_engine {
     uint64_t *keys = nullptr, *keys_s = nullptr;
     uint32_t *keys32 = nullptr, *keys32_s = nullptr;
     uint32_t *idx = nullptr, *perm = nullptr;
+    uint32_t *perm2 = nullptr;  // the pipelined step's overlapped build's permutation
     int8_t *cpl = nullptr;
     uint32_t *cnt = nullptr, *base = nullptr;
     uint32_t *cell_start = nullptr;
@@ -233,6 +234,7 @@ struct bh_engine {
     uint32_t *spec_flag_h = nullptr;  // pinned: the crossing flag of the last LET build
     uint32_t *sub_cnt_h = nullptr;    // pinned: the last selection's subset size (sub_cnt_ev)
     bool sub_cnt_pending = false;
+    bool let_spec = false;             // BH_LET_SPEC=1: the LET pipeline (evaluate_let)
     LetCell *pub_table = nullptr;     // in-process group: the table this member exchanges now
     hipEvent_t pub_table_ev = nullptr;
     int64_t spec_builds = 0, spec_fallbacks = 0;
@@ -430,6 +432,7 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(dev_alloc(e, e->keys32_s, cap));
         TRY(dev_alloc(e, e->idx, cap));
         TRY(dev_alloc(e, e->perm, cap));
+        TRY(dev_alloc(e, e->perm2, cap));
         TRY(dev_alloc(e, e->cpl, cap + 32));  // slack for word-wise scans
         TRY(dev_alloc(e, e->cnt, cap + 1));
         TRY(dev_alloc(e, e->base, cap + 1));
@@ -574,13 +577,19 @@ int collect_timings(bh_engine *e) {
 #endif
 // overlap: the pipelined step's build on stream `s` -- into nodes_alt and alt without the
 // velocities (permute_velocities follows) and without the final swap (the caller swaps)
-int build_into(bh_engine *e, hipStream_t s, bool overlap) {
+// overlap: the pipelined step's next tree, built beside the second traversal into nodes_alt /
+// alt with its own permutation (perm2; the traversal reads perm), velocities left to
+// permute_velocities.  keep_v: the velocities stay in the previous slot order (in alt after the
+// swap) for a traversal that permutes them as it kicks (KickArgs::perm).
+int build_into(bh_engine *e, hipStream_t s, bool overlap, bool keep_v = false) {
     const int64_t n = e->n;
     TreeBuffers tb = tree_buffers(e);
     if (overlap) {
         tb.src.vx = tb.src.vy = nullptr;
         tb.nodes = e->nodes_alt;
+        tb.perm = e->perm2;
     }
+    if (keep_v) tb.src.vx = tb.src.vy = nullptr;
     // Hilbert waves (every rank alike): re-sorted every BH_LANE_REFRESH builds, carried through
     // the build's permutation by k_emit_com in between
     const bool use_lanes = BH_LANE_REFRESH > 0 && n > 0 && e->p.theta != 0.0;
@@ -937,14 +946,12 @@ int sync_velocities(bh_engine *e) {
 int wave_order_for(bh_engine *e, int slot, int64_t lanes, hipStream_t s, WaveOrder &wo);
 int wave_order_next(bh_engine *e, int slot, int64_t lanes, hipStream_t s);
 
-#ifndef BH_LET_SPEC
-#define BH_LET_SPEC 1  // the LET pipeline: a step's first build beside the previous evaluation
-#endif
+// The LET pipeline (a step's first build beside the previous evaluation's rounds) is switched on
+// by BH_LET_SPEC=1 (e->let_spec): on one rank's share alone it measured no faster than building
+// in line (round 4: 3.46-3.51 against 3.41-3.43 ms per solo C4 / 8 step), the speculative build
+// taking wave slots from the rounds; an 8-GPU run, whose rounds wait on xGMI, may differ.
 #ifndef BH_SPEC_HIPRIO
 #define BH_SPEC_HIPRIO 1  // the speculative build's stream at the highest priority
-#endif
-#ifndef BH_SUB_TRACK
-#define BH_SUB_TRACK 1  // the subset capacity follows the previous selection within a call
 #endif
 int spec_events(bh_engine *e) {
     if (e->spec_stream) return BH_OK;
@@ -1137,7 +1144,7 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     // step that is not the call's last, no merge rule that can act (BHA:438), the next build a
     // LET build too.  Whether the jitter moved a body across a depth-8 cell is known after the
     // table exchange (every rank alike).
-    const bool spec_want = BH_LET_SPEC && !spec_used && kick == KICK_ONLY && e->spec_allowed &&
+    const bool spec_want = e->let_spec && !spec_used && kick == KICK_ONLY && e->spec_allowed &&
                            (e->p.merge_min_dist <= 0.0 || !e->heavy_possible) &&
                            e->let_age + 1 < BH_LET_REFRESH;
     if (!spec_used) {
@@ -1146,12 +1153,12 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         // a subset beyond it is an overflow every rank sees after the exchange, and bh_step replays
         // the call with the observed size (the first LET build of an engine reads its size once)
         // (the selection writes sub_src, sized for the whole state; padding up to S = n is harmless).
-        // Within a call the size follows the previous selection's (a contracting cloud's subsets
-        // grow by more than the headroom over a 100-step call: round 4 saw one replay of the C4 / 8
-        // call).  The wait costs the GPU nothing: that selection ran before the previous
-        // evaluation's build and rounds, which are still queued behind it.
-        if (BH_SUB_TRACK && e->let_known > 0 && e->sub_cnt_pending) {
-            HIPCHK(e, hipEventSynchronize(e->sub_cnt_ev));
+        // Within a call the size follows the previous selection's when its read-back has landed
+        // (a contracting cloud's subsets grow by more than the headroom over a 100-step call:
+        // round 4 saw one replay of the C4 / 8 call).  Never waited for: a blocking wait here cost
+        // 0.2 ms per solo C4 / 8 step (3.67 against 3.43-3.53 ms).
+        if (e->let_spec) TRY(spec_events(e));  // (its stream made before the round streams)
+        if (e->let_known > 0 && e->sub_cnt_pending && hipEventQuery(e->sub_cnt_ev) == hipSuccess) {
             e->sub_cnt_pending = false;
             e->let_known = std::max<int64_t>(e->let_known, *e->sub_cnt_h);
         }
@@ -1177,7 +1184,7 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
                             e->s_bcount};
         HIPCHK(e, let_select(e->st, ps, e->geo, pc, gap2, e->L, e->sub_src, S, e->scalars,
                              e->stream, mf));
-        if (BH_SUB_TRACK && e->let_known > 0) {
+        if (e->let_known > 0) {
             if (!e->sub_cnt_h) {
                 HIPCHK(e, hipHostMalloc((void **)&e->sub_cnt_h, 64, hipHostMallocDefault));
                 HIPCHK(e, hipEventCreateWithFlags(&e->sub_cnt_ev, hipEventDisableTiming));
@@ -1851,7 +1858,7 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     const bool merging = e->p.merge_min_dist > 0.0 && e->n > 1 && e->heavy_possible;
     if (merging) TRY(merge_bufs(e));
     TRY(mark(e, -1));
-    TRY(build(e));
+    TRY(build_into(e, s, false, true));  // velocities: permuted by the traversal's kick below
     TRY(mark(e, 0));
     const bool lanes = e->lanes_valid;
     copy_trav_inputs(n, e->st.m, e->m_trav, e->st.cidx, e->cidx_trav, lanes ? e->lanes : nullptr,
@@ -1860,7 +1867,12 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     HIPCHK(e, hipEventRecord(e->pipe_ev[0], s));
     HIPCHK(e, hipStreamWaitEvent(e->pipe_stream, e->pipe_ev[0], 0));
     const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};  // BHA:378
-    const KickArgs ka{KICK_ONLY, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
+    KickArgs ka{KICK_ONLY, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
+    if (n > 0) {  // (the build swapped: the previous order's velocities are in alt)
+        ka.svx = e->alt.vx;
+        ka.svy = e->alt.vy;
+        ka.perm = e->perm;
+    }
     WaveOrder wo;
     TRY(wave_order_for(e, 0, n, s, wo));
     traverse(e->nodes, e->node_cap, e->T_trav, e->st.x, e->st.y, e->m_trav, e->cidx_trav, 0, n,
@@ -1896,7 +1908,7 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     HIPCHK(e, hipEventRecord(e->pipe_ev[1], e->pipe_stream));
     HIPCHK(e, hipStreamWaitEvent(s, e->pipe_ev[1], 0));
     if (BH_DEEP_PIPE) TRY(mark(e, 1, 2));  // this traversal, the overlapped chain, the next a(t)
-    permute_velocities(n, e->perm, e->st.vx, e->st.vy, e->alt.vx, e->alt.vy, s);
+    permute_velocities(n, e->perm2, e->st.vx, e->st.vy, e->alt.vx, e->alt.vy, s);
     HIPCHK(e, hipGetLastError());
     TRY(mark(e, 0));  // the wait for the overlapped build and the velocity permutation
     std::swap(e->st, e->alt);
@@ -2075,6 +2087,7 @@ int engine_init(bh_engine *e, const bh_params *p, int device) {
     e->p = *p;
     TRY(make_geometry(e->p, e->geo, e->err));
     e->device = device;
+    if (const char *v = std::getenv("BH_LET_SPEC")) e->let_spec = std::strcmp(v, "0") != 0;
     if (const char *v = std::getenv("BH_LET")) {
         e->let_on = std::strcmp(v, "0") != 0;
         e->let_forced = std::strcmp(v, "1") == 0;
@@ -2407,7 +2420,7 @@ void bh_destroy(bh_engine *e) {
                     e->s_span_children, e->s_nodes};
     for (void *q : lets)
         if (q) (void)hipFree(q);
-    void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->keys32, e->keys32_s, e->idx, e->perm, e->cpl, e->cnt,
+    void *ptrs[] = {e->a2, e->ax, e->ay, e->keys, e->keys_s, e->keys32, e->keys32_s, e->idx, e->perm, e->perm2, e->cpl, e->cnt,
                     e->base, e->cell_start, e->nodes, e->span_list, e->super_list,
                     e->span_children, e->scalars, e->visits32, e->contrib32, e->lanes, e->wave_iters, e->wave_blocks, e->heavy, e->keep,
                     e->pos, e->box, e->dlog, e->dead_sorted, e->rkeys, e->ridx, e->mbits, e->mslot, e->scratch,

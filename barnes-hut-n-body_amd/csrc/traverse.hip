@@ -248,8 +248,17 @@ __device__ __forceinline__ void trav_wave(uint32_t v, uint64_t t_start,
         }
         *reinterpret_cast<double2_t *>(a2 + 2 * q) = o;
     } else {  // k_kick_drift / k_kick (integrate.hip), operation for operation
-        const double vxi = kick.vx[p] + acc.x * kick.dtHalf;
-        const double vyi = kick.vy[p] + acc.y * kick.dtHalf;
+        double v0x, v0y;
+        if (KICK == KICK_ONLY && kick.perm) {
+            const uint32_t sp = kick.perm[p];
+            v0x = kick.svx[sp];
+            v0y = kick.svy[sp];
+        } else {
+            v0x = kick.vx[p];
+            v0y = kick.vy[p];
+        }
+        const double vxi = v0x + acc.x * kick.dtHalf;
+        const double vyi = v0y + acc.y * kick.dtHalf;
         kick.vx[p] = vxi;
         kick.vy[p] = vyi;
         if (KICK == KICK_DRIFT) {

@@ -1208,8 +1208,9 @@ def test_let_speculative_build_matches_single(world, edge_pairs, monkeypatch):
     equals the single-GPU engine's bit for bit.  With coincident pairs straddling depth-8 grid
     lines (x = 1200 and y = 400 are depth-8 cell edges at the 2400x800 root) the jitter moves bodies into the
     neighbouring cell: those evaluations call the speculation off (and select anew) and the
-    states still match."""
+    states still match.  (BH_LET_SPEC=1 switches the pipeline on.)"""
     monkeypatch.setenv("BH_LET", "1")
+    monkeypatch.setenv("BH_LET_SPEC", "1")
     x, y, vx, vy, m = (a.copy() for a in scenes.uniform(150_000, 0.5, seed=29))
     if edge_pairs:
         ex = np.repeat(np.concatenate([1200.0 + np.array([-6e-4, -4e-4, -2e-4, 2e-4, 4e-4, 6e-4]),
