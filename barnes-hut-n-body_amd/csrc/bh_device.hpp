@@ -518,6 +518,13 @@ hipError_t mirror_index(int64_t n, const uint32_t *cidx, uint32_t *keep, uint32_
                         size_t tmp_bytes, hipStream_t s);
 void mirror_scatter(int64_t n, const uint32_t *cidx, const uint32_t *pos, int k,
                     const double *const *src, double *const *dst, hipStream_t s);
+// *dst = *src by one thread at the chain's wave priority (a 4-byte hipMemcpyAsync beside the
+// traversal is a blit kernel that waits ~0.5 ms for a wave slot, with the merge rule behind it)
+void copy_u32(uint32_t *dst, const uint32_t *src, hipStream_t s);
+// The end-of-call read-back of the merge bookkeeping in one copy: out[0..3] = scal[0..3],
+// out[4..11] = the mailbox header, out[12] = scal[8], out[16 + i] = dlog[i] for i < ahead
+void pack_readback(const uint32_t *scal, const MergePair *box, const uint32_t *dlog, uint32_t ahead,
+                   uint32_t *out, hipStream_t s);
 // dst[perm[a]] = src[a] for x and y: positions of a sorted build (jitter included) back into the
 // state's own slot order (multi-rank getTreeForDebug, engine.cpp bh_get_quads)
 void unpermute_positions(int64_t n, const uint32_t *perm, const double *sx, const double *sy,

@@ -157,7 +157,8 @@ struct bh_engine {
     bool heavy_possible = true;  // false once a step saw no heavy body (heavies never appear)
     bool merge_ran = false;      // the running bh_step call launched the merge rule
     std::vector<int64_t> removed;  // removals of the last bh_step call, ascending (BHA:519)
-    void *pin = nullptr;  // pinned staging for small read-backs
+    void *pin = nullptr;  // pinned staging for small read-backs (coherent: kernels write it too)
+    void *pin_dev = nullptr;
     size_t pin_bytes = 0;
 
     void *scratch = nullptr;
@@ -234,6 +235,7 @@ struct bh_engine {
     uint32_t *spec_flag_h = nullptr;  // pinned: the crossing flag of the last LET build
     uint32_t *sub_cnt_h = nullptr;    // pinned: the last selection's subset size (sub_cnt_ev)
     bool sub_cnt_pending = false;
+
     bool let_spec = false;             // BH_LET_SPEC=1: the LET pipeline (evaluate_let)
     LetCell *pub_table = nullptr;     // in-process group: the table this member exchanges now
     hipEvent_t pub_table_ev = nullptr;
@@ -290,6 +292,7 @@ struct bh_engine {
     hipEvent_t mir_ev = nullptr;   // copy-out complete
     hipEvent_t mir_ev2 = nullptr;  // the mirror's kernels are done reading the state
     hipEvent_t mir_in[2] = {nullptr, nullptr};
+    hipEvent_t mir_ev3 = nullptr;
     // one GPU: the previous evaluation's wave durations and the longest-first run order
     // (slot 0: the one-GPU launch over all lanes; 1 + k: LET round k's piece)
     uint32_t *wave_cost = nullptr, *run_order = nullptr;
@@ -1460,7 +1463,9 @@ int pinned_reserve(bh_engine *e, size_t bytes) {
     if (e->pin) (void)hipHostFree(e->pin);
     e->pin = nullptr;
     size_t nb = std::max<size_t>(bytes, 1 << 16);
-    HIPCHK(e, hipHostMalloc(&e->pin, nb, hipHostMallocDefault));
+    // coherent: kernels write their small results here directly (finish_merges' read-back)
+    HIPCHK(e, hipHostMalloc(&e->pin, nb, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(e, hipHostGetDevicePointer(&e->pin_dev, e->pin, 0));
     e->pin_bytes = nb;
     return BH_OK;
 }
@@ -1525,13 +1530,12 @@ int finish_merges(bh_engine *e, uint32_t *overflow, uint32_t *tree_flags = nullp
     TRY(pinned_reserve(e, 64 + 2 * sizeof(uint32_t) * DLOG_AHEAD));
     uint32_t *h = static_cast<uint32_t *>(e->pin);
     uint32_t *hlog = h + 16, *hsorted = h + 16 + DLOG_AHEAD;
-    HIPCHK(e, hipMemcpyAsync(h, e->scalars, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(e, hipMemcpyAsync(h + 4, e->box, sizeof(MergeHeader), hipMemcpyDeviceToHost, e->stream));
-    HIPCHK(e, hipMemcpyAsync(h + 12, e->scalars + 8, sizeof(uint32_t), hipMemcpyDeviceToHost,
-                             e->stream));
+    // (one kernel writes it all into the pinned buffer: no copies -- four were four blit kernels,
+    // and a DMA copy queued behind the mirror's 40 MB on the same engine, round 4 trace)
     const uint32_t ahead = (uint32_t)std::min<int64_t>(DLOG_AHEAD, e->dlog_cap);
-    HIPCHK(e, hipMemcpyAsync(hlog, e->dlog, sizeof(uint32_t) * ahead, hipMemcpyDeviceToHost,
-                             e->stream));
+    pack_readback(e->scalars, e->box, e->dlog, ahead, static_cast<uint32_t *>(e->pin_dev),
+                  e->stream);
+    HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipStreamSynchronize(e->stream));
     if (tree_flags) *tree_flags = h[1];
     if (have_flags) *have_flags = true;
@@ -1745,7 +1749,7 @@ int pipe_alloc(bh_engine *e, bool last) {
     }
     if (last && e->lt_walk_cap < e->cap) {
         TRY(dev_alloc(e, e->lt_keys, (size_t)e->cap));
-        TRY(dev_alloc(e, e->lt_cpl, (size_t)e->cap));
+        TRY(dev_alloc(e, e->lt_cpl, (size_t)e->cap + 32));  // (as cpl: they trade places)
         TRY(dev_alloc(e, e->lt_base, (size_t)e->cap + 1));
         e->lt_walk_cap = e->cap;
     }
@@ -1797,7 +1801,7 @@ int mirror_alloc(bh_engine *e) {
         int lo = 0, hi = 0;
         HIPCHK(e, hipDeviceGetStreamPriorityRange(&lo, &hi));
         HIPCHK(e, hipStreamCreateWithPriority(&e->mir_stream, hipStreamNonBlocking, hi));
-        for (hipEvent_t *ev : {&e->mir_ev, &e->mir_ev2, &e->mir_in[0], &e->mir_in[1]})
+        for (hipEvent_t *ev : {&e->mir_ev, &e->mir_ev2, &e->mir_ev3, &e->mir_in[0], &e->mir_in[1]})
             HIPCHK(e, hipEventCreateWithFlags(ev, hipEventDisableTiming));
     }
     return BH_OK;
@@ -1806,41 +1810,71 @@ int mirror_alloc(bh_engine *e) {
 // src: the state the caller sees (tombstones of the running call still in it); its positions,
 // masses and caller indices are final once after_pos's queued work is, its velocities once
 // after_vel's is.  e->n bodies (before the call's compaction).
-int mirror_launch(bh_engine *e, const BodyState &src, hipStream_t after_pos, hipStream_t after_vel) {
+// The velocities are gathered on after_vel itself, right behind their producer: queued on the
+// mirror stream they waited for the positions' host copies (~0.35 ms in the one-step call,
+// which waits for them before its compaction -- round 4 drop-in trace).  (Kernels storing
+// straight into coherent pinned memory instead of the staging copies measured slower: one-step
+// calls with the mirror 3.33 against 3.20 ms.)
+// (in two parts, so that the positions can be queued before the work after_vel still gets)
+// in_line: the index and the gather run on after_pos itself, only the copies on the mirror
+// stream (before a traversal: queued beside it they wait for its first waves to retire)
+int mirror_pos(bh_engine *e, const BodyState &src, hipStream_t after_pos, bool in_line = false) {
     TRY(mirror_alloc(e));
     const int64_t n = e->n;
     const int64_t c = e->mir_cap;
     hipStream_t ms = e->mir_stream;
-    HIPCHK(e, hipEventRecord(e->mir_in[0], after_pos));
-    HIPCHK(e, hipEventRecord(e->mir_in[1], after_vel));
-    HIPCHK(e, hipStreamWaitEvent(ms, e->mir_in[0], 0));
+    hipStream_t ws = in_line ? after_pos : ms;
+    if (!in_line) {
+        HIPCHK(e, hipEventRecord(e->mir_in[0], after_pos));
+        HIPCHK(e, hipStreamWaitEvent(ms, e->mir_in[0], 0));
+    }
     if (n > 0) {
         double *st = e->mir_stage;
         HIPCHK(e, mirror_index(n, src.cidx, e->mir_keep, e->mir_pos, e->mir_tmp, e->mir_tmp_bytes,
-                               ms));
+                               ws));
+        HIPCHK(e, hipEventRecord(e->mir_in[1], ws));  // the caller positions are known
         const double *s3[3] = {src.x, src.y, src.m};
         double *d3[3] = {st, st + c, st + 4 * c};
-        mirror_scatter(n, src.cidx, e->mir_pos, 3, s3, d3, ms);
+        mirror_scatter(n, src.cidx, e->mir_pos, 3, s3, d3, ws);
         HIPCHK(e, hipGetLastError());
+        HIPCHK(e, hipEventRecord(e->mir_ev3, ws));  // the positions' gather is done
+        if (in_line) HIPCHK(e, hipStreamWaitEvent(ms, e->mir_ev3, 0));
         for (int j : {0, 1, 4})  // (the survivors are a prefix of each array)
             HIPCHK(e, hipMemcpyAsync(e->mir + j * c, st + j * c, sizeof(double) * n,
                                      hipMemcpyDeviceToHost, ms));
-        HIPCHK(e, hipStreamWaitEvent(ms, e->mir_in[1], 0));
+    }
+    return BH_OK;
+}
+
+int mirror_vel(bh_engine *e, const BodyState &src, hipStream_t after_vel) {
+    const int64_t n = e->n;
+    const int64_t c = e->mir_cap;
+    hipStream_t ms = e->mir_stream;
+    if (n > 0) {
+        double *st = e->mir_stage;
+        HIPCHK(e, hipStreamWaitEvent(after_vel, e->mir_in[1], 0));
         const double *s2[2] = {src.vx, src.vy};
         double *d2[2] = {st + 2 * c, st + 3 * c};
-        mirror_scatter(n, src.cidx, e->mir_pos, 2, s2, d2, ms);
+        mirror_scatter(n, src.cidx, e->mir_pos, 2, s2, d2, after_vel);
         HIPCHK(e, hipGetLastError());
-        HIPCHK(e, hipEventRecord(e->mir_ev2, ms));
+        HIPCHK(e, hipStreamWaitEvent(after_vel, e->mir_ev3, 0));
+        HIPCHK(e, hipEventRecord(e->mir_ev2, after_vel));  // no mirror kernel reads the state
+        HIPCHK(e, hipStreamWaitEvent(ms, e->mir_ev2, 0));
         for (int j : {2, 3})
             HIPCHK(e, hipMemcpyAsync(e->mir + j * c, st + j * c, sizeof(double) * n,
                                      hipMemcpyDeviceToHost, ms));
     } else {
-        HIPCHK(e, hipStreamWaitEvent(ms, e->mir_in[1], 0));
-        HIPCHK(e, hipEventRecord(e->mir_ev2, ms));
+        HIPCHK(e, hipEventRecord(e->mir_ev2, after_vel));
+        HIPCHK(e, hipStreamWaitEvent(ms, e->mir_ev2, 0));
     }
     HIPCHK(e, hipEventRecord(e->mir_ev, ms));
     e->mir_launched = true;
     return BH_OK;
+}
+
+int mirror_launch(bh_engine *e, const BodyState &src, hipStream_t after_pos, hipStream_t after_vel) {
+    TRY(mirror_pos(e, src, after_pos));
+    return mirror_vel(e, src, after_vel);
 }
 
 // The second evaluation of a pipelined step: build, second traversal with the fused kick, and
@@ -1864,6 +1898,17 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     copy_trav_inputs(n, e->st.m, e->m_trav, e->st.cidx, e->cidx_trav, lanes ? e->lanes : nullptr,
                      e->lanes_trav, e->base + n, e->T_trav, s, merging ? e->box : nullptr);
     HIPCHK(e, hipGetLastError());
+    // With the mirror on, a call's last step runs the merge rule and the mirror's caller-order
+    // gather of positions and masses before the traversal (~0.15 ms in line): the mirror's 40 MB
+    // cross PCIe from then on instead of from when the overlapped merge rule and gather find wave
+    // slots beside the traversal, ~0.45 ms later (round 4 drop-in trace)
+    const bool early = last && e->mirror_on;
+    if (early) {
+        copy_u32(e->scalars + 8, e->scalars + 2, s);  // the removals before the last merge rule
+        HIPCHK(e, hipGetLastError());
+        TRY(merge(e, s, merging));  // BHA:438 (the traversal reads its own copies of m, cidx)
+        TRY(mirror_pos(e, e->st, s, true));
+    }
     HIPCHK(e, hipEventRecord(e->pipe_ev[0], s));
     HIPCHK(e, hipStreamWaitEvent(e->pipe_stream, e->pipe_ev[0], 0));
     const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};  // BHA:378
@@ -1882,19 +1927,19 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     TRY(wave_order_next(e, 0, n, s));
     if (last) {
         hipStream_t ps = e->pipe_stream;
-        // lastTree's walk (bh_get_quads): sorted keys, prefix lengths, node offsets
-        HIPCHK(e, hipMemcpyAsync(e->lt_keys, e->keys_s, sizeof(uint64_t) * n,
-                                 hipMemcpyDeviceToDevice, ps));
-        HIPCHK(e, hipMemcpyAsync(e->lt_cpl, e->cpl, (size_t)n, hipMemcpyDeviceToDevice, ps));
-        HIPCHK(e, hipMemcpyAsync(e->lt_base, e->base, sizeof(uint32_t) * (n + 1),
-                                 hipMemcpyDeviceToDevice, ps));
-        // the call's removal count before its last merge rule (finish_merges, BHA:526)
-        HIPCHK(e, hipMemcpyAsync(e->scalars + 8, e->scalars + 2, sizeof(uint32_t),
-                                 hipMemcpyDeviceToDevice, ps));
+        // lastTree's walk (bh_get_quads): this build's sorted keys, prefix lengths and node
+        // offsets stay where they are, the overlapped build below writes the other set (a copy
+        // aside ran as a blit beside the traversal: ~0.5 ms, with the merge rule queued behind it)
+        std::swap(e->keys_s, e->lt_keys);
+        std::swap(e->cpl, e->lt_cpl);
+        std::swap(e->base, e->lt_base);
+        if (!early) {  // the call's removal count before its last merge rule (BHA:526)
+            copy_u32(e->scalars + 8, e->scalars + 2, ps);
+            HIPCHK(e, hipGetLastError());
+        }
     }
-    TRY(merge(e, e->pipe_stream, merging));         // BHA:438
-    if (last && e->mirror_on)  // positions and masses are final: the caller-order copy-out starts
-        TRY(mirror_launch(e, e->st, e->pipe_stream, s));
+    if (!early) TRY(merge(e, e->pipe_stream, merging));  // BHA:438
+    if (early) TRY(mirror_vel(e, e->st, s));  // the velocities once the kick is done
     TRY(build_into(e, e->pipe_stream, true));       // step s+1's first tree (BHA:359)
     if (BH_DEEP_PIPE) {
         // ... and a(t) of step s+1 on it (BHA:407-408): a force evaluation reads positions and
@@ -2385,7 +2430,7 @@ void bh_destroy(bh_engine *e) {
         (void)hipStreamSynchronize(e->mir_stream);
         (void)hipStreamDestroy(e->mir_stream);
     }
-    for (hipEvent_t ev : {e->mir_ev, e->mir_ev2, e->mir_in[0], e->mir_in[1]})
+    for (hipEvent_t ev : {e->mir_ev, e->mir_ev2, e->mir_ev3, e->mir_in[0], e->mir_in[1]})
         if (ev) (void)hipEventDestroy(ev);
     if (e->mir) (void)hipHostFree(e->mir);
     free_state(e->view);
@@ -2553,7 +2598,9 @@ int bh_step(bh_engine *e, int32_t k) {
         // a copy-out launched by the last pipelined step reads the state the compaction (or a
         // replay's restore) below rewrites
         if (e->mir_launched) HIPCHK(e, hipStreamWaitEvent(e->stream, e->mir_ev2, 0));
-        HIPCHK(e, hipStreamSynchronize(e->stream));
+        // (one GPU: no wait here -- the merge bookkeeping's read-back below, or the tree flags'
+        // when nothing merged, is queued behind the steps and waited for once)
+        if (may_let) HIPCHK(e, hipStreamSynchronize(e->stream));
         if (may_let) {  // LET subset sizes of this call: [4] some rank overflowed, [5] largest
             uint32_t ls[2] = {0, 0};
             // [4] can be set after the cell tables were exchanged (k_let_guard, k_let_w): on one

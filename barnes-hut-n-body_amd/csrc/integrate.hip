@@ -136,6 +136,11 @@ __global__ __launch_bounds__(TB) void k_mirror_keep(int64_t n, const uint32_t *_
     keep[c & ~CIDX_DEAD] = (c & CIDX_DEAD) ? 0u : 1u;
 }
 
+__global__ void k_copy_u32(uint32_t *dst, const uint32_t *src) {
+    chain_prio();
+    *dst = *src;
+}
+
 __global__ __launch_bounds__(TB) void k_mirror_scatter(int64_t n, const uint32_t *__restrict__ cidx,
                                                        const uint32_t *__restrict__ pos, int k,
                                                        Ptrs5 p) {
@@ -702,6 +707,31 @@ hipError_t mirror_index(int64_t n, const uint32_t *cidx, uint32_t *keep, uint32_
                                             rocprim::plus<uint32_t>(), s);
     if (st != hipSuccess) return st;
     return hipGetLastError();
+}
+
+void copy_u32(uint32_t *dst, const uint32_t *src, hipStream_t s) {
+    k_copy_u32<<<1, 1, 0, s>>>(dst, src);
+}
+
+__global__ __launch_bounds__(TB) void k_pack_readback(const uint32_t *__restrict__ scal,
+                                                      const uint32_t *__restrict__ hdr,
+                                                      const uint32_t *__restrict__ dlog,
+                                                      uint32_t ahead, uint32_t *__restrict__ out) {
+    const uint32_t i = blockIdx.x * TB + threadIdx.x;
+    if (i >= 16u + ahead) return;
+    uint32_t v = 0u;
+    if (i < 4u) v = scal[i];
+    else if (i < 12u) v = hdr[i - 4u];
+    else if (i == 12u) v = scal[8];
+    else if (i >= 16u) v = dlog[i - 16u];
+    out[i] = v;
+}
+
+void pack_readback(const uint32_t *scal, const MergePair *box, const uint32_t *dlog, uint32_t ahead,
+                   uint32_t *out, hipStream_t s) {
+    static_assert(sizeof(MergeHeader) == 8 * sizeof(uint32_t), "header words");
+    k_pack_readback<<<grid_for(16 + (int64_t)ahead), TB, 0, s>>>(
+        scal, reinterpret_cast<const uint32_t *>(box), dlog, ahead, out);
 }
 
 void mirror_scatter(int64_t n, const uint32_t *cidx, const uint32_t *pos, int k,

@@ -367,7 +367,7 @@ def single_gpu_leg(bh_amd, params, device, arrs, steps, warmup):
             "note": "rank 0's GPU alone, single-GPU engine, same scene / steps / warmup"}
 
 
-def drop_in_leg(eng, steps, warmup=2):
+def drop_in_leg(eng, steps, warmup=5):
     """The front-end's own call pattern (NBodyPanel.kt:290-293 tick() -> engine.step(), then
     paintComponent reads every body, NBodyPanel.kt:302-306): one bh_step(1) call per frame.
     Timed on the engine's current state (after the batched timed region), three ways:

@@ -24,7 +24,13 @@ def main():
     ap.add_argument("--calls", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--get-bodies", action="store_true")
+    ap.add_argument("--torch", action="store_true",
+                    help="initialise torch's GPU context first, as bench.py does")
     a = ap.parse_args()
+    if a.torch:
+        import torch
+        torch.zeros(1, device="cuda")
+        torch.cuda.synchronize()
     eng = bh_amd.Engine(bh_amd.default_params(theta=0.5))
     eng.reset_bodies(*scenes.config_scene(a.config))
     eng.set_mirror(not a.get_bodies)
@@ -43,7 +49,9 @@ def main():
             eng.map_bodies()
         t.append((t1 - t0, time.perf_counter() - t1))
     print({"step_ms": [round(1e3 * s, 3) for s, _ in t],
-           "read_ms": [round(1e3 * r, 3) for _, r in t]})
+           "read_ms": [round(1e3 * r, 3) for _, r in t],
+           "frame_ms_mean": round(1e3 * sum(s + r for s, r in t) / len(t), 3),
+           "torch": a.torch, "get_bodies": a.get_bodies})
 
 
 if __name__ == "__main__":
