@@ -60,10 +60,13 @@ __host__ __device__ inline uint32_t span_groups(uint32_t span_stride) {
 }
 
 // Adaptive bucket sort (tree_build.hip): splitter spacing of the previous build's sorted
-// order = the expected bucket size (896, so that drift rarely pushes a bucket past the
-// 1024-element network, measured within noise at C3 and C4).
+// order = the expected bucket size.  512 (LDS capacity 2 048 per bucket, 17 KB per workgroup:
+// up to 9 buckets in flight per CU) against 1 024 (4 096, 34 KB): build 5.8 -> 5.35 ms per 20 C3
+// steps, C4 10.5 -> 9.8 ms per 5 steps; 384 within noise of 512, 256 and 2 048 slower (round 4,
+// profiles/r04t_sort_bucket_ab.txt).  98-99 % of the buckets take the LDS bin radix path
+// (tools/sort_stats.py).
 #ifndef BH_SORT_B
-#define BH_SORT_B 1024
+#define BH_SORT_B 512
 #endif
 constexpr int SORT_B = BH_SORT_B;
 __host__ __device__ inline uint32_t sort_buckets(int64_t n) {

@@ -88,7 +88,10 @@ __global__ __launch_bounds__(TB) void k_morton(int64_t n, const double *__restri
 // Splitters are (re)written by k_prep of every build; the first build after a reset uses
 // rocprim (the splitters would describe other bodies).
 constexpr int SORT_TB = 256;
-constexpr int SORT_CAP = 4096;  // LDS bucket capacity (32 KB of composites)
+#ifndef BH_SORT_CAP
+#define BH_SORT_CAP 2048
+#endif
+constexpr int SORT_CAP = BH_SORT_CAP;  // LDS bucket capacity (16 KB of composites; 4 x SORT_B)
 
 __global__ __launch_bounds__(SORT_TB) void k_bucket_count(int64_t n,
                                                           const uint32_t *__restrict__ keys32,
@@ -170,6 +173,12 @@ constexpr int RADIX_CAP = SORT_CAP / 2;  // the bin-grouped copy lives in the up
 constexpr int RADIX_BINS = 256;
 constexpr uint32_t RADIX_MAXBIN = 48;
 
+#ifdef BH_SORT_STATS  // diagnostic build: which path each bucket took (radix / bitonic / global)
+__device__ unsigned long long g_sort_stats[8];
+#define SORT_STAT(q, v) (threadIdx.x == 0 ? (void)atomicAdd(&g_sort_stats[(q)], (unsigned long long)(v)) : (void)0)
+#else
+#define SORT_STAT(q, v) (void)0
+#endif
 __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restrict__ starts,
                                                          uint32_t *__restrict__ counts,
                                                          uint64_t *comp,
@@ -263,13 +272,19 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
                         emit(bs + rank, v);
                     }
                 }
+                SORT_STAT(0, 1);
+                SORT_STAT(1, s);
                 return;
             }
         }
+        SORT_STAT(2, 1);
+        SORT_STAT(3, s);
         bitonic_sort<true>(L, s);
         __syncthreads();
         for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) emit(j, L[j]);
     } else {  // oversized bucket: the same network on global memory, in place
+        SORT_STAT(4, 1);
+        SORT_STAT(5, s);
         uint64_t *A = comp + b0;
         bitonic_sort<false>(A, s);
         for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) emit(j, A[j]);  // own j: in place
@@ -1581,6 +1596,12 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
                                              b.super_list, n_groups, b.nodes);
     return hipGetLastError();
 }
+
+#ifdef BH_SORT_STATS
+extern "C" int bh_debug_sort_stats(unsigned long long *out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sort_stats), sizeof(unsigned long long) * 8);
+}
+#endif
 
 #ifdef BH_SPAN_TIMING
 extern "C" int bh_debug_span_times(uint64_t *out, uint32_t *launches) {
