@@ -804,6 +804,7 @@ void swap_let_sets(bh_engine *e) {
 TreeBuffers let_tree_buffers(bh_engine *e) {
     TreeBuffers b;
     b.src = e->sub_src;
+    b.src.vy = nullptr;  // (a subset's vx carries the replicated slot; its vy is never read)
     b.dst = e->sub_dst;
     b.keys = e->s_keys;
     b.keys_s = e->s_keys_s;
@@ -1020,6 +1021,7 @@ int spec_let_build(bh_engine *e, int64_t n_sub, const LetPieces &pc) {
     if (rc == BH_OK) {
         TreeBuffers sb = let_tree_buffers(e);
         sb.src = src;
+        sb.src.vy = nullptr;
         sb.keys_ready = false;
         hipError_t hr = tree_build(sb, n_sub, e->geo, ss);
         if (hr == hipSuccess) {

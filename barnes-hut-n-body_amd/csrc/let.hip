@@ -232,8 +232,7 @@ __global__ __launch_bounds__(TB) void k_let_gather(int64_t n, PosSrc ps,
         if (i < S && i >= n_real) {
             sub.x[i] = 0.0;
             sub.y[i] = 0.0;
-            sub.vx[i] = __longlong_as_double(-1ll);  // no replicated slot
-            sub.vy[i] = 0.0;
+            sub.vx[i] = __longlong_as_double(-1ll);  // no replicated slot (vy: unused)
             sub.m[i] = 0.0;
             sub.cidx[i] = CIDX_DEAD;
             if (mf.keys) let_fuse_key(g, mf, i, sentinel_key(g.J));
@@ -252,8 +251,7 @@ __global__ __launch_bounds__(TB) void k_let_gather(int64_t n, PosSrc ps,
     slot_pos(ps, st.x, st.y, i, px, py);
     sub.x[j] = px;
     sub.y[j] = py;
-    sub.vx[j] = __longlong_as_double((long long)i);  // payload: the replicated slot
-    sub.vy[j] = 0.0;
+    sub.vx[j] = __longlong_as_double((long long)i);  // payload: the replicated slot (vy unused)
     sub.m[j] = st.m[i];
     const uint32_t ci = st.cidx[i];
     sub.cidx[j] = ci;

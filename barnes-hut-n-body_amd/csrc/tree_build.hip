@@ -351,10 +351,10 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
         spl[a / SORT_B] = ((k >> key32_shift(J)) << 32) | (uint64_t)a;
     dst.x[a] = src.x[i];
     dst.y[a] = src.y[i];
-    if (src.vx) {  // null: the velocities are still being written (the pipelined step)
-        dst.vx[a] = src.vx[i];
-        dst.vy[a] = src.vy[i];
-    }
+    // null: the velocities are still being written (the pipelined step) / a subset build carries
+    // only the replicated slot in vx (LET)
+    if (src.vx) dst.vx[a] = src.vx[i];
+    if (src.vy) dst.vy[a] = src.vy[i];
     dst.m[a] = src.m[i];
     dst.cidx[a] = src.cidx[i];
     int c_cur = -1, c_prev = -1;
