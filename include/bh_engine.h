@@ -227,7 +227,9 @@ int bh_set_profiling(bh_engine *e, int enabled);
  * + i): the pieces of round k are adjacent there and are all-gathered in place (one
  * ncclAllGather per round) on a second stream while round k + 1 is evaluated.  Host-only; used
  * by the engine itself. */
+#ifndef BH_SHARD_ROUNDS
 #define BH_SHARD_ROUNDS 4
+#endif
 int bh_shard_range(int64_t n, int rank, int world, int round, int64_t *lo, int64_t *hi);
 int64_t bh_gather_slot(int64_t n, int world, int64_t lane);
 
