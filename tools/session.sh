@@ -21,7 +21,7 @@
 #   kstats         C3 bench under rocprofv3 --kernel-trace --stats per library (KSTATS_LIBS)
 # Every GPU step runs under its own time limit; a failing step (any rc but 0) ends the session, so
 # nothing else touches the GPU after a fault, an abort or a timeout.
-# (Round 3's one-off session scripts are kept in tools/archive/: committed profiles cite them.)
+# (Older one-off session scripts are kept in tools/archive/: committed profiles cite them; see tools/README.md.)
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
