@@ -9,6 +9,7 @@ waiting for peers.  The peers' bodies get zero acceleration, so the scene is not
     python tools/solo_rank.py --world 8 --rank 0 --steps 10 --warmup 2 [--config c4]
 """
 import argparse
+import ctypes
 import json
 import os
 import sys
@@ -47,6 +48,12 @@ def main():
            "phase_ms_per_step": {k: round(v / a.steps, 4) for k, v in ph.items()},
            "traverse_launch_ms": round(trav_ms, 4), "traverse_launches": launches,
            "let": eng.let_stats()}
+    lib = bh_amd.load_library()
+    if hasattr(lib, "bh_debug_sort_stats"):  # a -DBH_SORT_STATS build: bucket paths (all builds)
+        st = (ctypes.c_ulonglong * 8)()
+        if lib.bh_debug_sort_stats(st) == 0:
+            out["sort_stats"] = dict(zip(("radix", "radix_el", "bitonic", "bitonic_el", "global",
+                                          "global_el"), (int(v) for v in st[:6])))
     print(json.dumps(out))
     eng.close()
 
