@@ -1740,6 +1740,35 @@ bool pipelined(const bh_engine *e, bool last) {
            !e->group && !e->solo && e->p.theta != 0.0;
 }
 
+// The overlap and mirror streams of a one-GPU engine.  HIP hands a process's streams its few
+// hardware queues in creation order, so bh_create makes them right after the engine's own stream:
+// made lazily, after another engine's streams (bench.py's counter probe), the mirror's copies
+// shared a queue with the step's kernels (C3 one-step calls with the mirror: 3.25 -> 2.3 ms).
+int pipe_streams(bh_engine *e) {
+    for (hipEvent_t &ev : e->pipe_ev)
+        if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+    if (!e->pipe_stream) {
+        // the traversal fills every wave slot with a queue of waiting workgroups: at the default
+        // priority the overlapped kernels would be dispatched only in its tail
+        int lo = 0, hi = 0;
+        HIPCHK(e, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(e, hipStreamCreateWithPriority(&e->pipe_stream, hipStreamNonBlocking,
+                                              BH_PIPE_PRIORITY ? hi : lo));
+    }
+    return BH_OK;
+}
+
+int mirror_streams(bh_engine *e) {
+    if (!e->mir_stream) {
+        int lo = 0, hi = 0;
+        HIPCHK(e, hipDeviceGetStreamPriorityRange(&lo, &hi));
+        HIPCHK(e, hipStreamCreateWithPriority(&e->mir_stream, hipStreamNonBlocking, hi));
+        for (hipEvent_t *ev : {&e->mir_ev, &e->mir_ev2, &e->mir_ev3, &e->mir_in[0], &e->mir_in[1]})
+            HIPCHK(e, hipEventCreateWithFlags(ev, hipEventDisableTiming));
+    }
+    return BH_OK;
+}
+
 int pipe_alloc(bh_engine *e, bool last) {
     if (e->nodes_alt_cap < e->node_cap) {
         TRY(dev_alloc(e, e->nodes_alt, e->node_cap));
@@ -1762,17 +1791,7 @@ int pipe_alloc(bh_engine *e, bool last) {
         if (!e->T_trav) TRY(dev_alloc(e, e->T_trav, 1));
         e->trav_cap = e->cap;
     }
-    for (hipEvent_t &ev : e->pipe_ev)
-        if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
-    if (!e->pipe_stream) {
-        // the traversal fills every wave slot with a queue of waiting workgroups: at the default
-        // priority the overlapped kernels would be dispatched only in its tail
-        int lo = 0, hi = 0;
-        HIPCHK(e, hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIPCHK(e, hipStreamCreateWithPriority(&e->pipe_stream, hipStreamNonBlocking,
-                                              BH_PIPE_PRIORITY ? hi : lo));
-    }
-    return BH_OK;
+    return pipe_streams(e);
 }
 
 // ---- the pinned caller-order mirror (bh_set_mirror / bh_map_bodies) -------------------
@@ -1799,14 +1818,7 @@ int mirror_alloc(bh_engine *e) {
         e->mir_cap = e->cap;
         e->mir_fresh = false;
     }
-    if (!e->mir_stream) {
-        int lo = 0, hi = 0;
-        HIPCHK(e, hipDeviceGetStreamPriorityRange(&lo, &hi));
-        HIPCHK(e, hipStreamCreateWithPriority(&e->mir_stream, hipStreamNonBlocking, hi));
-        for (hipEvent_t *ev : {&e->mir_ev, &e->mir_ev2, &e->mir_ev3, &e->mir_in[0], &e->mir_in[1]})
-            HIPCHK(e, hipEventCreateWithFlags(ev, hipEventDisableTiming));
-    }
-    return BH_OK;
+    return mirror_streams(e);
 }
 
 // src: the state the caller sees (tombstones of the running call still in it); its positions,
@@ -2265,6 +2277,8 @@ int bh_create(const bh_params *p, int device, bh_engine **out) {
     *out = nullptr;
     bh_engine *e = new bh_engine();
     int rc = engine_init(e, p, device);
+    if (rc == BH_OK) rc = pipe_streams(e);
+    if (rc == BH_OK) rc = mirror_streams(e);
     if (rc != BH_OK) {
         std::fprintf(stderr, "bh_create: %s\n", e->err.c_str());
         bh_destroy(e);

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--calls", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--get-bodies", action="store_true")
+    ap.add_argument("--before", default="",
+                    help="calls made before the mirror is switched on, as bench.py's drop_in leg "
+                         "does: 's' = 45 x step(1), 'g' = 45 x (step(1) + get_bodies), e.g. 'sg'")
     ap.add_argument("--torch", action="store_true",
                     help="initialise torch's GPU context first, as bench.py does")
     a = ap.parse_args()
@@ -33,8 +36,14 @@ def main():
         torch.cuda.synchronize()
     eng = bh_amd.Engine(bh_amd.default_params(theta=0.5))
     eng.reset_bodies(*scenes.config_scene(a.config))
-    eng.set_mirror(not a.get_bodies)
     bufs = [np.zeros(eng.num_bodies()) for _ in range(5)]
+    for c in a.before:
+        for _ in range(45):
+            eng.step(1)
+            if c == "g":
+                eng.get_bodies(out=bufs)
+        eng.synchronize()
+    eng.set_mirror(not a.get_bodies)
     for _ in range(a.warmup):
         eng.step(1)
     eng.synchronize()
@@ -51,7 +60,7 @@ def main():
     print({"step_ms": [round(1e3 * s, 3) for s, _ in t],
            "read_ms": [round(1e3 * r, 3) for _, r in t],
            "frame_ms_mean": round(1e3 * sum(s + r for s, r in t) / len(t), 3),
-           "torch": a.torch, "get_bodies": a.get_bodies})
+           "torch": a.torch, "get_bodies": a.get_bodies, "before": a.before})
 
 
 if __name__ == "__main__":
