@@ -295,6 +295,12 @@ void permute_velocities(int64_t n, const uint32_t *perm, const double *svx, cons
 // slot in keys32).  Uses keys32 / keys32_s / idx.
 hipError_t lane_order(const TreeBuffers &b, int64_t n, int J, bool refresh, uint32_t *lanes,
                       hipStream_t s);
+// The refresh half of lane_order on its own buffers (the pipelined step runs it beside the next
+// first traversal, engine.cpp): Hilbert keys of the sorted Morton keys, radix-sorted with slots.
+hipError_t lane_order_into(const uint64_t *keys_s, int64_t n, int J, uint32_t *hkey,
+                           uint32_t *hkey_s, uint32_t *slot, void *scratch, size_t scratch_bytes,
+                           uint32_t *lanes, hipStream_t s);
+size_t lane_sort_bytes(int64_t n);
 
 // ---- launchers (traverse.hip) ----------------------------------------------------
 // Accelerations F/m of slots [lo, hi), written interleaved to a2[2p], a2[2p+1].

@@ -190,6 +190,17 @@ struct bh_engine {
     uint32_t *lanes = nullptr;
     bool lanes_valid = false;  // the map is a permutation of the current slots
     int lanes_age = 0;         // builds since the last Hilbert sort
+    // a due re-sort of the pipelined step's lane map, run beside the next first traversal on its
+    // own buffers (lane_refresh_beside) and swapped in before the second build
+    bool lane_defer = false;   // this overlapped build may leave a due re-sort to that
+    bool lane_hold = false;    // this second build leaves a due re-sort to the next overlapped one
+    bool lr_pending = false;   // a re-sort is due from the prebuilt tree's keys
+    bool lr_ready = false;     // lanes_next holds it once lr_ev completes
+    uint32_t *lanes_next = nullptr, *lr_hkey = nullptr, *lr_hkey_s = nullptr, *lr_slot = nullptr;
+    void *lr_scratch = nullptr;
+    size_t lr_scratch_bytes = 0;
+    int64_t lr_cap = 0;
+    hipEvent_t lr_ev = nullptr;
     const uint32_t *a2_lanes = nullptr;  // the last evaluation wrote a2 by lane of this map
     GatherLayout a2_layout{};            // ... at the lane's gather slot (multi-rank rounds)
 
@@ -442,7 +453,7 @@ int ensure_capacity(bh_engine *e, int64_t n) {
         TRY(dev_alloc(e, e->visits32, cap));
         TRY(dev_alloc(e, e->contrib32, cap));
         TRY(dev_alloc(e, e->lanes, cap));
-        e->lanes_valid = false;
+        e->lanes_valid = e->lr_pending = e->lr_ready = false;
         e->inv_valid = false;
         TRY(dev_alloc(e, e->wave_iters, cap / 64 + 2));
         TRY(dev_alloc(e, e->wave_blocks, cap / 64 + 2));
@@ -576,7 +587,13 @@ int collect_timings(bh_engine *e) {
 
 // ---- buildTree() (BHA:359-366): sort + build; the state moves to the new Morton order ----
 #ifndef BH_LANE_REFRESH
-#define BH_LANE_REFRESH 16  // builds between Hilbert re-sorts of the lane map (0: Morton lanes)
+// builds between Hilbert re-sorts of the lane map (0: Morton lanes).  With the re-sort beside the
+// first traversal (BH_LANE_DEFER) a fresher map pays: C3 1.84-1.85 ms per step at 16, 1.82-1.83 at
+// 8, 1.814-1.820 at 6, 1.82-1.83 at 4 (round 4, profiles/r04L2_lane_refresh_ab.txt)
+#define BH_LANE_REFRESH 6
+#endif
+#ifndef BH_LANE_DEFER
+#define BH_LANE_DEFER 1  // pipelined steps re-sort beside the first traversal (lane_refresh_beside)
 #endif
 // overlap: the pipelined step's build on stream `s` -- into nodes_alt and alt without the
 // velocities (permute_velocities follows) and without the final swap (the caller swaps)
@@ -596,7 +613,11 @@ int build_into(bh_engine *e, hipStream_t s, bool overlap, bool keep_v = false) {
     // Hilbert waves (every rank alike): re-sorted every BH_LANE_REFRESH builds, carried through
     // the build's permutation by k_emit_com in between
     const bool use_lanes = BH_LANE_REFRESH > 0 && n > 0 && e->p.theta != 0.0;
-    const bool refresh = use_lanes && (!e->lanes_valid || e->lanes_age >= BH_LANE_REFRESH);
+    const bool due = use_lanes && e->lanes_valid && e->lanes_age >= BH_LANE_REFRESH;
+    // (pipelined steps: the re-sort is left to the next first traversal's side, see
+    // lane_refresh_beside; the map is carried through this build meanwhile)
+    const bool defer = due && BH_LANE_DEFER && ((overlap && e->lane_defer) || e->lane_hold);
+    const bool refresh = use_lanes && (!e->lanes_valid || (due && !defer));
     tb.lanes_remap = use_lanes && !refresh ? e->lanes : nullptr;
     tb.keys_ready = e->keys_ready && !overlap;
     e->keys_ready = false;
@@ -608,8 +629,9 @@ int build_into(bh_engine *e, hipStream_t s, bool overlap, bool keep_v = false) {
         if (refresh) HIPCHK(e, lane_order(tb, n, e->geo.J, true, e->lanes, s));
         e->lanes_valid = true;
         e->lanes_age = refresh ? 1 : e->lanes_age + 1;
+        if (defer && overlap) e->lr_pending = true;
     } else {
-        e->lanes_valid = false;  // this build's permutation was not applied to the map
+        e->lanes_valid = e->lr_pending = e->lr_ready = false;  // this build's permutation was not applied to the map
     }
     e->spl_nb = sort_buckets(n);  // k_prep wrote this build's splitters
     e->st_morton = true;
@@ -1658,7 +1680,7 @@ int restore(bh_engine *e) {
     e->spec_ready = false;
     e->spl_nb = 0;  // the splitters describe the discarded builds' order
     e->keys_ready = false;
-    e->lanes_valid = false;
+    e->lanes_valid = e->lr_pending = e->lr_ready = false;
     e->inv_valid = false;
     e->pos_pending = false;  // the snapshot holds every position
     e->heavy_possible = true;
@@ -1906,7 +1928,16 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     const bool merging = e->p.merge_min_dist > 0.0 && e->n > 1 && e->heavy_possible;
     if (merging) TRY(merge_bufs(e));
     TRY(mark(e, -1));
-    TRY(build_into(e, s, false, true));  // velocities: permuted by the traversal's kick below
+    if (e->lr_ready) {  // the re-sorted lane map (prebuilt order), carried on by this build
+        HIPCHK(e, hipStreamWaitEvent(s, e->lr_ev, 0));
+        std::swap(e->lanes, e->lanes_next);
+        e->lr_ready = false;
+        e->lanes_age = 0;
+    }
+    e->lane_hold = true;
+    const int rc_b2 = build_into(e, s, false, true);  // velocities: permuted by the kick below
+    e->lane_hold = false;
+    TRY(rc_b2);
     TRY(mark(e, 0));
     const bool lanes = e->lanes_valid;
     copy_trav_inputs(n, e->st.m, e->m_trav, e->st.cidx, e->cidx_trav, lanes ? e->lanes : nullptr,
@@ -1954,7 +1985,10 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     }
     if (!early) TRY(merge(e, e->pipe_stream, merging));  // BHA:438
     if (early) TRY(mirror_vel(e, e->st, s));  // the velocities once the kick is done
-    TRY(build_into(e, e->pipe_stream, true));       // step s+1's first tree (BHA:359)
+    e->lane_defer = !last;  // (a call ends with a compaction: its last build re-sorts in place)
+    const int rc_b1 = build_into(e, e->pipe_stream, true);  // step s+1's first tree (BHA:359)
+    e->lane_defer = false;
+    TRY(rc_b1);
     if (BH_DEEP_PIPE) {
         // ... and a(t) of step s+1 on it (BHA:407-408): a force evaluation reads positions and
         // masses only, so it runs beside this traversal, whose tail it fills; the next step's
@@ -2006,6 +2040,38 @@ int snapshot_positions(bh_engine *e) {
     return BH_OK;
 }
 
+// The lane map's due Hilbert re-sort (build_into), from the prebuilt tree's sorted keys, on the
+// overlap stream beside the first traversal -- which walks the map carried through that build --
+// into lanes_next, swapped in before the second build carries it on (evaluate_pipelined).  The
+// traversal writes none of these buffers (its fused epilogue writes keys / keys32, not keys_s).
+// Made in the overlapped build, the re-sort ran after the chain and outlasted the second
+// traversal by ~0.12 ms once every 8 steps (round 4 timeline).
+int lane_refresh_beside(bh_engine *e) {
+    e->lr_pending = false;
+    const int64_t n = e->n;
+    if (n <= 0 || !e->lanes_valid) return BH_OK;
+    if (e->lr_cap < e->cap) {
+        for (uint32_t **q : {&e->lanes_next, &e->lr_hkey, &e->lr_hkey_s, &e->lr_slot}) {
+            if (*q) (void)hipFree(*q);
+            *q = nullptr;
+        }
+        if (e->lr_scratch) (void)hipFree(e->lr_scratch);
+        e->lr_scratch = nullptr;
+        e->lr_cap = 0;
+        for (uint32_t **q : {&e->lanes_next, &e->lr_hkey, &e->lr_hkey_s, &e->lr_slot})
+            TRY(dev_alloc(e, *q, (size_t)e->cap));
+        e->lr_scratch_bytes = lane_sort_bytes(e->cap);
+        HIPCHK(e, hipMalloc(&e->lr_scratch, e->lr_scratch_bytes));
+        e->lr_cap = e->cap;
+    }
+    if (!e->lr_ev) HIPCHK(e, hipEventCreateWithFlags(&e->lr_ev, hipEventDisableTiming));
+    HIPCHK(e, lane_order_into(e->keys_s, n, e->geo.J, e->lr_hkey, e->lr_hkey_s, e->lr_slot,
+                              e->lr_scratch, e->lr_scratch_bytes, e->lanes_next, e->pipe_stream));
+    HIPCHK(e, hipEventRecord(e->lr_ev, e->pipe_stream));
+    e->lr_ready = true;
+    return BH_OK;
+}
+
 // ---- one PhysicsEngine.step() (BHA:405-439) ------------------------------------------
 // last: the final step of a bh_step call -- its second build is the full tree (lastTree,
 // BHA:435, for getTreeForDebug) also on a multi-rank engine that shards its builds.
@@ -2014,6 +2080,8 @@ int step_once(bh_engine *e, bool last) {
     const double dtHalf = e->p.dt * 0.5;  // BHA:412
     if (pipelined(e, last)) {
         TRY(pipe_alloc(e, last));
+        if (e->lr_pending && e->prebuilt) TRY(lane_refresh_beside(e));
+        e->lr_pending = false;
         bool fused = false;
         e->fuse_keys = true;  // and the second build's keys and bucket counts
         TRY(evaluate(e, nullptr, KICK_DRIFT, &fused, true));  // a(t), kick + drift fused
@@ -2489,10 +2557,12 @@ void bh_destroy(bh_engine *e) {
                     e->leaf_tmp, e->spl, e->bcount, e->bstart, e->nodes_alt, e->wave_cost, e->run_order,
                     e->m_trav, e->cidx_trav, e->lanes_trav, e->T_trav, e->solo_xchg,
                     e->lt_x, e->lt_y, e->a2_alt, e->lt_keys, e->lt_cpl, e->lt_base, e->mir_stage,
-                    e->mir_keep, e->mir_pos, e->mir_tmp};
+                    e->mir_keep, e->mir_pos, e->mir_tmp, e->lanes_next, e->lr_hkey, e->lr_hkey_s,
+                    e->lr_slot, e->lr_scratch};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
     for (hipEvent_t ev : e->ev) (void)hipEventDestroy(ev);
+    if (e->lr_ev) (void)hipEventDestroy(e->lr_ev);
     if (e->pin) (void)hipHostFree(e->pin);
     if (e->stream) (void)hipStreamDestroy(e->stream);
     delete e;
@@ -2516,7 +2586,7 @@ int bh_set_params(bh_engine *e, const bh_params *p) {
             // caller sees, in its own slot order (the lane map described the prebuilt order)
             std::swap(e->st, e->view);
             e->view_pending = false;
-            e->lanes_valid = false;
+            e->lanes_valid = e->lr_pending = e->lr_ready = false;
         }
         e->prebuilt = false;
         e->lt_aside = false;
@@ -2525,7 +2595,7 @@ int bh_set_params(bh_engine *e, const bh_params *p) {
         e->lazy_tree = false;
         e->spl_nb = 0;  // keys change meaning
         e->keys_ready = false;
-        e->lanes_valid = false;
+        e->lanes_valid = e->lr_pending = e->lr_ready = false;
         e->inv_valid = false;
         if (g.J != e->J_alloc) {  // tree workspace sized for another depth; the state stays
             HIPCHK(e, hipStreamSynchronize(e->stream));
@@ -2573,7 +2643,7 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     e->mir_fresh = false;
     e->spl_nb = 0;          // other bodies: the first build sorts from scratch
     e->keys_ready = false;
-    e->lanes_valid = false;
+    e->lanes_valid = e->lr_pending = e->lr_ready = false;
     e->st_morton = false;
     e->vel_stale = false;
     e->pos_pending = false;

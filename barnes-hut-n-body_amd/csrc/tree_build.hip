@@ -1516,11 +1516,27 @@ hipError_t lane_order(const TreeBuffers &b, int64_t n, int J, bool refresh, uint
         return hipGetLastError();
     }
     // keys32 / keys32_s / idx are free once the build has run
-    k_hilbert_keys<<<grid_for(n), TB, 0, s>>>(n, J, b.keys_s, b.keys32, b.idx);
-    size_t bytes = b.scratch_bytes;
-    return rocprim::radix_sort_pairs<LaneSortConfig>(b.scratch, bytes, b.keys32, b.keys32_s,
-                                                     b.idx, lanes, (size_t)n, LANE_SORT_LO_BIT,
-                                                     32u, s);
+    return lane_order_into(b.keys_s, n, J, b.keys32, b.keys32_s, b.idx, b.scratch, b.scratch_bytes,
+                           lanes, s);
+}
+
+hipError_t lane_order_into(const uint64_t *keys_s, int64_t n, int J, uint32_t *hkey,
+                           uint32_t *hkey_s, uint32_t *slot, void *scratch, size_t scratch_bytes,
+                           uint32_t *lanes, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    k_hilbert_keys<<<grid_for(n), TB, 0, s>>>(n, J, keys_s, hkey, slot);
+    size_t bytes = scratch_bytes;
+    return rocprim::radix_sort_pairs<LaneSortConfig>(scratch, bytes, hkey, hkey_s, slot, lanes,
+                                                     (size_t)n, LANE_SORT_LO_BIT, 32u, s);
+}
+
+size_t lane_sort_bytes(int64_t n) {
+    size_t bytes = 0;
+    (void)rocprim::radix_sort_pairs<LaneSortConfig>(nullptr, bytes, (uint32_t *)nullptr,
+                                                    (uint32_t *)nullptr, (uint32_t *)nullptr,
+                                                    (uint32_t *)nullptr, (size_t)n,
+                                                    LANE_SORT_LO_BIT, 32u);
+    return bytes;
 }
 
 size_t tree_scratch_bytes(int64_t n, int J) {
