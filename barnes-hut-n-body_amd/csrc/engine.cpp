@@ -592,6 +592,9 @@ int collect_timings(bh_engine *e) {
 // 8, 1.814-1.820 at 6, 1.82-1.83 at 4 (round 4, profiles/r04L2_lane_refresh_ab.txt)
 #define BH_LANE_REFRESH 6
 #endif
+#ifndef BH_LANE_REFRESH_SHARDED
+#define BH_LANE_REFRESH_SHARDED 16  // multi-rank engines (no pipelined step: the re-sort is in line)
+#endif
 #ifndef BH_LANE_DEFER
 #define BH_LANE_DEFER 1  // pipelined steps re-sort beside the first traversal (lane_refresh_beside)
 #endif
@@ -613,7 +616,8 @@ int build_into(bh_engine *e, hipStream_t s, bool overlap, bool keep_v = false) {
     // Hilbert waves (every rank alike): re-sorted every BH_LANE_REFRESH builds, carried through
     // the build's permutation by k_emit_com in between
     const bool use_lanes = BH_LANE_REFRESH > 0 && n > 0 && e->p.theta != 0.0;
-    const bool due = use_lanes && e->lanes_valid && e->lanes_age >= BH_LANE_REFRESH;
+    const int every = (e->comm || e->group || e->solo) ? BH_LANE_REFRESH_SHARDED : BH_LANE_REFRESH;
+    const bool due = use_lanes && e->lanes_valid && e->lanes_age >= every;
     // (pipelined steps: the re-sort is left to the next first traversal's side, see
     // lane_refresh_beside; the map is carried through this build meanwhile)
     const bool defer = due && BH_LANE_DEFER && ((overlap && e->lane_defer) || e->lane_hold);

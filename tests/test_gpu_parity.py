@@ -1060,7 +1060,7 @@ def test_profiling_timings_do_not_change_results():
 def test_pipelined_call_equals_single_steps():
     """One GPU, theta > 0: inside a bh_step(k) call every step but the last overlaps its second
     traversal with the merge rule and the next step's first build (engine.cpp, the pipelined
-    step).  k = 20 in one call (two lane-map refreshes, merges mid-call) against 20 calls of one
+    step).  k = 20 in one call (lane-map re-sorts beside the first traversal, merges mid-call) against 20 calls of one
     step each (never pipelined): the same state bit for bit and the same last tree, both equal
     to the oracle's -- lastTree (BHA:435) is the last step's tree also when earlier steps of the
     call merged bodies (BHA:526 clears it only for the last step's merge)."""
