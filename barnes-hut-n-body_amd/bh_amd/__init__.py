@@ -44,7 +44,9 @@ EXPORTED_SYMBOLS = (
     "bh_nbody3d_step", "bh_nbody3d_accelerations", "bh_nbody3d_get", "bh_nbody3d_last_ms",
     "bh_local_group_create", "bh_local_group_destroy", "bh_create_local",
     "bh_save_state", "bh_load_state", "bh_let_stats", "bh_create_solo", "bh_comm_ranks",
-    "bh_debug_inject", "bh_set_mirror", "bh_map_bodies", "bh_let_spec_stats",
+    "bh_debug_inject", "bh_set_mirror", "bh_map_bodies", "bh_create_multi",
+    "bh_create_multi_list", "bh_multi_world", "bh_multi_member", "bh_collective_log",
+    "bh_collective_log_clear",
 )
 
 
@@ -97,6 +99,14 @@ def load_library(path: str | None = None):
                                     ctypes.POINTER(_VP)]
     lib.bh_create_solo.argtypes = [ctypes.POINTER(BhParams), ctypes.c_int, ctypes.c_int,
                                    ctypes.c_int, ctypes.POINTER(_VP)]
+    lib.bh_create_multi.argtypes = [ctypes.POINTER(BhParams), ctypes.c_uint32, ctypes.POINTER(_VP)]
+    lib.bh_create_multi_list.argtypes = [ctypes.POINTER(BhParams), ctypes.POINTER(ctypes.c_int32),
+                                         ctypes.c_int32, ctypes.POINTER(_VP)]
+    lib.bh_multi_world.argtypes = [_VP]
+    lib.bh_multi_member.argtypes = [_VP, ctypes.c_int]
+    lib.bh_multi_member.restype = _VP
+    lib.bh_collective_log.argtypes = [_VP, _I64P, ctypes.c_int64, _I64P]
+    lib.bh_collective_log_clear.argtypes = [_VP]
     lib.bh_destroy.argtypes = [_VP]
     lib.bh_destroy.restype = None
     lib.bh_last_error.argtypes = [_VP]
@@ -125,7 +135,6 @@ def load_library(path: str | None = None):
     lib.bh_traversal_stats.argtypes = [_VP, _I64P, _I64P, _I64P]
     lib.bh_traversal_counters.argtypes = [_VP, _I64P]
     lib.bh_let_stats.argtypes = [_VP, _I64P]
-    lib.bh_let_spec_stats.argtypes = [_VP, _I64P]
     lib.bh_comm_ranks.argtypes = [_VP, ctypes.POINTER(ctypes.c_int32),
                                   ctypes.POINTER(ctypes.c_int32)]
     lib.bh_debug_inject.argtypes = [_VP, ctypes.c_int]
@@ -299,11 +308,22 @@ class Engine:
 
     def __init__(self, params: BhParams | None = None, device: int = 0, rank: int = 0,
                  world: int = 1, unique_id: bytes | None = None,
-                 local_group: "LocalGroup | None" = None, solo: bool = False):
+                 local_group: "LocalGroup | None" = None, solo: bool = False,
+                 devices=None, device_mask: int | None = None):
         self._lib = load_library()
         self._h = _VP()
+        self._owned = True
         self.params = params if params is not None else default_params()
-        if solo:  # measurement: one rank's share of a `world`-rank step, alone (bh_create_solo)
+        if devices is not None:  # one handle over these devices, repeats allowed (multi.cpp)
+            arr = (ctypes.c_int32 * len(devices))(*[int(d) for d in devices])
+            rc = self._lib.bh_create_multi_list(ctypes.byref(self.params), arr, len(devices),
+                                                ctypes.byref(self._h))
+            world = len(devices)
+        elif device_mask is not None:  # one handle over every GPU of the mask (0: all)
+            rc = self._lib.bh_create_multi(ctypes.byref(self.params), int(device_mask),
+                                           ctypes.byref(self._h))
+            world = None
+        elif solo:  # measurement: one rank's share of a `world`-rank step, alone (bh_create_solo)
             rc = self._lib.bh_create_solo(ctypes.byref(self.params), device, rank, world,
                                           ctypes.byref(self._h))
         elif local_group is not None:
@@ -317,6 +337,8 @@ class Engine:
             rc = self._lib.bh_create(ctypes.byref(self.params), device, ctypes.byref(self._h))
         if rc != BH_OK:
             raise BhError(rc, "engine creation failed (is a GPU visible?)")
+        if world is None:
+            world = int(self._lib.bh_multi_world(self._h))
         self.rank, self.world = rank, world
 
     def _check(self, rc):
@@ -324,9 +346,41 @@ class Engine:
             raise BhError(rc, self._lib.bh_last_error(self._h).decode())
 
     def close(self):
-        if self._h:
+        if self._h and self._owned:
             self._lib.bh_destroy(self._h)
-            self._h = _VP()
+        self._h = _VP()
+
+    # ---- multi-device handle ------------------------------------------------------------
+    def multi_world(self) -> int:
+        """Members of a bh_create_multi handle (1 for any other engine)."""
+        return int(self._lib.bh_multi_world(self._h))
+
+    def member(self, rank: int) -> "Engine":
+        """Member `rank` of a multi-device handle, for diagnostics (a non-owning view: never
+        step it alone -- its peers would wait for it)."""
+        h = self._lib.bh_multi_member(self._h, int(rank))
+        if not h:
+            raise BhError(BH_E_INVALID, f"no member {rank}")
+        m = Engine.__new__(Engine)
+        m._lib, m._h, m._owned = self._lib, _VP(h), False
+        m.params, m.rank, m.world = self.params, rank, self.world
+        m._parent = self  # keeps the handle alive
+        return m
+
+    def collective_log(self):
+        """(api call, site, bytes, stream) rows of every collective this engine issued
+        (bh_collective_log)."""
+        need = ctypes.c_int64(0)
+        rc = self._lib.bh_collective_log(self._h, None, 0, ctypes.byref(need))
+        if rc not in (BH_OK, BH_E_CAPACITY):
+            self._check(rc)
+        out = np.zeros((need.value, 4), dtype=np.int64)
+        self._check(self._lib.bh_collective_log(self._h, out.ctypes.data_as(_I64P), need.value,
+                                                ctypes.byref(need)))
+        return out
+
+    def collective_log_clear(self):
+        self._check(self._lib.bh_collective_log_clear(self._h))
 
     def __del__(self):
         try:
@@ -425,9 +479,6 @@ class Engine:
         self._check(self._lib.bh_let_stats(self._h, out.ctypes.data_as(_I64P)))
         d = dict(zip(("let_builds", "full_builds", "subset", "let_nodes", "overflows"),
                      out.tolist()))
-        sp = np.zeros(2, dtype=np.int64)
-        self._check(self._lib.bh_let_spec_stats(self._h, sp.ctypes.data_as(_I64P)))
-        d["spec_builds"], d["spec_fallbacks"] = int(sp[0]), int(sp[1])
         return d
 
     def comm_ranks(self):
@@ -548,11 +599,12 @@ class PhysicsEngine:
     """PhysicsEngine(initialBodies) (BHA:287) — writes results back into the same Body
     objects (BHA:414-432) and shrinks the caller's list on a merge (BHA:519)."""
 
-    def __init__(self, initial_bodies: list, device: int = 0):
+    def __init__(self, initial_bodies: list, device: int = 0, devices=None):
         self._bodies = initial_bodies
         self.merge_max_mass = 4_000.0          # BHA:315
         self.merge_min_dist = Config.MIN_R     # BHA:321
-        self._eng = Engine(self._params(), device=device)
+        # devices: one handle over several GPUs (bh_create_multi_list), else one GPU
+        self._eng = Engine(self._params(), device=device, devices=devices)
         self._push()
 
     def _params(self) -> BhParams:

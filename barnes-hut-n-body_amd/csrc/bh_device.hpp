@@ -459,16 +459,13 @@ hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
 // gslot[lanes[q]] = gather_slot(gl, q) (lanes null: the identity map)
 void let_gather_slots(int64_t n, const uint32_t *lanes, GatherLayout gl, uint32_t *gslot,
                       hipStream_t s);
-// after tree_build over the subset: the own cells' exchange table; detect_cross: flag (status
-// record's tag) a body the build's jitter moved into another depth-LET_P cell (tb.src / tb.dst)
+// after tree_build over the subset: the own cells' exchange table
 hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const TreeBuffers &tb,
-                     hipStream_t s, bool detect_cross = false);
+                     hipStream_t s);
 // after the exchange (L.tables, LET_TSTRIDE per rank): any rank's overflow -> scal[4]; top
-// levels, layout, node array, lane map; tree size posc[LET_CELLS]; cross (nullable) <- whether
-// any rank flagged a jitter move across a depth-LET_P cell
+// levels, layout, node array, lane map; tree size posc[LET_CELLS]
 hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, const LetBufs &L,
-                        const TreeBuffers &tb, uint32_t *scal, hipStream_t s,
-                        uint32_t *cross = nullptr);
+                        const TreeBuffers &tb, uint32_t *scal, hipStream_t s);
 // owner integration: a2 (gather slots) holds every lane's (x, y) -> the replicated state; the
 // solo fill writes the current positions of all lanes first
 void let_set_pos(int64_t n, const uint32_t *lanes, const double *a2, GatherLayout gl, double *x,
@@ -530,6 +527,8 @@ void mirror_scatter(int64_t n, const uint32_t *cidx, const uint32_t *pos, int k,
 // *dst = *src by one thread at the chain's wave priority (a 4-byte hipMemcpyAsync beside the
 // traversal is a blit kernel that waits ~0.5 ms for a wave slot, with the merge rule behind it)
 void copy_u32(uint32_t *dst, const uint32_t *src, hipStream_t s);
+// *dst |= *src | set; *src = 0 (one thread): hands a flag word over to another
+void take_u32(uint32_t *dst, uint32_t *src, hipStream_t s, uint32_t set = 0u);
 // The end-of-call read-back of the merge bookkeeping in one copy: out[0..3] = scal[0..3],
 // out[4..11] = the mailbox header, out[12] = scal[8], out[16 + i] = dlog[i] for i < ahead
 void pack_readback(const uint32_t *scal, const MergePair *box, const uint32_t *dlog, uint32_t ahead,

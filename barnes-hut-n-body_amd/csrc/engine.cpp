@@ -34,6 +34,7 @@
 
 #include "bh_device.hpp"
 #include "bh_engine.h"
+#include "multi.hpp"
 
 using namespace bh;
 
@@ -69,33 +70,14 @@ struct bh_local_group {
     }
 };
 
-// The buffers a locally essential tree build writes (everything but the selection's), once more:
-// a step's first LET build is made speculatively beside the previous evaluation's rounds, which
-// still read the other set (engine.cpp spec_let_build; swap_let_sets exchanges the two).
-struct LetAlt {
-    BodyState sub_dst{};
-    uint64_t *s_keys = nullptr, *s_keys_s = nullptr, *s_spl = nullptr;
-    uint32_t *s_keys32 = nullptr, *s_keys32_s = nullptr, *s_idx = nullptr, *s_perm = nullptr;
-    int8_t *s_cpl = nullptr;
-    uint32_t *s_cnt = nullptr, *s_base = nullptr, *s_cell_start = nullptr;
-    uint32_t *s_span_list = nullptr, *s_super_list = nullptr, *s_bcount = nullptr,
-             *s_bstart = nullptr;
-    bh::SpanSlot *s_span_children = nullptr;
-    Node *s_nodes = nullptr;
-    uint32_t s_spl_nb = 0;
-    int64_t let_sub_cap = 0;
-    int let_J = -1;
-    size_t let_node_cap = 0;
-    hipEvent_t table_ev = nullptr;
-    int64_t set_cap = 0;
-    uint32_t *cstart = nullptr, *w = nullptr, *posc = nullptr, *bsz = nullptr, *csrc = nullptr,
-             *ccnt = nullptr, *cpos = nullptr, *lanes = nullptr, *subpos = nullptr;
-    LetCell *table = nullptr, *tables = nullptr, *levels = nullptr;
-    Node *nodes = nullptr;
-    uint32_t node_cap = 0;
-};
-
 struct bh_engine {
+    bh::Multi *multi = nullptr;  // a multi-device handle (multi.cpp): the members do the work
+    // ... or, for a body list below multi_min bodies, one pipelined single-GPU engine on the first
+    // device (like the reference's min(cores, n) workers, BHA:377): a step of a few 1e5 bodies is
+    // launch-bound, and splitting it only adds launches and exchanges
+    bh_engine *one = nullptr;
+    bool use_one = false;
+    int64_t multi_min = 0;
     bh_params p{};
     Geometry geo{};
     int device = 0;
@@ -234,24 +216,16 @@ struct bh_engine {
     bh::SpanSlot *s_span_children = nullptr;
     Node *s_nodes = nullptr;
     hipEvent_t table_ev = nullptr;
-    int64_t set_cap = 0;        // n capacity of this set's per-body arrays (L.lanes, L.subpos)
-    LetAlt la{};                // the other set (the speculative build's)
-    // the LET pipeline: step s+1's first build made beside step s's second evaluation
-    bool spec_allowed = false;  // set by step_once: the running evaluation is not the call's last
-    bool spec_ready = false;    // la holds the next evaluation's tree (spec_ev on spec_stream)
-    int64_t spec_n_sub = 0;
-    hipStream_t spec_stream = nullptr;
-    hipEvent_t spec_src_ev = nullptr, spec_ev = nullptr, spec_tab_ev = nullptr,
-               spec_flag_ev = nullptr, sub_cnt_ev = nullptr;
-    uint32_t *spec_flag_h = nullptr;  // pinned: the crossing flag of the last LET build
+    int64_t set_cap = 0;        // n capacity of the per-body arrays L.lanes, L.subpos
+    hipEvent_t sub_cnt_ev = nullptr;
     uint32_t *sub_cnt_h = nullptr;    // pinned: the last selection's subset size (sub_cnt_ev)
     bool sub_cnt_pending = false;
 
-    bool let_spec = false;             // BH_LET_SPEC=1: the LET pipeline (evaluate_let)
     LetCell *pub_table = nullptr;     // in-process group: the table this member exchanges now
     hipEvent_t pub_table_ev = nullptr;
-    int64_t spec_builds = 0, spec_fallbacks = 0;
     bool inject_guard = false;  // bh_debug_inject(1): the next LET build trips k_let_guard
+    int inject_build = -1;      // bh_debug_inject(2 + k): the k-th next full build raises its
+                                // jitter flag (as the unsupported-geometry guard would)
     bool agree_failed = false;  // in-process group: this member could not read a peer's flags
     // pipelined step (one GPU): the next step's first build runs on pipe_stream while this step's
     // second traversal runs; it builds into nodes_alt / alt, and the traversal reads copies of
@@ -262,6 +236,9 @@ struct bh_engine {
     uint32_t *cidx_trav = nullptr, *lanes_trav = nullptr, *T_trav = nullptr;
     int64_t trav_cap = 0;
     bool prebuilt = false;  // the current step's first build was made by the previous step
+    // ... by the previous call's last step: that build's error flags are in scalars[10] (they
+    // belong to the step that uses the tree, the next call's first, which takes them over)
+    bool carried_flags = false;
     // deep pipeline: the previous step also evaluated a(t) on that tree (beside its own second
     // traversal), by lane of the current map, with these force parameters
     bool forces_ready = false;
@@ -338,6 +315,11 @@ struct bh_engine {
     std::vector<double> trav_samples;  // per-launch traversal times of the last call (ms)
     bool timings_pending = false;
 
+    // the collectives this rank issued, in host issue order (bh_collective_log): every rank of a
+    // decomposition must issue the same sequence, or RCCL pairs mismatched calls and hangs
+    std::vector<int64_t> coll_log;  // (api call, site, bytes, stream) per collective
+    int64_t api_calls = 0;          // state-changing API calls made on this engine
+
     std::string err;
 };
 
@@ -366,6 +348,23 @@ namespace {
         int _rc = (expr);              \
         if (_rc != BH_OK) return _rc;  \
     } while (0)
+
+// One collective of a multi-rank engine (RCCL call, or its in-process copies): logged so that
+// tests can check that every rank issues the same sequence (bh_collective_log).
+enum CollSite {
+    COLL_ACC = 1,       // a round of accelerations (full evaluation), in-place all-gather
+    COLL_POS = 2,       // a round of new positions (LET evaluation)
+    COLL_VEL = 3,       // a round of owners' velocities (before a full build, at a call's end)
+    COLL_TABLE = 4,     // the LET cell tables
+    COLL_FLAGS = 5,     // the end-of-call LET status words, max all-reduce
+    COLL_SETTINGS = 6,  // the per-process settings check at creation (min and max all-reduce)
+};
+enum CollStream { CS_MAIN = 0, CS_COMM = 1 };
+void coll_log(bh_engine *e, int site, int64_t bytes, int stream) {
+    if (e->world <= 1 && !e->comm) return;
+    if (e->coll_log.size() >= ((size_t)1 << 22)) return;  // (bounded: 1 M entries)
+    e->coll_log.insert(e->coll_log.end(), {e->api_calls, (int64_t)site, bytes, (int64_t)stream});
+}
 
 // Root cell (BHA:360-361) and the exact per-depth half-sizes (BHA:74).
 int make_geometry(const bh_params &p, Geometry &g, std::string &err) {
@@ -604,7 +603,9 @@ int collect_timings(bh_engine *e) {
 // alt with its own permutation (perm2; the traversal reads perm), velocities left to
 // permute_velocities.  keep_v: the velocities stay in the previous slot order (in alt after the
 // swap) for a traversal that permutes them as it kicks (KickArgs::perm).
-int build_into(bh_engine *e, hipStream_t s, bool overlap, bool keep_v = false) {
+// carry: a call's last overlapped build, whose tree the next call uses -- its error flags go to
+// scalars[10] instead of the running call's scalars[1] (evaluate / bh_get_quads take them over)
+int build_into(bh_engine *e, hipStream_t s, bool overlap, bool keep_v = false, bool carry = false) {
     const int64_t n = e->n;
     TreeBuffers tb = tree_buffers(e);
     if (overlap) {
@@ -612,6 +613,7 @@ int build_into(bh_engine *e, hipStream_t s, bool overlap, bool keep_v = false) {
         tb.nodes = e->nodes_alt;
         tb.perm = e->perm2;
     }
+    if (carry) tb.scalars = e->scalars + 9;  // (the build writes scalars[1] of its buffers)
     if (keep_v) tb.src.vx = tb.src.vy = nullptr;
     // Hilbert waves (every rank alike): re-sorted every BH_LANE_REFRESH builds, carried through
     // the build's permutation by k_emit_com in between
@@ -627,6 +629,10 @@ int build_into(bh_engine *e, hipStream_t s, bool overlap, bool keep_v = false) {
     e->keys_ready = false;
     if (!overlap) e->mir_fresh = false;  // the jitter may move bodies
     HIPCHK(e, tree_build(tb, n, e->geo, s));
+    if (e->inject_build >= 0 && e->inject_build-- == 0) {  // bh_debug_inject(2 + k)
+        take_u32(tb.scalars + 1, e->scalars + 11, s, 1u);
+        HIPCHK(e, hipGetLastError());
+    }
     ++e->full_builds;
     e->inv_valid = false;  // the map follows this build's permutation
     if (use_lanes) {
@@ -678,6 +684,23 @@ int ensure_direct(bh_engine *e) {
     e->leaf_tmp_bytes = tb;
     e->leaf_node_cap = e->node_cap;
     e->leaf_cap = e->cap;
+    return BH_OK;
+}
+
+// The previous call's carried tree is used now: its build's error flags become this call's.
+int take_carried_flags(bh_engine *e) {
+    if (!e->carried_flags) return BH_OK;
+    e->carried_flags = false;
+    take_u32(e->scalars + 1, e->scalars + 10, e->stream);
+    HIPCHK(e, hipGetLastError());
+    return BH_OK;
+}
+
+// ... or it is dropped unused (resetBodies, a root-cell change, a replay).
+int drop_carried_flags(bh_engine *e) {
+    if (!e->carried_flags) return BH_OK;
+    e->carried_flags = false;
+    HIPCHK(e, hipMemsetAsync(e->scalars + 10, 0, sizeof(uint32_t), e->stream));
     return BH_OK;
 }
 
@@ -783,50 +806,6 @@ int let_alloc(bh_engine *e, int64_t n_sub, hipStream_t s = nullptr) {
     return BH_OK;
 }
 
-// Exchange the current LET build's buffers with the other set (LetAlt).
-void swap_let_sets(bh_engine *e) {
-    LetAlt &a = e->la;
-    LetBufs &L = e->L;
-    std::swap(e->sub_dst, a.sub_dst);
-    std::swap(e->s_keys, a.s_keys);
-    std::swap(e->s_keys_s, a.s_keys_s);
-    std::swap(e->s_spl, a.s_spl);
-    std::swap(e->s_keys32, a.s_keys32);
-    std::swap(e->s_keys32_s, a.s_keys32_s);
-    std::swap(e->s_idx, a.s_idx);
-    std::swap(e->s_perm, a.s_perm);
-    std::swap(e->s_cpl, a.s_cpl);
-    std::swap(e->s_cnt, a.s_cnt);
-    std::swap(e->s_base, a.s_base);
-    std::swap(e->s_cell_start, a.s_cell_start);
-    std::swap(e->s_span_list, a.s_span_list);
-    std::swap(e->s_super_list, a.s_super_list);
-    std::swap(e->s_bcount, a.s_bcount);
-    std::swap(e->s_bstart, a.s_bstart);
-    std::swap(e->s_span_children, a.s_span_children);
-    std::swap(e->s_nodes, a.s_nodes);
-    std::swap(e->s_spl_nb, a.s_spl_nb);
-    std::swap(e->let_sub_cap, a.let_sub_cap);
-    std::swap(e->let_J, a.let_J);
-    std::swap(e->let_node_cap, a.let_node_cap);
-    std::swap(e->table_ev, a.table_ev);
-    std::swap(e->set_cap, a.set_cap);
-    std::swap(L.cstart, a.cstart);
-    std::swap(L.w, a.w);
-    std::swap(L.posc, a.posc);
-    std::swap(L.bsz, a.bsz);
-    std::swap(L.csrc, a.csrc);
-    std::swap(L.ccnt, a.ccnt);
-    std::swap(L.cpos, a.cpos);
-    std::swap(L.lanes, a.lanes);
-    std::swap(L.subpos, a.subpos);
-    std::swap(L.table, a.table);
-    std::swap(L.tables, a.tables);
-    std::swap(L.levels, a.levels);
-    std::swap(L.nodes, a.nodes);
-    std::swap(L.node_cap, a.node_cap);
-}
-
 TreeBuffers let_tree_buffers(bh_engine *e) {
     TreeBuffers b;
     b.src = e->sub_src;
@@ -888,10 +867,11 @@ bool solo_xchg_on() {
     return on;
 }
 
-int gather_round(bh_engine *e, const GatherLayout &gl, int k, int W, int ev_round) {
+int gather_round(bh_engine *e, const GatherLayout &gl, int k, int W, int ev_round, int site) {
     const int64_t size = gl.off[k + 1] - gl.off[k];
     double *piece = e->a2 + W * (int64_t)e->world * gl.off[k];  // round k, rank 0
     if (size <= 0) return BH_OK;
+    coll_log(e, site, (int64_t)sizeof(double) * W * size * e->world, CS_COMM);
     if (e->comm) {
         NCCLCHK(e, ncclAllGather(piece + W * e->rank * size, piece, (size_t)(W * size),
                                  ncclDouble, e->comm, e->comm_stream));
@@ -960,7 +940,7 @@ int sync_velocities(bh_engine *e) {
     HIPCHK(e, hipEventRecord(e->round_ev[0], e->stream));
     HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[0], 0));
     if (e->group) e->group->barrier();
-    for (int k = 0; k < R; ++k) TRY(gather_round(e, gl, k, 2, k == 0 ? 0 : -1));
+    for (int k = 0; k < R; ++k) TRY(gather_round(e, gl, k, 2, k == 0 ? 0 : -1, COLL_VEL));
     HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
     HIPCHK(e, hipStreamWaitEvent(e->stream, e->gathered_ev, 0));
     let_unpack_vel(n, lanes, e->a2, gl, e->st.vx, e->st.vy, e->stream);
@@ -976,42 +956,14 @@ int sync_velocities(bh_engine *e) {
 int wave_order_for(bh_engine *e, int slot, int64_t lanes, hipStream_t s, WaveOrder &wo);
 int wave_order_next(bh_engine *e, int slot, int64_t lanes, hipStream_t s);
 
-// The LET pipeline (a step's first build beside the previous evaluation's rounds) is switched on
-// by BH_LET_SPEC=1 (e->let_spec): on one rank's share alone it measured no faster than building
-// in line (round 4: 3.46-3.51 against 3.41-3.43 ms per solo C4 / 8 step), the speculative build
-// taking wave slots from the rounds; an 8-GPU run, whose rounds wait on xGMI, may differ.
-#ifndef BH_SPEC_HIPRIO
-#define BH_SPEC_HIPRIO 1  // the speculative build's stream at the highest priority
-#endif
-int spec_events(bh_engine *e) {
-    if (e->spec_stream) return BH_OK;
-    int lo = 0, hi = 0;
-    HIPCHK(e, hipDeviceGetStreamPriorityRange(&lo, &hi));
-    HIPCHK(e, hipStreamCreateWithPriority(&e->spec_stream, hipStreamNonBlocking,
-                                          BH_SPEC_HIPRIO ? hi : lo));
-    for (hipEvent_t *ev : {&e->spec_src_ev, &e->spec_ev, &e->spec_tab_ev, &e->spec_flag_ev})
-        HIPCHK(e, hipEventCreateWithFlags(ev, hipEventDisableTiming));
-    HIPCHK(e, hipHostMalloc((void **)&e->spec_flag_h, 64, hipHostMallocDefault));
-    return BH_OK;
-}
-
-// Every rank's LET cell table into L.tables, on stream s.  RCCL: one all-gather -- on the engine's
-// stream for the evaluation's own build, on the comm stream behind the rounds' gathers already
-// queued there for the speculative one (collectives keep one order on every rank).  In-process
-// group: each member publishes its table and event, then copies every member's.
-int exchange_tables(bh_engine *e, hipStream_t s, bool spec) {
+// Every rank's LET cell table into L.tables, on stream s.  RCCL: one all-gather on the engine's
+// stream.  In-process group: each member publishes its table and event, then copies every
+// member's.
+int exchange_tables(bh_engine *e, hipStream_t s) {
     const size_t tbytes = sizeof(LetCell) * (size_t)LET_TSTRIDE;
+    coll_log(e, COLL_TABLE, (int64_t)(tbytes * (size_t)e->world), CS_MAIN);
     if (e->comm) {
-        if (!spec) {
-            NCCLCHK(e, ncclAllGather(e->L.table, e->L.tables, tbytes, ncclUint8, e->comm, s));
-        } else {
-            HIPCHK(e, hipEventRecord(e->spec_tab_ev, s));
-            HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->spec_tab_ev, 0));
-            NCCLCHK(e, ncclAllGather(e->L.table, e->L.tables, tbytes, ncclUint8, e->comm,
-                                     e->comm_stream));
-            HIPCHK(e, hipEventRecord(e->spec_tab_ev, e->comm_stream));
-            HIPCHK(e, hipStreamWaitEvent(s, e->spec_tab_ev, 0));
-        }
+        NCCLCHK(e, ncclAllGather(e->L.table, e->L.tables, tbytes, ncclUint8, e->comm, s));
     } else if (e->solo) {  // own values first, the rest from the last full build
         HIPCHK(e, hipMemcpyAsync(e->L.tables, e->L.table, tbytes, hipMemcpyDeviceToDevice, s));
         if (e->world > 1 && e->solo_table)
@@ -1034,107 +986,6 @@ int exchange_tables(bh_engine *e, hipStream_t s, bool spec) {
     return BH_OK;
 }
 
-// The next evaluation's LET build, made now on spec_stream beside this evaluation's rounds: the
-// same subset (no body changed cells: checked), with the positions this evaluation's build left
-// (sub_dst, its jitter applied), built into the other buffer set; the next evaluation takes it
-// over (evaluate_let, spec_ready) instead of selecting and building.
-int spec_let_build(bh_engine *e, int64_t n_sub, const LetPieces &pc) {
-    hipStream_t ss = e->spec_stream;
-    HIPCHK(e, hipStreamWaitEvent(ss, e->spec_src_ev, 0));
-    const BodyState src = e->sub_dst;  // this evaluation's subset, as its build left it
-    swap_let_sets(e);
-    int rc = let_alloc(e, n_sub, ss);
-    if (rc == BH_OK) {
-        TreeBuffers sb = let_tree_buffers(e);
-        sb.src = src;
-        sb.src.vy = nullptr;
-        sb.keys_ready = false;
-        hipError_t hr = tree_build(sb, n_sub, e->geo, ss);
-        if (hr == hipSuccess) {
-            e->s_spl_nb = sort_buckets(n_sub);
-            hr = hipMemsetAsync(e->L.table + LET_CELLS, 0, sizeof(LetCell), ss);  // status: none
-        }
-        if (hr == hipSuccess) hr = let_table(n_sub, e->geo, e->L, sb, ss);
-        if (hr != hipSuccess) {
-            e->err = std::string("spec_let_build: ") + hipGetErrorString(hr);
-            rc = BH_E_DEVICE;
-        }
-        if (rc == BH_OK) rc = exchange_tables(e, ss, true);
-        if (rc == BH_OK) {
-            hr = let_assemble(n_sub, e->geo, pc, e->L, sb, e->scalars, ss);
-            if (hr == hipSuccess) hr = hipEventRecord(e->spec_ev, ss);
-            if (hr != hipSuccess) {
-                e->err = std::string("spec_let_build: ") + hipGetErrorString(hr);
-                rc = BH_E_DEVICE;
-            }
-        }
-    }
-    swap_let_sets(e);  // the current set stays this evaluation's until the next one takes over
-    if (rc != BH_OK) return rc;
-    e->spec_ready = true;
-    e->spec_n_sub = n_sub;
-    return BH_OK;
-}
-
-// BH_SPEC_CHECK=1 (diagnostic): a speculative build is not taken over; the evaluation selects and
-// builds as usual and the two trees are compared on the host (mismatch counts on stderr).
-bool spec_check_on() {
-    static const bool on = [] {
-        const char *v = std::getenv("BH_SPEC_CHECK");
-        return v && std::strcmp(v, "0") != 0;
-    }();
-    return on;
-}
-
-template <typename T>
-int64_t count_diff(bh_engine *e, const T *a, const T *b, int64_t n, int64_t *first) {
-    std::vector<T> ha((size_t)n), hb((size_t)n);
-    *first = -1;
-    if (n <= 0) return 0;
-    if (hipMemcpy(ha.data(), a, sizeof(T) * n, hipMemcpyDeviceToHost) != hipSuccess ||
-        hipMemcpy(hb.data(), b, sizeof(T) * n, hipMemcpyDeviceToHost) != hipSuccess)
-        return -1;
-    int64_t d = 0;
-    for (int64_t i = 0; i < n; ++i)
-        if (std::memcmp(&ha[i], &hb[i], sizeof(T)) != 0) {
-            if (*first < 0) *first = i;
-            ++d;
-        }
-    (void)e;
-    return d;
-}
-
-int spec_compare(bh_engine *e, int64_t n_sub, const LetPieces &pc) {
-    HIPCHK(e, hipStreamSynchronize(e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->spec_stream));
-    const LetAlt &a = e->la;
-    uint32_t cnt[2] = {0, 0};
-    HIPCHK(e, hipMemcpy(cnt, e->L.posc + LET_CELLS, 4, hipMemcpyDeviceToHost));
-    HIPCHK(e, hipMemcpy(cnt + 1, a.posc + LET_CELLS, 4, hipMemcpyDeviceToHost));
-    int64_t f[8];
-    const int64_t nn = std::min<int64_t>(cnt[0], cnt[1]);
-    const int64_t m = std::min<int64_t>(n_sub, e->spec_n_sub);
-    const int64_t dn = count_diff(e, e->L.nodes, a.nodes, nn, f + 0);
-    const int64_t dx = count_diff(e, e->sub_dst.x, a.sub_dst.x, m, f + 1);
-    const int64_t dy = count_diff(e, e->sub_dst.y, a.sub_dst.y, m, f + 2);
-    const int64_t dm = count_diff(e, e->sub_dst.m, a.sub_dst.m, m, f + 3);
-    const int64_t dc = count_diff(e, e->sub_dst.cidx, a.sub_dst.cidx, m, f + 4);
-    const int64_t dv = count_diff(e, e->sub_dst.vx, a.sub_dst.vx, m, f + 5);
-    const int64_t lo = (int64_t)pc.rank * pc.rounds * pc.sub;
-    const int64_t nl = std::max<int64_t>(0, std::min<int64_t>(pc.n, lo + (int64_t)pc.rounds * pc.sub) - lo);
-    const int64_t dl = count_diff(e, e->L.lanes + lo, a.lanes + lo, nl, f + 6);
-    const int64_t dt = count_diff(e, e->L.tables, a.tables, (int64_t)e->world * LET_TSTRIDE, f + 7);
-    std::fprintf(stderr,
-                 "SPEC_CHECK rank %d: n_sub %lld/%lld nodes %u/%u diff nodes %lld@%lld x %lld@%lld "
-                 "y %lld@%lld m %lld@%lld cidx %lld@%lld vx %lld@%lld lanes %lld@%lld tables "
-                 "%lld@%lld\n",
-                 e->rank, (long long)n_sub, (long long)e->spec_n_sub, cnt[0], cnt[1], (long long)dn,
-                 (long long)f[0], (long long)dx, (long long)f[1], (long long)dy, (long long)f[2],
-                 (long long)dm, (long long)f[3], (long long)dc, (long long)f[4], (long long)dv,
-                 (long long)f[5], (long long)dl, (long long)f[6], (long long)dt, (long long)f[7]);
-    return BH_OK;
-}
-
 int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     *done = false;
     if (kick != KICK_DRIFT && kick != KICK_ONLY) return BH_OK;
@@ -1154,31 +1005,7 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
             if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->gathered_ev, 0));
     }
     int64_t n_sub = 0;
-    bool spec_used = false, spec_check = false;
-    if (e->spec_ready) {
-        e->spec_ready = false;
-        if (kick == KICK_DRIFT && e->spec_n_sub > 0 && spec_check_on()) {
-            HIPCHK(e, hipStreamWaitEvent(e->stream, e->spec_ev, 0));
-            spec_check = true;  // select and build as usual, then compare the two trees
-        } else if (kick == KICK_DRIFT && e->spec_n_sub > 0) {
-            // this tree was built beside the previous evaluation's rounds (spec_let_build)
-            HIPCHK(e, hipStreamWaitEvent(e->stream, e->spec_ev, 0));
-            swap_let_sets(e);
-            n_sub = e->spec_n_sub;
-            ++e->let_builds;
-            ++e->spec_builds;
-            spec_used = true;
-        }
-    }
-    // may the next evaluation's first build be made speculatively beside this one's rounds?  Only
-    // where nothing but this build's jitter moves a body in between: the second evaluation of a
-    // step that is not the call's last, no merge rule that can act (BHA:438), the next build a
-    // LET build too.  Whether the jitter moved a body across a depth-8 cell is known after the
-    // table exchange (every rank alike).
-    const bool spec_want = e->let_spec && !spec_used && kick == KICK_ONLY && e->spec_allowed &&
-                           (e->p.merge_min_dist <= 0.0 || !e->heavy_possible) &&
-                           e->let_age + 1 < BH_LET_REFRESH;
-    if (!spec_used) {
+    {
         TRY(let_alloc(e, 0));
         // subset capacity: the largest subset of the previous call + headroom, no host round trip;
         // a subset beyond it is an overflow every rank sees after the exchange, and bh_step replays
@@ -1188,7 +1015,6 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         // (a contracting cloud's subsets grow by more than the headroom over a 100-step call:
         // round 4 saw one replay of the C4 / 8 call).  Never waited for: a blocking wait here cost
         // 0.2 ms per solo C4 / 8 step (3.67 against 3.43-3.53 ms).
-        if (e->let_spec) TRY(spec_events(e));  // (its stream made before the round streams)
         if (e->let_known > 0 && e->sub_cnt_pending && hipEventQuery(e->sub_cnt_ev) == hipSuccess) {
             e->sub_cnt_pending = false;
             e->let_known = std::max<int64_t>(e->let_known, *e->sub_cnt_h);
@@ -1241,27 +1067,17 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         sb.keys_ready = fuse && e->s_spl_nb > 0;  // (let_alloc above kept the buffers: S fitted)
         HIPCHK(e, tree_build(sb, n_sub, e->geo, e->stream));
         e->s_spl_nb = sort_buckets(n_sub);  // k_prep wrote this build's splitters
-        if (spec_want) TRY(spec_events(e));
-        HIPCHK(e, let_table(n_sub, e->geo, e->L, sb, e->stream, spec_want));
-        TRY(exchange_tables(e, e->stream, false));
+        HIPCHK(e, let_table(n_sub, e->geo, e->L, sb, e->stream));
+        TRY(exchange_tables(e, e->stream));
         {
             // bh_debug_inject: a node array of one record makes k_let_guard fire on this rank only,
             // exactly as a broken invariant would (empty tree, idle lanes, replay flag set)
             const uint32_t node_cap = e->L.node_cap;
             if (e->inject_guard) e->L.node_cap = 1u;
             e->inject_guard = false;
-            const hipError_t rc = let_assemble(n_sub, e->geo, pc, e->L, sb, e->scalars, e->stream,
-                                               spec_want ? e->scalars + 10 : nullptr);
+            const hipError_t rc = let_assemble(n_sub, e->geo, pc, e->L, sb, e->scalars, e->stream);
             e->L.node_cap = node_cap;
             HIPCHK(e, rc);
-        }
-        if (spec_check) TRY(spec_compare(e, n_sub, pc));
-        if (spec_want) {  // the crossing flag, read while the rounds below run
-            HIPCHK(e, hipMemcpyAsync(e->spec_flag_h, e->scalars + 10, sizeof(uint32_t),
-                                     hipMemcpyDeviceToHost, e->stream));
-            HIPCHK(e, hipEventRecord(e->spec_flag_ev, e->stream));
-            // sub_dst is final, and the assembly's scans are done with the shared scratch
-            HIPCHK(e, hipEventRecord(e->spec_src_ev, e->stream));
         }
     }
     TRY(mark(e, 0));
@@ -1289,12 +1105,7 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         HIPCHK(e, hipEventRecord(e->round_ev[k], rs));
         HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
         if (e->group) e->group->barrier();
-        TRY(gather_round(e, gl, k, W, k));
-    }
-    if (spec_want) {
-        HIPCHK(e, hipEventSynchronize(e->spec_flag_ev));
-        if (*e->spec_flag_h == 0u) TRY(spec_let_build(e, n_sub, pc));
-        else ++e->spec_fallbacks;  // a body changed cells: the next evaluation selects anew
+        TRY(gather_round(e, gl, k, W, k, COLL_POS));
     }
     TRY(mark(e, 1));
     HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
@@ -1362,11 +1173,11 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
         }
     }
     e->let_age = 0;
-    e->spec_ready = false;  // (a speculative LET build is only ever taken by a LET evaluation)
     const int64_t n = e->n;
     bool have_forces = false;  // a(t) on this tree, evaluated ahead by the previous step
     if (e->prebuilt) {  // the pipelined step built this tree (single GPU: nothing deferred)
         e->prebuilt = false;
+        TRY(take_carried_flags(e));
         e->view_pending = false;  // its jitter is now part of the state (BHA:146-151)
         e->mir_fresh = false;
         have_forces = e->forces_ready;
@@ -1457,7 +1268,7 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
         HIPCHK(e, hipEventRecord(e->round_ev[k], rs));
         HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
         if (e->group) e->group->barrier();  // every member recorded round k
-        TRY(gather_round(e, gl, k, 2, k));
+        TRY(gather_round(e, gl, k, 2, k, COLL_ACC));
     }
     TRY(mark(e, 1));
     HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
@@ -1677,11 +1488,11 @@ int snapshot(bh_engine *e) {
 int restore(bh_engine *e) {
     TRY(copy_state(e, e->snap, e->st, e->snap_n));
     e->n = e->snap_n;
+    TRY(drop_carried_flags(e));
     e->prebuilt = false;
     e->view_pending = false;
     e->lt_aside = false;
     e->mir_fresh = false;
-    e->spec_ready = false;
     e->spl_nb = 0;  // the splitters describe the discarded builds' order
     e->keys_ready = false;
     e->lanes_valid = e->lr_pending = e->lr_ready = false;
@@ -1700,6 +1511,7 @@ int restore(bh_engine *e) {
 int agree_let_flags(bh_engine *e, uint32_t ls[2], uint32_t *own_sub) {
     HIPCHK(e, hipMemcpy(ls, e->scalars + 4, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
     *own_sub = ls[1];
+    if (!e->solo) coll_log(e, COLL_FLAGS, 2 * sizeof(uint32_t), CS_MAIN);
     if (e->comm) {
         NCCLCHK(e, ncclAllReduce(e->scalars + 4, e->scalars + 4, 2, ncclUint32, ncclMax, e->comm,
                                  e->stream));
@@ -1767,9 +1579,11 @@ bool pipelined(const bh_engine *e, bool last) {
 }
 
 // The overlap and mirror streams of a one-GPU engine.  HIP hands a process's streams its few
-// hardware queues in creation order, so bh_create makes them right after the engine's own stream:
-// made lazily, after another engine's streams (bench.py's counter probe), the mirror's copies
-// shared a queue with the step's kernels (C3 one-step calls with the mirror: 3.25 -> 2.3 ms).
+// hardware queues (GPU_MAX_HW_QUEUES = 4) in creation order, so bh_create makes the overlap
+// stream right after the engine's own, and a caller that reads the mirror enables it right after
+// bh_create: made later, after another engine's streams (bench.py's counter probe), the mirror's
+// copies shared a queue with the step's kernels (C3 one-step calls with the mirror: 3.25 -> 2.3
+// ms).  An engine that never enables the mirror holds two queues, not three.
 int pipe_streams(bh_engine *e) {
     for (hipEvent_t &ev : e->pipe_ev)
         if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
@@ -1990,7 +1804,7 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     if (!early) TRY(merge(e, e->pipe_stream, merging));  // BHA:438
     if (early) TRY(mirror_vel(e, e->st, s));  // the velocities once the kick is done
     e->lane_defer = !last;  // (a call ends with a compaction: its last build re-sorts in place)
-    const int rc_b1 = build_into(e, e->pipe_stream, true);  // step s+1's first tree (BHA:359)
+    const int rc_b1 = build_into(e, e->pipe_stream, true, false, last);  // step s+1's first tree (BHA:359)
     e->lane_defer = false;
     TRY(rc_b1);
     if (BH_DEEP_PIPE) {
@@ -2012,6 +1826,7 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     std::swap(e->nodes, e->nodes_alt);
     std::swap(e->node_cap, e->nodes_alt_cap);
     e->prebuilt = true;
+    e->carried_flags = last;
     e->forces_ready = BH_DEEP_PIPE != 0;
     e->fp_ready = fp;
     if (last) {  // the previous order's state (kicked, merged, not yet jittered) is what the caller sees
@@ -2114,10 +1929,7 @@ int step_once(bh_engine *e, bool last) {
         const bool lazy = last && BH_LAZY_LASTTREE && (e->comm || e->group || e->solo);
         if (lazy) TRY(snapshot_positions(e));
         bool let2 = false;
-        e->spec_allowed = !last;  // the next step's first build may be made beside this evaluation
-        const int rc2 = evaluate(e, nullptr, KICK_ONLY, &fused, !last || lazy, &let2);  // a(t+dt)
-        e->spec_allowed = false;
-        TRY(rc2);
+        TRY(evaluate(e, nullptr, KICK_ONLY, &fused, !last || lazy, &let2));  // a(t+dt)
         if (!fused) {
             TRY(mark(e, -1));
             kick(n, e->a2, e->st.vx, e->st.vy, dtHalf, e->stream, e->a2_lanes, e->a2_layout);
@@ -2218,7 +2030,6 @@ int engine_init(bh_engine *e, const bh_params *p, int device) {
     e->p = *p;
     TRY(make_geometry(e->p, e->geo, e->err));
     e->device = device;
-    if (const char *v = std::getenv("BH_LET_SPEC")) e->let_spec = std::strcmp(v, "0") != 0;
     if (const char *v = std::getenv("BH_LET")) {
         e->let_on = std::strcmp(v, "0") != 0;
         e->let_forced = std::strcmp(v, "1") == 0;
@@ -2305,6 +2116,7 @@ static int agree_settings(bh_engine *e) {
     // happened locally, so a local failure cannot leave the peers waiting in a collective
     double *d = static_cast<double *>(e->scratch);
     double lo[K], hi[K];
+    coll_log(e, COLL_SETTINGS, (int64_t)sizeof(double) * 2 * K, CS_MAIN);
     ncclResult_t nr = ncclSuccess;
     if (!d || e->scratch_bytes < sizeof(double) * 3 * K) {
         e->err = "agree_settings: no device scratch";
@@ -2337,6 +2149,163 @@ static int agree_settings(bh_engine *e) {
     return BH_OK;
 }
 
+// ---- the multi-device handle's pieces (multi.hpp) -----------------------------------------
+#ifndef BH_MULTI_MIN_BODIES
+// body lists below this run on one GPU behind a multi-device handle.  A LET evaluation costs ~40
+// launches of >= 4.5 us per build (two per step) plus 8 round launches and the exchanges
+// whatever the size, ~0.6 ms per step; one GPU steps 1e5 bodies in 0.55 ms and 1e6 in 1.8 ms,
+// so the split pays from a few 1e5 bodies on (an estimate: no multi-GPU box was available).
+#define BH_MULTI_MIN_BODIES 400000
+#endif
+int bh::facade_create(const bh_params *p, bh::Multi *mu, bh_engine **out) {
+    bh_engine *f = new bh_engine();
+    f->p = *p;
+    if (make_geometry(f->p, f->geo, f->err) != BH_OK) {
+        delete f;
+        return BH_E_INVALID;
+    }
+    f->multi = mu;
+    f->world = multi_world(mu);
+    f->multi_min = 0;
+    if (const char *v = std::getenv("BH_MULTI_MIN_BODIES")) f->multi_min = std::atoll(v);
+    else f->multi_min = BH_MULTI_MIN_BODIES;
+    *out = f;
+    return BH_OK;
+}
+
+int bh::member_agree(bh_engine *e) {
+    if (!e->comm) return BH_OK;
+    HIPCHK(e, hipSetDevice(e->device));  // (a pool thread: RCCL calls on the member's device)
+    return agree_settings(e);
+}
+
+// (comm: an RCCL communicator made in this process; on failure it stays the caller's)
+int bh::member_create(const bh_params *p, int device, int rank, int world, void *comm,
+                      bh_local_group *group, bh_engine **out) {
+    if (group) return bh_create_local(p, device, rank, group, out);
+    if (!out || !comm || world < 1 || rank < 0 || rank >= world) return BH_E_INVALID;
+    *out = nullptr;
+    bh_engine *e = new bh_engine();
+    e->rank = rank;
+    e->world = world;
+    int rc = engine_init(e, p, device);
+    if (rc == BH_OK) {
+        e->comm = static_cast<ncclComm_t>(comm);
+        hipError_t hr = hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking);
+        for (int k = 0; k < BH_SHARD_ROUNDS && hr == hipSuccess; ++k)
+            hr = hipEventCreateWithFlags(&e->round_ev[k], hipEventDisableTiming);
+        if (hr == hipSuccess) hr = hipEventCreateWithFlags(&e->gathered_ev, hipEventDisableTiming);
+        if (hr != hipSuccess) {
+            e->err = std::string("comm stream/events: ") + hipGetErrorString(hr);
+            rc = BH_E_DEVICE;
+        }
+    }
+    if (rc == BH_OK) {  // the accelerations buffer in rounds x world pieces
+        const int64_t cap = e->cap;
+        e->cap = 0;
+        rc = ensure_capacity(e, cap);
+    }
+    if (rc != BH_OK) {
+        std::fprintf(stderr, "bh_create_multi (rank %d): %s\n", rank, e->err.c_str());
+        e->comm = nullptr;
+        bh_destroy(e);
+        return rc;
+    }
+    *out = e;
+    return BH_OK;
+}
+
+// getTreeForDebug (BHA:329-332): lastTree if the last step kept it, else a fresh tree -- built
+// here, its jitter applied to the state as the reference's buildTree applies it.
+int bh::quads_prepare(bh_engine *e) {
+    HIPCHK(e, hipSetDevice(e->device));
+    const int64_t n = e->n;
+    TRY(materialize_positions(e));
+    if (!e->tree_valid && (e->comm || e->group || e->solo)) {
+        // multi-rank: the tree is built into the workspace from the positions of the call's last
+        // build (the lazy lastTree) or the current ones (getTreeForDebug's fresh tree), and the
+        // state stays as it is -- a rank's slot order and lane map must not change on its own
+        HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
+        if (n > 0) {
+            TreeBuffers tb = tree_buffers(e);
+            if (e->lazy_tree) {
+                tb.src.x = e->lt_x;
+                tb.src.y = e->lt_y;
+            }
+            tb.src.vx = tb.src.vy = nullptr;  // positions, masses and flags are all it reads
+            tb.spl_nb = 0;                    // the caller's splitters describe another order
+            tb.lanes_remap = nullptr;
+            HIPCHK(e, tree_build(tb, n, e->geo, e->stream));
+            if (!e->lazy_tree) {
+                // getTreeForDebug's fresh buildTree moves the bodies it jitters (BHA:146-151,
+                // 329-331): the moved positions go back into the replica in its own slot order
+                // (every rank makes the same calls, so the replicas stay equal)
+                unpermute_positions(n, e->perm, tb.dst.x, tb.dst.y, e->st.x, e->st.y, e->stream);
+                HIPCHK(e, hipGetLastError());
+                e->mir_fresh = false;
+            }
+            e->spl_nb = 0;  // k_prep wrote splitters of this order
+            e->keys_ready = false;
+            TRY(check_tree_flags(e));
+        } else {
+            HIPCHK(e, hipMemsetAsync(e->base, 0, sizeof(uint32_t), e->stream));
+        }
+        e->tree_valid = true;  // until the next step (a second call walks the same tree)
+    } else if (!e->tree_valid && e->view_pending) {
+        // getTreeForDebug's fresh tree (BHA:329-332) is the one the pipelined call already built
+        // from the caller's bodies after its merge rule: its jitter becomes part of the state, and
+        // the next step builds its own first tree from these positions (BHA:407)
+        e->view_pending = false;
+        e->prebuilt = false;
+        e->mir_fresh = false;
+        e->tree_valid = true;
+        HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
+        TRY(take_carried_flags(e));
+        if (n > 0) TRY(check_tree_flags(e));
+    } else if (!e->tree_valid) {  // getTreeForDebug builds a fresh tree (BHA:329-332)
+        HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
+        TRY(build(e));
+        if (n > 0) TRY(check_tree_flags(e));
+    }
+    return BH_OK;
+}
+
+// A multi-device handle's calls: on the engine that holds the bodies -- every member, or the
+// single-GPU engine of a small body list -- and, for the settings (params, profiling, mirror),
+// on both, so that either is current when a reset switches between them.
+namespace {
+int multi_fan(bh_engine *e, const std::function<int(bh_engine *, int)> &fn, bool both) {
+    int rc = BH_OK;
+    if (e->use_one) {
+        rc = fn(e->one, 0);
+        if (rc != BH_OK) e->err = bh_last_error(e->one);
+    }
+    if (!e->use_one || both) {
+        const int r2 = multi_all(e->multi, e, fn);
+        if (rc == BH_OK) rc = r2;
+    }
+    if (both && !e->use_one && e->one && rc == BH_OK) {
+        rc = fn(e->one, 0);
+        if (rc != BH_OK) e->err = bh_last_error(e->one);
+    }
+    return rc;
+}
+bh_engine *multi_active0(const bh_engine *e) { return e->use_one ? e->one : multi_member(e->multi, 0); }
+}  // namespace
+#define MULTI_FAN(e, both, call)                                                        \
+    do {                                                                                \
+        if ((e)->multi)                                                                 \
+            return multi_fan((e), [&](bh_engine *m_, int r_) {                          \
+                (void)r_;                                                               \
+                return call;                                                            \
+            }, both);                                                                   \
+    } while (0)
+#define MULTI_ALL(e, call) MULTI_FAN(e, false, call)
+#define MULTI_BOTH(e, call) MULTI_FAN(e, true, call)
+// the calls that only read the state: the active engine's member 0 (every replica is complete at
+// the API boundary)
+#define MULTI_M0(e) ((e)->multi ? multi_active0(e) : (e))
+
 // =========================================================================================
 extern "C" {
 
@@ -2349,8 +2318,10 @@ int bh_create(const bh_params *p, int device, bh_engine **out) {
     *out = nullptr;
     bh_engine *e = new bh_engine();
     int rc = engine_init(e, p, device);
+    // the overlap stream right after the engine's own (HIP hands a process's few hardware queues
+    // out in stream creation order); the mirror's is made by bh_set_mirror, which a caller that
+    // reads the mirror calls right after bh_create (the shims do)
     if (rc == BH_OK) rc = pipe_streams(e);
-    if (rc == BH_OK) rc = mirror_streams(e);
     if (rc != BH_OK) {
         std::fprintf(stderr, "bh_create: %s\n", e->err.c_str());
         bh_destroy(e);
@@ -2492,10 +2463,15 @@ int bh_create_solo(const bh_params *p, int device, int rank, int world, bh_engin
 
 void bh_destroy(bh_engine *e) {
     if (!e) return;
+    if (e->multi) {  // the members, their threads and the exchange; then the handle itself
+        bh_destroy(e->one);
+        multi_destroy(e->multi);
+        delete e;
+        return;
+    }
     (void)hipSetDevice(e->device);
     if (e->stream) (void)hipStreamSynchronize(e->stream);
     if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
-    if (e->spec_stream) (void)hipStreamSynchronize(e->spec_stream);
     if (e->comm) (void)ncclCommDestroy(e->comm);
     if (e->group && e->rank < (int)e->group->members.size() && e->group->members[e->rank] == e)
         e->group->members[e->rank] = nullptr;
@@ -2527,22 +2503,7 @@ void bh_destroy(bh_engine *e) {
     free_state(e->snap);
     free_state(e->sub_src);
     free_state(e->sub_dst);
-    {
-        LetAlt &a = e->la;
-        free_state(a.sub_dst);
-        void *alts[] = {a.s_keys, a.s_keys_s, a.s_spl, a.s_keys32, a.s_keys32_s, a.s_idx,
-                        a.s_perm, a.s_cpl, a.s_cnt, a.s_base, a.s_cell_start, a.s_span_list,
-                        a.s_super_list, a.s_bcount, a.s_bstart, a.s_span_children, a.s_nodes,
-                        a.cstart, a.w, a.posc, a.bsz, a.csrc, a.ccnt, a.cpos, a.lanes, a.subpos,
-                        a.table, a.tables, a.levels, a.nodes};
-        for (void *q : alts)
-            if (q) (void)hipFree(q);
-        if (a.table_ev) (void)hipEventDestroy(a.table_ev);
-    }
-    if (e->spec_stream) (void)hipStreamDestroy(e->spec_stream);
-    for (hipEvent_t ev : {e->spec_src_ev, e->spec_ev, e->spec_tab_ev, e->spec_flag_ev, e->sub_cnt_ev})
-        if (ev) (void)hipEventDestroy(ev);
-    if (e->spec_flag_h) (void)hipHostFree(e->spec_flag_h);
+    if (e->sub_cnt_ev) (void)hipEventDestroy(e->sub_cnt_ev);
     if (e->sub_cnt_h) (void)hipHostFree(e->sub_cnt_h);
     if (e->table_ev) (void)hipEventDestroy(e->table_ev);
     void *lets[] = {e->inv_lanes, e->L.csrc, e->L.ccnt, e->L.cpos, e->solo_table, e->solo_all, e->solo_cstart, e->L.ecell, e->L.hcell, e->L.own, e->L.subpos, e->L.flag_all, e->L.flag8, e->L.sel, e->L.selpos, e->L.cstart,
@@ -2578,6 +2539,11 @@ int bh_set_params(bh_engine *e, const bh_params *p) {
     if (!e || !p) return BH_E_INVALID;
     Geometry g;
     TRY(make_geometry(*p, g, e->err));
+    if (e->multi) {
+        e->p = *p;
+        e->geo = g;
+    }
+    MULTI_BOTH(e, bh_set_params(m_, p));
     HIPCHK(e, hipSetDevice(e->device));
     const bool geo_changed = std::memcmp(&g, &e->geo, sizeof(g)) != 0;
     if (p->merge_max_mass != e->p.merge_max_mass || p->merge_min_dist != e->p.merge_min_dist)
@@ -2592,6 +2558,7 @@ int bh_set_params(bh_engine *e, const bh_params *p) {
             e->view_pending = false;
             e->lanes_valid = e->lr_pending = e->lr_ready = false;
         }
+        TRY(drop_carried_flags(e));
         e->prebuilt = false;
         e->lt_aside = false;
         e->geo = g;
@@ -2611,6 +2578,7 @@ int bh_set_params(bh_engine *e, const bh_params *p) {
 
 int bh_get_params(const bh_engine *e, bh_params *p) {
     if (!e || !p) return BH_E_INVALID;
+    e = MULTI_M0(e);
     *p = e->p;
     return BH_OK;
 }
@@ -2622,8 +2590,27 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
         e->err = "too many bodies";
         return BH_E_INVALID;
     }
+    if (e->multi) {  // resetBodies picks the engine for this body list (BHA:377's min(cores, n))
+        const bool one = n < e->multi_min;
+        if (one && !e->one) {
+            bh_engine *m0 = multi_member(e->multi, 0);
+            bh_engine *o = nullptr;
+            const int rc = bh_create(&m0->p, m0->device, &o);
+            if (rc != BH_OK) {
+                e->err = "the single-GPU engine for a small body list could not be created";
+                return rc;
+            }
+            if (m0->mirror_on) TRY(bh_set_mirror(o, 1));
+            TRY(bh_set_profiling(o, m0->profiling ? 1 : 0));
+            e->one = o;
+        }
+        e->use_one = one;
+    }
+    MULTI_ALL(e, bh_reset_bodies(m_, n, x, y, vx, vy, m));
+    ++e->api_calls;
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipStreamSynchronize(e->stream));
+    TRY(drop_carried_flags(e));
     TRY(ensure_capacity(e, n));
     if (n > 0) {  // slot order = caller order until the first build
         HIPCHK(e, hipMemcpyAsync(e->st.x, x, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));
@@ -2641,7 +2628,6 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     e->tree_valid = false;  // BHA:348
     e->lazy_tree = false;
     e->prebuilt = false;    // other bodies: the pipelined call's next tree is void
-    e->spec_ready = false;
     e->view_pending = false;
     e->lt_aside = false;
     e->mir_fresh = false;
@@ -2657,6 +2643,8 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
 
 int bh_step(bh_engine *e, int32_t k) {
     if (!e || k < 0) return BH_E_INVALID;
+    MULTI_ALL(e, bh_step(m_, k));  // every GPU's share of every step, joined (BHA:374-395, 408)
+    ++e->api_calls;
     HIPCHK(e, hipSetDevice(e->device));
     const bool may_merge = k > 0 && e->n > 1 && e->p.merge_min_dist > 0.0 && e->heavy_possible;
     // a multi-rank call with LET builds may have to be replayed with a larger subset capacity
@@ -2683,7 +2671,6 @@ int bh_step(bh_engine *e, int32_t k) {
         if (k > 0) e->prebuilt = first && carried;
         e->lazy_tree = false;
         e->mir_launched = false;
-        e->spec_ready = false;
         for (int32_t s = 0; s < k; ++s) TRY(step_once(e, s + 1 == k));
         // a copy-out launched by the last pipelined step reads the state the compaction (or a
         // replay's restore) below rewrites
@@ -2759,11 +2746,16 @@ int bh_step(bh_engine *e, int32_t k) {
     return BH_OK;
 }
 
-int64_t bh_num_bodies(const bh_engine *e) { return e ? e->n : -1; }
+int64_t bh_num_bodies(const bh_engine *e) { return e ? MULTI_M0(e)->n : -1; }
 
 int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, double *m,
                   int64_t cap, int64_t *n_out) {
     if (!e) return BH_E_INVALID;
+    if (e->multi) {  // every replica is complete at the API boundary: member 0's
+        const int rc = bh_get_bodies(MULTI_M0(e), x, y, vx, vy, m, cap, n_out);
+        if (rc != BH_OK) e->err = bh_last_error(MULTI_M0(e));
+        return rc;
+    }
     if (n_out) *n_out = e->n;
     if (cap < e->n) return BH_E_CAPACITY;
     HIPCHK(e, hipSetDevice(e->device));
@@ -2787,6 +2779,8 @@ int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, do
 
 int bh_set_mirror(bh_engine *e, int enabled) {
     if (!e) return BH_E_INVALID;
+    // (member 0's replica fills the mirror; the others' bh_set_mirror only reserves its stream)
+    MULTI_BOTH(e, r_ == 0 ? bh_set_mirror(m_, enabled) : BH_OK);
     HIPCHK(e, hipSetDevice(e->device));
     e->mirror_on = enabled != 0;
     if (e->mirror_on) TRY(mirror_alloc(e));
@@ -2796,6 +2790,11 @@ int bh_set_mirror(bh_engine *e, int enabled) {
 int bh_map_bodies(bh_engine *e, const double **x, const double **y, const double **vx,
                   const double **vy, const double **m, int64_t *n_out) {
     if (!e) return BH_E_INVALID;
+    if (e->multi) {
+        const int rc = bh_map_bodies(MULTI_M0(e), x, y, vx, vy, m, n_out);
+        if (rc != BH_OK) e->err = bh_last_error(MULTI_M0(e));
+        return rc;
+    }
     HIPCHK(e, hipSetDevice(e->device));
     if (!e->mir_fresh || e->mir_cap < e->n) {  // not written by the last call: copy out now
         TRY(materialize_positions(e));
@@ -2819,6 +2818,18 @@ int bh_map_bodies(bh_engine *e, const double **x, const double **y, const double
 
 int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visits) {
     if (!e) return BH_E_INVALID;
+    // (every member builds and evaluates -- the build may jitter every replica alike; member 0
+    // hands the results out)
+    if (e->multi) {  // (the visit-counting walk is not sharded: every member counts)
+        std::vector<std::vector<int64_t>> vis((size_t)multi_world(e->multi));
+        const int64_t nb = bh_num_bodies(e);
+        if (visits)
+            for (size_t r = 1; r < vis.size(); ++r) vis[r].resize((size_t)std::max<int64_t>(nb, 1));
+        MULTI_ALL(e, bh_compute_accelerations(m_, r_ == 0 ? ax : nullptr, r_ == 0 ? ay : nullptr,
+                                              !visits ? nullptr
+                                                      : r_ == 0 ? visits : vis[(size_t)r_].data()));
+    }
+    ++e->api_calls;
     HIPCHK(e, hipSetDevice(e->device));
     const int64_t n = e->n;
     e->ev_used = 0;
@@ -2868,52 +2879,16 @@ int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visi
 
 int bh_get_quads(bh_engine *e, double *cx, double *cy, double *h, int64_t cap, int64_t *n_out) {
     if (!e || cap < 0 || (cap > 0 && (!cx || !cy || !h))) return BH_E_INVALID;
-    HIPCHK(e, hipSetDevice(e->device));
-    const int64_t n = e->n;
-    TRY(materialize_positions(e));
-    if (!e->tree_valid && (e->comm || e->group || e->solo)) {
-        // multi-rank: the tree is built into the workspace from the positions of the call's last
-        // build (the lazy lastTree) or the current ones (getTreeForDebug's fresh tree), and the
-        // state stays as it is -- a rank's slot order and lane map must not change on its own
-        HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
-        if (n > 0) {
-            TreeBuffers tb = tree_buffers(e);
-            if (e->lazy_tree) {
-                tb.src.x = e->lt_x;
-                tb.src.y = e->lt_y;
-            }
-            tb.src.vx = tb.src.vy = nullptr;  // positions, masses and flags are all it reads
-            tb.spl_nb = 0;                    // the caller's splitters describe another order
-            tb.lanes_remap = nullptr;
-            HIPCHK(e, tree_build(tb, n, e->geo, e->stream));
-            if (!e->lazy_tree) {
-                // getTreeForDebug's fresh buildTree moves the bodies it jitters (BHA:146-151,
-                // 329-331): the moved positions go back into the replica in its own slot order
-                // (every rank makes the same calls, so the replicas stay equal)
-                unpermute_positions(n, e->perm, tb.dst.x, tb.dst.y, e->st.x, e->st.y, e->stream);
-                HIPCHK(e, hipGetLastError());
-                e->mir_fresh = false;
-            }
-            e->spl_nb = 0;  // k_prep wrote splitters of this order
-            e->keys_ready = false;
-            TRY(check_tree_flags(e));
-        } else {
-            HIPCHK(e, hipMemsetAsync(e->base, 0, sizeof(uint32_t), e->stream));
-        }
-        e->tree_valid = true;  // until the next step (a second call walks the same tree)
-    } else if (!e->tree_valid && e->view_pending) {
-        // getTreeForDebug's fresh tree (BHA:329-332) is the one the pipelined call already built
-        // from the caller's bodies after its merge rule: its jitter becomes part of the state, and
-        // the next step builds its own first tree from these positions (BHA:407)
-        e->view_pending = false;
-        e->prebuilt = false;
-        e->mir_fresh = false;
-        e->tree_valid = true;
-    } else if (!e->tree_valid) {  // getTreeForDebug builds a fresh tree (BHA:329-332)
-        HIPCHK(e, hipMemsetAsync(e->scalars + 1, 0, sizeof(uint32_t), e->stream));
-        TRY(build(e));
-        if (n > 0) TRY(check_tree_flags(e));
+    if (e->multi) {  // every member builds getTreeForDebug's tree (the same jitter in every
+                     // replica); member 0 walks it
+        const int rc = multi_fan(e, [](bh_engine *m, int) { return quads_prepare(m); }, false);
+        if (rc != BH_OK) return rc;
+        const int rc0 = bh_get_quads(MULTI_M0(e), cx, cy, h, cap, n_out);
+        if (rc0 != BH_OK) e->err = bh_last_error(MULTI_M0(e));
+        return rc0;
     }
+    TRY(quads_prepare(e));
+    const int64_t n = e->n;
     std::vector<uint64_t> keys((size_t)n);
     std::vector<int8_t> cpl((size_t)n);
     std::vector<uint32_t> base((size_t)n + 1);
@@ -2939,6 +2914,7 @@ int bh_get_quads(bh_engine *e, double *cx, double *cy, double *h, int64_t cap, i
 
 int bh_last_removed(const bh_engine *e, int64_t *idx, int64_t cap, int64_t *n_out) {
     if (!e || cap < 0 || (cap > 0 && !idx)) return BH_E_INVALID;
+    e = MULTI_M0(e);
     // caller indices are not renumbered inside a call, so the log is already relative to the
     // list before the call
     if (n_out) *n_out = (int64_t)e->removed.size();
@@ -2949,11 +2925,13 @@ int bh_last_removed(const bh_engine *e, int64_t *idx, int64_t cap, int64_t *n_ou
 
 int bh_last_timings(const bh_engine *e, double *out5) {
     if (!e || !out5) return BH_E_INVALID;
+    e = MULTI_M0(e);
     for (int k = 0; k < kPhases; ++k) out5[k] = e->phase_ms[k];
     return BH_OK;
 }
 
 int64_t bh_last_tree_nodes(const bh_engine *e) {
+    if (e) e = MULTI_M0(e);
     if (!e || e->n <= 0) return 0;
     uint32_t T = 0;
     const uint32_t *base = e->lt_aside ? e->lt_base : e->base;
@@ -2964,6 +2942,7 @@ int64_t bh_last_tree_nodes(const bh_engine *e) {
 
 int bh_traverse_kernel_ms(const bh_engine *e, double *avg_ms, int64_t *launches) {
     if (!e || !avg_ms) return BH_E_INVALID;
+    e = MULTI_M0(e);
     *avg_ms = e->trav_launches ? e->trav_ms_sum / (double)e->trav_launches : 0.0;
     if (launches) *launches = e->trav_launches;
     return BH_OK;
@@ -2971,6 +2950,7 @@ int bh_traverse_kernel_ms(const bh_engine *e, double *avg_ms, int64_t *launches)
 
 int bh_traverse_kernel_samples(const bh_engine *e, double *ms, int64_t cap, int64_t *n_out) {
     if (!e || cap < 0 || (cap > 0 && !ms)) return BH_E_INVALID;
+    e = MULTI_M0(e);
     const int64_t n = (int64_t)e->trav_samples.size();
     if (n_out) *n_out = n;
     if (n > cap) return BH_E_CAPACITY;
@@ -2981,6 +2961,7 @@ int bh_traverse_kernel_samples(const bh_engine *e, double *ms, int64_t cap, int6
 int bh_traversal_stats(const bh_engine *e, int64_t *lane_visits, int64_t *wave_iters,
                        int64_t *waves) {
     if (!e || !lane_visits || !wave_iters || !waves) return BH_E_INVALID;
+    e = MULTI_M0(e);
     *lane_visits = e->stat_lane_visits;
     *wave_iters = e->stat_wave_iters;
     *waves = e->stat_waves;
@@ -2989,6 +2970,7 @@ int bh_traversal_stats(const bh_engine *e, int64_t *lane_visits, int64_t *wave_i
 
 int bh_traversal_counters(const bh_engine *e, int64_t *out5) {
     if (!e || !out5) return BH_E_INVALID;
+    e = MULTI_M0(e);
     out5[0] = e->stat_lane_visits;
     out5[1] = e->stat_lane_contrib;
     out5[2] = e->stat_wave_iters;
@@ -2999,6 +2981,7 @@ int bh_traversal_counters(const bh_engine *e, int64_t *out5) {
 
 int bh_let_stats(const bh_engine *e, int64_t *out4) {
     if (!e || !out4) return BH_E_INVALID;
+    e = MULTI_M0(e);
     out4[4] = e->let_overflows;
     out4[0] = e->let_builds;
     out4[1] = e->full_builds;
@@ -3011,15 +2994,9 @@ int bh_let_stats(const bh_engine *e, int64_t *out4) {
     return BH_OK;
 }
 
-int bh_let_spec_stats(const bh_engine *e, int64_t *out2) {
-    if (!e || !out2) return BH_E_INVALID;
-    out2[0] = e->spec_builds;
-    out2[1] = e->spec_fallbacks;
-    return BH_OK;
-}
-
 int bh_set_profiling(bh_engine *e, int enabled) {
     if (!e) return BH_E_INVALID;
+    MULTI_BOTH(e, bh_set_profiling(m_, enabled));
     e->profiling = enabled != 0;
     return BH_OK;
 }
@@ -3056,6 +3033,7 @@ int bh_selftest_fast_math(int device, int64_t n, uint64_t seed, int64_t *mismatc
 
 int bh_synchronize(bh_engine *e) {
     if (!e) return BH_E_INVALID;
+    MULTI_ALL(e, bh_synchronize(m_));
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     return BH_OK;
@@ -3063,6 +3041,7 @@ int bh_synchronize(bh_engine *e) {
 
 int bh_comm_ranks(const bh_engine *e, int32_t *nranks, int32_t *rank) {
     if (!e || !nranks || !rank) return BH_E_INVALID;
+    e = MULTI_M0(e);
     *nranks = 0;
     *rank = e->rank;
     if (!e->comm) return BH_OK;
@@ -3076,11 +3055,42 @@ int bh_comm_ranks(const bh_engine *e, int32_t *nranks, int32_t *rank) {
 
 int bh_debug_inject(bh_engine *e, int what) {
     if (!e) return BH_E_INVALID;
-    if (what != 1) {
+    MULTI_ALL(e, bh_debug_inject(m_, what));  // (one member alone: bh_multi_member)
+    if (what < 1) {
         e->err = "bh_debug_inject: unknown fault";
         return BH_E_INVALID;
     }
-    e->inject_guard = true;
+    if (what == 1) e->inject_guard = true;
+    else e->inject_build = what - 2;
+    return BH_OK;
+}
+
+int bh_multi_world(const bh_engine *e) {
+    if (!e) return 0;
+    return e->multi && !e->use_one ? multi_world(e->multi) : 1;
+}
+
+bh_engine *bh_multi_member(bh_engine *e, int rank) {
+    if (!e) return nullptr;
+    if (!e->multi) return rank == 0 ? e : nullptr;
+    if (e->use_one) return rank == 0 ? e->one : nullptr;
+    return multi_member(e->multi, rank);
+}
+
+int bh_collective_log(const bh_engine *e, int64_t *out4, int64_t cap, int64_t *n_out) {
+    if (!e || cap < 0 || (cap > 0 && !out4)) return BH_E_INVALID;
+    e = MULTI_M0(e);
+    const int64_t n = (int64_t)e->coll_log.size() / 4;
+    if (n_out) *n_out = n;
+    if (n > cap) return BH_E_CAPACITY;
+    std::copy(e->coll_log.begin(), e->coll_log.end(), out4);
+    return BH_OK;
+}
+
+int bh_collective_log_clear(bh_engine *e) {
+    if (!e) return BH_E_INVALID;
+    MULTI_BOTH(e, bh_collective_log_clear(m_));
+    e->coll_log.clear();
     return BH_OK;
 }
 

@@ -713,6 +713,15 @@ void copy_u32(uint32_t *dst, const uint32_t *src, hipStream_t s) {
     k_copy_u32<<<1, 1, 0, s>>>(dst, src);
 }
 
+__global__ void k_take_u32(uint32_t *dst, uint32_t *src, uint32_t set) {
+    *dst |= *src | set;
+    *src = 0u;
+}
+
+void take_u32(uint32_t *dst, uint32_t *src, hipStream_t s, uint32_t set) {
+    k_take_u32<<<1, 1, 0, s>>>(dst, src, set);
+}
+
 __global__ __launch_bounds__(TB) void k_pack_readback(const uint32_t *__restrict__ scal,
                                                       const uint32_t *__restrict__ hdr,
                                                       const uint32_t *__restrict__ dlog,

@@ -270,23 +270,6 @@ __device__ __forceinline__ void let_guard(const LetBufs &L, uint32_t *__restrict
 }
 __global__ void k_let_guard(LetBufs L, uint32_t *__restrict__ scal) { let_guard(L, scal); }
 
-// The speculative next build (engine.cpp, the LET pipeline) reuses this build's subset with the
-// positions this build left (its jitter, BHA:146-151, applied); that is the next build's subset
-// only if the jitter moved no body into another depth-P cell -- an own body into a cell that is not
-// an own cell, or a body from beyond some rank's halo into it.  Any such move anywhere is flagged
-// in the table's status record (tag) and, all-gathered, seen by every rank alike.
-__global__ __launch_bounds__(TB) void k_let_cross(int64_t n_sub, BodyState src, BodyState dst,
-                                                  const uint32_t *__restrict__ perm, Geometry g,
-                                                  LetCell *__restrict__ table) {
-    const int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (a >= n_sub) return;
-    const uint32_t i = perm[a];
-    const double ox = src.x[i], oy = src.y[i], nx = dst.x[a], ny = dst.y[a];
-    if (ox == nx && oy == ny) return;  // not jittered
-    if (cell_of(g, ox, oy) != cell_of(g, nx, ny) || in_root(g, ox, oy) != in_root(g, nx, ny))
-        table[LET_CELLS].tag = 1u;
-}
-
 // ---- after the subset build ----------------------------------------------------------------
 // depth-P node of a cell with >= 2 subset bodies starting at sorted a: the internal nodes whose
 // first body is a are depths c(a-1)+1 .. c(a) at base[a] + (depth - c(a-1) - 1) (k_prep)
@@ -375,19 +358,12 @@ static_assert(LET_P == 8, "k_let_top_hi assumes 256 depth-LET_P cells per depth-
 __global__ __launch_bounds__(256) void k_let_top_hi(int world, Geometry g,
                                                     const LetCell *__restrict__ tables,
                                                     LetCell *__restrict__ levels,
-                                                    uint32_t *__restrict__ scal,
-                                                    uint32_t *__restrict__ cross) {
+                                                    uint32_t *__restrict__ scal) {
     __shared__ LetCell sh[256];
     const uint32_t b = blockIdx.x, t = threadIdx.x;
-    if (b == 0 && t == 0) {  // some rank's subset overflowed: every rank replays the call
-        uint32_t any_cross = 0;
-        for (int q = 0; q < world; ++q) {
-            const LetCell st = tables[(int64_t)q * LET_TSTRIDE + LET_CELLS];
-            if (st.cnt) scal[4] = 1u;
-            any_cross |= st.tag;
-        }
-        if (cross) *cross = any_cross;  // the same on every rank: the tables are all-gathered
-    }
+    if (b == 0 && t == 0)  // some rank's subset overflowed: every rank replays the call
+        for (int q = 0; q < world; ++q)
+            if (tables[(int64_t)q * LET_TSTRIDE + LET_CELLS].cnt) scal[4] = 1u;
     {
         const uint32_t c = b * 256u + t;
         LetCell r{0.0, 0.0, 0.0, 0u, 0u};
@@ -775,16 +751,14 @@ hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
 }
 
 hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const TreeBuffers &tb,
-                     hipStream_t s, bool detect_cross) {
-    if (detect_cross && n_sub > 0)
-        k_let_cross<<<grid_for(n_sub), TB, 0, s>>>(n_sub, tb.src, tb.dst, tb.perm, g, L.table);
+                     hipStream_t s) {
     k_let_table<<<grid_for(LET_CELLS + 1), TB, 0, s>>>(n_sub, g.J, L, tb);
     return hipGetLastError();
 }
 
 hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, const LetBufs &L,
-                        const TreeBuffers &tb, uint32_t *scal, hipStream_t s, uint32_t *cross) {
-    k_let_top_hi<<<256, 256, 0, s>>>(pc.world, g, L.tables, L.levels, scal, cross);
+                        const TreeBuffers &tb, uint32_t *scal, hipStream_t s) {
+    k_let_top_hi<<<256, 256, 0, s>>>(pc.world, g, L.tables, L.levels, scal);
     k_let_top_lo<<<1, 256, 0, s>>>(g, L.levels);
     k_let_w<<<grid_for(LET_CELLS + 1), TB, 0, s>>>(L, tb, scal);
     size_t bytes = L.scratch_bytes;

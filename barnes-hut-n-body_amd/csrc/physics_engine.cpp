@@ -28,6 +28,21 @@ PhysicsEngine::PhysicsEngine(std::vector<Body> &initialBodies, int device)
     bh_default_params(&p);
     int rc = bh_create(&p, device, &eng_);
     if (rc != BH_OK) throw std::runtime_error("bh_create failed (rc=" + std::to_string(rc) + ")");
+    init();
+}
+
+PhysicsEngine::PhysicsEngine(std::vector<Body> &initialBodies, const std::vector<int> &devices)
+    : bodies_(&initialBodies) {
+    bh_params p;
+    bh_default_params(&p);
+    std::vector<int32_t> d(devices.begin(), devices.end());
+    int rc = bh_create_multi_list(&p, d.data(), (int32_t)d.size(), &eng_);
+    if (rc != BH_OK)
+        throw std::runtime_error("bh_create_multi_list failed (rc=" + std::to_string(rc) + ")");
+    init();
+}
+
+void PhysicsEngine::init() {
     check(bh_set_mirror(eng_, 1));  // every step writes the caller-order bodies to pinned memory
     pushParams();
     pushBodies();

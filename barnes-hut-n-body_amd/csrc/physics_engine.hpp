@@ -62,6 +62,8 @@ class PhysicsEngine {
 public:
     // PhysicsEngine(initialBodies) — adopts the caller's list (BHA:295) on HIP device `device`.
     explicit PhysicsEngine(std::vector<Body> &initialBodies, int device = 0);
+    // ... over several GPUs behind one handle (bh_create_multi_list; repeats allowed)
+    PhysicsEngine(std::vector<Body> &initialBodies, const std::vector<int> &devices);
     ~PhysicsEngine();
     PhysicsEngine(const PhysicsEngine &) = delete;
     PhysicsEngine &operator=(const PhysicsEngine &) = delete;
@@ -77,6 +79,7 @@ public:
     bh_engine *handle() { return eng_; }
 
 private:
+    void init();
     void pushParams();
     void pushBodies();
     bool bodiesChanged() const;

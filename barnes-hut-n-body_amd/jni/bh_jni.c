@@ -20,11 +20,11 @@ static void throw_rt(JNIEnv *env, const bh_engine *e, const char *what) {
     if (rt) (*env)->ThrowNew(env, rt, e ? bh_last_error(e) : what);
 }
 
-/* external fun create(device: Int): Long */
-JNIEXPORT jlong JNICALL Java_Native_create(JNIEnv *env, jobject self, jint device) {
+/* external fun create(deviceMask: Int): Long  (bit d = HIP device d; 0 = every visible GPU) */
+JNIEXPORT jlong JNICALL Java_Native_create(JNIEnv *env, jobject self, jint deviceMask) {
     (void)self;
     bh_engine *e = NULL;
-    if (bh_shim_create((int)device, &e) != BH_OK) {
+    if (bh_shim_create((uint32_t)deviceMask, &e) != BH_OK) {
         throw_rt(env, NULL, "bh_create failed (no HIP device?)");
         return 0;
     }
@@ -71,27 +71,31 @@ JNIEXPORT void JNICALL Java_Native_step(JNIEnv *env, jobject self, jlong h, jint
     if (bh_shim_step(e, (int32_t)k) != BH_OK) throw_rt(env, e, "step");
 }
 
-/* external fun get(h: Long): DoubleArray  (SoA, length 5 N)
- * Filled from the engine's pinned caller-order mirror (bh_map_bodies), which the step wrote
- * itself: five SetDoubleArrayRegion copies, no device call while a Java array is held. */
-JNIEXPORT jdoubleArray JNICALL Java_Native_get(JNIEnv *env, jobject self, jlong h) {
+/* external fun getInto(h: Long, soa: DoubleArray): Int  (n, or -n if soa is shorter than 5 n)
+ * Fills the caller's reusable array from the engine's pinned caller-order mirror
+ * (bh_map_bodies), which the step wrote itself: five SetDoubleArrayRegion copies, no allocation,
+ * no device call while a Java array is held. */
+JNIEXPORT jint JNICALL Java_Native_getInto(JNIEnv *env, jobject self, jlong h, jdoubleArray soa) {
     (void)self;
     bh_engine *e = (bh_engine *)(intptr_t)h;
     const double *f[5] = {NULL, NULL, NULL, NULL, NULL};
     int64_t n = 0;
+    if (!soa) {
+        throw_rt(env, NULL, "getInto: null array");
+        return 0;
+    }
     if (bh_shim_map(e, f, &n) != BH_OK) {
-        throw_rt(env, e, "get");
-        return NULL;
+        throw_rt(env, e, "getInto");
+        return 0;
     }
     if (n > INT32_MAX / 5) {
-        throw_rt(env, NULL, "get: more bodies than a Java array holds (5 n >= 2^31)");
-        return NULL;
+        throw_rt(env, NULL, "getInto: more bodies than a Java array holds (5 n >= 2^31)");
+        return 0;
     }
-    jdoubleArray out = (*env)->NewDoubleArray(env, (jsize)(5 * n));
-    if (!out || n == 0) return out; /* NULL: OutOfMemoryError is pending */
-    for (int k = 0; k < 5; ++k)
-        (*env)->SetDoubleArrayRegion(env, out, (jsize)(k * n), (jsize)n, f[k]);
-    return out;
+    if ((int64_t)(*env)->GetArrayLength(env, soa) < 5 * n) return (jint)(-n);
+    for (int k = 0; k < 5 && n > 0; ++k)
+        (*env)->SetDoubleArrayRegion(env, soa, (jsize)(k * n), (jsize)n, f[k]);
+    return (jint)n;
 }
 
 /* external fun quads(h: Long): DoubleArray  ([cx0, cy0, h0, cx1, ...], visitQuads order) */

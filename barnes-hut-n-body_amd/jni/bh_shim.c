@@ -3,10 +3,29 @@
 
 #include <stdlib.h>
 
-int bh_shim_create(int device, bh_engine **out) {
+/* BH_DEVICES="0,1,2" (repeats allowed) overrides the mask with an explicit device list */
+static int create_from_env(const bh_params *p, const char *list, bh_engine **out) {
+    int32_t dev[64];
+    int32_t n = 0;
+    const char *q = list;
+    while (*q && n < 64) {
+        char *end = NULL;
+        const long d = strtol(q, &end, 10);
+        if (end == q || d < 0 || d > 1023) return BH_E_INVALID;
+        dev[n++] = (int32_t)d;
+        q = *end == ',' ? end + 1 : end;
+        if (*end && *end != ',') return BH_E_INVALID;
+    }
+    if (n == 0 || *q) return BH_E_INVALID;
+    return bh_create_multi_list(p, dev, n, out);
+}
+
+int bh_shim_create(uint32_t device_mask, bh_engine **out) {
     bh_params p;
     bh_default_params(&p); /* Config.kt defaults (CFG:5-23); setParams follows before any step */
-    int rc = bh_create(&p, device, out);
+    *out = NULL;
+    const char *list = getenv("BH_DEVICES");
+    int rc = list && *list ? create_from_env(&p, list, out) : bh_create_multi(&p, device_mask, out);
     if (rc == BH_OK) rc = bh_set_mirror(*out, 1); /* getBodies after every frame (PNL:302) */
     if (rc != BH_OK && *out) {
         bh_destroy(*out);

@@ -20,9 +20,12 @@
 extern "C" {
 #endif
 
-/* Native.create(device): PhysicsEngine's engine (BHA:287) on HIP device `device`, with the
- * pinned body mirror on (every step writes the caller-order bodies to host memory itself). */
-int bh_shim_create(int device, bh_engine **out);
+/* Native.create(deviceMask): PhysicsEngine's engine (BHA:287) over the HIP devices of
+ * `device_mask` (bit d = device d, 0 = every visible device; bh_create_multi: one handle, the
+ * step fanned out over the GPUs and joined), with the pinned body mirror on (every step writes
+ * the caller-order bodies to host memory itself).  BH_DEVICES="0,1,..." in the environment
+ * overrides the mask with an explicit device list (repeats allowed: bh_create_multi_list). */
+int bh_shim_create(uint32_t device_mask, bh_engine **out);
 
 /* Native.setParams: Config.G / DT / theta / SOFT2 / WIDTH_PX / HEIGHT_PX (CFG:5-23) and
  * mergeMaxMass / mergeMinDist (BHA:315,321), read live before every step. */

@@ -10,8 +10,9 @@ object Native {
         System.loadLibrary("bh_jni")
     }
 
-    /** bh_create on HIP device `device`; the engine fills its pinned body mirror every step. */
-    external fun create(device: Int): Long
+    /** bh_create_multi over the HIP devices of `deviceMask` (bit d = device d, 0 = every visible
+     *  GPU); the engine fills its pinned body mirror every step. */
+    external fun create(deviceMask: Int): Long
 
     /** bh_set_params: Config.G/DT/theta/SOFT2/WIDTH_PX/HEIGHT_PX (CFG:5-23) + merge knobs. */
     external fun setParams(
@@ -25,8 +26,9 @@ object Native {
     /** bh_step(k). */
     external fun step(h: Long, k: Int)
 
-    /** The bodies as SoA (length 5 N), caller order (bh_map_bodies: the pinned mirror). */
-    external fun get(h: Long): DoubleArray
+    /** The bodies into the caller's SoA array [x[0..n) y[n..2n) vx vy m] from the engine's pinned
+     *  mirror (bh_map_bodies), no allocation; returns n, or -n if soa holds fewer than 5 n. */
+    external fun getInto(h: Long, soa: DoubleArray): Int
 
     /** bh_get_quads as interleaved (cx, cy, h) triples in visitQuads order. */
     external fun quads(h: Long): DoubleArray

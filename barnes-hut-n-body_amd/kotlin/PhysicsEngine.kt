@@ -27,8 +27,13 @@ class QuadList(private val q: DoubleArray) {
 
 class PhysicsEngine(initialBodies: MutableList<Body>) {
     private var bodies: MutableList<Body> = initialBodies
-    private val handle: Long = Native.create(0)            // bh_create on HIP device 0
-    private var shadow = DoubleArray(0)                     // SoA of what the engine holds
+    // bh_create_multi over the GPUs of -Dbh.deviceMask (bit d = HIP device d; default 0 = every
+    // visible GPU): one handle, every step fanned out over the GPUs and joined (BHA:374-395)
+    private val handle: Long = Native.create(Integer.decode(System.getProperty("bh.deviceMask", "0")))
+    // SoA of what the engine holds (x[0..n) y[n..2n) vx vy m), reused frame after frame: no
+    // per-frame allocation that grows with N
+    private var shadow = DoubleArray(0)
+    private var shadowN = -1
 
     /** BHA:315 -- bodies heavier than this absorb neighbours closer than mergeMinDist. */
     var mergeMaxMass: Double = 4_000.0
@@ -53,8 +58,7 @@ class PhysicsEngine(initialBodies: MutableList<Body>) {
     /** BHA:405-439: one step; Config is read live, as the reference reads it. */
     fun step() {
         params()
-        val cur = soa()
-        if (!cur.contentEquals(shadow)) push(cur)           // upload only if the caller edited bodies
+        if (changed()) push()                                // upload only if the caller edited bodies
         Native.step(handle, 1)
         pull(afterStep = true)
     }
@@ -72,31 +76,49 @@ class PhysicsEngine(initialBodies: MutableList<Body>) {
         Config.WIDTH_PX, Config.HEIGHT_PX, mergeMaxMass, mergeMinDist
     )
 
-    private fun soa(): DoubleArray {
+    /** Whether the caller's bodies differ (bitwise) from what the engine holds -- in place. */
+    private fun changed(): Boolean {
         val n = bodies.size
-        val a = DoubleArray(5 * n)
+        if (n != shadowN) return true
+        val a = shadow
+        for (i in 0 until n) {
+            val b = bodies[i]
+            if (b.x.toRawBits() != a[i].toRawBits() || b.y.toRawBits() != a[n + i].toRawBits() ||
+                b.vx.toRawBits() != a[2 * n + i].toRawBits() ||
+                b.vy.toRawBits() != a[3 * n + i].toRawBits() ||
+                b.m.toRawBits() != a[4 * n + i].toRawBits()) return true
+        }
+        return false
+    }
+
+    private fun push() {
+        val n = bodies.size
+        if (shadow.size < 5 * n) shadow = DoubleArray(5 * n)
+        val a = shadow
         for ((i, b) in bodies.withIndex()) {
             a[i] = b.x; a[n + i] = b.y; a[2 * n + i] = b.vx; a[3 * n + i] = b.vy; a[4 * n + i] = b.m
         }
-        return a
-    }
-
-    private fun push(a: DoubleArray = soa()) {
-        Native.reset(handle, bodies.size, a)
-        shadow = a
+        Native.reset(handle, n, a)
+        shadowN = n
     }
 
     /** afterStep: apply the step's removals (BHA:519) once, highest index first. */
     private fun pull(afterStep: Boolean) {
-        if (afterStep)
-            for (j in Native.lastRemoved(handle).sortedDescending()) bodies.removeAt(j)
-        val a = Native.get(handle)                          // SoA from the engine's pinned mirror
-        val n = a.size / 5
+        if (afterStep) {
+            val rem = Native.lastRemoved(handle)            // ascending; usually empty
+            for (k in rem.indices.reversed()) bodies.removeAt(rem[k])
+        }
+        var n = Native.getInto(handle, shadow)              // the engine's pinned mirror, SoA
+        if (n < 0) {                                        // (only after a reset to more bodies)
+            shadow = DoubleArray(-5 * n)
+            n = Native.getInto(handle, shadow)
+        }
         check(n == bodies.size) { "engine and caller body lists diverged" }
+        val a = shadow
         for (i in 0 until n) {
             val b = bodies[i]
             b.x = a[i]; b.y = a[n + i]; b.vx = a[2 * n + i]; b.vy = a[3 * n + i]; b.m = a[4 * n + i]
         }
-        shadow = a
+        shadowN = n
     }
 }

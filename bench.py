@@ -80,6 +80,15 @@ def parse():
     ap.add_argument("--drop-in-calls", type=int, default=40)
     ap.add_argument("--dry-run", action="store_true",
                     help="print the launch plan (the torchrun child command for N > 1) and exit")
+    ap.add_argument("--single-process", action="store_true",
+                    help="N > 1: one process, one engine handle over the N GPUs "
+                         "(bh_create_multi: a host thread per GPU, RCCL communicators made "
+                         "in-process) -- the front-end's own way to drive N GPUs -- instead "
+                         "of torchrun with one process per GPU")
+    ap.add_argument("--devices", default=None,
+                    help="--single-process rehearsal on fewer GPUs: the handle's device list, "
+                         "e.g. 0,0 (a repeated device exchanges by device-to-device copies, "
+                         "not RCCL)")
     return ap.parse_args()
 
 
@@ -242,6 +251,10 @@ def verify_leg(bh_amd, eng, case, arrs, dist, rank, world):
     mine.update({f: _sha(a) for f, a in zip(FIELDS, state)})
     match = mine["n"] == want["n"] and all(mine[f] == want[f] for f in FIELDS)
     agree = True
+    if eng.multi_world() > 1:  # one handle over several GPUs: every member's replica
+        for r in range(1, eng.multi_world()):
+            st = eng.member(r).get_bodies()
+            agree = agree and all(_sha(a) == mine[f] for f, a in zip(FIELDS, st))
     if world > 1:
         gathered = [None] * world
         dist.all_gather_object(gathered, mine)
@@ -249,7 +262,7 @@ def verify_leg(bh_amd, eng, case, arrs, dist, rank, world):
         match = match and all(g["n"] == want["n"] and all(g[f] == want[f] for f in FIELDS)
                               for g in gathered)
     return {"case": case, "steps": want["steps"], "n": want["n"], "digest_match": bool(match),
-            "ranks_agree": bool(agree), "ranks": world,
+            "ranks_agree": bool(agree), "ranks": max(world, eng.multi_world()),
             "bad_fields": [f for f in FIELDS if mine[f] != want[f]],
             "seconds": round(time.perf_counter() - t0, 3),
             "source": "tests/golden/digests.json (SHA-256 of the CPU oracle's final state)"}
@@ -426,27 +439,36 @@ def drop_in_leg(eng, steps, warmup=5):
 def main():
     args = parse()
     env_world = os.environ.get("WORLD_SIZE")
-    if env_world is None and args.gpus is not None and args.gpus > 1:
+    single_proc = args.single_process and args.gpus is not None and args.gpus > 1
+    if single_proc and env_world is not None and int(env_world) > 1:
+        print("bench.py: --single-process runs in one process, not under torchrun",
+              file=sys.stderr)
+        sys.exit(2)
+    if env_world is None and args.gpus is not None and args.gpus > 1 and not single_proc:
         sys.exit(spawn_torchrun(args))  # before anything touches the GPU
     world = int(env_world) if env_world is not None else 1
     if args.gpus is None:
         args.gpus = world
-    if args.gpus != world:
+    # n_gpus: GPUs measured; world: processes (torchrun ranks)
+    n_gpus = args.gpus if single_proc else world
+    if args.gpus != n_gpus:
         print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}: refusing to measure a "
               f"different number of GPUs than asked", file=sys.stderr)
         sys.exit(2)
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if args.config is None:  # BASELINE's metric on one GPU; the north-star cloud on N > 1
-        args.config = "c3" if world == 1 else "c4"
+        args.config = "c3" if n_gpus == 1 else "c4"
     if args.theta is None:
         args.theta = 0.0 if args.config == "c5" else 0.5
     direct = args.theta == 0.0
     if args.verify is None:
         args.verify = True
     if args.dry_run:
-        print(json.dumps({"launch": "in-process", "world": world, "config": args.config,
-                          "theta": args.theta, "verify": args.verify}), flush=True)
+        print(json.dumps({"launch": "single process, one handle over the GPUs" if single_proc
+                          else "in-process", "world": world, "n_gpus": n_gpus,
+                          "config": args.config, "theta": args.theta, "verify": args.verify}),
+              flush=True)
         return
 
     import numpy as np
@@ -474,10 +496,36 @@ def main():
                 print(f"bench.py: RCCL communicator {views} does not span the {world} ranks",
                       file=sys.stderr)
             sys.exit(3)
+    elif single_proc:
+        # one handle over GPUs 0..N-1 (the decomposition at every body count: bench sizes are the
+        # point), in-process RCCL communicators
+        os.environ.setdefault("BH_MULTI_MIN_BODIES", "0")
+        devs = ([int(d) for d in args.devices.split(",")] if args.devices
+                else list(range(n_gpus)))
+        if len(devs) != n_gpus:
+            print(f"bench.py: --devices lists {len(devs)} devices for --gpus {n_gpus}",
+                  file=sys.stderr)
+            sys.exit(2)
+        eng = bh_amd.Engine(params, devices=devs)
+        nr, ur = eng.comm_ranks()
+        members = [eng.member(r).comm_ranks() for r in range(eng.multi_world())]
+        repeated = len(set(devs)) < len(devs)
+        rccl = {"comm_count": nr, "user_ranks": [m[1] for m in members], "devices": devs,
+                "communicators": "device-to-device copies (a device listed twice)" if repeated
+                else "ncclCommInitAll, one per GPU, one host thread each"}
+        if eng.multi_world() != n_gpus or (not repeated and any(m[0] != n_gpus for m in members)):
+            print(f"bench.py: the handle's RCCL communicators {members} do not span {n_gpus} GPUs",
+                  file=sys.stderr)
+            sys.exit(3)
     else:
         eng = bh_amd.Engine(params, device=local_rank)
+        # the drop-in leg reads the pinned mirror: its stream is made now, right after the
+        # engine's own streams and before the counter probe's (hardware queues go out in stream
+        # creation order), and the mirror stays off until that leg
+        eng.set_mirror(True)
+        eng.set_mirror(False)
 
-    arrs, scene_name, scaling = scene_for(args.config, world)
+    arrs, scene_name, scaling = scene_for(args.config, n_gpus)
     n0 = len(arrs[0])
 
     eng.reset_bodies(*arrs)
@@ -523,6 +571,13 @@ def main():
         gathered = [None] * world
         dist.all_gather_object(gathered, mine)
         per_rank = gathered
+    elif single_proc:
+        per_rank = []
+        for r in range(eng.multi_world()):
+            m = eng.member(r)
+            mine = {k: round(v / max(args.steps, 1), 3) for k, v in m.last_timings().items()}
+            mine["let"] = m.let_stats()
+            per_rank.append(mine)
     cnt_end = None
     if not direct and not args.no_counters and rank == 0:
         cnt_end = traversal_counters(bh_amd, params, local_rank, eng.get_bodies())
@@ -540,7 +595,7 @@ def main():
     # figure is SURVEY §8d's 20 flop per point-force interaction (BHA:250-259, the IEEE sqrt
     # and each division counted as one flop; the criterion's compare work is not counted).
     if direct:
-        bodies_per_launch = bodies / world
+        bodies_per_launch = bodies / n_gpus
         flops_per_launch = FLOP_PER_INTERACTION * bodies_per_launch * (bodies - 1)
         kernel = "k_direct"
         ips = flops_per_launch / FLOP_PER_INTERACTION / (trav_ms * 1e-3) if trav_ms > 0 else 0
@@ -554,13 +609,13 @@ def main():
                 "interactions_per_s": round(ceil),
                 "frac": round(ips / ceil, 4)}
     else:
-        kernel = "k_traverse" if world == 1 else "k_traverse (one rank's 4 rounds, 2 streams)"
+        kernel = "k_traverse" if n_gpus == 1 else "k_traverse (one rank's 4 rounds, 2 streams)"
         cs = [c for c in (cnt_start, cnt_end) if c]
         contrib = float(np.mean([c["contrib_per_body"] for c in cs])) if cs else 0.0
         vbar = float(np.mean([c["vbar"] for c in cs])) if cs else 0.0
         # world > 1: one timed interval spans a rank's 4 round launches (its 1 / world of the
         # bodies), from the first round's start to the last even round's end on its stream
-        bodies_per_launch = bodies / world
+        bodies_per_launch = bodies / n_gpus
         flops_per_launch = FLOP_PER_INTERACTION * contrib * bodies_per_launch
         node_bytes = (NODE_BYTES * vbar + BODY_EVAL_BYTES) * bodies_per_launch
         extra = {
@@ -602,11 +657,11 @@ def main():
 
     # rank 0's extra legs; the other ranks wait at the next collective
     drop_in = None
-    if world == 1 and not args.no_drop_in:
+    if n_gpus == 1 and not args.no_drop_in:
         drop_in = drop_in_leg(eng, args.drop_in_calls)
         drop_in["ms_per_step_batched"] = round(ms_per_step, 4)
     single = None
-    if rank == 0 and world > 1 and not args.no_single_gpu:
+    if rank == 0 and n_gpus > 1 and not args.no_single_gpu:
         single = single_gpu_leg(bh_amd, params, local_rank, arrs, args.steps, args.warmup)
     cpu_baseline = None
     if rank == 0 and not args.no_cpu_baseline:
@@ -617,8 +672,8 @@ def main():
         dist.barrier()  # rank 0's extra legs are done: the verify leg's collectives start together
     if args.verify:
         from bh_amd import scenes
-        case = "c4_k10" if world > 1 else "c3_k10"
-        golden_scene = "c4" if world > 1 else "c3"
+        case = "c4_k10" if n_gpus > 1 else "c3_k10"
+        golden_scene = "c4" if n_gpus > 1 else "c3"
         varrs = arrs if scene_name == golden_scene else scenes.config_scene(golden_scene)
         verify = verify_leg(bh_amd, eng, case, varrs, dist, rank, world)
 
@@ -628,7 +683,7 @@ def main():
             if args.config == "c3" else f"body-steps/sec ({scene_name}, theta={args.theta})",
             "value": round(value, 1),
             "unit": "body-steps/s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms_per_step, 4),
@@ -647,8 +702,10 @@ def main():
                 "root": "2400x800",
                 "evals_per_step": 2,
                 "parallelism": f"replicated state, build sharded as locally essential trees, "
-                               f"force sharded x{world} (RCCL all-gather)"
-                if world > 1 else "single GPU",
+                               f"force sharded x{n_gpus} (RCCL all-gather)"
+                               + (", one process: one handle over the GPUs (bh_create_multi)"
+                                  if single_proc else ", one process per GPU")
+                if n_gpus > 1 else "single GPU",
             },
             "phase_ms": {k: round(v, 3) for k, v in phases.items()},
             "roofline": roofline,

@@ -57,6 +57,44 @@ typedef struct bh_engine bh_engine;
 /* new PhysicsEngine(...) (BHA:287) on HIP device `device`, single GPU. */
 int bh_create(const bh_params *p, int device, bh_engine **out);
 
+/* new PhysicsEngine(...) (BHA:287) over every GPU of `device_mask` (bit d = HIP device d; 0 = every
+ * visible device) behind ONE handle: the reference's step() fans its force evaluation out over
+ * worker threads and joins them (computeAccelerations, BHA:374-395, inside runBlocking, BHA:408,
+ * 426); this handle fans every step out over the GPUs and returns when all are done, so the one
+ * PhysicsEngine object of the front-end (NBodyPanel.kt:103, 290-293) drives all of them.
+ * Inside: one member engine per GPU -- the ranks of bh_create_dist's decomposition (replicated
+ * state, locally essential tree builds, every exchange an in-place RCCL all-gather over xGMI on
+ * communicators made in this process by ncclCommInitAll) -- each driven by its own host thread
+ * (member 0 by the caller's).  Every call of this header takes the handle: calls that change the
+ * state run on every member, calls that read it read member 0's replica (complete at every API
+ * boundary), bh_set_mirror / bh_map_bodies use member 0's mirror.  One set bit = bh_create (the
+ * pipelined one-GPU engine).  Results are bit-identical to bh_create's for any mask. */
+int bh_create_multi(const bh_params *p, uint32_t device_mask, bh_engine **out);
+
+/* The same over an explicit device list, repeats allowed: a device listed twice hosts two members
+ * (RCCL refuses two ranks per device), so a list with repeats -- or BH_MULTI_EXCHANGE=copy in the
+ * environment -- exchanges by device-to-device copies between the members (an in-process group,
+ * bh_create_local) instead of RCCL; the pieces, rounds and layout are the same. */
+int bh_create_multi_list(const bh_params *p, const int32_t *devices, int32_t count,
+                         bh_engine **out);
+
+/* Members of a multi-device handle (1 for any other engine) and member `rank`'s own handle, for
+ * diagnostics (per-rank timings, LET statistics, collective logs, bh_debug_inject on one rank).
+ * Owned by the handle: never bh_destroy a member, and never bh_step one on its own (its peers
+ * would wait for it).  A plain engine is its own member 0. */
+int bh_multi_world(const bh_engine *e);
+bh_engine *bh_multi_member(bh_engine *e, int rank);
+
+/* Multi-rank engines log every collective they issue, in host issue order: 4 int64 per entry --
+ * the engine's state-changing API call count when it was issued, the site (1 a round of
+ * accelerations, 2 a round of new positions, 3 a round of velocities, 4 the LET cell tables,
+ * 5 the end-of-call LET status all-reduce, 6 the settings check at creation), the bytes every
+ * rank receives, and the stream (0 the engine's, 1 the exchange stream).  Every rank of a
+ * decomposition must log the same sequence: RCCL pairs the n-th call of every rank.  The
+ * in-process exchange logs the same entries.  BH_E_CAPACITY + *n_out if cap is too small. */
+int bh_collective_log(const bh_engine *e, int64_t *out4, int64_t cap, int64_t *n_out);
+int bh_collective_log_clear(bh_engine *e);
+
 /* Multi-GPU member: one process per GPU; `unique_id` is the 128-byte RCCL id produced by
  * bh_comm_unique_id() on rank 0 and broadcast by the caller (e.g. torch.distributed).
  * Replaces computeAccelerations' fan-out over worker threads (BHA:374-395) by a fan-out over
@@ -85,9 +123,12 @@ int bh_comm_unique_id(void *out128);
  * (single GPU, in-process group, solo). */
 int bh_comm_ranks(const bh_engine *e, int32_t *nranks, int32_t *rank);
 
-/* Test hook: what == 1 -- the next locally essential tree build of this rank trips the node
+/* Test hooks.  what == 1: the next locally essential tree build of this rank trips the node
  * array guard (let.hip k_let_guard), as a broken invariant on one rank would; the call must then
- * be replayed by every rank of the group alike. */
+ * be replayed by every rank of the group alike.  what == 2 + k: the k-th next full tree build
+ * (k = 0: the next one) raises the jitter replay's error flag, as the unsupported-geometry guard
+ * would; the bh_step call whose step uses that tree returns BH_E_STATE -- for a call's last
+ * pipelined build (the next call's first tree) that is the next call. */
 int bh_debug_inject(bh_engine *e, int what);
 
 /* In-process rank group (testing the multi-GPU decomposition on one device, where RCCL refuses
@@ -208,12 +249,6 @@ int bh_traversal_counters(const bh_engine *e, int64_t *out5);
  * on every multi-rank engine (2 ranks up); BH_LET=1 in the environment before creating an engine
  * enables them also on one rank, BH_LET=0 keeps every build full. */
 int bh_let_stats(const bh_engine *e, int64_t *out5);
-
-/* The LET pipeline of multi-rank engines: out2[0] LET builds made speculatively beside the
- * previous evaluation's rounds (a step's first build, reusing the second build's subset with the
- * positions it left) and taken over, out2[1] evaluations whose speculation was called off because
- * the build's jitter (BHA:146-151) moved a body into another depth-8 cell on some rank. */
-int bh_let_spec_stats(const bh_engine *e, int64_t *out2);
 
 /* Enable/disable per-phase event timing (default off: no events in the hot loop). */
 int bh_set_profiling(bh_engine *e, int enabled);

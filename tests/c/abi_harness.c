@@ -15,10 +15,12 @@
  *
  * Exit status 0 = pass; the last line says what was checked.
  */
+#define _POSIX_C_SOURCE 200809L
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #include "bh_engine.h"
 #include "bh_oracle.h"
@@ -51,7 +53,7 @@ static void fail(const char *what, long frame) {
 typedef struct {
     jlong h; /* Native.create's handle */
     List *bodies;
-    double *shadow; /* 5 * n SoA of what the engine holds */
+    jdoubleArray shadow; /* the shim's reusable DoubleArray: SoA of what the engine holds */
     long shadow_n;
     double mergeMaxMass, mergeMinDist; /* BHA:315,321 */
 } Shim;
@@ -84,31 +86,42 @@ static void soa_of(const List *l, double *a) {
     }
 }
 
-static void shim_push(Shim *s) {
-    long n = s->bodies->n;
-    free(s->shadow);
-    s->shadow = malloc(sizeof(double) * (5 * n + 1));
-    soa_of(s->bodies, s->shadow);
-    s->shadow_n = n;
-    jdoubleArray a = fake_jvm_double_array((jsize)(5 * n), s->shadow);
-    Java_Native_reset(env, NULL, s->h, (jint)n, a);
-    jni_check("reset");
-    fake_jvm_free(a);
+static long shadow_allocs; /* DoubleArray allocations of the shim after its constructor */
+
+static void shim_grow(Shim *s, long n) { /* `shadow = DoubleArray(5 n)` when too small */
+    if (s->shadow && fake_jvm_length(s->shadow) >= 5 * n) return;
+    if (s->shadow) fake_jvm_free(s->shadow);
+    s->shadow = fake_jvm_double_array((jsize)(5 * n), NULL);
+    ++shadow_allocs;
 }
 
+static void shim_push(Shim *s) {
+    long n = s->bodies->n;
+    shim_grow(s, n);
+    soa_of(s->bodies, fake_jvm_doubles(s->shadow));
+    Java_Native_reset(env, NULL, s->h, (jint)n, s->shadow);
+    jni_check("reset");
+    s->shadow_n = n;
+}
+
+/* changed(): field by field against the shadow, in place (toRawBits compares) */
 static int shim_changed(Shim *s) {
     long n = s->bodies->n;
     if (n != s->shadow_n) return 1;
-    double *a = malloc(sizeof(double) * (5 * n + 1));
-    soa_of(s->bodies, a);
-    int diff = memcmp(a, s->shadow, sizeof(double) * 5 * n) != 0;
-    free(a);
-    return diff;
+    const double *a = fake_jvm_doubles(s->shadow);
+    for (long i = 0; i < n; ++i) {
+        const Body *b = &s->bodies->b[i];
+        if (memcmp(&b->x, &a[i], 8) || memcmp(&b->y, &a[n + i], 8) ||
+            memcmp(&b->vx, &a[2 * n + i], 8) || memcmp(&b->vy, &a[3 * n + i], 8) ||
+            memcmp(&b->m, &a[4 * n + i], 8))
+            return 1;
+    }
+    return 0;
 }
 
 /* pull(afterStep): removals are applied once, right after the step that made them */
-static void shim_pull(Shim *s, int after_step) {
-    if (after_step) {
+static void shim_apply_removed(Shim *s) {
+    {
         jintArray rem = Java_Native_lastRemoved(env, NULL, s->h);
         jni_check("lastRemoved");
         const jint *r = fake_jvm_ints(rem);
@@ -120,10 +133,21 @@ static void shim_pull(Shim *s, int after_step) {
         }
         fake_jvm_free(rem);
     }
-    jdoubleArray arr = Java_Native_get(env, NULL, s->h);
-    jni_check("get");
-    const long n = (long)fake_jvm_length(arr) / 5;
-    const double *a = fake_jvm_doubles(arr);
+}
+
+static long shim_get(Shim *s) {
+    jint got = Java_Native_getInto(env, NULL, s->h, s->shadow);
+    jni_check("getInto");
+    if (got < 0) { /* the shadow is too small (after a reset to more bodies): grow, again */
+        shim_grow(s, -(long)got);
+        got = Java_Native_getInto(env, NULL, s->h, s->shadow);
+        jni_check("getInto");
+    }
+    return (long)got;
+}
+
+static void shim_unpack(Shim *s, long n) {
+    const double *a = fake_jvm_doubles(s->shadow);
     if (n != s->bodies->n) {
         fprintf(stderr, "abi_harness: engine N %ld vs caller list %ld\n", n, s->bodies->n);
         exit(1);
@@ -136,18 +160,20 @@ static void shim_pull(Shim *s, int after_step) {
         b->vy = a[3 * n + i];
         b->m = a[4 * n + i];
     }
-    free(s->shadow);
-    s->shadow = malloc(sizeof(double) * (5 * n + 1));
-    memcpy(s->shadow, a, sizeof(double) * 5 * n);
     s->shadow_n = n;
-    fake_jvm_free(arr);
 }
 
-static void shim_create(Shim *s, List *initial) {
+static void shim_pull(Shim *s, int after_step) {
+    if (after_step) shim_apply_removed(s);
+    shim_unpack(s, shim_get(s));
+}
+
+static void shim_create(Shim *s, List *initial, jint device_mask) {
     memset(s, 0, sizeof(*s));
     s->mergeMaxMass = 4000.0;
     s->mergeMinDist = 8.0;
-    s->h = Java_Native_create(env, NULL, 0);
+    s->shadow_n = -1;
+    s->h = Java_Native_create(env, NULL, device_mask);
     if (fake_jvm_take_exception() || !s->h) {
         fprintf(stderr, "abi_harness: Native.create failed (no GPU?)\n");
         exit(1);
@@ -259,14 +285,75 @@ static void compare(const List *l, oracle_engine *o, long frame) {
     }
 }
 
-int main(void) {
+static double now_ms(void) {
+    struct timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return (double)t.tv_sec * 1e3 + (double)t.tv_nsec * 1e-6;
+}
+
+/* --c3-frames K: the shim's per-frame host work at C3 (8e5 + 2e5 galaxy disks, NBodyPanel's
+ * two disks scaled), timed beside the GPU step: NBodyPanel's tick() -> step() (PNL:290-293),
+ * K frames after 5 warm-up frames.  Prints one JSON line.  (The bodies are C structs here, not
+ * JVM objects behind an ArrayList: the loops are a lower bound of the JVM's.) */
+static int c3_frames(long frames, jint mask) {
+    List list = {NULL, 0};
+    add_galaxy(&list, 800000, 1200.0, 400.0, 0.0, 300.0, 50000.0, 5000.0, 1);
+    add_galaxy(&list, 200000, 1200.0, 160.0, -50.0, 100.0, 5000.0, 500.0, 2);
+    Shim s;
+    shim_create(&s, &list, mask);
+    for (int w = 0; w < 5; ++w) shim_step(&s);
+    const long allocs0 = shadow_allocs, uploads0 = shim_steps_uploaded;
+    double t[6] = {0, 0, 0, 0, 0, 0}; /* params, changed, step, removals, getInto, unpack */
+    const long n0 = s.bodies->n;
+    const double t0 = now_ms();
+    for (long f = 0; f < frames; ++f) {
+        double a = now_ms(), b;
+        shim_params(&s);
+        b = now_ms(); t[0] += b - a; a = b;
+        if (shim_changed(&s)) {
+            shim_push(&s);
+            ++shim_steps_uploaded;
+        }
+        b = now_ms(); t[1] += b - a; a = b;
+        Java_Native_step(env, NULL, s.h, 1);
+        jni_check("step");
+        b = now_ms(); t[2] += b - a; a = b;
+        shim_apply_removed(&s);
+        b = now_ms(); t[3] += b - a; a = b;
+        const long n = shim_get(&s);
+        b = now_ms(); t[4] += b - a; a = b;
+        shim_unpack(&s, n);
+        b = now_ms(); t[5] += b - a;
+    }
+    const double total = now_ms() - t0;
+    const double host = t[0] + t[1] + t[3] + t[4] + t[5];
+    printf("{\"frames\": %ld, \"bodies\": %ld, \"devices\": %d, \"ms_per_frame\": %.4f, "
+           "\"step_ms\": %.4f, \"host_ms\": %.4f, \"params_ms\": %.4f, \"changed_ms\": %.4f, "
+           "\"removals_ms\": %.4f, \"getInto_ms\": %.4f, \"unpack_ms\": %.4f, "
+           "\"allocations_per_frame\": %.3f, \"uploads\": %ld}\n",
+           frames, n0, bh_multi_world((bh_engine *)(intptr_t)s.h), total / frames, t[2] / frames,
+           host / frames, t[0] / frames, t[1] / frames, t[3] / frames, t[4] / frames, t[5] / frames,
+           (double)(shadow_allocs - allocs0) / frames, shim_steps_uploaded - uploads0);
+    bh_destroy((bh_engine *)(intptr_t)s.h);
+    return 0;
+}
+
+int main(int argc, char **argv) {
     env = fake_jvm_env();
+    jint mask = 1; /* GPU 0; BH_DEVICES="0,0,0" in the environment: one handle over a list */
+    long timing_frames = 0;
+    for (int i = 1; i < argc; ++i) {
+        if (!strcmp(argv[i], "--mask") && i + 1 < argc) mask = (jint)strtol(argv[++i], NULL, 0);
+        else if (!strcmp(argv[i], "--c3-frames") && i + 1 < argc) timing_frames = atol(argv[++i]);
+    }
+    if (timing_frames > 0) return c3_frames(timing_frames, mask);
     List list = {NULL, 0};
     /* defaultBodies() (PNL:83-100), scaled down */
     add_galaxy(&list, 3000, 1200.0, 400.0, 0.0, 300.0, 50000.0, 5000.0, 1);
     add_galaxy(&list, 800, 1200.0, 160.0, -50.0, 100.0, 5000.0, 500.0, 2);
     Shim s;
-    shim_create(&s, &list); /* PNL:103 */
+    shim_create(&s, &list, mask); /* PNL:103 */
+    const long allocs0 = shadow_allocs;
     oracle_engine *o = oracle_of(&list, &s);
     List list2 = {NULL, 0}, list3 = {NULL, 0};
     long removed_total = 0, quads_checked = 0;
@@ -313,10 +400,11 @@ int main(void) {
         }
     }
     if (removed_total == 0) fail("the scene never merged: identity bookkeeping untested", 40);
-    printf("abi_harness: 40 frames through the JNI glue (%ld native calls) bit-identical to the "
-           "oracle; %ld bodies merged away, %ld quads checked, %ld uploads after the "
-           "constructor/resets\n",
-           jni_calls, removed_total, quads_checked, shim_steps_uploaded);
+    printf("abi_harness: 40 frames through the JNI glue on %d device(s) (%ld native calls) "
+           "bit-identical to the oracle; %ld bodies merged away, %ld quads checked, %ld uploads "
+           "after the constructor/resets, %ld shadow allocations after the constructor\n",
+           bh_multi_world((bh_engine *)(intptr_t)s.h), jni_calls, removed_total, quads_checked,
+           shim_steps_uploaded, shadow_allocs - allocs0);
     oracle_destroy(o);
     bh_destroy((bh_engine *)(intptr_t)s.h); /* the Kotlin object lives as long as the app */
     return 0;

@@ -19,12 +19,12 @@ jsize fake_jvm_length(jarray a);
 void fake_jvm_free(jarray a);
 
 /* the glue's natives (bh_jni.c), declared for the harness */
-jlong Java_Native_create(JNIEnv *env, jobject self, jint device);
+jlong Java_Native_create(JNIEnv *env, jobject self, jint deviceMask);
 void Java_Native_setParams(JNIEnv *env, jobject self, jlong h, jdouble G, jdouble dt,
                            jdouble theta, jdouble soft2, jint w, jint hgt, jdouble mm, jdouble md);
 void Java_Native_reset(JNIEnv *env, jobject self, jlong h, jint n, jdoubleArray soa);
 void Java_Native_step(JNIEnv *env, jobject self, jlong h, jint k);
-jdoubleArray Java_Native_get(JNIEnv *env, jobject self, jlong h);
+jint Java_Native_getInto(JNIEnv *env, jobject self, jlong h, jdoubleArray soa);
 jdoubleArray Java_Native_quads(JNIEnv *env, jobject self, jlong h);
 jintArray Java_Native_lastRemoved(JNIEnv *env, jobject self, jlong h);
 

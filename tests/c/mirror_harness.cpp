@@ -12,6 +12,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <vector>
 
 #include "bh_oracle.h"
@@ -104,12 +105,22 @@ void compare(const std::vector<bh::Body> &l, oracle_engine *o, long frame) {
 
 }  // namespace
 
-int main() {
+int main(int argc, char **argv) {
     bh::Config::theta = 0.5;
     std::vector<bh::Body> bodies;  // defaultBodies() (PNL:83-100), scaled down
     galaxy(bodies, 3000, 1200.0, 400.0, 0.0, 300.0, 50000.0, 5000.0, 1);
     galaxy(bodies, 800, 1200.0, 160.0, -50.0, 100.0, 5000.0, 500.0, 2);
-    bh::PhysicsEngine engine(bodies);  // PNL:103
+    // argv[1] = "0,0,0": one PhysicsEngine over that device list (bh_create_multi_list)
+    std::vector<int> devices;
+    for (const char *q = argc > 1 ? argv[1] : ""; *q;) {
+        char *end = nullptr;
+        devices.push_back((int)std::strtol(q, &end, 10));
+        q = *end == ',' ? end + 1 : end;
+    }
+    std::unique_ptr<bh::PhysicsEngine> owner =
+        devices.empty() ? std::make_unique<bh::PhysicsEngine>(bodies)
+                        : std::make_unique<bh::PhysicsEngine>(bodies, devices);
+    bh::PhysicsEngine &engine = *owner;  // PNL:103
     oracle_engine *o = oracle_of(bodies, engine);
     std::vector<bh::Body> list2, list3;
     long removed = 0, quads = 0;
@@ -155,8 +166,9 @@ int main() {
         }
     }
     if (removed == 0) fail("the scene never merged: identity bookkeeping untested", 40);
-    std::printf("mirror_harness: 40 frames of bh::PhysicsEngine bit-identical to the oracle; "
-                "%ld bodies merged away, %ld quads checked\n", removed, quads);
+    std::printf("mirror_harness: 40 frames of bh::PhysicsEngine on %d device(s) bit-identical to "
+                "the oracle; %ld bodies merged away, %ld quads checked\n",
+                bh_multi_world(engine.handle()), removed, quads);
     oracle_destroy(o);
     return 0;
 }

@@ -19,13 +19,7 @@ tree of oracle/py_oracle.py in place of the HIP kernels:
     owners) and all-gathers the new positions, 16 B per body, in the bh_gather_slot layout;
   * velocities are all-gathered (same rounds and slots) before the next full build;
   * the merge rule (BHA:463-532) is replicated: removed bodies are tombstones until the end of
-    the call, then every replica compacts;
-  * the LET pipeline (engine.cpp spec_let_build): where no merge rule can act, a step's first LET
-    build reuses the previous (second) evaluation's subset, cells and halo with the positions
-    that build left in the rank's own copies (its jitter applied) -- nothing is selected and no
-    position is read from the exchange -- unless that build's jitter moved a body into another
-    depth-8 cell on some rank (a flag every rank learns from the exchanged tables; here one
-    all-reduce), in which case the next evaluation selects anew.
+    the call, then every replica compacts.
 
 The exchanged data is exactly what the engine exchanges, so a bit-identical final state on every
 rank (tests/test_dist_gloo.py) shows that the protocol carries everything the reference's
@@ -134,9 +128,7 @@ class MirrorRank:
         self.p = dict(params)
         self.rank, self.world, self.comm = rank, world, comm
         self.geo = Geometry(params["width_px"], params["height_px"])
-        self.stats = {"let": 0, "full": 0, "vel_syncs": 0, "max_subset": 0, "merged": 0,
-                      "spec": 0, "spec_off": 0}
-        self.spec = None
+        self.stats = {"let": 0, "full": 0, "vel_syncs": 0, "max_subset": 0, "merged": 0}
 
     # ---- caller-facing API (bh_reset_bodies / bh_step / bh_get_bodies) --------------------
     def reset_bodies(self, x, y, vx, vy, m):
@@ -147,17 +139,12 @@ class MirrorRank:
         self.st_morton = False
         self.vel_stale = False
         self.let_age = 0
-        self.spec = None
-        self._spec_allowed = False
 
     def step(self, k):
         for s in range(k):
             self._evaluate("drift", allow_let=True)
-            self._spec_allowed = s + 1 < k  # not the call's last step (engine.cpp spec_allowed)
             self._evaluate("kick", allow_let=s + 1 < k)  # the call's last build: the full tree
-            self._spec_allowed = False
             self._merge()
-        self.spec = None
         keep = ~self.dead  # one compaction per call; caller indices renumbered in order
         order = np.argsort(self.cidx[keep], kind="stable")
         rank_of = np.empty(len(order), dtype=np.int64)
@@ -204,7 +191,6 @@ class MirrorRank:
             self._evaluate_let(kick, gap2)
             self.let_age += 1
             return
-        self.spec = None
         self.let_age = 0
         self._sync_velocities()
         # full build, replicated: slots take the Morton order, then the reference's serial
@@ -265,9 +251,6 @@ class MirrorRank:
         n = len(self.x)
         sub, _ = shard_layout(None, n, self.world)
         own = list(self._own_lanes(n, sub))
-        spec, self.spec = self.spec, None
-        if kick == "drift" and spec is not None:  # the speculative build (engine.cpp)
-            return self._let_walk_and_exchange(kick, n, own, *spec, speculative=True)
         own_set = set(own)
         ecell = np.zeros(LET_CELLS, dtype=bool)
         flag_all = False
@@ -298,16 +281,7 @@ class MirrorRank:
                   or (not inside[i] and i in own_set)]
         self.stats["max_subset"] = max(self.stats["max_subset"], len(subset))
         pos = {i: (float(self.x[i]), float(self.y[i])) for i in subset}
-        return self._let_walk_and_exchange(kick, n, own, subset, ecell, hcell, pos,
-                                           speculative=False)
-
-    def _let_walk_and_exchange(self, kick, n, own, subset, ecell, hcell, pos, speculative):
-        """The subset's tree from positions `pos`, the table exchange, the walk of the own bodies,
-        the owner's kick and the position exchange (the part every LET evaluation shares)."""
-        import torch
-        g = self.geo
         self.stats["let"] += 1
-        self.stats["spec"] += int(speculative)
         # the subset's tree: insertion in caller order; jitter moves the subset's copies only
         bodies = {i: py_oracle.Body(pos[i][0], pos[i][1], 0.0, 0.0, float(self.m[i]))
                   for i in subset}
@@ -316,20 +290,6 @@ class MirrorRank:
         cells = {i: g.cell_of(bodies[i].x, bodies[i].y) if inside[i] else -1 for i in subset}
         ins = sorted((i for i in subset if inside[i]), key=lambda i: self.cidx[i])
         root = self._tree(ins, bodies)
-        if kick == "kick" and self._spec_allowed and not self._heavy_left():
-            # k_let_cross: did this build's jitter move a subset body into another cell?
-            def cell_now(i):
-                b = bodies[i]
-                return g.cell_of(b.x, b.y) if g.in_root(b.x, b.y) and not self.dead[i] else -1
-            crossed = any(cell_now(i) != cells[i]
-                          for i in subset if (bodies[i].x, bodies[i].y) != pos[i])
-            flag = torch.tensor([1 if crossed else 0], dtype=torch.int64)
-            self.comm.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
-            if int(flag.item()) == 0:
-                self.spec = (subset, ecell, hcell,
-                             {i: (bodies[i].x, bodies[i].y) for i in subset})
-            else:
-                self.stats["spec_off"] += 1
         members = {}
         for i in ins:
             members.setdefault(cells[i], []).append(i)
@@ -436,12 +396,6 @@ class MirrorRank:
 
         visit(0, 0)
         return acc[0], acc[1]
-
-    def _heavy_left(self):
-        """Whether the merge rule can still act (engine.cpp: heavy_possible)."""
-        if self.p["merge_min_dist"] <= 0.0:
-            return False
-        return bool(np.any(~self.dead & (self.m > self.p["merge_max_mass"])))
 
     # ---- merge (BHA:463-532), replicated -----------------------------------------------------
     def _merge(self):

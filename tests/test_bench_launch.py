@@ -38,8 +38,21 @@ def test_single_gpu_runs_in_process_with_verification():
     r = _run(["--dry-run"])
     assert r.returncode == 0, r.stderr
     plan = json.loads(r.stdout.strip().splitlines()[-1])
-    assert plan == {"launch": "in-process", "world": 1, "config": "c3", "theta": 0.5,
-                    "verify": True}
+    assert plan == {"launch": "in-process", "world": 1, "n_gpus": 1, "config": "c3",
+                    "theta": 0.5, "verify": True}
     r = _run(["--gpus", "4", "--dry-run"], {"WORLD_SIZE": "4", "RANK": "0", "LOCAL_RANK": "0"})
     plan = json.loads(r.stdout.strip().splitlines()[-1])
     assert plan["world"] == 4 and plan["config"] == "c4" and plan["verify"] is True
+
+
+def test_single_process_multi_gpu_stays_in_process():
+    """--single-process: one process, one engine handle over the N GPUs (bh_create_multi), no
+    torchrun child; refused under torchrun."""
+    r = _run(["--gpus", "8", "--single-process", "--dry-run"])
+    assert r.returncode == 0, r.stderr
+    plan = json.loads(r.stdout.strip().splitlines()[-1])
+    assert plan["launch"].startswith("single process") and plan["n_gpus"] == 8
+    assert plan["world"] == 1 and plan["config"] == "c4" and plan["verify"] is True
+    r = _run(["--gpus", "4", "--single-process", "--dry-run"],
+             {"WORLD_SIZE": "4", "RANK": "0", "LOCAL_RANK": "0"})
+    assert r.returncode == 2 and "torchrun" in r.stderr

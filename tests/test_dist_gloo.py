@@ -71,9 +71,9 @@ def _worker(rank, world, port, out_dir, params=None):
 
 @pytest.mark.parametrize("world,merge", [(2, True), (3, True), (2, False), (3, False)])
 def test_exchange_protocol_matches_the_reference_step(tmp_path, world, merge):
-    """merge=False: no merge rule, so the LET pipeline runs -- a step's first LET build reuses
-    the previous evaluation's subset with the positions its build left (engine.cpp
-    spec_let_build)."""
+    """Every rank of a world-2/3 gloo group runs the engine's exchange protocol (LET builds,
+    table and position all-gathers, velocity syncs, replicated merge rule) with and without the
+    merge rule; every rank's final state equals the oracle's bit for bit."""
     import bh_amd  # noqa: F401  (the engine library's host-only shard layout must load)
     import oracle
 
@@ -94,10 +94,6 @@ def test_exchange_protocol_matches_the_reference_step(tmp_path, world, merge):
         assert stats["let"] == 2 * sum(CALLS) - len(CALLS) - 1 and stats["full"] == len(CALLS) + 1
         assert stats["vel_syncs"] == len(CALLS)
         assert stats["merged"] == len(arrs[0]) - len(want[0])
-        # speculative builds: the first build of every step after the first of each call
-        assert stats["spec"] + stats["spec_off"] == (0 if merge else sum(CALLS) - len(CALLS)), stats
-        if not merge:
-            assert stats["spec"] >= 1, stats
         # every rank owns bodies; at world 3 a rank builds a part of the scene only
         assert 0 < stats["max_subset"] <= len(arrs[0])
         if world == 3:

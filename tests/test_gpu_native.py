@@ -18,11 +18,41 @@ pytestmark = pytest.mark.gpu
 BIN = os.path.join(os.path.dirname(__file__), "c", "bin")
 
 
-@pytest.mark.parametrize("exe", ["abi_harness", "mirror_harness"])
-def test_native_harness(exe):
+@pytest.mark.parametrize("exe,devices", [("abi_harness", None), ("mirror_harness", None),
+                                         ("abi_harness", "0,0,0"), ("mirror_harness", "0,0")])
+def test_native_harness(exe, devices):
+    """devices: the same frames through ONE engine handle over that device list (repeats: the
+    members exchange by device-to-device copies) -- the Kotlin drop-in's Native.create with
+    BH_DEVICES set, the C++ mirror's multi-device constructor."""
     path = os.path.join(BIN, exe)
     assert os.path.exists(path), f"{path} missing: run __graft_entry__.build()"
-    r = subprocess.run([path], capture_output=True, text=True, timeout=110)
+    env = dict(os.environ)
+    args = [path]
+    if devices:
+        env["BH_MULTI_MIN_BODIES"] = "0"  # the decomposition even for these small scenes
+        if exe == "abi_harness":
+            env["BH_DEVICES"] = devices
+        else:
+            args.append(devices)
+    r = subprocess.run(args, capture_output=True, text=True, timeout=110, env=env)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "bit-identical to the oracle" in r.stdout
+    if devices:
+        assert f"on {len(devices.split(','))} device(s)" in r.stdout, r.stdout
+    if exe == "abi_harness":
+        assert "0 shadow allocations after the constructor" in r.stdout, r.stdout
     print(r.stdout.strip())
+
+
+def test_drop_in_frame_cost_at_c3():
+    """The Kotlin drop-in's per-frame host work at C3 (1e6 bodies) beside the GPU step, through
+    the real JNI glue: no allocation per frame, and the host side (in-place compare, getInto
+    from the pinned mirror, unpack into the Body objects) reported in ms per frame."""
+    import json
+    path = os.path.join(BIN, "abi_harness")
+    r = subprocess.run([path, "--c3-frames", "20"], capture_output=True, text=True, timeout=110)
+    assert r.returncode == 0, r.stdout + r.stderr
+    line = json.loads(r.stdout.strip().splitlines()[-1])
+    assert line["bodies"] > 990_000 and line["allocations_per_frame"] == 0.0, line
+    assert line["uploads"] == 0, line  # the caller never edited the bodies
+    print(json.dumps(line))

@@ -1200,41 +1200,37 @@ def test_one_step_calls_then_reconfigure_checkpoint_and_evaluate(tmp_path):
     assert eng.num_bodies() < len(x) - nh // 2
 
 
-@pytest.mark.parametrize("world,edge_pairs", [(4, False), (8, False), (4, True)])
-def test_let_speculative_build_matches_single(world, edge_pairs, monkeypatch):
-    """The LET pipeline: a step's first locally essential tree is built beside the previous
-    evaluation's rounds from that evaluation's subset, with the positions its build left (the
-    jitter, BHA:146-151, applied), and taken over by the next evaluation -- every rank's state
-    equals the single-GPU engine's bit for bit.  With coincident pairs straddling depth-8 grid
-    lines (x = 1200 and y = 400 are depth-8 cell edges at the 2400x800 root) the jitter moves bodies into the
-    neighbouring cell: those evaluations call the speculation off (and select anew) and the
-    states still match.  (BH_LET_SPEC=1 switches the pipeline on.)"""
-    monkeypatch.setenv("BH_LET", "1")
-    monkeypatch.setenv("BH_LET_SPEC", "1")
-    x, y, vx, vy, m = (a.copy() for a in scenes.uniform(150_000, 0.5, seed=29))
-    if edge_pairs:
-        ex = np.repeat(np.concatenate([1200.0 + np.array([-6e-4, -4e-4, -2e-4, 2e-4, 4e-4, 6e-4]),
-                                       np.linspace(300.0, 700.0, 10)]), 2)
-        ey = np.repeat(np.concatenate([np.linspace(100.0, 700.0, 6),
-                                       400.0 + np.linspace(-6e-4, 6e-4, 10)]), 2)
-        k = len(ex)
-        x, y = np.concatenate([x, ex]), np.concatenate([y, ey])
-        vx, vy = np.concatenate([vx, np.zeros(k)]), np.concatenate([vy, np.zeros(k)])
-        m = np.concatenate([m, np.full(k, 0.5)])
-    arrs = (x, y, vx, vy, m)
-    params = bh_amd.default_params(theta=0.5, merge_min_dist=0.0)
-    single = bh_amd.Engine(params, device=0)
-    single.reset_bodies(*arrs)
-    for k in (5, 4):
-        single.step(k)
-    want = single.get_bodies()
-    single.close()
-    got, stats = _run_group(world, params, arrs, (5, 4))
-    for r in range(world):
-        assert stats[r]["spec_builds"] >= 1, stats[r]
-        if edge_pairs:
-            assert stats[r]["spec_fallbacks"] >= 1, stats[r]
-        assert stats[r]["spec_builds"] + stats[r]["spec_fallbacks"] == 7, stats[r]
-        for k, name in enumerate(FIELDS):
-            assert bits_equal(got[r][k], want[k]), f"rank {r}: {name}"
-    assert len({tuple(s.values()) for s in stats}) <= world  # (stats may differ by subset size)
+def test_carried_tree_error_is_reported_by_the_call_that_uses_it():
+    """A call's last step builds the next call's first tree beside its second traversal
+    (BH_PIPE_LAST).  That build belongs to the next step() (BHA:407): an error flag it raises
+    (injected here: bh_debug_inject(2 + k) flags the k-th next full build as the jitter replay's
+    unsupported-geometry guard would) must fail the NEXT call, not the one that queued it -- and
+    the call after that must check its own tree again.  The states stay the oracle's throughout
+    (the injected flag does not change the tree)."""
+    arrs = _frames_scene()
+    eng, ref = _pair(arrs, theta=0.5)
+    for _ in range(2):
+        eng.step(1)
+        ref.step(1)
+    eng.debug_inject(3)  # build #0: this call's second build; #1: its last (carried) build
+    eng.step(1)          # the carried tree's flag is not this call's
+    ref.step(1)
+    _assert_state_equal(eng, ref)
+    with pytest.raises(bh_amd.BhError) as err:
+        eng.step(1)      # this call's first step uses the flagged tree
+    assert err.value.rc == bh_amd.BH_E_STATE
+    ref.step(1)
+    _assert_state_equal(eng, ref)
+    eng.step(1)          # a clean tree again
+    ref.step(1)
+    _assert_state_equal(eng, ref)
+    eng.debug_inject(2)  # the next build: this call's own second build
+    with pytest.raises(bh_amd.BhError) as err:
+        eng.step(1)
+    assert err.value.rc == bh_amd.BH_E_STATE
+    ref.step(1)
+    _assert_state_equal(eng, ref)
+    for _ in range(3):
+        eng.step(1)
+        ref.step(1)
+    _assert_state_equal(eng, ref)
