@@ -144,6 +144,21 @@ __device__ __forceinline__ void chain_prio() {
 #define BH_XCD_RUN 16
 #endif
 #ifdef __HIP__  // HIP translation units only (engine.cpp is host C++)
+// Max over the wave of max(|vx|, |vy|) (every lane of the wave must call it; lanes without a body
+// pass 0) into *vmax as the bits of a non-negative double -- ordered like the values -- with one
+// atomic per wave; a non-finite speed counts as +inf.
+__device__ __forceinline__ void wave_vmax(unsigned long long *vmax, double vx, double vy) {
+    const double ax = __builtin_fabs(vx), ay = __builtin_fabs(vy);
+    double v = ax > ay ? ax : ay;
+    if (!(ax <= 1.7976931348623157e308 && ay <= 1.7976931348623157e308)) v = __builtin_inf();
+    unsigned long long b = (unsigned long long)__double_as_longlong(v);
+    for (int o = 32; o > 0; o >>= 1) {
+        const unsigned long long c = __shfl_xor(b, o, 64);
+        b = c > b ? c : b;
+    }
+    if ((threadIdx.x & 63) == 0 && b) atomicMax(vmax, b);
+}
+
 template <uint32_t RUN = BH_XCD_RUN>
 __device__ __forceinline__ uint32_t xcd_block() {
     uint32_t b = blockIdx.x;
@@ -335,6 +350,9 @@ struct KickArgs {
     // sv[perm[p]] + a dt/2 (the build's permutation of v, fused; null: in place)
     const double *svx = nullptr, *svy = nullptr;
     const uint32_t *perm = nullptr;
+    // KICK_OWN_DRIFT: max over the launch's bodies of max(|vx|, |vy|) after the kick, as the bits
+    // of a non-negative double (atomicMax; non-finite -> +inf): the drift's displacement bound
+    unsigned long long *vmax = nullptr;
 };
 // Diagnostic counters of the counting walk (all per evaluation): per body, the non-empty
 // nodes visited (BHA:216 passed) and the point-force contributions (accepted internal nodes
@@ -432,7 +450,30 @@ struct LetBufs {
     uint32_t *lanes;          // [n] lane -> subset slot (own pieces)
     void *scratch;
     size_t scratch_bytes;
+    // the selection's restriction to candidate slot blocks (let_select, LetSweep)
+    uint8_t *own_blk;         // [n / 256 + 2] the block holds an own body
+    uint32_t *rowmask;        // [256 * 8] built cells as one 256-bit mask per grid row
+    unsigned long long *vmax; // [nvmax] drift speed bounds: own, then every rank's (cleared
+    int nvmax;                //   by the selection, after every reader of the last ones)
 };
+// Which 256-slot blocks of the replicated state the selection scans.  The state keeps the slot
+// order of the last full build between full builds, so each block's bodies then occupied a small
+// box of depth-LET_P cells (box: col_lo | col_hi << 8 | row_lo << 16 | row_hi << 24; lo > hi: no
+// body in the root).  Since then no body moved farther than disp[0] (the drifts' bound: max
+// speed x dt per drift, every rank's maximum exchanged) + allow (jitter, 2 x 2e-3 per build), so a
+// body that lies in a built cell now lies in its block's box widened by floor(D / w) + 1 cells.
+// Blocks whose widened box holds no built cell and no own body are skipped: the subset is the
+// same, bit for bit (valid = false, or a bound beyond 64 cells: every block is scanned).
+struct LetSweep {
+    const uint32_t *box;
+    const double *disp;
+    double allow;
+    bool valid;
+};
+// the boxes of the state's 256-slot blocks (after a full build, every rank alike)
+void let_boxes(int64_t n, const BodyState &st, const Geometry &g, uint32_t *box, hipStream_t s);
+// disp[0] += max(bits of vmax[0 .. k)) x dt (non-finite: +inf)
+void let_disp_add(double *disp, const unsigned long long *vmax, int k, double dt, hipStream_t s);
 // Largest gap^2 (in cells) at which a depth-LET_P cell may still be opened by a body of a cell
 // at that gap; cells beyond it are accepted by every such body.  < 0: the LET does not apply.
 double let_include_gap2(const Geometry &g, double theta2, double soft2);
@@ -455,7 +496,8 @@ struct PosSrc {
 // assignment (k_morton + k_bucket_count of tree_build, which then sets keys_ready)
 hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
                       const LetPieces &pc, double gap2, const LetBufs &L, const BodyState &sub,
-                      int64_t S, uint32_t *scal, hipStream_t s, const MortonFuse &mf = {});
+                      int64_t S, uint32_t *scal, hipStream_t s, const MortonFuse &mf = {},
+                      const LetSweep &sw = {});
 // gslot[lanes[q]] = gather_slot(gl, q) (lanes null: the identity map)
 void let_gather_slots(int64_t n, const uint32_t *lanes, GatherLayout gl, uint32_t *gslot,
                       hipStream_t s);
@@ -497,7 +539,7 @@ void direct_forces(const LeafList &L, const uint32_t *d_count, const double *x, 
 // lane q's acceleration at a2[2 * gather_slot(gl, q)]
 void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
                 double dtHalf, double dt, hipStream_t s, const uint32_t *lanes = nullptr,
-                GatherLayout gl = GatherLayout{});
+                GatherLayout gl = GatherLayout{}, unsigned long long *vmax = nullptr);
 struct MergePair;
 // (box: the merge mailbox, whose header it clears for the overlapped merge rule, or null)
 void copy_trav_inputs(int64_t n, const double *m, double *m_t, const uint32_t *cidx,

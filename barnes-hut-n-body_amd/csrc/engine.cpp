@@ -203,6 +203,13 @@ struct bh_engine {
                                 // others are exchanged before the next full build
     LetBufs L{};
     int64_t let_cap = 0;        // n capacity of the per-body LET arrays
+    // the selection's candidate blocks (let.hip LetSweep): the boxes of the state's 256-slot
+    // blocks at the last full build, and the displacement bound since (disp[0]; the speed words
+    // after it: own, then every rank's, exchanged at the end of every drifting LET evaluation)
+    uint32_t *let_box = nullptr;
+    double *disp = nullptr;
+    bool boxes_valid = false;
+    int builds_since_box = 0;   // builds since then that may have jittered positions
     int64_t let_sub_cap = 0;    // subset capacity of the subset tree workspace
     int let_J = -1;
     size_t let_node_cap = 0;
@@ -358,6 +365,7 @@ enum CollSite {
     COLL_TABLE = 4,     // the LET cell tables
     COLL_FLAGS = 5,     // the end-of-call LET status words, max all-reduce
     COLL_SETTINGS = 6,  // the per-process settings check at creation (min and max all-reduce)
+    COLL_VMAX = 7,      // every rank's drift speed bound (LET selection), after a drifting round
 };
 enum CollStream { CS_MAIN = 0, CS_COMM = 1 };
 void coll_log(bh_engine *e, int site, int64_t bytes, int stream) {
@@ -749,6 +757,14 @@ int let_alloc(bh_engine *e, int64_t n_sub, hipStream_t s = nullptr) {
         TRY(dev_alloc(e, e->inv_lanes, cap));
         e->inv_valid = false;
         TRY(dev_alloc(e, L.own, cap));
+        TRY(dev_alloc(e, L.own_blk, let_sel_blocks(cap) + 2));
+        TRY(dev_alloc(e, L.rowmask, 256 * 8));
+        TRY(dev_alloc(e, e->let_box, let_sel_blocks(cap) + 2));
+        TRY(dev_alloc(e, e->disp, 2 + (size_t)e->world));
+        HIPCHK(e, hipMemsetAsync(e->disp, 0, sizeof(double) * (2 + (size_t)e->world), s));
+        L.vmax = reinterpret_cast<unsigned long long *>(e->disp + 1);
+        L.nvmax = 1 + e->world;
+        e->boxes_valid = false;
         TRY(alloc_state(e, e->sub_src, cap));
         e->let_cap = cap;
     }
@@ -986,6 +1002,24 @@ int exchange_tables(bh_engine *e, hipStream_t s) {
     return BH_OK;
 }
 
+// Every rank's drift speed bound (its own bodies' max |v| after the kick, L.vmax[0]) into
+// L.vmax[1 + rank], on the exchange stream behind the rounds (which it waited for): RCCL, or the
+// peers' words copied (in-process group).  A solo rank has no peers: its own word is the bound.
+int gather_vmax(bh_engine *e) {
+    coll_log(e, COLL_VMAX, (int64_t)sizeof(unsigned long long) * e->world, CS_COMM);
+    if (e->comm) {
+        NCCLCHK(e, ncclAllGather(e->L.vmax, e->L.vmax + 1, 1, ncclUint64, e->comm,
+                                 e->comm_stream));
+    } else if (e->group) {
+        for (bh_engine *peer : e->group->members)
+            if (peer != e)
+                HIPCHK(e, hipMemcpyAsync(e->L.vmax + 1 + peer->rank, peer->L.vmax,
+                                         sizeof(unsigned long long), hipMemcpyDeviceToDevice,
+                                         e->comm_stream));
+    }
+    return BH_OK;
+}
+
 int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     *done = false;
     if (kick != KICK_DRIFT && kick != KICK_ONLY) return BH_OK;
@@ -1039,8 +1073,13 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         if (fuse)
             mf = MortonFuse{e->s_keys, e->s_keys32, e->s_spl, e->s_spl_nb, e->s_cnt, e->s_base,
                             e->s_bcount};
+        // only the slot blocks that may hold a body of a built cell (LetSweep): the jitter of
+        // every build since the boxes moved a body by at most 2 x 2e-3 per axis (BHA:146-151)
+        const LetSweep sw{e->let_box, e->disp, 4.0e-3 * (double)(e->builds_since_box + 1),
+                          e->boxes_valid};
         HIPCHK(e, let_select(e->st, ps, e->geo, pc, gap2, e->L, e->sub_src, S, e->scalars,
-                             e->stream, mf));
+                             e->stream, mf, sw));
+        ++e->builds_since_box;
         if (e->let_known > 0) {
             if (!e->sub_cnt_h) {
                 HIPCHK(e, hipHostMalloc((void **)&e->sub_cnt_h, 64, hipHostMallocDefault));
@@ -1083,8 +1122,10 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     TRY(mark(e, 0));
     const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};
     const int W = 2;  // (x, y) per lane
-    const KickArgs ka{kick == KICK_DRIFT ? KICK_OWN_DRIFT : KICK_OWN_ONLY, e->st.vx, e->st.vy,
-                      e->p.dt * 0.5, e->p.dt, lanes};  // BHA:412
+    KickArgs ka{kick == KICK_DRIFT ? KICK_OWN_DRIFT : KICK_OWN_ONLY, e->st.vx, e->st.vy,
+                e->p.dt * 0.5, e->p.dt, lanes};  // BHA:412
+    const bool bound = kick == KICK_DRIFT && e->boxes_valid;  // the drift's speed bound
+    if (bound) ka.vmax = e->L.vmax;
     const GatherLayout gl = shard_layout(n, e->world);
     // measurement: the peers' bodies keep their positions (already in a2 after a LET evaluation)
     if (e->solo && !e->pos_pending) let_fill_pos(n, lanes, e->st.x, e->st.y, e->a2, gl, e->stream);
@@ -1107,9 +1148,14 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         if (e->group) e->group->barrier();
         TRY(gather_round(e, gl, k, W, k, COLL_POS));
     }
+    if (bound) TRY(gather_vmax(e));  // behind the last round, on the exchange stream
     TRY(mark(e, 1));
     HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
     HIPCHK(e, hipStreamWaitEvent(e->stream, e->gathered_ev, 0));
+    if (bound) {  // the bound now covers every rank's drift
+        let_disp_add(e->disp, e->L.vmax, e->L.nvmax, e->p.dt, e->stream);
+        HIPCHK(e, hipGetLastError());
+    }
     TRY(mark(e, 4));
     e->pos_pending = true;  // every body's new position is in a2 (by lane, gather slots)
     e->pos_lanes = lanes;
@@ -1186,6 +1232,16 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
         TRY(sync_velocities(e));        // before the full build permutes the state
         TRY(mark(e, -1));
         TRY(build(e));
+        if ((e->comm || e->group || e->solo) && let_active(e) && e->p.theta != 0.0 && n > 0) {
+            // the LET selections until the next full build scan only the slot blocks whose box
+            // (the cells of their bodies now, in this build's slot order) may reach a built cell
+            TRY(let_alloc(e, 0));
+            let_boxes(n, e->st, e->geo, e->let_box, e->stream);
+            HIPCHK(e, hipGetLastError());
+            HIPCHK(e, hipMemsetAsync(e->disp, 0, sizeof(double), e->stream));
+            e->boxes_valid = true;
+            e->builds_since_box = 0;
+        }
         TRY(mark(e, 0));
     }
     e->forces_ready = false;
@@ -1413,6 +1469,7 @@ int finish_merges(bh_engine *e, uint32_t *overflow, uint32_t *tree_flags = nullp
     HIPCHK(e, compact_state(n, e->keep, e->st, e->alt, e->dead_sorted, nd, e->pos, e->scratch,
                             e->scratch_bytes, e->stream));
     std::swap(e->st, e->alt);
+    e->boxes_valid = false;  // the slots moved
     if (e->lanes_valid) {  // carry the wave grouping over the removals (no re-sort)
         HIPCHK(e, compact_lanes(n, e->lanes, e->keep, e->pos, e->idx, e->keys32, e->keys32_s,
                                 e->scratch, e->scratch_bytes, e->stream));
@@ -1498,6 +1555,7 @@ int restore(bh_engine *e) {
     e->lanes_valid = e->lr_pending = e->lr_ready = false;
     e->inv_valid = false;
     e->pos_pending = false;  // the snapshot holds every position
+    e->boxes_valid = false;
     e->heavy_possible = true;
     e->tree_valid = false;
     e->st_morton = false;
@@ -1919,8 +1977,12 @@ int step_once(bh_engine *e, bool last) {
         if (!fused) {
             TRY(mark(e, -1));
             kick_drift(n, e->a2, e->st.x, e->st.y, e->st.vx, e->st.vy, dtHalf, e->p.dt,
-                       e->stream, e->a2_lanes, e->a2_layout);
+                       e->stream, e->a2_lanes, e->a2_layout, e->boxes_valid ? e->L.vmax : nullptr);
             HIPCHK(e, hipGetLastError());
+            if (e->boxes_valid) {  // every rank drifted every body: its own bound is everyone's
+                let_disp_add(e->disp, e->L.vmax, e->L.nvmax, e->p.dt, e->stream);
+                HIPCHK(e, hipGetLastError());
+            }
             TRY(mark(e, 2));
         }
         // the call's last build: a full tree for getTreeForDebug (lastTree, BHA:435) -- or, on a
@@ -2243,6 +2305,7 @@ int bh::quads_prepare(bh_engine *e) {
                 unpermute_positions(n, e->perm, tb.dst.x, tb.dst.y, e->st.x, e->st.y, e->stream);
                 HIPCHK(e, hipGetLastError());
                 e->mir_fresh = false;
+                ++e->builds_since_box;  // (its jitter, for the LET selection's bound)
             }
             e->spl_nb = 0;  // k_prep wrote splitters of this order
             e->keys_ready = false;
@@ -2506,7 +2569,7 @@ void bh_destroy(bh_engine *e) {
     if (e->sub_cnt_ev) (void)hipEventDestroy(e->sub_cnt_ev);
     if (e->sub_cnt_h) (void)hipHostFree(e->sub_cnt_h);
     if (e->table_ev) (void)hipEventDestroy(e->table_ev);
-    void *lets[] = {e->inv_lanes, e->L.csrc, e->L.ccnt, e->L.cpos, e->solo_table, e->solo_all, e->solo_cstart, e->L.ecell, e->L.hcell, e->L.own, e->L.subpos, e->L.flag_all, e->L.flag8, e->L.sel, e->L.selpos, e->L.cstart,
+    void *lets[] = {e->L.own_blk, e->L.rowmask, e->let_box, e->disp, e->inv_lanes, e->L.csrc, e->L.ccnt, e->L.cpos, e->solo_table, e->solo_all, e->solo_cstart, e->L.ecell, e->L.hcell, e->L.own, e->L.subpos, e->L.flag_all, e->L.flag8, e->L.sel, e->L.selpos, e->L.cstart,
                     e->L.table, e->L.tables, e->L.levels, e->L.w, e->L.posc, e->L.bsz,
                     e->L.nodes, e->L.lanes, e->s_keys, e->s_keys_s, e->s_spl, e->s_keys32,
                     e->s_keys32_s, e->s_idx, e->s_perm, e->s_cpl, e->s_cnt, e->s_base,
@@ -2561,6 +2624,7 @@ int bh_set_params(bh_engine *e, const bh_params *p) {
         TRY(drop_carried_flags(e));
         e->prebuilt = false;
         e->lt_aside = false;
+        e->boxes_valid = false;  // another grid
         e->geo = g;
         e->tree_valid = false;
         e->lazy_tree = false;
@@ -2638,6 +2702,7 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     e->vel_stale = false;
     e->pos_pending = false;
     e->inv_valid = false;
+    e->boxes_valid = false;
     return BH_OK;
 }
 

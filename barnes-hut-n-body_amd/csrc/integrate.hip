@@ -20,17 +20,21 @@ __global__ __launch_bounds__(TB) void k_kick_drift(int64_t n, const double *__re
                                                    double *__restrict__ vx,
                                                    double *__restrict__ vy, double dtHalf,
                                                    double dt, const uint32_t *__restrict__ lanes,
-                                                   GatherLayout gl) {
+                                                   GatherLayout gl,
+                                                   unsigned long long *__restrict__ vmax) {
     int64_t i = (int64_t)blockIdx.x * TB + threadIdx.x;
-    if (i >= n) return;
-    const double2_t a = *reinterpret_cast<const double2_t *>(a2 + 2 * gather_slot(gl, i));
-    const int64_t p = lanes ? (int64_t)lanes[i] : i;
-    double vxi = vx[p] + a.x * dtHalf;
-    double vyi = vy[p] + a.y * dtHalf;
-    vx[p] = vxi;
-    vy[p] = vyi;
-    x[p] = x[p] + vxi * dt;
-    y[p] = y[p] + vyi * dt;
+    double vxi = 0.0, vyi = 0.0;
+    if (i < n) {
+        const double2_t a = *reinterpret_cast<const double2_t *>(a2 + 2 * gather_slot(gl, i));
+        const int64_t p = lanes ? (int64_t)lanes[i] : i;
+        vxi = vx[p] + a.x * dtHalf;
+        vyi = vy[p] + a.y * dtHalf;
+        vx[p] = vxi;
+        vy[p] = vyi;
+        x[p] = x[p] + vxi * dt;
+        y[p] = y[p] + vyi * dt;
+    }
+    if (vmax) wave_vmax(vmax, vxi, vyi);  // (multi-rank: the LET selection's displacement bound)
 }
 
 // The same kick + drift by lane of the traversal's lane map, after an evaluation that was made
@@ -659,8 +663,10 @@ hipError_t compact_lanes(int64_t n, const uint32_t *lanes, const uint32_t *keep,
 }
 
 void kick_drift(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,
-                double dtHalf, double dt, hipStream_t s, const uint32_t *lanes, GatherLayout gl) {
-    if (n > 0) k_kick_drift<<<grid_for(n), TB, 0, s>>>(n, a2, x, y, vx, vy, dtHalf, dt, lanes, gl);
+                double dtHalf, double dt, hipStream_t s, const uint32_t *lanes, GatherLayout gl,
+                unsigned long long *vmax) {
+    if (n > 0)
+        k_kick_drift<<<grid_for(n), TB, 0, s>>>(n, a2, x, y, vx, vy, dtHalf, dt, lanes, gl, vmax);
 }
 
 void kick_drift_keys(int64_t n, const double *a2, double *x, double *y, double *vx, double *vy,

@@ -110,6 +110,7 @@ __global__ __launch_bounds__(TB) void k_let_mark(LetPieces pc, PosSrc ps,
                                                  const double *__restrict__ y,
                                                  const uint32_t *__restrict__ cidx, Geometry g,
                                                  uint8_t *__restrict__ own,
+                                                 uint8_t *__restrict__ own_blk,
                                                  uint8_t *__restrict__ ecell,
                                                  uint32_t *__restrict__ flag_all) {
     const int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
@@ -118,6 +119,7 @@ __global__ __launch_bounds__(TB) void k_let_mark(LetPieces pc, PosSrc ps,
     if (q >= pc.n) return;
     const int64_t i = pc.lanes ? (int64_t)pc.lanes[q] : q;
     own[i] = 1;
+    own_blk[i >> 8] = 1;  // the selection scans this slot's block whatever its box
     if (cidx[i] & CIDX_DEAD) return;  // tombstones do not walk
     double px, py;
     if (ps.a2) {  // lane q's position in the exchange buffer
@@ -140,7 +142,8 @@ __global__ __launch_bounds__(TB) void k_let_mark(LetPieces pc, PosSrc ps,
 __global__ __launch_bounds__(TB) void k_let_halo(const uint8_t *__restrict__ ecell,
                                                  const uint32_t *__restrict__ flag_all,
                                                  double gap2, int K,
-                                                 uint8_t *__restrict__ hcell) {
+                                                 uint8_t *__restrict__ hcell,
+                                                 uint32_t *__restrict__ rowmask) {
     const int64_t c = (int64_t)blockIdx.x * TB + threadIdx.x;
     if (c >= LET_CELLS) return;
     uint8_t h = (*flag_all != 0u) ? 1 : ecell[c];
@@ -162,6 +165,71 @@ __global__ __launch_bounds__(TB) void k_let_halo(const uint8_t *__restrict__ ece
         }
     }
     hcell[c] = h;
+    if (h) atomicOr(rowmask + iy * 8 + (ix >> 5), 1u << (ix & 31));
+}
+
+// Whether the rectangle [c0, c1] x [r0, r1] of grid cells holds a built cell (rowmask): the
+// wave's lanes take a row each.
+__device__ __forceinline__ bool rect_any(const uint32_t *__restrict__ rowmask, int c0, int c1,
+                                         int r0, int r1) {
+    bool any = false;
+    const int w0 = c0 >> 5, w1 = c1 >> 5;
+    for (int r = r0 + (int)(threadIdx.x & 63); r <= r1 && !any; r += 64)
+        for (int w = w0; w <= w1; ++w) {
+            uint32_t m = rowmask[r * 8 + w];
+            if (w == w0) m &= ~0u << (c0 & 31);
+            if (w == w1 && (c1 & 31) != 31) m &= (2u << (c1 & 31)) - 1u;
+            if (m) {
+                any = true;
+                break;
+            }
+        }
+    return __ballot(any) != 0ull;
+}
+
+// The box of depth-LET_P cells of each 256-slot block's bodies (one wave per block, four slots
+// per lane): live bodies with a finite position, those outside the root by the cell of their
+// projection (grid_col clamps; a clamped column moves no more than the body does).
+__global__ __launch_bounds__(64) void k_let_boxes(int64_t n, const double *__restrict__ x,
+                                                  const double *__restrict__ y,
+                                                  const uint32_t *__restrict__ cidx, Geometry g,
+                                                  uint32_t *__restrict__ box) {
+    const int64_t b0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    const double w = 2.0 * g.h[LET_P];
+    const int top = (1 << LET_P) - 1;
+    uint32_t clo = 255, chi = 0, rlo = 255, rhi = 0;
+    bool any = false;
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+        const int64_t i = b0 + 64 * u;
+        if (i >= n || (cidx[i] & CIDX_DEAD)) continue;
+        const double px = x[i], py = y[i];
+        if (!__builtin_isfinite(px) || !__builtin_isfinite(py)) continue;
+        const uint32_t c = grid_col(px, g.root_cx - g.root_h, w, top);
+        const uint32_t r = grid_col(py, g.root_cy - g.root_h, w, top);
+        clo = min(clo, c);
+        chi = max(chi, c);
+        rlo = min(rlo, r);
+        rhi = max(rhi, r);
+        any = true;
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        clo = min(clo, (uint32_t)__shfl_xor((int)clo, o, 64));
+        chi = max(chi, (uint32_t)__shfl_xor((int)chi, o, 64));
+        rlo = min(rlo, (uint32_t)__shfl_xor((int)rlo, o, 64));
+        rhi = max(rhi, (uint32_t)__shfl_xor((int)rhi, o, 64));
+    }
+    const bool some = __ballot(any) != 0ull;
+    if (threadIdx.x == 0)
+        box[blockIdx.x] = some ? (clo | chi << 8 | rlo << 16 | rhi << 24) : 0x00FF00FFu;
+}
+
+__global__ void k_let_disp_add(double *disp, const unsigned long long *vmax, int k, double dt) {
+    unsigned long long b = 0;
+    for (int q = 0; q < k; ++q) b = vmax[q] > b ? vmax[q] : b;
+    const double v = __longlong_as_double((long long)b);
+    const double d = disp[0] + v * dt;
+    disp[0] = d >= 0.0 ? d : __builtin_inf();  // (NaN: no bound)
 }
 
 // the subset: bodies of built cells, and own bodies outside the tree (they still walk it, or
@@ -176,8 +244,33 @@ __global__ __launch_bounds__(64) void k_let_flags(LetPieces pc, PosSrc ps,
                                                   const uint8_t *__restrict__ hcell,
                                                   const uint8_t *__restrict__ own,
                                                   uint8_t *__restrict__ flag8,
-                                                  uint32_t *__restrict__ bcnt) {
+                                                  uint32_t *__restrict__ bcnt, LetBufs L,
+                                                  LetSweep sw) {
     const int64_t b0 = (int64_t)blockIdx.x * 256 + threadIdx.x;
+    if (sw.valid && *L.flag_all == 0u && !L.own_blk[blockIdx.x]) {
+        // a candidate block: its box widened by the displacement bound holds a built cell
+        const uint32_t bx = sw.box[blockIdx.x];
+        const int clo = (int)(bx & 255u), chi = (int)((bx >> 8) & 255u);
+        const int rlo = (int)((bx >> 16) & 255u), rhi = (int)(bx >> 24);
+        const double D = (sw.disp[0] + sw.allow) * (1.0 + 1e-9);
+        const double mw = D * (1.0 / (2.0 * g.h[LET_P]));
+        bool cand = true;
+        if (clo > chi) {
+            cand = false;  // no live finite body in this block at the full build
+        } else if (mw < 64.0) {
+            const int m = (int)mw + 1;
+            const int top = (1 << LET_P) - 1;
+            cand = rect_any(L.rowmask, max(clo - m, 0), min(chi + m, top), max(rlo - m, 0),
+                            min(rhi + m, top));
+        }
+        if (!cand) {  // (flag8 stays stale here: k_let_gather skips empty blocks)
+            if (threadIdx.x == 0) {
+                bcnt[blockIdx.x] = 0u;
+                if (blockIdx.x + 1 == gridDim.x) bcnt[gridDim.x] = 0u;
+            }
+            return;
+        }
+    }
     uint32_t count = 0;
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
@@ -238,6 +331,7 @@ __global__ __launch_bounds__(TB) void k_let_gather(int64_t n, PosSrc ps,
             if (mf.keys) let_fuse_key(g, mf, i, sentinel_key(g.J));
         }
     }
+    if (bpos[blockIdx.x + 1] == bpos[blockIdx.x]) return;  // nothing selected (or not scanned)
     const bool f = i < n && flag8[i];
     const uint64_t m = __ballot(f);
     const uint32_t w = threadIdx.x >> 6;
@@ -712,35 +806,45 @@ size_t let_scratch_bytes(int64_t n) {
 static_assert(LET_CELLS % 16 == 0, "ecell is cleared in 16-byte stores");
 __global__ __launch_bounds__(TB) void k_let_clear(int64_t n, uint8_t *__restrict__ own,
                                                   uint8_t *__restrict__ ecell,
-                                                  uint32_t *__restrict__ flag_all) {
+                                                  uint32_t *__restrict__ flag_all,
+                                                  uint8_t *__restrict__ own_blk, int64_t nb,
+                                                  uint32_t *__restrict__ rowmask,
+                                                  unsigned long long *__restrict__ vmax,
+                                                  int nvmax) {
     const int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
     const uint4 z = make_uint4(0u, 0u, 0u, 0u);
     const int64_t nv = n >> 4;
     if (t < nv) reinterpret_cast<uint4 *>(own)[t] = z;
     if (t < (n & 15)) own[(nv << 4) + t] = 0;
     if (t < LET_CELLS / 16) reinterpret_cast<uint4 *>(ecell)[t] = z;
+    if (t < nb) own_blk[t] = 0;
+    if (t < 256 * 8) rowmask[t] = 0u;
+    if (t < nvmax) vmax[t] = 0ull;  // the drift bound's words (read at the last evaluation's end)
     if (t == 0) *flag_all = 0u;
 }
 
 hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
                       const LetPieces &pc, double gap2, const LetBufs &L, const BodyState &sub,
-                      int64_t S, uint32_t *scal, hipStream_t s, const MortonFuse &mf) {
+                      int64_t S, uint32_t *scal, hipStream_t s, const MortonFuse &mf,
+                      const LetSweep &sw) {
     if (pc.n <= 0) {
         hipError_t e = hipMemsetAsync(L.ecell, 0, LET_CELLS, s);
         return e == hipSuccess ? hipMemsetAsync(L.flag_all, 0, sizeof(uint32_t), s) : e;
     }
-    const int64_t clear = std::max<int64_t>(pc.n >> 4, LET_CELLS / 16);
-    k_let_clear<<<grid_for(clear), TB, 0, s>>>(pc.n, L.own, L.ecell, L.flag_all);
+    const int64_t nb = let_sel_blocks(pc.n);
+    const int64_t clear = std::max<int64_t>({pc.n >> 4, LET_CELLS / 16, nb, 256 * 8});
+    k_let_clear<<<grid_for(clear), TB, 0, s>>>(pc.n, L.own, L.ecell, L.flag_all, L.own_blk, nb,
+                                               L.rowmask, L.vmax, L.nvmax);
     hipError_t e;
     const int64_t marks = (int64_t)pc.rounds * pc.sub;
     if (marks > 0)
         k_let_mark<<<grid_for(marks), TB, 0, s>>>(pc, ps, st.x, st.y, st.cidx, g, L.own,
-                                                  L.ecell, L.flag_all);
+                                                  L.own_blk, L.ecell, L.flag_all);
     const int K = (int)std::floor(std::sqrt(gap2 > 0.0 ? gap2 : 0.0)) + 1;
-    k_let_halo<<<grid_for(LET_CELLS), TB, 0, s>>>(L.ecell, L.flag_all, gap2, K, L.hcell);
-    const int64_t nb = let_sel_blocks(pc.n);
+    k_let_halo<<<grid_for(LET_CELLS), TB, 0, s>>>(L.ecell, L.flag_all, gap2, K, L.hcell,
+                                                  L.rowmask);
     k_let_flags<<<(unsigned)nb, 64, 0, s>>>(pc, ps, st.x, st.y, st.cidx, g, L.hcell, L.own,
-                                            L.flag8, L.sel);
+                                            L.flag8, L.sel, L, sw);
     size_t bytes = L.scratch_bytes;
     e = rocprim::exclusive_scan(L.scratch, bytes, L.sel, L.selpos, 0u, (size_t)(nb + 1),
                                 rocprim::plus<uint32_t>(), s);
@@ -748,6 +852,15 @@ hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
     k_let_gather<<<(unsigned)nb, TB, 0, s>>>(pc.n, ps, L.flag8, L.selpos, st, sub, S,
                                              L.selpos + nb, L.table, scal, g, mf);
     return hipGetLastError();
+}
+
+void let_boxes(int64_t n, const BodyState &st, const Geometry &g, uint32_t *box, hipStream_t s) {
+    if (n > 0)
+        k_let_boxes<<<(unsigned)let_sel_blocks(n), 64, 0, s>>>(n, st.x, st.y, st.cidx, g, box);
+}
+
+void let_disp_add(double *disp, const unsigned long long *vmax, int k, double dt, hipStream_t s) {
+    k_let_disp_add<<<1, 1, 0, s>>>(disp, vmax, k, dt);
 }
 
 hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const TreeBuffers &tb,

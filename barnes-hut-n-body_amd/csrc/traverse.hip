@@ -161,6 +161,30 @@ constexpr int TRAV_TIMING_MAX = 1 << 18;
 __device__ uint64_t g_trav_times[4 * TRAV_TIMING_MAX];
 #endif
 
+// k_kick_drift / k_kick of lane q's own body, operation for operation (BHA:412-432): the new
+// position -- drifted, or as the build left it -- goes to the exchange, the velocity stays with
+// the owner.  (ax, ay) = F / m (BHA:390-391).
+template <int KICK>
+__device__ __forceinline__ void own_kick(int64_t q, double bx, double by, double ax, double ay,
+                                         const KickArgs &kick, double *__restrict__ a2,
+                                         double &vxi, double &vyi) {
+    typedef double double2_t __attribute__((ext_vector_type(2)));
+    const int64_t r = kick.rep ? (int64_t)kick.rep[q] : q;
+    vxi = kick.vx[r] + ax * kick.dtHalf;
+    vyi = kick.vy[r] + ay * kick.dtHalf;
+    kick.vx[r] = vxi;
+    kick.vy[r] = vyi;
+    double2_t o;
+    if (KICK == KICK_OWN_DRIFT) {
+        o.x = bx + vxi * kick.dt;
+        o.y = by + vyi * kick.dt;
+    } else {
+        o.x = bx;
+        o.y = by;
+    }
+    *reinterpret_cast<double2_t *>(a2 + 2 * q) = o;
+}
+
 // KICK (KickMode): the integration step that follows the evaluation is applied by the lane
 // itself after its walk -- the body's x, y are only ever read by its own lane (other lanes see
 // it through the leaf records), so the update in place is race-free and a2 is not written.
@@ -222,6 +246,16 @@ __device__ __forceinline__ void trav_wave(uint32_t v, uint64_t t_start,
         t[3] = __builtin_amdgcn_s_getreg((31 << 11) | 20);   // XCC_ID
     }
 #endif
+    if (KICK == KICK_OWN_DRIFT && kick.vmax) {  // the drift's speed bound: every lane takes part
+        double vxi = 0.0, vyi = 0.0;
+        if (valid) own_kick<KICK>(q, bx, by, fx / bm, fy / bm, kick, a2, vxi, vyi);
+        wave_vmax(kick.vmax, vxi, vyi);
+        if (COUNT && valid) {
+            cnt.visits[p] = nvis;
+            cnt.contrib[p] = ncontrib;
+        }
+        return;
+    }
     if (!valid) return;
     // BHA:390-391, interleaved (ax, ay): coalesced 16-byte stores in Morton order
     typedef double double2_t __attribute__((ext_vector_type(2)));
@@ -231,22 +265,8 @@ __device__ __forceinline__ void trav_wave(uint32_t v, uint64_t t_start,
     if (KICK == KICK_NONE) {  // by lane with a lane map (the multi-GPU pieces stay contiguous)
         *reinterpret_cast<double2_t *>(a2 + 2 * q) = acc;
     } else if (KICK == KICK_OWN_DRIFT || KICK == KICK_OWN_ONLY) {
-        // k_kick_drift / k_kick of the own body, operation for operation (BHA:414-432); the new
-        // position goes to the exchange, the velocity stays with the owner
-        const int64_t r = kick.rep ? (int64_t)kick.rep[q] : q;
-        const double vxi = kick.vx[r] + acc.x * kick.dtHalf;
-        const double vyi = kick.vy[r] + acc.y * kick.dtHalf;
-        kick.vx[r] = vxi;
-        kick.vy[r] = vyi;
-        double2_t o;
-        if (KICK == KICK_OWN_DRIFT) {
-            o.x = bx + vxi * kick.dt;
-            o.y = by + vyi * kick.dt;
-        } else {
-            o.x = bx;
-            o.y = by;
-        }
-        *reinterpret_cast<double2_t *>(a2 + 2 * q) = o;
+        double vxi, vyi;
+        own_kick<KICK>(q, bx, by, acc.x, acc.y, kick, a2, vxi, vyi);
     } else {  // k_kick_drift / k_kick (integrate.hip), operation for operation
         double v0x, v0y;
         if (KICK == KICK_ONLY && kick.perm) {

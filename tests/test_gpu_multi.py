@@ -23,7 +23,7 @@ from test_gpu_parity import FIELDS, _assert_arrays_equal, _frames_scene, _let_sc
 
 pytestmark = pytest.mark.gpu
 
-SITES = {1: "acc", 2: "pos", 3: "vel", 4: "table", 5: "flags", 6: "settings"}
+SITES = {1: "acc", 2: "pos", 3: "vel", 4: "table", 5: "flags", 6: "settings", 7: "vmax"}
 
 
 @pytest.fixture(autouse=True)
@@ -247,4 +247,34 @@ def test_small_body_lists_step_on_one_gpu(monkeypatch):
         ref.step(2)
         _assert_arrays_equal(eng.map_bodies(), ref.get_bodies(), f"world {world}")
         ref.close()
+    eng.close()
+
+
+def test_let_selection_bound_with_fast_movers():
+    """The LET selection scans only the slot blocks whose box (their bodies' cells at the last
+    full build) widened by the displacement bound since (max speed x dt per drift, every rank's
+    maximum exchanged, plus the jitter) reaches a built cell.  Streams of fast bodies (up to 3
+    depth-8 cells per step) cross every rank's region, and a few run off the root and come back;
+    4 members over 24 steps (two refresh-free calls of 12): the state equals the single-GPU
+    engine's bit for bit -- a body the bound missed would be left out of a subset."""
+    rng = np.random.default_rng(91)
+    x, y, vx, vy, m = (a.copy() for a in scenes.uniform(120_000, 0.5, seed=90))
+    k = 3000
+    sx, sy = rng.uniform(0, 2400, k), rng.uniform(0, 800, k)
+    ang = rng.uniform(0, 2 * np.pi, k)
+    sp = rng.uniform(500.0, 5600.0, k)  # 5600 px/unit x 0.005 = 28 px = 3 cells per step
+    arrs = (np.concatenate([x, sx]), np.concatenate([y, sy]),
+            np.concatenate([vx, sp * np.cos(ang)]), np.concatenate([vy, sp * np.sin(ang)]),
+            np.concatenate([m, np.full(k, 0.5)]))
+    params = bh_amd.default_params(theta=0.5, merge_min_dist=0.0)
+    want, want_q = _single(params, arrs, (12, 12))
+    eng = bh_amd.Engine(params, devices=[0, 0, 0, 0])
+    eng.reset_bodies(*arrs)
+    for kk in (12, 12):
+        eng.step(kk)
+    got = eng.get_bodies()
+    for j, name in enumerate(FIELDS):
+        assert bits_equal(got[j], want[j]), name
+    log = _logs_agree(eng)
+    assert _count(log, 7) > 0  # the speed bounds were exchanged
     eng.close()

@@ -11,6 +11,8 @@
 #   profile        rocprofv3 kernel trace + stats and FETCH_SIZE / WRITE_SIZE passes of C3
 #                  (tools/profile.sh; CONFIG=c5 etc. for another workload) -> prof_<CONFIG>/
 #   sq             SQ counters of the traversal (tools/profile_sq.sh)
+#   timed          the C3 bench's timed call alone: kernel trace, FETCH / WRITE passes, summarised
+#                  over that call only (tools/timed_window.py)               -> ${TAG}_c3_timed*
 #   timeline       one C3 bench under a kernel trace, summarised per step (tools/timeline.py)
 #   dropin         the front-end's one-step calls under a kernel + copy trace (tools/dropin_calls.py,
 #                  summarised by tools/timeline.py)                             -> ${TAG}_dropin_*
@@ -52,6 +54,20 @@ for step in "$@"; do
       bench_line --config c5 --steps 2 --warmup 1 ;;
     profile) run 1800 ${O}_profile.log bash tools/profile.sh ;;
     sq) run 900 ${O}_sq.log bash tools/profile_sq.sh ;;
+    timed)  # the driver's C3 call alone under rocprofv3 (no drop-in / counter / verify legs):
+            # kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes, summarised over the timed
+            # call's window only (tools/timed_window.py)                    -> ${TAG}_c3_timed*
+      export TMPDIR=/tmp
+      TA="--no-cpu-baseline --no-counters --no-drop-in --no-verify"
+      run 600 ${O}_timed_trace.log rocprofv3 --kernel-trace --stats -d ${O}_timed_trace -o run \
+        --output-format csv -- python3 bench.py --steps 20 --warmup 5 $TA
+      grep '^{' ${O}_timed_trace.log | tail -1 >> ${O}_bench_lines.jsonl
+      run 300 ${O}_timed_fetch.log timeout -s KILL 240 rocprofv3 --pmc FETCH_SIZE --kernel-trace \
+        -d ${O}_timed_fetch -o run --output-format csv -- python3 bench.py --steps 4 --warmup 2 $TA
+      run 300 ${O}_timed_write.log timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace \
+        -d ${O}_timed_write -o run --output-format csv -- python3 bench.py --steps 4 --warmup 2 $TA
+      run 120 ${O}_timed_sum.log python3 tools/timed_window.py ${O}_timed_trace 40 ${O}_c3 \
+        ${O}_timed_fetch ${O}_timed_write 8 ;;
     timeline)
       run 600 ${O}_timeline.log rocprofv3 --kernel-trace -d ${O}_tl -o run --output-format csv \
         -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-counters --no-drop-in ;;
