@@ -1490,6 +1490,17 @@ int finish_merges(bh_engine *e, uint32_t *overflow, uint32_t *tree_flags = nullp
     }
     e->n = n - (int64_t)nd;
     e->inv_valid = false;  // another n: another exchange layout
+    if ((e->comm || e->group || e->solo) && let_active(e) && e->p.theta != 0.0 && e->n > 0 &&
+        e->st_morton && !e->pos_pending) {
+        // the LET selections until the next full build: boxes of the compacted slots from the
+        // positions now (materialized at the call's end), the displacement bound restarting here
+        TRY(let_alloc(e, 0));
+        let_boxes(e->n, e->st, e->geo, e->let_box, e->stream);
+        HIPCHK(e, hipGetLastError());
+        HIPCHK(e, hipMemsetAsync(e->disp, 0, sizeof(double), e->stream));
+        e->boxes_valid = true;
+        e->builds_since_box = 0;
+    }
     e->removed.assign(dead.begin(), dead.end());
     // BHA:526: lastTree = null only when the last step's merge rule removed a body.  Bodies
     // removed by earlier steps were tombstones in the last build (sentinel keys: the tail of its

@@ -17,9 +17,19 @@ tree of oracle/py_oracle.py in place of the HIP kernels:
     computes the top levels from all tables (computeMass, BHA:184-200), walks own bodies through
     top + local subtrees + remote cell records, kicks its OWN bodies (velocities stay with their
     owners) and all-gathers the new positions, 16 B per body, in the bh_gather_slot layout;
-  * velocities are all-gathered (same rounds and slots) before the next full build;
+  * velocities are all-gathered (same rounds and slots) before the next full build and at the
+    end of a call whose last evaluation was a LET one (every evaluation may be: the call's last
+    build's full tree is built on demand by getTreeForDebug, engine.cpp lazy lastTree);
   * the merge rule (BHA:463-532) is replicated: removed bodies are tombstones until the end of
-    the call, then every replica compacts.
+    the call, then every replica compacts;
+  * at the end of every call with LET builds the ranks agree on the LET status (an all-reduce:
+    engine.cpp agree_let_flags), and after every drifting LET evaluation they exchange their
+    drift speed bound (the LET selection's displacement bound, engine.cpp gather_vmax) while the
+    full build's slot-block boxes are valid.
+
+Every collective is logged as the engine logs it (bh_collective_log: API call count, site,
+bytes every rank receives), so the CPU protocol and the engine's recorded sequence compare
+entry by entry (tests/test_dist_gloo.py, tests/test_gpu_multi.py).
 
 The exchanged data is exactly what the engine exchanges, so a bit-identical final state on every
 rank (tests/test_dist_gloo.py) shows that the protocol carries everything the reference's
@@ -36,6 +46,10 @@ from oracle import py_oracle
 LET_P = 8                    # depth of the exchanged cells (bh_device.hpp)
 LET_CELLS = 1 << (2 * LET_P)
 LET_REFRESH = 32             # LET builds between full builds (engine.cpp BH_LET_REFRESH)
+LET_TSTRIDE = LET_CELLS + 1  # cell records + status record per exchanged table (bh_device.hpp)
+LETCELL_BYTES = 32
+# collective sites (engine.cpp CollSite)
+COLL_ACC, COLL_POS, COLL_VEL, COLL_TABLE, COLL_FLAGS, COLL_VMAX = 1, 2, 3, 4, 5, 7
 
 
 class Geometry:
@@ -129,6 +143,9 @@ class MirrorRank:
         self.rank, self.world, self.comm = rank, world, comm
         self.geo = Geometry(params["width_px"], params["height_px"])
         self.stats = {"let": 0, "full": 0, "vel_syncs": 0, "max_subset": 0, "merged": 0}
+        self.log = []        # (api call, site, bytes) per collective, as bh_collective_log
+        self.api_calls = 0
+        self.boxes_valid = False
 
     # ---- caller-facing API (bh_reset_bodies / bh_step / bh_get_bodies) --------------------
     def reset_bodies(self, x, y, vx, vy, m):
@@ -139,12 +156,28 @@ class MirrorRank:
         self.st_morton = False
         self.vel_stale = False
         self.let_age = 0
+        self.boxes_valid = False
+        self.api_calls += 1
 
     def step(self, k):
+        self.api_calls += 1
+        n0 = len(self.x)
+        may_let = k > 0 and n0 > 0 and self.world >= 2 and self.p["theta"] != 0.0
         for s in range(k):
             self._evaluate("drift", allow_let=True)
-            self._evaluate("kick", allow_let=s + 1 < k)  # the call's last build: the full tree
+            self._evaluate("kick", allow_let=True)  # (the last build's full tree: on demand)
             self._merge()
+        if may_let:  # the end-of-call agreement on the LET status (max all-reduce)
+            import torch
+            flag = torch.zeros(2, dtype=torch.int64)
+            self.comm.all_reduce(flag, op=torch.distributed.ReduceOp.MAX)
+            self._log(COLL_FLAGS, 8)
+        if k > 0:
+            self._sync_velocities()  # every replica complete at the API boundary
+        if bool(np.any(self.dead)):  # the compaction moves the slots: the engine recomputes
+            # the selection's boxes from the positions at the call's end (finish_merges)
+            self.boxes_valid = (self.world >= 2 and self.p["theta"] != 0.0
+                                and int(np.count_nonzero(~self.dead)) > 0)
         keep = ~self.dead  # one compaction per call; caller indices renumbered in order
         order = np.argsort(self.cidx[keep], kind="stable")
         rank_of = np.empty(len(order), dtype=np.int64)
@@ -163,12 +196,18 @@ class MirrorRank:
         R = _rounds()
         return range(min(n, self.rank * R * sub), min(n, (self.rank + 1) * R * sub))
 
-    def _exchange(self, n, per_lane):
+    def _log(self, site, nbytes):
+        self.log.append((self.api_calls, site, int(nbytes)))
+
+    def _exchange(self, n, per_lane, site):
         """per_lane: {own lane q: (a, b)} -> (a, b) of every lane, through the engine's in-place
         round-by-round all-gather layout (gather slot of lane q)."""
         import torch
         sub, slots = shard_layout(None, n, self.world)
         R = _rounds()
+        if sub > 0:
+            for _ in range(R):
+                self._log(site, 8 * 2 * sub * self.world)
         buf = np.zeros(2 * sub * self.world * R)
         for q, (a, b) in per_lane.items():
             buf[2 * slots[q]] = a
@@ -210,7 +249,9 @@ class MirrorRank:
         acc = {}
         for q in self._own_lanes(n, sub):
             acc[q] = (0.0, 0.0) if self.dead[q] else self._force(root, bodies[q])
-        ax, ay = self._exchange(n, acc)
+        ax, ay = self._exchange(n, acc, COLL_ACC)
+        if theta2 != 0.0 and self.world >= 2 and n > 0:  # the selection's boxes (engine.cpp)
+            self.boxes_valid = True
         dt_half = self.p["dt"] * 0.5  # BHA:412
         live = ~self.dead
         self.vx[live] += ax[live] * dt_half
@@ -240,7 +281,8 @@ class MirrorRank:
         self.vel_stale = False
         n = len(self.x)
         sub, _ = shard_layout(None, n, self.world)
-        vx, vy = self._exchange(n, {q: (self.vx[q], self.vy[q]) for q in self._own_lanes(n, sub)})
+        vx, vy = self._exchange(n, {q: (self.vx[q], self.vy[q]) for q in self._own_lanes(n, sub)},
+                                COLL_VEL)
         self.vx[:], self.vy[:] = vx, vy
         self.stats["vel_syncs"] += 1
 
@@ -307,6 +349,7 @@ class MirrorRank:
                 table[c] = (0.0, 0.0, 0.0, 0, 1, -1)
         parts = [torch.zeros(LET_CELLS * 6, dtype=torch.float64) for _ in range(self.world)]
         self.comm.all_gather(parts, torch.from_numpy(table.ravel().copy()))
+        self._log(COLL_TABLE, LETCELL_BYTES * LET_TSTRIDE * self.world)
         tables = [t.numpy().reshape(LET_CELLS, 6) for t in parts]
         levels = self._top(tables)
         dt_half, dt = self.p["dt"] * 0.5, self.p["dt"]
@@ -324,7 +367,12 @@ class MirrorRank:
                 new_pos[q] = (b.x + self.vx[q] * dt, b.y + self.vy[q] * dt)
             else:
                 new_pos[q] = (b.x, b.y)  # as the build left it (jitter)
-        x, y = self._exchange(n, new_pos)  # 16 B per body: every replica's positions
+        x, y = self._exchange(n, new_pos, COLL_POS)  # 16 B per body: every replica's positions
+        if kick == "drift" and self.boxes_valid:  # the drift's speed bound, every rank's
+            vmax = torch.zeros(1, dtype=torch.float64)
+            got = [torch.zeros(1, dtype=torch.float64) for _ in range(self.world)]
+            self.comm.all_gather(got, vmax)
+            self._log(COLL_VMAX, 8 * self.world)
         self.x[:], self.y[:] = x, y
         self.vel_stale = True
 

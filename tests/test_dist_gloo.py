@@ -26,6 +26,47 @@ PARAMS = dict(G=80.0, dt=0.005, theta=0.5, soft2=1.0, width_px=2400, height_px=8
 CALLS = (3, 2)
 
 
+COLL_ACC, COLL_POS, COLL_VEL, COLL_TABLE, COLL_FLAGS, COLL_VMAX = 1, 2, 3, 4, 5, 7
+
+
+def check_log(log, world, n0, n_min, calls):
+    """The collective sequence of a rank (bh_collective_log entries: API call, site, bytes) for
+    a reset and bh_step calls of k steps each, LET from the second build on: per call the
+    evaluations' exchanges in order, then the LET-status agreement and the velocity gather.
+    Sizes: only the call's pieces matter (bodies removed by a call's merges change the next
+    call's sizes; the byte counts are checked for internal consistency: every round of a
+    per-body exchange carries the same size within a call, the table 32 (65536 + 1) B a rank)."""
+    from let_mirror import _rounds
+    R = _rounds()
+    table_bytes = 32 * 65537 * world
+    calls_seen = sorted({c for c, _, _ in log})
+    assert calls_seen == list(range(2, 2 + len(calls))), calls_seen  # reset = API call 1
+    boxes = False
+    for ci, k in enumerate(calls):
+        got = [(s, b) for c, s, b in log if c == 2 + ci]
+        want_sites = []
+        for step in range(k):
+            for kick in ("drift", "kick"):
+                if ci == 0 and step == 0 and kick == "drift":
+                    want_sites += [COLL_ACC] * R  # the first (full) build
+                    boxes = True
+                    continue
+                want_sites += [COLL_TABLE] + [COLL_POS] * R
+                if kick == "drift" and boxes:
+                    want_sites.append(COLL_VMAX)
+        want_sites += [COLL_FLAGS] + [COLL_VEL] * R
+        assert [s for s, _ in got] == want_sites, (ci, [s for s, _ in got])
+        per_body = {b for s, b in got if s in (COLL_ACC, COLL_POS, COLL_VEL)}
+        assert len(per_body) == 1  # R rounds of `sub` bodies a rank, 16 B each: >= n bodies
+        b = per_body.pop()
+        assert b % (16 * world) == 0 and R * b >= 16 * n_min
+        assert R * b < 16 * (n0 + R * world * 256)  # (padded pieces)
+        assert {b for s, b in got if s == COLL_TABLE} == {table_bytes}
+        assert {b for s, b in got if s == COLL_FLAGS} == {8}
+        assert {b for s, b in got if s == COLL_VMAX} <= {8 * world}
+        boxes = True  # (valid again after a compaction: recomputed at the call's end)
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))
@@ -64,7 +105,7 @@ def _worker(rank, world, port, out_dir, params=None):
         mr.step(k)
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), *mr.get_bodies())
     with open(os.path.join(out_dir, f"stats{rank}.json"), "w") as fh:
-        json.dump(mr.stats, fh)
+        json.dump(dict(mr.stats, log=mr.log), fh)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -89,10 +130,12 @@ def test_exchange_protocol_matches_the_reference_step(tmp_path, world, merge):
     for r in range(world):
         got = np.load(tmp_path / f"rank{r}.npz")
         stats = json.load(open(tmp_path / f"stats{r}.json"))
-        # per call: the first build after the reset / the call's last build are full, the rest
-        # are LET builds; velocities are gathered before every full build that follows LET ones
-        assert stats["let"] == 2 * sum(CALLS) - len(CALLS) - 1 and stats["full"] == len(CALLS) + 1
+        # the first build after the reset is full, every later one a LET build (fewer than
+        # BH_LET_REFRESH); the velocities are gathered at the end of every call
+        assert stats["let"] == 2 * sum(CALLS) - 1 and stats["full"] == 1
         assert stats["vel_syncs"] == len(CALLS)
+        check_log(stats["log"], world, n0=len(arrs[0]), n_min=len(want[0]), calls=CALLS)
+        assert stats["log"] == json.load(open(tmp_path / "stats0.json"))["log"]
         assert stats["merged"] == len(arrs[0]) - len(want[0])
         # every rank owns bodies; at world 3 a rank builds a part of the scene only
         assert 0 < stats["max_subset"] <= len(arrs[0])

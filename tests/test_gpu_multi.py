@@ -278,3 +278,31 @@ def test_let_selection_bound_with_fast_movers():
     log = _logs_agree(eng)
     assert _count(log, 7) > 0  # the speed bounds were exchanged
     eng.close()
+
+
+@pytest.mark.parametrize("world,merge", [(2, True), (3, False)])
+def test_collective_sequence_equals_the_protocol_mirror(tmp_path, world, merge):
+    """The engine's recorded collective sequence (every member's bh_collective_log: API call,
+    site, bytes) equals, entry by entry, the one the CPU protocol mirror issues over gloo for the
+    same scene and calls (tests/let_mirror.py, one process per rank) -- the sequence the CPU suite
+    checks (test_dist_gloo.check_log) is the engine's own, and so are the final states."""
+    import json
+    import torch.multiprocessing as mp
+    import test_dist_gloo as tg
+
+    params = dict(tg.PARAMS, merge_min_dist=8.0 if merge else 0.0)
+    mp.spawn(tg._worker, args=(world, tg._free_port(), str(tmp_path), params), nprocs=world,
+             join=True)
+    eng = bh_amd.Engine(bh_amd.default_params(**params), devices=[0] * world)
+    eng.reset_bodies(*tg.scene())
+    for k in tg.CALLS:
+        eng.step(k)
+    got = eng.get_bodies()
+    log = _logs_agree(eng)[:, :3].tolist()
+    for r in range(world):
+        st = json.load(open(tmp_path / f"stats{r}.json"))
+        assert log == st["log"], f"rank {r}: {_first_diff(np.array(log), np.array(st['log']))}"
+        mine = np.load(tmp_path / f"rank{r}.npz")
+        for k, name in enumerate(FIELDS):
+            assert bits_equal(got[k], mine[f"arr_{k}"]), f"rank {r}: {name}"
+    eng.close()
