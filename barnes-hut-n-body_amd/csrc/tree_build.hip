@@ -172,6 +172,12 @@ __device__ __forceinline__ void bitonic_sort(uint64_t *A, uint32_t s) {
 constexpr int RADIX_CAP = SORT_CAP / 2;  // the bin-grouped copy lives in the upper half of L
 constexpr int RADIX_BINS = 256;
 constexpr uint32_t RADIX_MAXBIN = 48;
+// A bucket whose key prefixes are all equal (the dead bodies' sentinel run -- the LET subset's
+// padding --, or a dense depth-16 cell) is binned by its slots instead: the composites' order is
+// then the slot order, and the bins are slot ranges.
+#ifndef BH_SORT_SLOT_RADIX
+#define BH_SORT_SLOT_RADIX 1
+#endif
 
 #ifdef BH_SORT_STATS  // diagnostic build: which path each bucket took (radix / bitonic / global)
 __device__ unsigned long long g_sort_stats[8];
@@ -189,7 +195,7 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
     chain_prio();
     __shared__ uint64_t L[SORT_CAP];
     __shared__ uint32_t s_cnt[RADIX_BINS], s_start[RADIX_BINS];
-    __shared__ uint32_t s_min, s_max, s_maxbin;
+    __shared__ uint32_t s_min, s_max, s_maxbin, s_smin, s_smax;
     const uint32_t t = blockIdx.x;
     const uint32_t b0 = starts[t], s = starts[t + 1] - b0;
     if (threadIdx.x == 0) counts[t] = 0;  // ready for the next build (counts were scanned)
@@ -201,34 +207,44 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
     };
     if (s <= (uint32_t)SORT_CAP) {
         if (threadIdx.x == 0) {
-            s_min = 0xFFFFFFFFu;
-            s_max = 0;
+            s_min = s_smin = 0xFFFFFFFFu;
+            s_max = s_smax = 0;
             s_maxbin = 0;
         }
         if (threadIdx.x < RADIX_BINS) s_cnt[threadIdx.x] = 0;
         __syncthreads();
-        uint32_t kmin = 0xFFFFFFFFu, kmax = 0;
+        uint32_t kmin = 0xFFFFFFFFu, kmax = 0, smin = 0xFFFFFFFFu, smax = 0;
         for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) {
             const uint64_t v = comp[b0 + j];
             L[j] = v;
             kmin = min(kmin, (uint32_t)(v >> 32));
             kmax = max(kmax, (uint32_t)(v >> 32));
+            smin = min(smin, (uint32_t)v);
+            smax = max(smax, (uint32_t)v);
         }
         bool radix = s <= (uint32_t)RADIX_CAP;
         if (radix) {
             atomicMin(&s_min, kmin);
             atomicMax(&s_max, kmax);
+            if (BH_SORT_SLOT_RADIX) {
+                atomicMin(&s_smin, smin);
+                atomicMax(&s_smax, smax);
+            }
         }
         __syncthreads();
         if (radix) {
-            const uint32_t lo = s_min, span = s_max - s_min;
+            // (uniform) equal prefixes: bin by slot (the low half of the composite)
+            const bool by_slot = BH_SORT_SLOT_RADIX && s_min == s_max;
+            const int hs = by_slot ? 0 : 32;
+            const uint32_t lo = by_slot ? s_smin : s_min;
+            const uint32_t span = by_slot ? s_smax - s_smin : s_max - s_min;
             const int shift = span >= RADIX_BINS ? (32 - __clz(span)) - 8 : 0;  // span >> shift < 256
             uint32_t bin[RADIX_CAP / SORT_TB], off[RADIX_CAP / SORT_TB];
 #pragma unroll
             for (int r = 0; r < RADIX_CAP / SORT_TB; ++r) {
                 const uint32_t j = threadIdx.x + r * SORT_TB;
                 if (j < s) {
-                    bin[r] = ((uint32_t)(L[j] >> 32) - lo) >> shift;
+                    bin[r] = ((uint32_t)(L[j] >> hs) - lo) >> shift;
                     off[r] = atomicAdd(&s_cnt[bin[r]], 1u);
                 }
             }

@@ -2,6 +2,12 @@ import os
 import sys
 
 import pytest
+# torch first, as in bench.py and in a full collection (test_dist_gloo imports it): the engine
+# library then binds to the HIP runtime torch has loaded.  A test that imports torch only after
+# the engine library initialised HIP (the protocol-mirror test spawns gloo ranks) otherwise
+# brings torch's ROCm libraries in on top of another runtime, and the process aborts at exit
+# ("double free or corruption", round 5).
+import torch  # noqa: F401
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PKG_DIR = os.path.join(ROOT, "barnes-hut-n-body_amd")
