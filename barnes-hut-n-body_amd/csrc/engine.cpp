@@ -854,6 +854,16 @@ TreeBuffers let_tree_buffers(bh_engine *e) {
     return b;
 }
 
+// LET subset capacity: the largest subset seen + headroom (a subset beyond it replays the call)
+#ifndef BH_LET_HEADROOM_SHIFT
+#define BH_LET_HEADROOM_SHIFT 3
+#endif
+inline int64_t let_capacity(int64_t known) {
+    return known + (known >> BH_LET_HEADROOM_SHIFT) + 4096;
+}
+#ifndef BH_SPL_EXTEND
+#define BH_SPL_EXTEND 1
+#endif
 #ifndef BH_LET_MIN_WORLD
 #define BH_LET_MIN_WORLD 2
 #endif
@@ -1053,7 +1063,7 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
             e->sub_cnt_pending = false;
             e->let_known = std::max<int64_t>(e->let_known, *e->sub_cnt_h);
         }
-        int64_t S = e->let_known > 0 ? std::min<int64_t>(n, e->let_known + e->let_known / 8 + 4096) : n;
+        int64_t S = e->let_known > 0 ? std::min<int64_t>(n, let_capacity(e->let_known)) : n;
         PosSrc ps{nullptr, GatherLayout{}, nullptr};
         if (e->pos_pending && lanes != e->pos_lanes) TRY(materialize_positions(e));  // map changed
         if (e->pos_pending) {  // the previous LET evaluation's positions, straight from a2
@@ -1067,6 +1077,14 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         // the subset build's keys and buckets from the gather when its buffers and splitters are
         // those of the previous LET build (same S capacity and J; not the first build, which sorts
         // with rocprim and sizes the subset afterwards)
+        // a grown capacity S: splitters for its new padding tail (else one bucket takes it all
+        // and sorts it alone: up to 1 ms per build while the call's largest subset still grows)
+        if (BH_SPL_EXTEND && e->s_spl_nb > 0 && S <= e->let_sub_cap && e->geo.J == e->let_J &&
+            sort_buckets(S) > e->s_spl_nb) {
+            extend_splitters(e->s_spl, e->s_spl_nb, sort_buckets(S), e->geo.J, e->stream);
+            HIPCHK(e, hipGetLastError());
+            e->s_spl_nb = sort_buckets(S);
+        }
         MortonFuse mf{};
         const bool fuse = BH_LET_FUSE_KEYS && e->let_known > 0 && e->s_spl_nb > 0 &&
                           S <= e->let_sub_cap && e->geo.J == e->let_J && e->s_keys;
@@ -1097,7 +1115,7 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
                                      e->stream));
             HIPCHK(e, hipStreamSynchronize(e->stream));
             e->let_known = std::max<int64_t>(h[0], 1);
-            S = std::min<int64_t>(n, e->let_known + e->let_known / 8 + 4096);  // padded above
+            S = std::min<int64_t>(n, let_capacity(e->let_known));  // padded above
         }
         TRY(let_alloc(e, S));
         n_sub = S;  // padded: bodies past the real subset are dead

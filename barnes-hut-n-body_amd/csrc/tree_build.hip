@@ -181,9 +181,15 @@ constexpr uint32_t RADIX_MAXBIN = 48;
 
 #ifdef BH_SORT_STATS  // diagnostic build: which path each bucket took (radix / bitonic / global)
 __device__ unsigned long long g_sort_stats[8];
+// per launch (ring of SORT_LOG): largest bucket, buckets through the LDS bitonic network, through
+// the global one, elements of the latter
+constexpr int SORT_LOG = 256;
+__device__ unsigned long long g_sort_log[SORT_LOG][4];
 #define SORT_STAT(q, v) (threadIdx.x == 0 ? (void)atomicAdd(&g_sort_stats[(q)], (unsigned long long)(v)) : (void)0)
+#define SORT_LOGV(q, v) (threadIdx.x == 0 ? (void)atomicAdd(&g_sort_log[seq % SORT_LOG][(q)], (unsigned long long)(v)) : (void)0)
 #else
 #define SORT_STAT(q, v) (void)0
+#define SORT_LOGV(q, v) (void)0
 #endif
 __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restrict__ starts,
                                                          uint32_t *__restrict__ counts,
@@ -191,14 +197,18 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
                                                          const uint64_t *__restrict__ keys,
                                                          uint32_t *__restrict__ keys32_s,
                                                          uint32_t *__restrict__ perm,
-                                                         uint64_t *keys_s) {
+                                                         uint64_t *keys_s, uint32_t seq) {
     chain_prio();
+    (void)seq;
     __shared__ uint64_t L[SORT_CAP];
     __shared__ uint32_t s_cnt[RADIX_BINS], s_start[RADIX_BINS];
     __shared__ uint32_t s_min, s_max, s_maxbin, s_smin, s_smax;
     const uint32_t t = blockIdx.x;
     const uint32_t b0 = starts[t], s = starts[t + 1] - b0;
     if (threadIdx.x == 0) counts[t] = 0;  // ready for the next build (counts were scanned)
+#ifdef BH_SORT_STATS
+    if (threadIdx.x == 0) atomicMax(&g_sort_log[seq % SORT_LOG][0], (unsigned long long)s);
+#endif
     auto emit = [&](uint32_t j, uint64_t v) __attribute__((always_inline)) {
         const uint32_t src = (uint32_t)v;
         keys32_s[b0 + j] = (uint32_t)(v >> 32);
@@ -223,12 +233,23 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
             smax = max(smax, (uint32_t)v);
         }
         bool radix = s <= (uint32_t)RADIX_CAP;
-        if (radix) {
-            atomicMin(&s_min, kmin);
-            atomicMax(&s_max, kmax);
-            if (BH_SORT_SLOT_RADIX) {
-                atomicMin(&s_smin, smin);
-                atomicMax(&s_smax, smax);
+        if (radix) {  // wave minima / maxima first: one LDS atomic per wave
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) {
+                kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o, 64));
+                kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
+                if (BH_SORT_SLOT_RADIX) {
+                    smin = min(smin, (uint32_t)__shfl_xor((int)smin, o, 64));
+                    smax = max(smax, (uint32_t)__shfl_xor((int)smax, o, 64));
+                }
+            }
+            if ((threadIdx.x & 63) == 0) {
+                atomicMin(&s_min, kmin);
+                atomicMax(&s_max, kmax);
+                if (BH_SORT_SLOT_RADIX) {
+                    atomicMin(&s_smin, smin);
+                    atomicMax(&s_smax, smax);
+                }
             }
         }
         __syncthreads();
@@ -295,12 +316,15 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
         }
         SORT_STAT(2, 1);
         SORT_STAT(3, s);
+        SORT_LOGV(1, 1);
         bitonic_sort<true>(L, s);
         __syncthreads();
         for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) emit(j, L[j]);
     } else {  // oversized bucket: the same network on global memory, in place
         SORT_STAT(4, 1);
         SORT_STAT(5, s);
+        SORT_LOGV(2, 1);
+        SORT_LOGV(3, s);
         uint64_t *A = comp + b0;
         bitonic_sort<false>(A, s);
         for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) emit(j, A[j]);  // own j: in place
@@ -1500,6 +1524,18 @@ __global__ __launch_bounds__(TB) void k_permute_vel(int64_t n, const uint32_t *_
     dvy[a] = svy[i];
 }
 
+__global__ __launch_bounds__(TB) void k_spl_extend(uint64_t *__restrict__ spl, uint32_t from,
+                                                   uint32_t to, uint64_t sent32) {
+    const uint32_t t = from + blockIdx.x * TB + threadIdx.x;
+    if (t < to) spl[t] = (sent32 << 32) | ((uint64_t)t * SORT_B);
+}
+
+void extend_splitters(uint64_t *spl, uint32_t from, uint32_t to, int J, hipStream_t s) {
+    if (to <= from) return;
+    k_spl_extend<<<(to - from + TB - 1) / TB, TB, 0, s>>>(spl, from, to,
+                                                        sentinel_key(J) >> key32_shift(J));
+}
+
 void permute_velocities(int64_t n, const uint32_t *perm, const double *svx, const double *svy,
                         double *dvx, double *dvy, hipStream_t s) {
     if (n > 0) k_permute_vel<<<grid_for(n), TB, 0, s>>>(n, perm, svx, svy, dvx, dvy);
@@ -1592,8 +1628,13 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
                                      (size_t)b.spl_nb + 1, rocprim::plus<uint32_t>(), s);
         if (st != hipSuccess) return st;
         k_bucket_scatter<<<sg, SORT_TB, 0, s>>>(n, b.keys32, b.cnt, b.base, b.bstart, b.keys_s);
+        uint32_t seq = 0;
+#ifdef BH_SORT_STATS
+        static uint32_t sort_seq = 0;  // (diagnostic build: one engine, one thread)
+        seq = sort_seq++;
+#endif
         k_bucket_sort<<<b.spl_nb, SORT_TB, 0, s>>>(b.bstart, b.bcount, b.keys_s, b.keys,
-                                                   b.keys32_s, b.perm, b.keys_s);
+                                                   b.keys32_s, b.perm, b.keys_s, seq);
     } else {
         st = rocprim::radix_sort_pairs<SortConfig>(b.scratch, bytes, b.keys32, b.keys32_s, b.idx,
                                                    b.perm, (size_t)n, 0u, 32u, s);
@@ -1632,6 +1673,10 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
 #ifdef BH_SORT_STATS
 extern "C" int bh_debug_sort_stats(unsigned long long *out) {
     return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sort_stats), sizeof(unsigned long long) * 8);
+}
+extern "C" int bh_debug_sort_log(unsigned long long *out) {  // SORT_LOG x 4, by launch % SORT_LOG
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sort_log),
+                                    sizeof(unsigned long long) * 4 * SORT_LOG);
 }
 #endif
 

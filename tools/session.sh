@@ -17,6 +17,7 @@
 #   dropin         the front-end's one-step calls under a kernel + copy trace (tools/dropin_calls.py,
 #                  summarised by tools/timeline.py)                             -> ${TAG}_dropin_*
 #   solo           one rank's share of the 8-GPU C4 step, alone (tools/solo_rank.py, ranks 0, 5)
+#   soloprof       the solo rank-0 step under rocprofv3 --kernel-trace --stats -> ${TAG}_soloprof/
 #   soloab         the solo step of rank 0 (C4 / 8) alternately with lib/libA.so and the default
 #                  build (SOLO_LIBS="A default" to change), 2 rounds          -> ${TAG}_soloab.jsonl
 #   ab             A/B of in-tree library builds (tools/ab.sh; LIBS="A B", AB_ARGS=...)
@@ -83,6 +84,12 @@ for step in "$@"; do
         run 600 ${O}_solo$r.log python -u tools/solo_rank.py --config c4 --world 8 --rank $r
         grep '^{' ${O}_solo$r.log | tail -1 >> ${O}_solo.jsonl
       done ;;
+    soloprof)  # rocprofv3 kernel trace + stats of the solo C4 / 8 rank-0 step (LET builds)
+      export TMPDIR=/tmp
+      run 600 ${O}_soloprof.log rocprofv3 --kernel-trace --stats -d ${O}_soloprof -o run \
+        --output-format csv -- python3 tools/solo_rank.py --config c4 --world 8 --rank 0 \
+        --steps 10 --warmup 2
+      grep '^{' ${O}_soloprof.log | tail -1 >> ${O}_solo.jsonl ;;
     soloab)  # SOLO_LIBS="A B ..." (lib/lib<X>.so; "default" = the in-tree build)
       for rr in 1 2; do
         for L in ${SOLO_LIBS:-A default}; do

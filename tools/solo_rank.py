@@ -54,6 +54,11 @@ def main():
         if lib.bh_debug_sort_stats(st) == 0:
             out["sort_stats"] = dict(zip(("radix", "radix_el", "bitonic", "bitonic_el", "global",
                                           "global_el"), (int(v) for v in st[:6])))
+        lg = (ctypes.c_ulonglong * (256 * 4))()
+        if hasattr(lib, "bh_debug_sort_log") and lib.bh_debug_sort_log(lg) == 0:
+            # per bucket-sort launch in order: largest bucket, LDS-bitonic / global buckets
+            out["sort_log"] = [[int(v) for v in lg[4 * i:4 * i + 4]] for i in range(256)
+                               if lg[4 * i]]
     print(json.dumps(out))
     eng.close()
 
