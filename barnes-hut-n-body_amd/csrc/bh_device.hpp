@@ -350,8 +350,8 @@ struct KickArgs {
     double dtHalf, dt;
     const uint32_t *rep = nullptr;  // KICK_OWN_*: lane -> replicated slot (null: the lane)
     MortonFuse mf{};
-    // KICK_ONLY after a build that left the velocities in the previous slot order: v[p] =
-    // sv[perm[p]] + a dt/2 (the build's permutation of v, fused; null: in place)
+    // KICK_ONLY / KICK_DRIFT after a build that left the velocities in the previous slot order:
+    // v[p] = sv[perm[p]] + a dt/2 (the build's permutation of v, fused; null: in place)
     const double *svx = nullptr, *svy = nullptr;
     const uint32_t *perm = nullptr;
     // KICK_OWN_DRIFT: max over the launch's bodies of max(|vx|, |vy|) after the kick, as the bits

@@ -249,6 +249,9 @@ struct bh_engine {
     // deep pipeline: the previous step also evaluated a(t) on that tree (beside its own second
     // traversal), by lane of the current map, with these force parameters
     bool forces_ready = false;
+    // the velocities are still in the previous slot order, in alt (the overlapped build's
+    // permutation, read by the next step's first kick); null: st holds them
+    const uint32_t *vel_perm = nullptr;
     ForceParams fp_ready{0.0, 0.0, 0.0};
     double *a2_alt = nullptr;  // a2's compaction target (the carried forces over removals)
     int64_t a2_alt_cap = 0;
@@ -675,7 +678,24 @@ int build_into(bh_engine *e, hipStream_t s, bool overlap, bool keep_v = false, b
     return BH_OK;
 }
 
-int build(bh_engine *e) { return build_into(e, e->stream, false); }
+// The velocities left in the previous slot order by a pipelined step (vel_perm) -> st, for any
+// reader other than the next step's first kick (materialize_positions calls it: every reader of
+// the replica outside the step does that first).
+#ifndef BH_FOLD_VEL_PERM
+#define BH_FOLD_VEL_PERM 1
+#endif
+int materialize_velocities(bh_engine *e) {
+    if (!e->vel_perm) return BH_OK;
+    permute_velocities(e->n, e->vel_perm, e->alt.vx, e->alt.vy, e->st.vx, e->st.vy, e->stream);
+    e->vel_perm = nullptr;
+    HIPCHK(e, hipGetLastError());
+    return BH_OK;
+}
+
+int build(bh_engine *e) {
+    TRY(materialize_velocities(e));
+    return build_into(e, e->stream, false);
+}
 
 // theta = 0 workspace: flags per node slot, selected indices and the leaf list per body.
 int ensure_direct(bh_engine *e) {
@@ -934,6 +954,7 @@ int gather_round(bh_engine *e, const GatherLayout &gl, int k, int W, int ev_roun
 // the copy-out) or reuses a2 (accelerations, the velocity exchange).  A subset overflow (scalars[4],
 // the call is replayed) leaves the replica as it was.
 int materialize_positions(bh_engine *e) {
+    TRY(materialize_velocities(e));
     if (!e->pos_pending) return BH_OK;
     e->pos_pending = false;
     if (e->n <= 0) return BH_OK;
@@ -1289,6 +1310,13 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
     if ((!e->comm && !e->group && !e->solo) || visits) {
         if (BH_FUSE_KICK && kick != KICK_NONE && !direct && !visits && fused) {
             KickArgs ka{kick, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
+            if (e->vel_perm && kick == KICK_DRIFT && !have_forces) {  // v[p] = old v[perm[p]]
+                ka.svx = e->alt.vx;
+                ka.svy = e->alt.vy;
+                ka.perm = e->vel_perm;
+                e->vel_perm = nullptr;
+            }
+            TRY(materialize_velocities(e));  // (any other path: permuted first)
             if (BH_FUSE_KEYS && e->fuse_keys && kick == KICK_DRIFT && e->spl_nb > 0 && n > 0) {
                 ka.mf = MortonFuse{e->keys, e->keys32, e->spl, e->spl_nb, e->cnt, e->base,
                                    e->bcount};
@@ -1572,6 +1600,7 @@ int snapshot(bh_engine *e) {
 }
 
 int restore(bh_engine *e) {
+    e->vel_perm = nullptr;  // (the snapshot is complete)
     TRY(copy_state(e, e->snap, e->st, e->snap_n));
     e->n = e->snap_n;
     TRY(drop_carried_flags(e));
@@ -1906,8 +1935,12 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     HIPCHK(e, hipEventRecord(e->pipe_ev[1], e->pipe_stream));
     HIPCHK(e, hipStreamWaitEvent(s, e->pipe_ev[1], 0));
     if (BH_DEEP_PIPE) TRY(mark(e, 1, 2));  // this traversal, the overlapped chain, the next a(t)
-    permute_velocities(n, e->perm2, e->st.vx, e->st.vy, e->alt.vx, e->alt.vy, s);
-    HIPCHK(e, hipGetLastError());
+    if (!last && !BH_DEEP_PIPE && BH_FOLD_VEL_PERM) {
+        e->vel_perm = e->perm2;  // the next step's first kick reads them through the permutation
+    } else {
+        permute_velocities(n, e->perm2, e->st.vx, e->st.vy, e->alt.vx, e->alt.vy, s);
+        HIPCHK(e, hipGetLastError());
+    }
     TRY(mark(e, 0));  // the wait for the overlapped build and the velocity permutation
     std::swap(e->st, e->alt);
     std::swap(e->nodes, e->nodes_alt);
@@ -2704,6 +2737,7 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     HIPCHK(e, hipSetDevice(e->device));
     HIPCHK(e, hipStreamSynchronize(e->stream));
     TRY(drop_carried_flags(e));
+    e->vel_perm = nullptr;  // (the state is replaced)
     TRY(ensure_capacity(e, n));
     if (n > 0) {  // slot order = caller order until the first build
         HIPCHK(e, hipMemcpyAsync(e->st.x, x, sizeof(double) * n, hipMemcpyHostToDevice, e->stream));

@@ -269,7 +269,7 @@ __device__ __forceinline__ void trav_wave(uint32_t v, uint64_t t_start,
         own_kick<KICK>(q, bx, by, acc.x, acc.y, kick, a2, vxi, vyi);
     } else {  // k_kick_drift / k_kick (integrate.hip), operation for operation
         double v0x, v0y;
-        if (KICK == KICK_ONLY && kick.perm) {
+        if ((KICK == KICK_ONLY || KICK == KICK_DRIFT) && kick.perm) {
             const uint32_t sp = kick.perm[p];
             v0x = kick.svx[sp];
             v0y = kick.svy[sp];

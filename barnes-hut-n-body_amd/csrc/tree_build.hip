@@ -24,6 +24,7 @@
 //   k_span_*     the chunk-spanning nodes, levels J..0
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
+#include <rocprim/block/block_radix_sort.hpp>
 
 #include "bh_device.hpp"
 
@@ -178,6 +179,14 @@ constexpr uint32_t RADIX_MAXBIN = 48;
 #ifndef BH_SORT_SLOT_RADIX
 #define BH_SORT_SLOT_RADIX 1
 #endif
+// Any other bucket of up to SORT_CAP elements (keys clustered in a few bins -- a bucket that
+// spans a gap of the subset's key ranges --, or above RADIX_CAP -- the bucket that new halo
+// cells fall into after a drift): an LDS radix sort of its composites compressed to the bits
+// they span, (key32 - min) : (slot - min); else the bitonic network.
+#ifndef BH_SORT_BLOCK_RADIX
+#define BH_SORT_BLOCK_RADIX 1
+#endif
+using BucketRadix = rocprim::block_radix_sort<unsigned long long, SORT_TB, SORT_CAP / SORT_TB>;
 
 #ifdef BH_SORT_STATS  // diagnostic build: which path each bucket took (radix / bitonic / global)
 __device__ unsigned long long g_sort_stats[8];
@@ -200,7 +209,11 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
                                                          uint64_t *keys_s, uint32_t seq) {
     chain_prio();
     (void)seq;
-    __shared__ uint64_t L[SORT_CAP];
+    __shared__ union {
+        uint64_t L[SORT_CAP];
+        BucketRadix::storage_type brs;  // (after L is read into registers)
+    } shm;
+    uint64_t *L = shm.L;
     __shared__ uint32_t s_cnt[RADIX_BINS], s_start[RADIX_BINS];
     __shared__ uint32_t s_min, s_max, s_maxbin, s_smin, s_smax;
     const uint32_t t = blockIdx.x;
@@ -233,12 +246,14 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
             smax = max(smax, (uint32_t)v);
         }
         bool radix = s <= (uint32_t)RADIX_CAP;
-        if (radix) {  // wave minima / maxima first: one LDS atomic per wave
+        const bool need_minmax = radix || BH_SORT_BLOCK_RADIX;
+        const bool need_slots = BH_SORT_SLOT_RADIX || BH_SORT_BLOCK_RADIX;
+        if (need_minmax) {  // wave minima / maxima first: one LDS atomic per wave
 #pragma unroll
             for (int o = 32; o > 0; o >>= 1) {
                 kmin = min(kmin, (uint32_t)__shfl_xor((int)kmin, o, 64));
                 kmax = max(kmax, (uint32_t)__shfl_xor((int)kmax, o, 64));
-                if (BH_SORT_SLOT_RADIX) {
+                if (need_slots) {
                     smin = min(smin, (uint32_t)__shfl_xor((int)smin, o, 64));
                     smax = max(smax, (uint32_t)__shfl_xor((int)smax, o, 64));
                 }
@@ -246,7 +261,7 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
             if ((threadIdx.x & 63) == 0) {
                 atomicMin(&s_min, kmin);
                 atomicMax(&s_max, kmax);
-                if (BH_SORT_SLOT_RADIX) {
+                if (need_slots) {
                     atomicMin(&s_smin, smin);
                     atomicMax(&s_smax, smax);
                 }
@@ -317,6 +332,34 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
         SORT_STAT(2, 1);
         SORT_STAT(3, s);
         SORT_LOGV(1, 1);
+        if (BH_SORT_BLOCK_RADIX) {
+            constexpr int IPT = SORT_CAP / SORT_TB;
+            const uint32_t kmn = s_min, smn = s_smin;
+            const uint32_t kspan = s_max - kmn, sspan = s_smax - smn;
+            const int sb = sspan ? 32 - __clz(sspan) : 0;  // bits of the slot offset
+            const int kb = kspan ? 32 - __clz(kspan) : 0;
+            uint64_t v[IPT];  // blocked: thread t holds elements t * IPT + q
+#pragma unroll
+            for (int q = 0; q < IPT; ++q) {
+                const uint32_t j = threadIdx.x * IPT + q;
+                const uint64_t c = L[min(j, s - 1)];
+                v[q] = j < s ? ((uint64_t)((uint32_t)(c >> 32) - kmn) << sb) |
+                                   (uint64_t)((uint32_t)c - smn)
+                             : ~0ull;  // past the bucket: last (stable: after every element)
+            }
+            __syncthreads();  // L is read: its storage becomes the sort's
+            BucketRadix().sort(reinterpret_cast<unsigned long long(&)[IPT]>(v), shm.brs, 0u,
+                               (unsigned)max(kb + sb, 1));
+            const uint64_t smask = sb ? (~0ull >> (64 - sb)) : 0ull;
+#pragma unroll
+            for (int q = 0; q < IPT; ++q) {
+                const uint32_t j = threadIdx.x * IPT + q;
+                if (j < s)
+                    emit(j, ((uint64_t)((uint32_t)(v[q] >> sb) + kmn) << 32) |
+                                (uint64_t)((uint32_t)(v[q] & smask) + smn));
+            }
+            return;
+        }
         bitonic_sort<true>(L, s);
         __syncthreads();
         for (uint32_t j = threadIdx.x; j < s; j += SORT_TB) emit(j, L[j]);
@@ -672,6 +715,22 @@ __device__ __forceinline__ void node_com(Node *nodes, uint32_t ni, const Geometr
     nodes[ni] = nd;
 }
 
+constexpr uint32_t NO_SPAN = 0xFFFFFFFFu;
+constexpr uint32_t SPAN_REF = 1u << 31;  // child list entry: owner slot of a span child
+// span_list entry flag: the node also crosses a GROUP boundary (groups of SPAN_GROUP chunk
+// boundaries, finished by one workgroup each); such nodes are finished by k_com_span_top
+constexpr uint32_t SPAN_SUPER = 1u << 31;
+constexpr int SPAN_GROUP = 1024;
+#ifndef BH_EMIT_SPANS
+#define BH_EMIT_SPANS 1
+#endif
+struct SpanOut {  // k_emit_com's span-list outputs (BH_EMIT_SPANS)
+    uint32_t *list;
+    uint32_t stride;
+    uint32_t *super_list;
+    uint32_t n_groups;
+};
+
 // Chunk-local centre of mass (k_emit_com below): LDS capacity per chunk and its encoding.
 #ifndef BH_COM_CAP
 #define BH_COM_CAP 2048
@@ -726,7 +785,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
                                                      uint32_t *scratch, Node *nodes,
                                                      uint32_t *err,
                                                      const uint32_t *__restrict__ inv,
-                                                     uint32_t *__restrict__ lanes) {
+                                                     uint32_t *__restrict__ lanes, SpanOut so) {
     chain_prio();
     __shared__ double s_m[COM_CAP + 1], s_x[COM_CAP + 1], s_y[COM_CAP + 1];  // [COM_CAP]: pad
     __shared__ uint32_t s_next[COM_CAP];
@@ -801,6 +860,32 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
         }
     }
     if (threadIdx.x == 0) s_lmax = -1;
+    const uint32_t chunk = blockIdx.x;
+    if (BH_EMIT_SPANS) {  // this boundary's span list column: none until a skeleton says so
+        if ((int)threadIdx.x <= J) so.list[(size_t)threadIdx.x * so.stride + chunk] = NO_SPAN;
+        if (chunk + 1 == gridDim.x)  // (and every column past the last chunk)
+            for (uint32_t q = threadIdx.x; q < (uint32_t)(J + 1) * so.stride; q += EC_TB)
+                if (q % so.stride > chunk) so.list[q] = NO_SPAN;
+    }
+    // a chunk-spanning node at depth L, slot ni, ending at body e: listed by this boundary; the
+    // owner (this chunk) rides in its comX for k_span_children; SUPER when it also contains the
+    // first body past this chunk's group (k_com_span_top finishes it)
+    auto span_node = [&](uint32_t ni, int L, int64_t e, uint32_t nx) __attribute__((always_inline)) {
+        Node nd;
+        nd.comX = BH_EMIT_SPANS ? __longlong_as_double((long long)chunk) : 0.0;
+        nd.comY = 0.0;
+        nd.mass = 0.0;
+        nd.next = nx;
+        nd.meta = (uint32_t)(2 * L) | NODE_SPAN;  // 2 x depth
+        nodes[ni] = nd;
+        if (BH_EMIT_SPANS) {
+            const int64_t kG = (int64_t)(chunk / SPAN_GROUP) * SPAN_GROUP + SPAN_GROUP - 1;
+            const int64_t bG = (kG << COM_CHUNK_SHIFT) + (1 << COM_CHUNK_SHIFT) - 1;
+            const bool super = e > bG;
+            so.list[(size_t)L * so.stride + chunk] = ni | (super ? SPAN_SUPER : 0u);
+            if (super) so.super_list[(size_t)L * so.n_groups + (uint32_t)(kG / SPAN_GROUP)] = chunk;
+        }
+    };
     if (lanes) {  // the traversal's lane map through this build's permutation (lane_order)
         uint32_t nl[EC_PER];
 #pragma unroll
@@ -924,13 +1009,15 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
                 const bool span = (a >> COM_CHUNK_SHIFT) != (e[q] >> COM_CHUNK_SHIFT);
                 const uint32_t ni = b0 + (uint32_t)(L - cp - 1);
                 const uint32_t nx = nxs[q];
-                if (span || !lds) {
+                if (span) {
+                    span_node(ni, L, e[q], nx);
+                } else if (!lds) {
                     Node nd;
                     nd.comX = 0.0;
                     nd.comY = 0.0;
                     nd.mass = 0.0;
                     nd.next = nx;
-                    nd.meta = (uint32_t)(2 * L) | (span ? NODE_SPAN : 0u);  // 2 x depth
+                    nd.meta = (uint32_t)(2 * L);  // 2 x depth
                     nodes[ni] = nd;
                 }
                 if (lds)
@@ -973,15 +1060,7 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
             const uint32_t i = threadIdx.x + (uint32_t)r * EC_TB;
             const int L = Ls[r];
             const bool span = (as[r] >> COM_CHUNK_SHIFT) != (e[r] >> COM_CHUNK_SHIFT);
-            if (span) {
-                Node nd;
-                nd.comX = 0.0;
-                nd.comY = 0.0;
-                nd.mass = 0.0;
-                nd.next = nxs[r];
-                nd.meta = (uint32_t)(2 * L) | NODE_SPAN;  // 2 x depth
-                nodes[S0 + i] = nd;
-            }
+            if (span) span_node(S0 + i, L, e[r], nxs[r]);
             s_next[i] = span ? EC_SPAN : ((nxs[r] - S0) | ((uint32_t)(2 * L) << EC_D2_SHIFT));
         }
     }
@@ -1132,13 +1211,8 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
 
 // The nodes crossing the boundary between chunk k and k+1 (bodies b = end of chunk k and
 // b+1) are exactly b's ancestors at depths 0..c(b); each chunk-spanning node is listed once,
-// by the boundary of the chunk it starts in: span_list[L * stride + k] (or NO_SPAN).
-constexpr uint32_t NO_SPAN = 0xFFFFFFFFu;
-constexpr uint32_t SPAN_REF = 1u << 31;  // child list entry: owner slot of a span child
-// span_list entry flag: the node also crosses a GROUP boundary (groups of SPAN_GROUP chunk
-// boundaries, finished by one workgroup each); such nodes are finished by k_com_span_top
-constexpr uint32_t SPAN_SUPER = 1u << 31;
-constexpr int SPAN_GROUP = 1024;
+// by the boundary of the chunk it starts in: span_list[L * stride + k] (or NO_SPAN).  k_emit_com
+// lists them as it writes their skeletons (BH_EMIT_SPANS); k_span_find is the separate pass.
 
 __global__ __launch_bounds__(TB) void k_span_find(int64_t n, int J, int D0,
                                                   const uint64_t *__restrict__ keys_s,
@@ -1655,11 +1729,13 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
                                                                   n_super);
     k_emit_com<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), EC_TB, 0, s>>>(
         n, g, D0, b.keys_s, b.cpl, b.base, b.cell_start, b.dst.x, b.dst.y, b.dst.m, b.dst.cidx,
-        b.idx, b.nodes, b.scalars + 1, b.keys32, b.lanes_remap);
+        b.idx, b.nodes, b.scalars + 1, b.keys32, b.lanes_remap,
+        SpanOut{b.span_list, b.span_stride, b.super_list, n_groups});
     const dim3 span_grid((b.span_stride + TB - 1) / TB, g.J + 1);
-    k_span_find<<<span_grid, TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cpl, b.base, b.cell_start,
-                                         b.span_list, b.span_stride, b.super_list, n_groups,
-                                         b.nodes);
+    if (!BH_EMIT_SPANS)
+        k_span_find<<<span_grid, TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cpl, b.base, b.cell_start,
+                                             b.span_list, b.span_stride, b.super_list, n_groups,
+                                             b.nodes);
     k_span_children<<<span_grid, TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.nodes,
                                              b.span_children);
     k_com_span<<<n_groups, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
