@@ -501,7 +501,7 @@ struct PosSrc {
 hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
                       const LetPieces &pc, double gap2, const LetBufs &L, const BodyState &sub,
                       int64_t S, uint32_t *scal, hipStream_t s, const MortonFuse &mf = {},
-                      const LetSweep &sw = {});
+                      const LetSweep &sw = {}, bool clean = false);
 // gslot[lanes[q]] = gather_slot(gl, q) (lanes null: the identity map)
 void let_gather_slots(int64_t n, const uint32_t *lanes, GatherLayout gl, uint32_t *gslot,
                       hipStream_t s);
@@ -509,9 +509,11 @@ void let_gather_slots(int64_t n, const uint32_t *lanes, GatherLayout gl, uint32_
 hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const TreeBuffers &tb,
                      hipStream_t s);
 // after the exchange (L.tables, LET_TSTRIDE per rank): any rank's overflow -> scal[4]; top
-// levels, layout, node array, lane map; tree size posc[LET_CELLS]
+// levels, layout, node array, lane map; tree size posc[LET_CELLS].  *cleaned: the lane-map kernel
+// also cleared the selection's marks for the next selection (which may then skip k_let_clear)
 hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, const LetBufs &L,
-                        const TreeBuffers &tb, uint32_t *scal, hipStream_t s);
+                        const TreeBuffers &tb, uint32_t *scal, hipStream_t s,
+                        bool *cleaned = nullptr);
 // owner integration: a2 (gather slots) holds every lane's (x, y) -> the replicated state; the
 // solo fill writes the current positions of all lanes first
 void let_set_pos(int64_t n, const uint32_t *lanes, const double *a2, GatherLayout gl, double *x,

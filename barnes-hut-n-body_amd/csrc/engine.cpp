@@ -209,6 +209,9 @@ struct bh_engine {
     uint32_t *let_box = nullptr;
     double *disp = nullptr;
     bool boxes_valid = false;
+    // the selection's marks were cleared by the last LET build's lane map (for n bodies)
+    bool let_clean = false;
+    int64_t let_clean_n = -1;
     int builds_since_box = 0;   // builds since then that may have jittered positions
     int64_t let_sub_cap = 0;    // subset capacity of the subset tree workspace
     int let_J = -1;
@@ -785,6 +788,7 @@ int let_alloc(bh_engine *e, int64_t n_sub, hipStream_t s = nullptr) {
         L.vmax = reinterpret_cast<unsigned long long *>(e->disp + 1);
         L.nvmax = 1 + e->world;
         e->boxes_valid = false;
+        e->let_clean = false;  // (new buffers)
         TRY(alloc_state(e, e->sub_src, cap));
         e->let_cap = cap;
     }
@@ -1117,7 +1121,8 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         const LetSweep sw{e->let_box, e->disp, 4.0e-3 * (double)(e->builds_since_box + 1),
                           e->boxes_valid};
         HIPCHK(e, let_select(e->st, ps, e->geo, pc, gap2, e->L, e->sub_src, S, e->scalars,
-                             e->stream, mf, sw));
+                             e->stream, mf, sw, e->let_clean && e->let_clean_n == n));
+        e->let_clean = false;
         ++e->builds_since_box;
         if (e->let_known > 0) {
             if (!e->sub_cnt_h) {
@@ -1153,7 +1158,9 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
             const uint32_t node_cap = e->L.node_cap;
             if (e->inject_guard) e->L.node_cap = 1u;
             e->inject_guard = false;
-            const hipError_t rc = let_assemble(n_sub, e->geo, pc, e->L, sb, e->scalars, e->stream);
+            const hipError_t rc = let_assemble(n_sub, e->geo, pc, e->L, sb, e->scalars, e->stream,
+                                               &e->let_clean);
+            e->let_clean_n = n;
             e->L.node_cap = node_cap;
             HIPCHK(e, rc);
         }

@@ -25,6 +25,7 @@
 #include <cmath>
 
 #include <rocprim/device/device_scan.hpp>
+#include <rocprim/iterator/zip_iterator.hpp>
 
 #include "bh_device.hpp"
 
@@ -694,11 +695,28 @@ __global__ __launch_bounds__(TB) void k_let_subpos(int64_t n_sub, int64_t n,
 }
 
 // own lane -> subset slot of its body
+// The selection's marks cleared for the next selection (k_let_clear's stores, grid-strided):
+// the build's last kernel does it, none of its inputs being read after the assembly
+__device__ __forceinline__ void let_clear_marks(int64_t t, int64_t stride, int64_t n,
+                                                const LetBufs &L, int64_t nb) {
+    const uint4 z = make_uint4(0u, 0u, 0u, 0u);
+    const int64_t nv = n >> 4;
+    for (int64_t i = t; i < nv; i += stride) reinterpret_cast<uint4 *>(L.own)[i] = z;
+    if (t < (n & 15)) L.own[(nv << 4) + t] = 0;
+    for (int64_t i = t; i < LET_CELLS / 16; i += stride) reinterpret_cast<uint4 *>(L.ecell)[i] = z;
+    for (int64_t i = t; i < nb; i += stride) L.own_blk[i] = 0;
+    for (int64_t i = t; i < 256 * 8; i += stride) L.rowmask[i] = 0u;
+    if (t < L.nvmax) L.vmax[t] = 0ull;
+    if (t == 0) *L.flag_all = 0u;
+}
+
 __global__ __launch_bounds__(TB) void k_let_lanes(LetPieces pc, uint32_t n_sub,
                                                   const uint32_t *__restrict__ subpos,
                                                   const uint32_t *__restrict__ scal,
-                                                  uint32_t *__restrict__ lanes) {
+                                                  uint32_t *__restrict__ lanes, LetBufs L,
+                                                  int64_t nb_clear) {
     const int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (nb_clear >= 0) let_clear_marks(t, (int64_t)gridDim.x * TB, pc.n, L, nb_clear);
     if (t >= (int64_t)pc.rounds * pc.sub) return;
     const int64_t q = own_lane(pc, t);
     if (q >= pc.n) return;
@@ -792,13 +810,34 @@ double let_include_gap2(const Geometry &g, double theta2, double soft2) {
     return gap2 > 16.0 * 16.0 ? -1.0 : gap2;  // a halo this wide: the replicated build
 }
 
+// The assembly's two per-cell scans (record counts -> posc, copied-cell counts -> cpos) as one
+// scan of pairs (BH_LET_PAIR_SCAN): one lookback launch pair instead of two.
+#ifndef BH_LET_PAIR_SCAN
+#define BH_LET_PAIR_SCAN 1
+#endif
+using U32Pair = rocprim::tuple<uint32_t, uint32_t>;
+struct PairPlus {
+    __host__ __device__ U32Pair operator()(const U32Pair &a, const U32Pair &b) const {
+        return U32Pair(rocprim::get<0>(a) + rocprim::get<0>(b),
+                       rocprim::get<1>(a) + rocprim::get<1>(b));
+    }
+};
+hipError_t pair_scan(void *scratch, size_t &bytes, const uint32_t *a, const uint32_t *b,
+                     uint32_t *sa, uint32_t *sb, size_t count, hipStream_t s) {
+    auto in = rocprim::make_zip_iterator(rocprim::make_tuple(a, b));
+    auto out = rocprim::make_zip_iterator(rocprim::make_tuple(sa, sb));
+    return rocprim::exclusive_scan(scratch, bytes, in, out, U32Pair(0u, 0u), count, PairPlus(), s);
+}
+
 size_t let_scratch_bytes(int64_t n) {
-    size_t a = 0, b = 0;
+    size_t a = 0, b = 0, c = 0;
     (void)rocprim::exclusive_scan(nullptr, a, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u,
                                   (size_t)(n + 1), rocprim::plus<uint32_t>());
     (void)rocprim::exclusive_scan(nullptr, b, (const uint32_t *)nullptr, (uint32_t *)nullptr, 0u,
                                   (size_t)(LET_CELLS + 1), rocprim::plus<uint32_t>());
-    return std::max(a, b);
+    (void)pair_scan(nullptr, c, nullptr, nullptr, nullptr, nullptr, (size_t)(LET_CELLS + 1),
+                    nullptr);
+    return std::max({a, b, c});
 }
 
 // The selection's three clears in one launch (16-byte stores; the buffers are hipMalloc'd):
@@ -826,15 +865,16 @@ __global__ __launch_bounds__(TB) void k_let_clear(int64_t n, uint8_t *__restrict
 hipError_t let_select(const BodyState &st, const PosSrc &ps, const Geometry &g,
                       const LetPieces &pc, double gap2, const LetBufs &L, const BodyState &sub,
                       int64_t S, uint32_t *scal, hipStream_t s, const MortonFuse &mf,
-                      const LetSweep &sw) {
+                      const LetSweep &sw, bool clean) {
     if (pc.n <= 0) {
         hipError_t e = hipMemsetAsync(L.ecell, 0, LET_CELLS, s);
         return e == hipSuccess ? hipMemsetAsync(L.flag_all, 0, sizeof(uint32_t), s) : e;
     }
     const int64_t nb = let_sel_blocks(pc.n);
     const int64_t clear = std::max<int64_t>({pc.n >> 4, LET_CELLS / 16, nb, 256 * 8});
-    k_let_clear<<<grid_for(clear), TB, 0, s>>>(pc.n, L.own, L.ecell, L.flag_all, L.own_blk, nb,
-                                               L.rowmask, L.vmax, L.nvmax);
+    if (!clean)  // (else the previous LET build's lane map cleared them)
+        k_let_clear<<<grid_for(clear), TB, 0, s>>>(pc.n, L.own, L.ecell, L.flag_all, L.own_blk,
+                                                   nb, L.rowmask, L.vmax, L.nvmax);
     hipError_t e;
     const int64_t marks = (int64_t)pc.rounds * pc.sub;
     if (marks > 0)
@@ -869,19 +909,29 @@ hipError_t let_table(int64_t n_sub, const Geometry &g, const LetBufs &L, const T
     return hipGetLastError();
 }
 
+#ifndef BH_LET_CLEAR_AHEAD
+#define BH_LET_CLEAR_AHEAD 1
+#endif
 hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, const LetBufs &L,
-                        const TreeBuffers &tb, uint32_t *scal, hipStream_t s) {
+                        const TreeBuffers &tb, uint32_t *scal, hipStream_t s, bool *cleaned) {
+    if (cleaned) *cleaned = false;
     k_let_top_hi<<<256, 256, 0, s>>>(pc.world, g, L.tables, L.levels, scal);
     k_let_top_lo<<<1, 256, 0, s>>>(g, L.levels);
     k_let_w<<<grid_for(LET_CELLS + 1), TB, 0, s>>>(L, tb, scal);
     size_t bytes = L.scratch_bytes;
-    hipError_t e = rocprim::exclusive_scan(L.scratch, bytes, L.w, L.posc, 0u,
-                                           (size_t)(LET_CELLS + 1), rocprim::plus<uint32_t>(), s);
-    if (e != hipSuccess) return e;
-    bytes = L.scratch_bytes;
-    e = rocprim::exclusive_scan(L.scratch, bytes, L.ccnt, L.cpos, 0u, (size_t)(LET_CELLS + 1),
-                                rocprim::plus<uint32_t>(), s);
-    if (e != hipSuccess) return e;
+    hipError_t e;
+    if (BH_LET_PAIR_SCAN) {
+        e = pair_scan(L.scratch, bytes, L.w, L.ccnt, L.posc, L.cpos, (size_t)(LET_CELLS + 1), s);
+        if (e != hipSuccess) return e;
+    } else {
+        e = rocprim::exclusive_scan(L.scratch, bytes, L.w, L.posc, 0u, (size_t)(LET_CELLS + 1),
+                                    rocprim::plus<uint32_t>(), s);
+        if (e != hipSuccess) return e;
+        bytes = L.scratch_bytes;
+        e = rocprim::exclusive_scan(L.scratch, bytes, L.ccnt, L.cpos, 0u, (size_t)(LET_CELLS + 1),
+                                    rocprim::plus<uint32_t>(), s);
+        if (e != hipSuccess) return e;
+    }
     k_let_write_top_cells<<<grid_for(level_off(LET_P) + LET_CELLS), TB, 0, s>>>(L);
     k_let_copy_blocks<<<BH_LET_COPY_GRID, TB, 0, s>>>(L, tb.nodes);
     if (n_sub > 0)
@@ -889,9 +939,13 @@ hipError_t let_assemble(int64_t n_sub, const Geometry &g, const LetPieces &pc, c
     else
         k_let_guard<<<1, 1, 0, s>>>(L, scal);
     const int64_t own_lanes = (int64_t)pc.rounds * pc.sub;
-    if (own_lanes > 0 && pc.n > 0)
+    if (own_lanes > 0 && pc.n > 0) {
+        const bool clear = BH_LET_CLEAR_AHEAD && cleaned;
         k_let_lanes<<<grid_for(own_lanes), TB, 0, s>>>(pc, (uint32_t)n_sub, L.subpos, scal,
-                                                        L.lanes);
+                                                        L.lanes, L,
+                                                        clear ? let_sel_blocks(pc.n) : -1);
+        if (clear) *cleaned = true;
+    }
     return hipGetLastError();
 }
 

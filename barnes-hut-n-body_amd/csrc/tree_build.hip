@@ -387,12 +387,10 @@ __global__ __launch_bounds__(TB) void k_key_gather(int64_t n, const uint64_t *__
     if (a < n) keys_s[a] = keys[perm[a]];
 }
 
-__global__ __launch_bounds__(TB) void k_key_fixup(int64_t n, int J,
-                                                  const uint32_t *__restrict__ keys32_s,
-                                                  uint64_t *__restrict__ keys_s,
-                                                  uint32_t *__restrict__ perm) {
-    chain_prio();
-    const int64_t a = (int64_t)blockIdx.x * TB + threadIdx.x;
+__device__ __forceinline__ void key_fixup(int64_t a, int64_t n, int J,
+                                          const uint32_t *__restrict__ keys32_s,
+                                          uint64_t *__restrict__ keys_s,
+                                          uint32_t *__restrict__ perm) {
     if (a + 1 >= n) return;
     const uint32_t k = keys32_s[a];
     if (keys32_s[a + 1] != k || (a > 0 && keys32_s[a - 1] == k)) return;  // not a run start
@@ -411,6 +409,14 @@ __global__ __launch_bounds__(TB) void k_key_fixup(int64_t n, int J,
         keys_s[j] = ki;
         perm[j] = pi;
     }
+}
+
+__global__ __launch_bounds__(TB) void k_key_fixup(int64_t n, int J,
+                                                  const uint32_t *__restrict__ keys32_s,
+                                                  uint64_t *__restrict__ keys_s,
+                                                  uint32_t *__restrict__ perm) {
+    chain_prio();
+    key_fixup((int64_t)blockIdx.x * TB + threadIdx.x, n, J, keys32_s, keys_s, perm);
 }
 
 __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *__restrict__ keys_s,
@@ -457,13 +463,11 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
 // so bin 4^D0 starts at the first out-of-root body, i.e. at the in-root count).
 // Also fills the span super list [0, n_super) with 0xFF bytes for k_span_find (in place of a
 // memset launch; nothing reads it before k_span_find).
-__global__ __launch_bounds__(TB) void k_cells(int64_t n, int J, int D0,
-                                              const uint64_t *__restrict__ keys_s,
-                                              uint32_t *__restrict__ cell_start,
-                                              uint32_t *__restrict__ super_list, int64_t n_super) {
-    chain_prio();
-    const int64_t bin = (int64_t)blockIdx.x * TB + threadIdx.x;
-    for (int64_t k = bin; k < n_super; k += (int64_t)gridDim.x * TB) super_list[k] = 0xFFFFFFFFu;
+__device__ __forceinline__ void cells(int64_t bin, int64_t stride, int64_t n, int J, int D0,
+                                      const uint64_t *__restrict__ keys_s,
+                                      uint32_t *__restrict__ cell_start,
+                                      uint32_t *__restrict__ super_list, int64_t n_super) {
+    for (int64_t k = bin; k < n_super; k += stride) super_list[k] = 0xFFFFFFFFu;
     const int64_t nbins = (int64_t)1 << (2 * D0);
     if (bin > nbins) return;
     const int shift = 2 * (J - D0);
@@ -473,6 +477,34 @@ __global__ __launch_bounds__(TB) void k_cells(int64_t n, int J, int D0,
         if ((int64_t)(keys_s[mid] >> shift) < bin) lo = mid + 1; else hi = mid;
     }
     cell_start[bin] = (uint32_t)lo;
+}
+
+__global__ __launch_bounds__(TB) void k_cells(int64_t n, int J, int D0,
+                                              const uint64_t *__restrict__ keys_s,
+                                              uint32_t *__restrict__ cell_start,
+                                              uint32_t *__restrict__ super_list, int64_t n_super) {
+    chain_prio();
+    cells((int64_t)blockIdx.x * TB + threadIdx.x, (int64_t)gridDim.x * TB, n, J, D0, keys_s,
+          cell_start, super_list, n_super);
+}
+
+// k_key_fixup and k_cells in one launch (BH_FIXUP_CELLS): the depth-D0 cell starts depend on the
+// 32-bit prefixes only, final before the fixup -- which reorders bodies inside runs of one
+// prefix, so a search probing a run mid-reorder compares the same prefix whichever it reads
+#ifndef BH_FIXUP_CELLS
+#define BH_FIXUP_CELLS 1
+#endif
+__global__ __launch_bounds__(TB) void k_fixup_cells(int64_t n, int J, int D0,
+                                                    const uint32_t *__restrict__ keys32_s,
+                                                    uint64_t *__restrict__ keys_s,
+                                                    uint32_t *__restrict__ perm,
+                                                    uint32_t *__restrict__ cell_start,
+                                                    uint32_t *__restrict__ super_list,
+                                                    int64_t n_super) {
+    chain_prio();
+    const int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
+    cells(t, (int64_t)gridDim.x * TB, n, J, D0, keys_s, cell_start, super_list, n_super);
+    key_fixup(t, n, J, keys32_s, keys_s, perm);
 }
 
 // Largest e in [from, limit] with (keys_s[e] >> shift) == pref (keys_s[from] matches).
@@ -1715,18 +1747,23 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
         if (st != hipSuccess) return st;
         k_key_gather<<<grid_for(n), TB, 0, s>>>(n, b.keys, b.perm, b.keys_s);
     }
-    k_key_fixup<<<grid_for(n), TB, 0, s>>>(n, g.J, b.keys32_s, b.keys_s, b.perm);
+    const uint32_t n_groups = span_groups(b.span_stride);
+    const int64_t n_super = n_groups > 1 ? (int64_t)(g.J + 1) * n_groups : 0;
+    const int64_t nbins1 = ((int64_t)1 << (2 * D0)) + 1;
+    if (BH_FIXUP_CELLS)
+        k_fixup_cells<<<grid_for(std::max<int64_t>(n, nbins1)), TB, 0, s>>>(
+            n, g.J, D0, b.keys32_s, b.keys_s, b.perm, b.cell_start, b.super_list, n_super);
+    else
+        k_key_fixup<<<grid_for(n), TB, 0, s>>>(n, g.J, b.keys32_s, b.keys_s, b.perm);
     k_prep<<<grid_for(n + 1), TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.src, b.dst, b.cpl, b.cnt,
                                           b.spl, b.keys32);
     bytes = b.scratch_bytes;
     st = rocprim::exclusive_scan(b.scratch, bytes, b.cnt, b.base, 0u, (size_t)(n + 1),
                                  rocprim::plus<uint32_t>(), s);
     if (st != hipSuccess) return st;
-    const uint32_t n_groups = span_groups(b.span_stride);
-    const int64_t n_super = n_groups > 1 ? (int64_t)(g.J + 1) * n_groups : 0;
-    k_cells<<<grid_for(((int64_t)1 << (2 * D0)) + 1), TB, 0, s>>>(n, g.J, D0, b.keys_s,
-                                                                  b.cell_start, b.super_list,
-                                                                  n_super);
+    if (!BH_FIXUP_CELLS)
+        k_cells<<<grid_for(nbins1), TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cell_start, b.super_list,
+                                                n_super);
     k_emit_com<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), EC_TB, 0, s>>>(
         n, g, D0, b.keys_s, b.cpl, b.base, b.cell_start, b.dst.x, b.dst.y, b.dst.m, b.dst.cidx,
         b.idx, b.nodes, b.scalars + 1, b.keys32, b.lanes_remap,
