@@ -302,11 +302,11 @@ struct TreeBuffers {
 int cell_table_depth(int J, int64_t n);
 size_t tree_scratch_bytes(int64_t n, int J);
 hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStream_t s);
-// dst.v[a] = src.v[perm[a]]: the velocities of a build made with src.vx = null (k_prep skips them)
 // Splitters spl[from, to) for a bucket sort over more slots than the build that wrote spl[0,
 // from): (sentinel prefix, t * SORT_B) -- the tail of a grown subset capacity is dead padding
 // (sentinel keys in slot order), which would otherwise fall into one oversized last bucket.
 void extend_splitters(uint64_t *spl, uint32_t from, uint32_t to, int J, hipStream_t s);
+// dst.v[a] = src.v[perm[a]]: the velocities of a build made with src.vx = null (k_prep skips them)
 void permute_velocities(int64_t n, const uint32_t *perm, const double *svx, const double *svy,
                         double *dvx, double *dvy, hipStream_t s);
 // After a tree_build: lanes = the bodies in Hilbert order of their cells (refresh), or the
