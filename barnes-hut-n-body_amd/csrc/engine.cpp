@@ -1707,9 +1707,16 @@ bool pipelined(const bh_engine *e, bool last) {
 // bh_create: made later, after another engine's streams (bench.py's counter probe), the mirror's
 // copies shared a queue with the step's kernels (C3 one-step calls with the mirror: 3.25 -> 2.3
 // ms).  An engine that never enables the mirror holds two queues, not three.
+// The pipelined step's cross-stream events order work on this device only: no system-scope fence
+// when they are recorded (the default one writes back and invalidates the caches for the host)
+#ifndef BH_PIPE_EV_NOFENCE
+#define BH_PIPE_EV_NOFENCE 1
+#endif
+constexpr unsigned kPipeEvFlags =
+    hipEventDisableTiming | (BH_PIPE_EV_NOFENCE ? hipEventDisableSystemFence : 0u);
 int pipe_streams(bh_engine *e) {
     for (hipEvent_t &ev : e->pipe_ev)
-        if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, hipEventDisableTiming));
+        if (!ev) HIPCHK(e, hipEventCreateWithFlags(&ev, kPipeEvFlags));
     if (!e->pipe_stream) {
         // the traversal fills every wave slot with a queue of waiting workgroups: at the default
         // priority the overlapped kernels would be dispatched only in its tail
@@ -2010,7 +2017,7 @@ int lane_refresh_beside(bh_engine *e) {
         HIPCHK(e, hipMalloc(&e->lr_scratch, e->lr_scratch_bytes));
         e->lr_cap = e->cap;
     }
-    if (!e->lr_ev) HIPCHK(e, hipEventCreateWithFlags(&e->lr_ev, hipEventDisableTiming));
+    if (!e->lr_ev) HIPCHK(e, hipEventCreateWithFlags(&e->lr_ev, kPipeEvFlags));
     HIPCHK(e, lane_order_into(e->keys_s, n, e->geo.J, e->lr_hkey, e->lr_hkey_s, e->lr_slot,
                               e->lr_scratch, e->lr_scratch_bytes, e->lanes_next, e->pipe_stream));
     HIPCHK(e, hipEventRecord(e->lr_ev, e->pipe_stream));
