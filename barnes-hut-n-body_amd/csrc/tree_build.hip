@@ -1536,6 +1536,97 @@ __global__ __launch_bounds__(SPAN_TB) void k_com_span_top(int J,
     }
 }
 
+// The same pass with everything but the chain itself loaded up front (BH_SPAN_TOP_LDS, up to
+// SPAN_TOP_PAIRS (level, group boundary) pairs): every pair's record, and the values of its
+// children that are not group-crossing (local ones from the record, span ones from the node
+// array: k_com_span finished them), are staged in LDS by all threads at once; the levels then
+// run on LDS only -- a group-crossing child of (L, g) is the pair (L + 1, its owner's group).
+// The old pass made ~5 dependent global loads per level, a 22-level chain of ~1 us steps.
+#ifndef BH_SPAN_TOP_LDS
+#define BH_SPAN_TOP_LDS 1
+#endif
+constexpr int SPAN_TOP_PAIRS = 256;
+constexpr uint32_t TOP_CONST = 0xFFFFFFFFu;  // child value staged (no pair reference)
+__global__ __launch_bounds__(SPAN_TB) void k_com_span_top_lds(
+    int J, const uint32_t *__restrict__ span_list, uint32_t span_stride,
+    const SpanSlot *__restrict__ span_children, const uint32_t *__restrict__ super_list,
+    uint32_t n_groups, Node *nodes) {
+    chain_prio();
+    __shared__ uint32_t s_ni[SPAN_TOP_PAIRS];
+    __shared__ uint32_t s_ref[SPAN_TOP_PAIRS][4];
+    __shared__ double s_v[SPAN_TOP_PAIRS][4][3];
+    __shared__ double s_res[SPAN_TOP_PAIRS][3];
+    const uint32_t P = (uint32_t)(J + 1) * n_groups;
+    for (uint32_t p = threadIdx.x; p < P; p += SPAN_TB) {
+        const uint32_t L = p / n_groups, gi = p % n_groups;
+        const uint32_t ko = super_list[(size_t)L * n_groups + gi];
+        s_ni[p] = NO_SPAN;
+        if (ko == NO_SPAN) continue;
+        const size_t slot = (size_t)L * span_stride + ko;
+        const uint32_t ni = span_list[slot] & ~SPAN_SUPER;
+        const SpanSlot q = span_get(span_children, (size_t)(J + 1) * span_stride, slot);
+        for (int c = 0; c < 4; ++c) {
+            uint32_t ref = TOP_CONST;
+            double v0 = q.v[c][0], v1 = q.v[c][1], v2 = q.v[c][2];
+            if (q.ch[c] != 0xFFFFFFFFu && (q.ch[c] & SPAN_REF)) {
+                const uint32_t kc = q.ch[c] & ~SPAN_REF;
+                const uint32_t ec = span_list[(size_t)(L + 1) * span_stride + kc];
+                if (ec & SPAN_SUPER) {  // finished below in this pass: pair (L + 1, kc's group)
+                    ref = (L + 1) * n_groups + kc / SPAN_GROUP;
+                } else {  // finished by k_com_span (BHA:189-192: mass > 0 only; zeros add nothing)
+                    const Node cn = nodes[ec];
+                    v0 = v1 = v2 = 0.0;
+                    if (cn.mass > 0.0) {
+                        v0 = cn.mass;
+                        v1 = cn.comX * cn.mass;
+                        v2 = cn.comY * cn.mass;
+                    }
+                }
+            }
+            s_ref[p][c] = ref;
+            s_v[p][c][0] = v0;
+            s_v[p][c][1] = v1;
+            s_v[p][c][2] = v2;
+        }
+        s_ni[p] = ni;
+    }
+    __syncthreads();
+    for (int L = J; L >= 0; --L) {
+        for (uint32_t gi = threadIdx.x; gi < n_groups; gi += SPAN_TB) {
+            const uint32_t p = (uint32_t)L * n_groups + gi;
+            const uint32_t ni = s_ni[p];
+            if (ni == NO_SPAN) continue;
+            double mSum = 0.0, cx = 0.0, cy = 0.0;
+            for (int c = 0; c < 4; ++c) {  // children 0..3 in order (BHA:189-192)
+                const uint32_t ref = s_ref[p][c];
+                if (ref != TOP_CONST) {
+                    const double cm = s_res[ref][0];
+                    if (cm > 0.0) {
+                        mSum += cm;
+                        cx += s_res[ref][1] * cm;
+                        cy += s_res[ref][2] * cm;
+                    }
+                } else {
+                    mSum += s_v[p][c][0];
+                    cx += s_v[p][c][1];
+                    cy += s_v[p][c][2];
+                }
+            }
+            const double ox = mSum > 0.0 ? cx / mSum : 0.0;
+            const double oy = mSum > 0.0 ? cy / mSum : 0.0;
+            Node *dst = nodes + ni;
+            dst->mass = mSum;
+            dst->comX = ox;
+            dst->comY = oy;
+            if (!(mSum > 0.0)) dst->meta |= NODE_SKIP | NODE_LEAF;  // a skip-leaf
+            s_res[p][0] = mSum;
+            s_res[p][1] = ox;
+            s_res[p][2] = oy;
+        }
+        __syncthreads();
+    }
+}
+
 inline unsigned grid_for(int64_t n) { return (unsigned)((n + TB - 1) / TB); }
 
 }  // namespace
@@ -1777,7 +1868,11 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
                                              b.span_children);
     k_com_span<<<n_groups, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
                                             b.nodes);
-    if (n_groups > 1)
+    if (n_groups > 1 && BH_SPAN_TOP_LDS && (int64_t)(g.J + 1) * n_groups <= SPAN_TOP_PAIRS)
+        k_com_span_top_lds<<<1, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride,
+                                                 b.span_children, b.super_list, n_groups,
+                                                 b.nodes);
+    else if (n_groups > 1)
         k_com_span_top<<<1, SPAN_TB, 0, s>>>(g.J, b.span_list, b.span_stride, b.span_children,
                                              b.super_list, n_groups, b.nodes);
     return hipGetLastError();
