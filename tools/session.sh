@@ -54,7 +54,10 @@ for step in "$@"; do
       for c in c1_baseline c1_code c2 c4; do bench_line --config $c --steps 10 --warmup 2; done
       bench_line --config c5 --steps 2 --warmup 1 ;;
     profile) run 1800 ${O}_profile.log bash tools/profile.sh ;;
-    sq) run 900 ${O}_sq.log bash tools/profile_sq.sh ;;
+    sq)
+      run 900 ${O}_sq.log bash tools/profile_sq.sh
+      run 120 ${O}_sq_sum.log python3 tools/summarize_sq.py gpurun_out/prof_sq ${O}_c3
+      rm -rf gpurun_out/prof_sq/p* ;;  # (raw counter files: gpurun_out travels back only under 64 MiB)
     timed)  # the driver's C3 call alone under rocprofv3 (no drop-in / counter / verify legs):
             # kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes, summarised over the timed
             # call's window only (tools/timed_window.py)                    -> ${TAG}_c3_timed*
@@ -68,7 +71,9 @@ for step in "$@"; do
       run 300 ${O}_timed_write.log timeout -s KILL 240 rocprofv3 --pmc WRITE_SIZE --kernel-trace \
         -d ${O}_timed_write -o run --output-format csv -- python3 bench.py --steps 4 --warmup 2 $TA
       run 120 ${O}_timed_sum.log python3 tools/timed_window.py ${O}_timed_trace 40 ${O}_c3 \
-        ${O}_timed_fetch ${O}_timed_write 8 ;;
+        ${O}_timed_fetch ${O}_timed_write 8
+      cp "$(find ${O}_timed_trace -name '*kernel_stats.csv' | head -1)" ${O}_c3_timed_kernel_stats.csv
+      rm -rf ${O}_timed_trace ${O}_timed_fetch ${O}_timed_write ;;  # (raw traces: see sq)
     timeline)
       run 600 ${O}_timeline.log rocprofv3 --kernel-trace -d ${O}_tl -o run --output-format csv \
         -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-counters --no-drop-in ;;
@@ -89,7 +94,8 @@ for step in "$@"; do
       run 600 ${O}_soloprof.log rocprofv3 --kernel-trace --stats -d ${O}_soloprof -o run \
         --output-format csv -- python3 tools/solo_rank.py --config c4 --world 8 --rank 0 \
         --steps 10 --warmup 2
-      grep '^{' ${O}_soloprof.log | tail -1 >> ${O}_solo.jsonl ;;
+      grep '^{' ${O}_soloprof.log | tail -1 >> ${O}_solo.jsonl
+      cp "$(find ${O}_soloprof -name '*kernel_stats.csv' | head -1)" ${O}_solo_kernel_stats.csv ;;
     soloab)  # SOLO_LIBS="A B ..." (lib/lib<X>.so; "default" = the in-tree build)
       for rr in 1 2; do
         for L in ${SOLO_LIBS:-A default}; do
