@@ -125,11 +125,26 @@ static void shim_apply_removed(Shim *s) {
         jintArray rem = Java_Native_lastRemoved(env, NULL, s->h);
         jni_check("lastRemoved");
         const jint *r = fake_jvm_ints(rem);
-        for (jsize k = fake_jvm_length(rem); k-- > 0;) { /* removeAt, descending (BHA:519) */
-            long j = (long)r[k];
-            if (k > 0 && r[k - 1] >= r[k]) fail("lastRemoved is not ascending", -1);
-            memmove(&s->bodies->b[j], &s->bodies->b[j + 1], sizeof(Body) * (s->bodies->n - j - 1));
-            s->bodies->n -= 1;
+        const jsize nr = fake_jvm_length(rem);
+        for (jsize k = 1; k < nr; ++k)
+            if (r[k - 1] >= r[k]) fail("lastRemoved is not ascending", -1);
+        if (nr <= 2) {
+            for (jsize k = nr; k-- > 0;) { /* removeAt, descending (BHA:519) */
+                long j = (long)r[k];
+                memmove(&s->bodies->b[j], &s->bodies->b[j + 1],
+                        sizeof(Body) * (s->bodies->n - j - 1));
+                s->bodies->n -= 1;
+            }
+        } else { /* PhysicsEngine.kt: the same survivors in one pass, then one range removal */
+            long w = r[0], q = 0;
+            for (long i = r[0]; i < s->bodies->n; ++i) {
+                if (q < nr && r[q] == i) {
+                    ++q;
+                    continue;
+                }
+                s->bodies->b[w++] = s->bodies->b[i];
+            }
+            s->bodies->n = w;
         }
         fake_jvm_free(rem);
     }
