@@ -634,8 +634,13 @@ class PhysicsEngine:
         n = len(x)
         bs = self._bodies
         if after_step:
-            for j in self._eng.last_removed()[::-1]:  # BHA:519 removeAt on the caller's list
-                del bs[int(j)]
+            rem = self._eng.last_removed()  # BHA:519 removeAt on the caller's list ...
+            if len(rem) <= 2:
+                for j in rem[::-1]:
+                    del bs[int(j)]
+            elif len(rem):  # ... as one pass: the same survivors, objects and list kept
+                gone = set(int(j) for j in rem)
+                bs[:] = [b for i, b in enumerate(bs) if i not in gone]
         if len(bs) != n:
             raise RuntimeError("engine and caller body lists diverged")
         for i in range(n):

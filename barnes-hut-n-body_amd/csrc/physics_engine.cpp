@@ -90,7 +90,20 @@ void PhysicsEngine::pullBodies(bool afterStep) {
         if (rc != BH_OK && rc != BH_E_CAPACITY) check(rc);
         std::vector<int64_t> rem((size_t)cnt);
         check(bh_last_removed(eng_, rem.data(), cnt, &cnt));
-        for (auto it = rem.rbegin(); it != rem.rend(); ++it) bodies_->erase(bodies_->begin() + *it);
+        if (rem.size() <= 2) {
+            for (auto it = rem.rbegin(); it != rem.rend(); ++it)
+                bodies_->erase(bodies_->begin() + *it);
+        } else {  // the list those erase calls leave, in one pass (each erase shifts the tail)
+            size_t w = (size_t)rem[0], q = 0;
+            for (size_t i = (size_t)rem[0]; i < bodies_->size(); ++i) {
+                if (q < rem.size() && (size_t)rem[q] == i) {
+                    ++q;
+                    continue;
+                }
+                (*bodies_)[w++] = (*bodies_)[i];
+            }
+            bodies_->resize(w);
+        }
     }
     const double *x, *y, *vx, *vy, *m;  // the engine's pinned mirror, filled by the step itself
     int64_t got = 0;
