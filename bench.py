@@ -702,7 +702,10 @@ def main():
                 "root": "2400x800",
                 "evals_per_step": 2,
                 "parallelism": f"replicated state, build sharded as locally essential trees, "
-                               f"force sharded x{n_gpus} (RCCL all-gather)"
+                               f"force sharded x{n_gpus} "
+                               + ("(device-to-device copies: a device listed twice)"
+                                  if rccl and "copies" in str(rccl.get("communicators", ""))
+                                  else "(RCCL all-gather)")
                                + (", one process: one handle over the GPUs (bh_create_multi)"
                                   if single_proc else ", one process per GPU")
                 if n_gpus > 1 else "single GPU",
