@@ -1707,6 +1707,19 @@ bool pipelined(const bh_engine *e, bool last) {
 // bh_create: made later, after another engine's streams (bench.py's counter probe), the mirror's
 // copies shared a queue with the step's kernels (C3 one-step calls with the mirror: 3.25 -> 2.3
 // ms).  An engine that never enables the mirror holds two queues, not three.
+// The exchange stream (RCCL all-gathers, or the in-process copies) at the high priority: its
+// few workgroups are dispatched ahead of the traversal rounds' queued ones as soon as a slot
+// frees, instead of in the last round's tail (BH_COMM_PRIORITY=0: the default priority)
+#ifndef BH_COMM_PRIORITY
+#define BH_COMM_PRIORITY 1
+#endif
+hipError_t comm_stream_create(hipStream_t *s) {
+    int lo = 0, hi = 0;
+    hipError_t rc = hipDeviceGetStreamPriorityRange(&lo, &hi);
+    if (rc != hipSuccess) return rc;
+    return hipStreamCreateWithPriority(s, hipStreamNonBlocking, BH_COMM_PRIORITY ? hi : lo);
+}
+
 // The pipelined step's cross-stream events order work on this device only: no system-scope fence
 // when they are recorded (the default one writes back and invalidates the caches for the host)
 #ifndef BH_PIPE_EV_NOFENCE
@@ -2329,7 +2342,7 @@ int bh::member_create(const bh_params *p, int device, int rank, int world, void 
     int rc = engine_init(e, p, device);
     if (rc == BH_OK) {
         e->comm = static_cast<ncclComm_t>(comm);
-        hipError_t hr = hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking);
+        hipError_t hr = comm_stream_create(&e->comm_stream);
         for (int k = 0; k < BH_SHARD_ROUNDS && hr == hipSuccess; ++k)
             hr = hipEventCreateWithFlags(&e->round_ev[k], hipEventDisableTiming);
         if (hr == hipSuccess) hr = hipEventCreateWithFlags(&e->gathered_ev, hipEventDisableTiming);
@@ -2496,7 +2509,7 @@ int bh_create_dist(const bh_params *p, int device, int rank, int world, const vo
             e->err = std::string("ncclCommInitRank: ") + ncclGetErrorString(nr);
             rc = BH_E_COMM;
         }
-        hipError_t hr = hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking);
+        hipError_t hr = comm_stream_create(&e->comm_stream);
         for (int k = 0; k < BH_SHARD_ROUNDS && hr == hipSuccess; ++k)
             hr = hipEventCreateWithFlags(&e->round_ev[k], hipEventDisableTiming);
         if (hr == hipSuccess) hr = hipEventCreateWithFlags(&e->gathered_ev, hipEventDisableTiming);
@@ -2542,7 +2555,7 @@ int bh_create_local(const bh_params *p, int device, int rank, bh_local_group *gr
     e->world = group->world;
     int rc = engine_init(e, p, device);
     if (rc == BH_OK) {
-        hipError_t hr = hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking);
+        hipError_t hr = comm_stream_create(&e->comm_stream);
         for (int k = 0; k < BH_SHARD_ROUNDS && hr == hipSuccess; ++k)
             hr = hipEventCreateWithFlags(&e->round_ev[k], hipEventDisableTiming);
         if (hr == hipSuccess) hr = hipEventCreateWithFlags(&e->gathered_ev, hipEventDisableTiming);
@@ -2576,7 +2589,7 @@ int bh_create_solo(const bh_params *p, int device, int rank, int world, bh_engin
     e->world = world;
     int rc = engine_init(e, p, device);
     if (rc == BH_OK) {
-        hipError_t hr = hipStreamCreateWithFlags(&e->comm_stream, hipStreamNonBlocking);
+        hipError_t hr = comm_stream_create(&e->comm_stream);
         for (int k = 0; k < BH_SHARD_ROUNDS && hr == hipSuccess; ++k)
             hr = hipEventCreateWithFlags(&e->round_ev[k], hipEventDisableTiming);
         if (hr == hipSuccess) hr = hipEventCreateWithFlags(&e->gathered_ev, hipEventDisableTiming);
