@@ -371,7 +371,7 @@ int main(int argc, char **argv) {
     const long allocs0 = shadow_allocs;
     oracle_engine *o = oracle_of(&list, &s);
     List list2 = {NULL, 0}, list3 = {NULL, 0};
-    long removed_total = 0, quads_checked = 0;
+    long removed_total = 0, quads_checked = 0, removed_max = 0;
     for (long frame = 0; frame < 40; ++frame) {
         if (frame == 10) cfg_theta = 0.7; /* Z/X keys (PNL:247-248), read live */
         if (frame == 14) cfg_DT = 0.008;  /* O/P keys (PNL:255-257) */
@@ -399,6 +399,7 @@ int main(int argc, char **argv) {
         shim_step(&s); /* PNL:291 */
         oracle_step(o, 1);
         removed_total += before - s.bodies->n;
+        if (before - s.bodies->n > removed_max) removed_max = before - s.bodies->n;
         compare(s.bodies, o, frame);
         if (frame % 4 == 3) { /* showTree: getTreeForDebug().visitQuads (PNL:333-340) */
             int64_t nq = 0;
@@ -416,10 +417,11 @@ int main(int argc, char **argv) {
     }
     if (removed_total == 0) fail("the scene never merged: identity bookkeeping untested", 40);
     printf("abi_harness: 40 frames through the JNI glue on %d device(s) (%ld native calls) "
-           "bit-identical to the oracle; %ld bodies merged away, %ld quads checked, %ld uploads "
-           "after the constructor/resets, %ld shadow allocations after the constructor\n",
-           bh_multi_world((bh_engine *)(intptr_t)s.h), jni_calls, removed_total, quads_checked,
-           shim_steps_uploaded, shadow_allocs - allocs0);
+           "bit-identical to the oracle; %ld bodies merged away (at most %ld in one frame), %ld "
+           "quads checked, %ld uploads after the constructor/resets, %ld shadow allocations after "
+           "the constructor\n",
+           bh_multi_world((bh_engine *)(intptr_t)s.h), jni_calls, removed_total, removed_max,
+           quads_checked, shim_steps_uploaded, shadow_allocs - allocs0);
     oracle_destroy(o);
     bh_destroy((bh_engine *)(intptr_t)s.h); /* the Kotlin object lives as long as the app */
     return 0;
