@@ -416,6 +416,7 @@ int main(int argc, char **argv) {
         }
     }
     if (removed_total == 0) fail("the scene never merged: identity bookkeeping untested", 40);
+    if (removed_max < 3) fail("no frame removed 3+ bodies: the one-pass removal is untested", 40);
     printf("abi_harness: 40 frames through the JNI glue on %d device(s) (%ld native calls) "
            "bit-identical to the oracle; %ld bodies merged away (at most %ld in one frame), %ld "
            "quads checked, %ld uploads after the constructor/resets, %ld shadow allocations after "

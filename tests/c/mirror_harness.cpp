@@ -167,6 +167,7 @@ int main(int argc, char **argv) {
         }
     }
     if (removed == 0) fail("the scene never merged: identity bookkeeping untested", 40);
+    if (removed_max < 3) fail("no frame removed 3+ bodies: the one-pass removal is untested", 40);
     std::printf("mirror_harness: 40 frames of bh::PhysicsEngine on %d device(s) bit-identical to "
                 "the oracle; %ld bodies merged away (at most %ld in one frame), %ld quads checked\n",
                 bh_multi_world(engine.handle()), removed, removed_max, quads);
