@@ -98,6 +98,37 @@ JNIEXPORT jint JNICALL Java_Native_getInto(JNIEnv *env, jobject self, jlong h, j
     return (jint)n;
 }
 
+/* external fun map(h: Long, info: LongArray): ByteBuffer
+ * The engine's pinned caller-order mirror itself (bh_map_bodies), which the step filled: a direct
+ * buffer over its five planes (x at 0, y at the stride, then vx, vy, m) and info = [n, stride in
+ * doubles].  Nothing is copied -- the shim compares and unpacks straight from pinned host memory
+ * -- and the buffer is valid until the next native call that steps, resets or builds the debug
+ * tree (the shim maps again after each). */
+JNIEXPORT jobject JNICALL Java_Native_map(JNIEnv *env, jobject self, jlong h, jlongArray info) {
+    (void)self;
+    bh_engine *e = (bh_engine *)(intptr_t)h;
+    const double *f[5] = {NULL, NULL, NULL, NULL, NULL};
+    int64_t n = 0;
+    static double empty[1];
+    if (!info || (*env)->GetArrayLength(env, info) < 2) {
+        throw_rt(env, NULL, "map: info must hold 2 longs");
+        return NULL;
+    }
+    if (bh_shim_map(e, f, &n) != BH_OK) {
+        throw_rt(env, e, "map");
+        return NULL;
+    }
+    const int64_t stride = n > 0 ? (int64_t)(f[1] - f[0]) : 0;
+    if (n > 0 && 5 * stride * (int64_t)sizeof(double) > INT32_MAX) {
+        throw_rt(env, NULL, "map: more bodies than a direct buffer addresses (40 stride >= 2^31)");
+        return NULL;
+    }
+    const jlong out[2] = {(jlong)n, (jlong)stride};
+    (*env)->SetLongArrayRegion(env, info, 0, 2, out);
+    return (*env)->NewDirectByteBuffer(env, n > 0 ? (void *)f[0] : (void *)empty,
+                                       (jlong)(5 * stride * (int64_t)sizeof(double)));
+}
+
 /* external fun quads(h: Long): DoubleArray  ([cx0, cy0, h0, cx1, ...], visitQuads order) */
 JNIEXPORT jdoubleArray JNICALL Java_Native_quads(JNIEnv *env, jobject self, jlong h) {
     (void)self;

@@ -5,6 +5,8 @@
 // and run with -Djava.library.path=barnes-hut-n-body_amd/lib.
 // tests/test_kotlin_dropin.py checks these declarations against bh_jni.c's exports.
 
+import java.nio.ByteBuffer
+
 object Native {
     init {
         System.loadLibrary("bh_jni")
@@ -29,6 +31,11 @@ object Native {
     /** The bodies into the caller's SoA array [x[0..n) y[n..2n) vx vy m] from the engine's pinned
      *  mirror (bh_map_bodies), no allocation; returns n, or -n if soa holds fewer than 5 n. */
     external fun getInto(h: Long, soa: DoubleArray): Int
+
+    /** The engine's pinned caller-order mirror itself as a direct buffer (five fp64 planes x, y,
+     *  vx, vy, m at multiples of info[1] doubles; info[0] = n): nothing copied.  Valid until the
+     *  next step / reset / quads call. */
+    external fun map(h: Long, info: LongArray): ByteBuffer
 
     /** bh_get_quads as interleaved (cx, cy, h) triples in visitQuads order. */
     external fun quads(h: Long): DoubleArray

@@ -13,6 +13,9 @@
 // caller's list with the same removeAt calls (BHA:519), so every surviving Body keeps its
 // identity; the quadtree jitter (BHA:146-151) moves bodies exactly as the reference does.
 
+import java.nio.ByteOrder
+import java.nio.DoubleBuffer
+
 /** getTreeForDebug()'s result: the engine's quad list in visitQuads order (BHA:265-274). */
 class QuadList(private val q: DoubleArray) {
     /** Pre-order over every cell (root, then children 0..3 recursively), as BHTree.visitQuads. */
@@ -30,10 +33,14 @@ class PhysicsEngine(initialBodies: MutableList<Body>) {
     // bh_create_multi over the GPUs of -Dbh.deviceMask (bit d = HIP device d; default 0 = every
     // visible GPU): one handle, every step fanned out over the GPUs and joined (BHA:374-395)
     private val handle: Long = Native.create(Integer.decode(System.getProperty("bh.deviceMask", "0")))
-    // SoA of what the engine holds (x[0..n) y[n..2n) vx vy m), reused frame after frame: no
-    // per-frame allocation that grows with N
-    private var shadow = DoubleArray(0)
-    private var shadowN = -1
+    // What the engine holds, read in place: its pinned caller-order mirror (Native.map, five
+    // planes of `stride` doubles), mapped again after every native call that changes it; the
+    // upload array is reused (grown only) -- no per-frame allocation that grows with N
+    private val info = LongArray(2)
+    private var mirror: DoubleBuffer = DoubleBuffer.allocate(0)
+    private var stride = 0
+    private var mirrorN = -1
+    private var upload = DoubleArray(0)
 
     /** BHA:315 -- bodies heavier than this absorb neighbours closer than mergeMinDist. */
     var mergeMaxMass: Double = 4_000.0
@@ -79,27 +86,37 @@ class PhysicsEngine(initialBodies: MutableList<Body>) {
     /** Whether the caller's bodies differ (bitwise) from what the engine holds -- in place. */
     private fun changed(): Boolean {
         val n = bodies.size
-        if (n != shadowN) return true
-        val a = shadow
+        if (n != mirrorN) return true
+        val a = mirror
+        val s = stride
         for (i in 0 until n) {
             val b = bodies[i]
-            if (b.x.toRawBits() != a[i].toRawBits() || b.y.toRawBits() != a[n + i].toRawBits() ||
-                b.vx.toRawBits() != a[2 * n + i].toRawBits() ||
-                b.vy.toRawBits() != a[3 * n + i].toRawBits() ||
-                b.m.toRawBits() != a[4 * n + i].toRawBits()) return true
+            if (b.x.toRawBits() != a.get(i).toRawBits() ||
+                b.y.toRawBits() != a.get(s + i).toRawBits() ||
+                b.vx.toRawBits() != a.get(2 * s + i).toRawBits() ||
+                b.vy.toRawBits() != a.get(3 * s + i).toRawBits() ||
+                b.m.toRawBits() != a.get(4 * s + i).toRawBits()) return true
         }
         return false
     }
 
+    /** The engine's mirror, mapped after a native call that changed it; returns n. */
+    private fun map(): Int {
+        mirror = Native.map(handle, info).order(ByteOrder.nativeOrder()).asDoubleBuffer()
+        stride = info[1].toInt()
+        mirrorN = info[0].toInt()
+        return mirrorN
+    }
+
     private fun push() {
         val n = bodies.size
-        if (shadow.size < 5 * n) shadow = DoubleArray(5 * n)
-        val a = shadow
+        if (upload.size < 5 * n) upload = DoubleArray(5 * n)
+        val a = upload
         for ((i, b) in bodies.withIndex()) {
             a[i] = b.x; a[n + i] = b.y; a[2 * n + i] = b.vx; a[3 * n + i] = b.vy; a[4 * n + i] = b.m
         }
         Native.reset(handle, n, a)
-        shadowN = n
+        map()                                               // (the engine's copy, as uploaded)
     }
 
     /** afterStep: apply the step's removals (BHA:519) once -- the list the reference's removeAt
@@ -121,17 +138,14 @@ class PhysicsEngine(initialBodies: MutableList<Body>) {
                 bodies.subList(w, n0).clear()               // the tail, one range removal
             }
         }
-        var n = Native.getInto(handle, shadow)              // the engine's pinned mirror, SoA
-        if (n < 0) {                                        // (only after a reset to more bodies)
-            shadow = DoubleArray(-5 * n)
-            n = Native.getInto(handle, shadow)
-        }
+        val n = map()                                       // the engine's pinned mirror, in place
         check(n == bodies.size) { "engine and caller body lists diverged" }
-        val a = shadow
+        val a = mirror
+        val s = stride
         for (i in 0 until n) {
             val b = bodies[i]
-            b.x = a[i]; b.y = a[n + i]; b.vx = a[2 * n + i]; b.vy = a[3 * n + i]; b.m = a[4 * n + i]
+            b.x = a.get(i); b.y = a.get(s + i); b.vx = a.get(2 * s + i); b.vy = a.get(3 * s + i)
+            b.m = a.get(4 * s + i)
         }
-        shadowN = n
     }
 }

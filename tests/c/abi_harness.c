@@ -53,8 +53,11 @@ static void fail(const char *what, long frame) {
 typedef struct {
     jlong h; /* Native.create's handle */
     List *bodies;
-    jdoubleArray shadow; /* the shim's reusable DoubleArray: SoA of what the engine holds */
-    long shadow_n;
+    jdoubleArray shadow; /* the shim's reusable upload DoubleArray (grown only) */
+    jlongArray info;     /* Native.map's [n, stride] */
+    const double *mir;   /* the engine's pinned mirror, read in place (Native.map) */
+    long mir_stride;
+    long shadow_n;       /* bodies in the mapped mirror (-1: none) */
     double mergeMaxMass, mergeMinDist; /* BHA:315,321 */
 } Shim;
 
@@ -95,25 +98,39 @@ static void shim_grow(Shim *s, long n) { /* `shadow = DoubleArray(5 n)` when too
     ++shadow_allocs;
 }
 
+/* map(): the engine's pinned mirror as a direct buffer (Native.map), read in place; returns n */
+static long shim_map(Shim *s) {
+    jobject buf = Java_Native_map(env, NULL, s->h, s->info);
+    jni_check("map");
+    const jlong *in = fake_jvm_longs(s->info);
+    jlong cap = 0;
+    s->mir = (const double *)fake_jvm_direct_address(buf, &cap);
+    s->mir_stride = (long)in[1];
+    s->shadow_n = (long)in[0];
+    if (cap != 5 * (jlong)sizeof(double) * in[1]) fail("map: buffer capacity is not 5 planes", -1);
+    fake_jvm_free(buf); /* (the JVM's buffer object; the memory is the engine's) */
+    return s->shadow_n;
+}
+
 static void shim_push(Shim *s) {
     long n = s->bodies->n;
     shim_grow(s, n);
     soa_of(s->bodies, fake_jvm_doubles(s->shadow));
     Java_Native_reset(env, NULL, s->h, (jint)n, s->shadow);
     jni_check("reset");
-    s->shadow_n = n;
+    shim_map(s); /* the engine's copy, as uploaded */
 }
 
-/* changed(): field by field against the shadow, in place (toRawBits compares) */
+/* changed(): field by field against the mapped mirror, in place (toRawBits compares) */
 static int shim_changed(Shim *s) {
-    long n = s->bodies->n;
+    long n = s->bodies->n, st = s->mir_stride;
     if (n != s->shadow_n) return 1;
-    const double *a = fake_jvm_doubles(s->shadow);
+    const double *a = s->mir;
     for (long i = 0; i < n; ++i) {
         const Body *b = &s->bodies->b[i];
-        if (memcmp(&b->x, &a[i], 8) || memcmp(&b->y, &a[n + i], 8) ||
-            memcmp(&b->vx, &a[2 * n + i], 8) || memcmp(&b->vy, &a[3 * n + i], 8) ||
-            memcmp(&b->m, &a[4 * n + i], 8))
+        if (memcmp(&b->x, &a[i], 8) || memcmp(&b->y, &a[st + i], 8) ||
+            memcmp(&b->vx, &a[2 * st + i], 8) || memcmp(&b->vy, &a[3 * st + i], 8) ||
+            memcmp(&b->m, &a[4 * st + i], 8))
             return 1;
     }
     return 0;
@@ -150,19 +167,9 @@ static void shim_apply_removed(Shim *s) {
     }
 }
 
-static long shim_get(Shim *s) {
-    jint got = Java_Native_getInto(env, NULL, s->h, s->shadow);
-    jni_check("getInto");
-    if (got < 0) { /* the shadow is too small (after a reset to more bodies): grow, again */
-        shim_grow(s, -(long)got);
-        got = Java_Native_getInto(env, NULL, s->h, s->shadow);
-        jni_check("getInto");
-    }
-    return (long)got;
-}
-
 static void shim_unpack(Shim *s, long n) {
-    const double *a = fake_jvm_doubles(s->shadow);
+    const double *a = s->mir;
+    const long st = s->mir_stride;
     if (n != s->bodies->n) {
         fprintf(stderr, "abi_harness: engine N %ld vs caller list %ld\n", n, s->bodies->n);
         exit(1);
@@ -170,17 +177,16 @@ static void shim_unpack(Shim *s, long n) {
     for (long i = 0; i < n; ++i) { /* into the SAME Body objects (BHA:414-432) */
         Body *b = &s->bodies->b[i];
         b->x = a[i];
-        b->y = a[n + i];
-        b->vx = a[2 * n + i];
-        b->vy = a[3 * n + i];
-        b->m = a[4 * n + i];
+        b->y = a[st + i];
+        b->vx = a[2 * st + i];
+        b->vy = a[3 * st + i];
+        b->m = a[4 * st + i];
     }
-    s->shadow_n = n;
 }
 
 static void shim_pull(Shim *s, int after_step) {
     if (after_step) shim_apply_removed(s);
-    shim_unpack(s, shim_get(s));
+    shim_unpack(s, shim_map(s));
 }
 
 static void shim_create(Shim *s, List *initial, jint device_mask) {
@@ -188,6 +194,7 @@ static void shim_create(Shim *s, List *initial, jint device_mask) {
     s->mergeMaxMass = 4000.0;
     s->mergeMinDist = 8.0;
     s->shadow_n = -1;
+    s->info = fake_jvm_long_array(2);
     s->h = Java_Native_create(env, NULL, device_mask);
     if (fake_jvm_take_exception() || !s->h) {
         fprintf(stderr, "abi_harness: Native.create failed (no GPU?)\n");
@@ -318,7 +325,7 @@ static int c3_frames(long frames, jint mask) {
     shim_create(&s, &list, mask);
     for (int w = 0; w < 5; ++w) shim_step(&s);
     const long allocs0 = shadow_allocs, uploads0 = shim_steps_uploaded;
-    double t[6] = {0, 0, 0, 0, 0, 0}; /* params, changed, step, removals, getInto, unpack */
+    double t[6] = {0, 0, 0, 0, 0, 0}; /* params, changed, step, removals, map, unpack */
     const long n0 = s.bodies->n;
     const double t0 = now_ms();
     for (long f = 0; f < frames; ++f) {
@@ -335,7 +342,7 @@ static int c3_frames(long frames, jint mask) {
         b = now_ms(); t[2] += b - a; a = b;
         shim_apply_removed(&s);
         b = now_ms(); t[3] += b - a; a = b;
-        const long n = shim_get(&s);
+        const long n = shim_map(&s);
         b = now_ms(); t[4] += b - a; a = b;
         shim_unpack(&s, n);
         b = now_ms(); t[5] += b - a;
@@ -344,7 +351,7 @@ static int c3_frames(long frames, jint mask) {
     const double host = t[0] + t[1] + t[3] + t[4] + t[5];
     printf("{\"frames\": %ld, \"bodies\": %ld, \"devices\": %d, \"ms_per_frame\": %.4f, "
            "\"step_ms\": %.4f, \"host_ms\": %.4f, \"params_ms\": %.4f, \"changed_ms\": %.4f, "
-           "\"removals_ms\": %.4f, \"getInto_ms\": %.4f, \"unpack_ms\": %.4f, "
+           "\"removals_ms\": %.4f, \"map_ms\": %.4f, \"unpack_ms\": %.4f, "
            "\"allocations_per_frame\": %.3f, \"uploads\": %ld}\n",
            frames, n0, bh_multi_world((bh_engine *)(intptr_t)s.h), total / frames, t[2] / frames,
            host / frames, t[0] / frames, t[1] / frames, t[3] / frames, t[4] / frames, t[5] / frames,
@@ -401,6 +408,18 @@ int main(int argc, char **argv) {
         removed_total += before - s.bodies->n;
         if (before - s.bodies->n > removed_max) removed_max = before - s.bodies->n;
         compare(s.bodies, o, frame);
+        if (frame == 5) { /* Native.getInto (a copy into a Java array) agrees with the mapped mirror */
+            jdoubleArray a = fake_jvm_double_array((jsize)(5 * s.bodies->n), NULL);
+            const jint got = Java_Native_getInto(env, NULL, s.h, a);
+            jni_check("getInto");
+            const double *g = fake_jvm_doubles(a);
+            const long n = s.bodies->n, st = s.mir_stride;
+            if (got != (jint)n) fail("getInto's count", frame);
+            for (int k = 0; k < 5; ++k)
+                if (memcmp(g + k * n, s.mir + k * st, sizeof(double) * (size_t)n))
+                    fail("getInto differs from the mapped mirror", frame);
+            fake_jvm_free(a);
+        }
         if (frame % 4 == 3) { /* showTree: getTreeForDebug().visitQuads (PNL:333-340) */
             int64_t nq = 0;
             double *q = shim_tree(&s, &nq);

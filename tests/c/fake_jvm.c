@@ -67,6 +67,29 @@ static void set_int_region(JNIEnv *env, jintArray a, jsize start, jsize len, con
     memcpy(a->data + sizeof(jint) * (size_t)start, buf, sizeof(jint) * (size_t)len);
 }
 
+static void set_long_region(JNIEnv *env, jlongArray a, jsize start, jsize len, const jlong *buf) {
+    (void)env;
+    if (start < 0 || len < 0 || start + len > a->len) {
+        snprintf(pending, sizeof(pending), "SetLongArrayRegion out of bounds");
+        has_pending = 1;
+        return;
+    }
+    memcpy(a->data + sizeof(jlong) * (size_t)start, buf, sizeof(jlong) * (size_t)len);
+}
+/* a direct buffer: no elements of its own, the address and capacity in its data */
+struct direct_buf {
+    void *address;
+    jlong capacity;
+};
+static jobject new_direct_buffer(JNIEnv *env, void *address, jlong capacity) {
+    (void)env;
+    struct fake_jobject *o = new_array((jsize)sizeof(struct direct_buf), 1);
+    o->len = -1; /* not an array */
+    struct direct_buf d = {address, capacity};
+    memcpy(o->data, &d, sizeof(d));
+    return o;
+}
+
 static const struct JNINativeInterface_ table = {
     .FindClass = find_class,
     .ThrowNew = throw_new,
@@ -76,6 +99,8 @@ static const struct JNINativeInterface_ table = {
     .GetDoubleArrayRegion = get_double_region,
     .NewIntArray = new_int_array,
     .SetIntArrayRegion = set_int_region,
+    .SetLongArrayRegion = set_long_region,
+    .NewDirectByteBuffer = new_direct_buffer,
 };
 static JNIEnv env_ptr = &table;
 
@@ -96,3 +121,12 @@ double *fake_jvm_doubles(jdoubleArray a) { return (double *)a->data; }
 jint *fake_jvm_ints(jintArray a) { return (jint *)a->data; }
 jsize fake_jvm_length(jarray a) { return a->len; }
 void fake_jvm_free(jarray a) { free(a); }
+
+jlongArray fake_jvm_long_array(jsize len) { return new_array(len, sizeof(jlong)); }
+jlong *fake_jvm_longs(jlongArray a) { return (jlong *)a->data; }
+void *fake_jvm_direct_address(jobject buf, jlong *capacity) {
+    struct direct_buf d;
+    memcpy(&d, buf->data, sizeof(d));
+    if (capacity) *capacity = d.capacity;
+    return d.address;
+}

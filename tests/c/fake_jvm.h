@@ -16,6 +16,10 @@ jdoubleArray fake_jvm_double_array(jsize len, const double *init); /* NULL init:
 double *fake_jvm_doubles(jdoubleArray a);
 jint *fake_jvm_ints(jintArray a);
 jsize fake_jvm_length(jarray a);
+jlongArray fake_jvm_long_array(jsize len);
+jlong *fake_jvm_longs(jlongArray a);
+/* a direct ByteBuffer's address and capacity (GetDirectBufferAddress / GetDirectBufferCapacity) */
+void *fake_jvm_direct_address(jobject buf, jlong *capacity);
 void fake_jvm_free(jarray a);
 
 /* the glue's natives (bh_jni.c), declared for the harness */
@@ -25,6 +29,7 @@ void Java_Native_setParams(JNIEnv *env, jobject self, jlong h, jdouble G, jdoubl
 void Java_Native_reset(JNIEnv *env, jobject self, jlong h, jint n, jdoubleArray soa);
 void Java_Native_step(JNIEnv *env, jobject self, jlong h, jint k);
 jint Java_Native_getInto(JNIEnv *env, jobject self, jlong h, jdoubleArray soa);
+jobject Java_Native_map(JNIEnv *env, jobject self, jlong h, jlongArray info);
 jdoubleArray Java_Native_quads(JNIEnv *env, jobject self, jlong h);
 jintArray Java_Native_lastRemoved(JNIEnv *env, jobject self, jlong h);
 

@@ -23,6 +23,7 @@ typedef jobject jclass;
 typedef jobject jarray;
 typedef jarray jdoubleArray;
 typedef jarray jintArray;
+typedef jarray jlongArray;
 
 struct JNINativeInterface_;
 typedef const struct JNINativeInterface_ *JNIEnv;
@@ -39,6 +40,9 @@ struct JNINativeInterface_ {
     jintArray (*NewIntArray)(JNIEnv *env, jsize len);
     void (*SetIntArrayRegion)(JNIEnv *env, jintArray array, jsize start, jsize len,
                               const jint *buf);
+    void (*SetLongArrayRegion)(JNIEnv *env, jlongArray array, jsize start, jsize len,
+                               const jlong *buf);
+    jobject (*NewDirectByteBuffer)(JNIEnv *env, void *address, jlong capacity);
 };
 
 #endif

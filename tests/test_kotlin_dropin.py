@@ -13,7 +13,8 @@ JNI_C = os.path.join(ROOT, "barnes-hut-n-body_amd", "jni", "bh_jni.c")
 
 # Kotlin parameter / return types -> the JNI C types javac -h would emit
 KT2JNI = {"Int": "jint", "Long": "jlong", "Double": "jdouble", "DoubleArray": "jdoubleArray",
-          "IntArray": "jintArray", "Unit": "void"}
+          "IntArray": "jintArray", "LongArray": "jlongArray", "ByteBuffer": "jobject",
+          "Unit": "void"}
 
 
 def kotlin_externals():
@@ -45,7 +46,7 @@ def test_native_externals_match_the_jni_exports():
     assert set(kt) == set(c), f"Kotlin {sorted(kt)} vs C {sorted(c)}"
     for name in kt:
         assert kt[name] == c[name], f"{name}: Kotlin {kt[name]} vs C {c[name]}"
-    assert len(kt) == 7
+    assert len(kt) == 8
 
 
 def test_physics_engine_offers_the_reference_surface():
