@@ -15,6 +15,10 @@
 
 import java.nio.ByteOrder
 import java.nio.DoubleBuffer
+import java.util.concurrent.atomic.AtomicBoolean
+import kotlinx.coroutines.Dispatchers
+import kotlinx.coroutines.launch
+import kotlinx.coroutines.runBlocking
 
 /** getTreeForDebug()'s result: the engine's quad list in visitQuads order (BHA:265-274). */
 class QuadList(private val q: DoubleArray) {
@@ -41,6 +45,7 @@ class PhysicsEngine(initialBodies: MutableList<Body>) {
     private var stride = 0
     private var mirrorN = -1
     private var upload = DoubleArray(0)
+    private var spare = arrayOfNulls<Body>(0)                // the removal pass's (grown only)
 
     /** BHA:315 -- bodies heavier than this absorb neighbours closer than mergeMinDist. */
     var mergeMaxMass: Double = 4_000.0
@@ -83,21 +88,40 @@ class PhysicsEngine(initialBodies: MutableList<Body>) {
         Config.WIDTH_PX, Config.HEIGHT_PX, mergeMaxMass, mergeMinDist
     )
 
+    // The O(N) passes over the caller's bodies in chunks on Dispatchers.Default, joined -- the
+    // reference's own fan-out (BHA:374-395, 408); short lists stay on the caller's thread
+    private val workers = Runtime.getRuntime().availableProcessors().coerceIn(1, 16)
+
+    private inline fun chunks(n: Int, crossinline body: (Int, Int) -> Unit) {
+        if (n < 65_536 || workers == 1) { body(0, n); return }
+        val per = (n + workers - 1) / workers
+        runBlocking {
+            for (w in 0 until workers) {
+                val lo = w * per
+                val hi = minOf(n, lo + per)
+                if (lo < hi) launch(Dispatchers.Default) { body(lo, hi) }
+            }
+        }
+    }
+
     /** Whether the caller's bodies differ (bitwise) from what the engine holds -- in place. */
     private fun changed(): Boolean {
         val n = bodies.size
         if (n != mirrorN) return true
         val a = mirror
         val s = stride
-        for (i in 0 until n) {
-            val b = bodies[i]
-            if (b.x.toRawBits() != a.get(i).toRawBits() ||
-                b.y.toRawBits() != a.get(s + i).toRawBits() ||
-                b.vx.toRawBits() != a.get(2 * s + i).toRawBits() ||
-                b.vy.toRawBits() != a.get(3 * s + i).toRawBits() ||
-                b.m.toRawBits() != a.get(4 * s + i).toRawBits()) return true
+        val diff = AtomicBoolean(false)
+        chunks(n) { lo, hi ->
+            for (i in lo until hi) {
+                val b = bodies[i]
+                if (b.x.toRawBits() != a.get(i).toRawBits() ||
+                    b.y.toRawBits() != a.get(s + i).toRawBits() ||
+                    b.vx.toRawBits() != a.get(2 * s + i).toRawBits() ||
+                    b.vy.toRawBits() != a.get(3 * s + i).toRawBits() ||
+                    b.m.toRawBits() != a.get(4 * s + i).toRawBits()) { diff.set(true); break }
+            }
         }
-        return false
+        return diff.get()
     }
 
     /** The engine's mirror, mapped after a native call that changed it; returns n. */
@@ -121,7 +145,9 @@ class PhysicsEngine(initialBodies: MutableList<Body>) {
 
     /** afterStep: apply the step's removals (BHA:519) once -- the list the reference's removeAt
      *  calls (highest index first) leave, made in one pass: each removeAt shifts the tail, tens of
-     *  them per C3 frame cost ~16 ms at 1e6 bodies (tests/c/abi_harness.c --c3-frames). */
+     *  them per C3 frame cost ~16 ms at 1e6 bodies (tests/c/abi_harness.c --c3-frames).  The
+     *  pass runs in chunks: survivors into a reused spare array, then back (set, no structural
+     *  change), so the caller keeps the same list object with the same Body objects in it. */
     private fun pull(afterStep: Boolean) {
         if (afterStep) {
             val rem = Native.lastRemoved(handle)            // ascending; usually empty
@@ -129,23 +155,33 @@ class PhysicsEngine(initialBodies: MutableList<Body>) {
                 for (k in rem.indices.reversed()) bodies.removeAt(rem[k])
             } else {
                 val n0 = bodies.size
-                var w = rem[0]                              // survivors slide down, in order
-                var r = 0
-                for (i in rem[0] until n0) {
-                    if (r < rem.size && rem[r] == i) { r++; continue }
-                    bodies[w++] = bodies[i]
+                val base = rem[0]                           // survivors slide down, in order:
+                if (spare.size < n0 - base) spare = arrayOfNulls(n0 - base)
+                val out = spare
+                chunks(n0 - base) { lo, hi ->               // into the spare array, chunk by chunk
+                    val k = rem.binarySearch(base + lo)
+                    var r = if (k >= 0) k else -k - 1       // removals below this chunk
+                    var w = lo - r
+                    for (i in base + lo until base + hi) {
+                        if (r < rem.size && rem[r] == i) { r++; continue }
+                        out[w++] = bodies[i]
+                    }
                 }
-                bodies.subList(w, n0).clear()               // the tail, one range removal
+                val m = n0 - base - rem.size
+                chunks(m) { lo, hi -> for (i in lo until hi) bodies[base + i] = out[i]!! }
+                bodies.subList(base + m, n0).clear()        // the tail, one range removal
             }
         }
         val n = map()                                       // the engine's pinned mirror, in place
         check(n == bodies.size) { "engine and caller body lists diverged" }
         val a = mirror
         val s = stride
-        for (i in 0 until n) {
-            val b = bodies[i]
-            b.x = a.get(i); b.y = a.get(s + i); b.vx = a.get(2 * s + i); b.vy = a.get(3 * s + i)
-            b.m = a.get(4 * s + i)
+        chunks(n) { lo, hi ->
+            for (i in lo until hi) {
+                val b = bodies[i]
+                b.x = a.get(i); b.y = a.get(s + i); b.vx = a.get(2 * s + i); b.vy = a.get(3 * s + i)
+                b.m = a.get(4 * s + i)
+            }
         }
     }
 }

@@ -16,6 +16,7 @@
  * Exit status 0 = pass; the last line says what was checked.
  */
 #define _POSIX_C_SOURCE 200809L
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -58,6 +59,10 @@ typedef struct {
     const double *mir;   /* the engine's pinned mirror, read in place (Native.map) */
     long mir_stride;
     long shadow_n;       /* bodies in the mapped mirror (-1: none) */
+    const jint *rem;     /* lastRemoved, ascending, while a removal pass runs */
+    long nrem;
+    Body *spare;         /* the survivors' target list (grown only; swapped with bodies->b) */
+    long spare_cap;
     double mergeMaxMass, mergeMinDist; /* BHA:315,321 */
 } Shim;
 
@@ -121,17 +126,74 @@ static void shim_push(Shim *s) {
     shim_map(s); /* the engine's copy, as uploaded */
 }
 
+/* The shim's O(N) passes in chunks over worker threads, as PhysicsEngine.kt runs them on
+ * Dispatchers.Default (the reference's own fan-out, BHA:374-395); short lists stay serial. */
+static int shim_threads = 8;
+static long shim_par_min = 65536; /* BH_SHIM_PAR_MIN: shorter lists stay serial */
+typedef struct {
+    Shim *s;
+    long lo, hi;
+    int (*fn)(Shim *, long, long);
+    int result;
+} Chunk;
+static void *chunk_run(void *p) {
+    Chunk *c = (Chunk *)p;
+    c->result = c->fn(c->s, c->lo, c->hi);
+    return NULL;
+}
+static int par_any(Shim *s, long n, int (*fn)(Shim *, long, long)) { /* OR of fn over chunks */
+    const int w = n < shim_par_min ? 1 : shim_threads;
+    if (w <= 1) return fn(s, 0, n);
+    Chunk c[64];
+    pthread_t t[64];
+    const long per = (n + w - 1) / w;
+    int any = 0;
+    for (int k = 0; k < w; ++k) {
+        c[k] = (Chunk){s, k * per, (k + 1) * per < n ? (k + 1) * per : n, fn, 0};
+        if (k > 0) pthread_create(&t[k], NULL, chunk_run, &c[k]);
+    }
+    chunk_run(&c[0]);
+    for (int k = 1; k < w; ++k) pthread_join(t[k], NULL);
+    for (int k = 0; k < w; ++k) any |= c[k].result;
+    return any;
+}
+
 /* changed(): field by field against the mapped mirror, in place (toRawBits compares) */
-static int shim_changed(Shim *s) {
-    long n = s->bodies->n, st = s->mir_stride;
-    if (n != s->shadow_n) return 1;
+static int changed_part(Shim *s, long lo, long hi) {
+    const long st = s->mir_stride;
     const double *a = s->mir;
-    for (long i = 0; i < n; ++i) {
+    for (long i = lo; i < hi; ++i) {
         const Body *b = &s->bodies->b[i];
         if (memcmp(&b->x, &a[i], 8) || memcmp(&b->y, &a[st + i], 8) ||
             memcmp(&b->vx, &a[2 * st + i], 8) || memcmp(&b->vy, &a[3 * st + i], 8) ||
             memcmp(&b->m, &a[4 * st + i], 8))
             return 1;
+    }
+    return 0;
+}
+static int shim_changed(Shim *s) {
+    long n = s->bodies->n;
+    if (n != s->shadow_n) return 1;
+    return par_any(s, n, changed_part);
+}
+
+static long removed_below(const Shim *s, long i) { /* lower_bound over lastRemoved */
+    long lo = 0, hi = s->nrem;
+    while (lo < hi) {
+        long mid = (lo + hi) / 2;
+        if (s->rem[mid] < i) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+static int compact_part(Shim *s, long lo, long hi) {
+    long q = removed_below(s, lo), w = lo - q;
+    for (long i = lo; i < hi; ++i) {
+        if (q < s->nrem && s->rem[q] == i) {
+            ++q;
+            continue;
+        }
+        s->spare[w++] = s->bodies->b[i];
     }
     return 0;
 }
@@ -152,7 +214,8 @@ static void shim_apply_removed(Shim *s) {
                         sizeof(Body) * (s->bodies->n - j - 1));
                 s->bodies->n -= 1;
             }
-        } else { /* PhysicsEngine.kt: the same survivors in one pass, then one range removal */
+        } else if (s->bodies->n < shim_par_min || shim_threads <= 1) {
+            /* PhysicsEngine.kt: the same survivors in one pass, then one range removal */
             long w = r[0], q = 0;
             for (long i = r[0]; i < s->bodies->n; ++i) {
                 if (q < nr && r[q] == i) {
@@ -162,19 +225,30 @@ static void shim_apply_removed(Shim *s) {
                 s->bodies->b[w++] = s->bodies->b[i];
             }
             s->bodies->n = w;
+        } else { /* in chunks: survivors into the spare list, which becomes the list (the Kotlin
+                  * shim copies the references back instead, the caller's ArrayList stays) */
+            const long n = s->bodies->n;
+            if (s->spare_cap < n) {
+                free(s->spare);
+                s->spare = (Body *)malloc(sizeof(Body) * n);
+                s->spare_cap = n;
+            }
+            s->rem = r;
+            s->nrem = nr;
+            (void)par_any(s, n, compact_part);
+            Body *old = s->bodies->b;
+            s->bodies->b = s->spare;
+            s->spare = old;
+            s->bodies->n = n - nr;
         }
         fake_jvm_free(rem);
     }
 }
 
-static void shim_unpack(Shim *s, long n) {
+static int unpack_part(Shim *s, long lo, long hi) {
     const double *a = s->mir;
     const long st = s->mir_stride;
-    if (n != s->bodies->n) {
-        fprintf(stderr, "abi_harness: engine N %ld vs caller list %ld\n", n, s->bodies->n);
-        exit(1);
-    }
-    for (long i = 0; i < n; ++i) { /* into the SAME Body objects (BHA:414-432) */
+    for (long i = lo; i < hi; ++i) { /* into the SAME Body objects (BHA:414-432) */
         Body *b = &s->bodies->b[i];
         b->x = a[i];
         b->y = a[st + i];
@@ -182,6 +256,14 @@ static void shim_unpack(Shim *s, long n) {
         b->vy = a[3 * st + i];
         b->m = a[4 * st + i];
     }
+    return 0;
+}
+static void shim_unpack(Shim *s, long n) {
+    if (n != s->bodies->n) {
+        fprintf(stderr, "abi_harness: engine N %ld vs caller list %ld\n", n, s->bodies->n);
+        exit(1);
+    }
+    (void)par_any(s, n, unpack_part);
 }
 
 static void shim_pull(Shim *s, int after_step) {
@@ -349,11 +431,12 @@ static int c3_frames(long frames, jint mask) {
     }
     const double total = now_ms() - t0;
     const double host = t[0] + t[1] + t[3] + t[4] + t[5];
-    printf("{\"frames\": %ld, \"bodies\": %ld, \"devices\": %d, \"ms_per_frame\": %.4f, "
+    printf("{\"frames\": %ld, \"bodies\": %ld, \"devices\": %d, \"threads\": %d, \"ms_per_frame\": %.4f, "
            "\"step_ms\": %.4f, \"host_ms\": %.4f, \"params_ms\": %.4f, \"changed_ms\": %.4f, "
            "\"removals_ms\": %.4f, \"map_ms\": %.4f, \"unpack_ms\": %.4f, "
            "\"allocations_per_frame\": %.3f, \"uploads\": %ld}\n",
-           frames, n0, bh_multi_world((bh_engine *)(intptr_t)s.h), total / frames, t[2] / frames,
+           frames, n0, bh_multi_world((bh_engine *)(intptr_t)s.h), shim_threads, total / frames,
+           t[2] / frames,
            host / frames, t[0] / frames, t[1] / frames, t[3] / frames, t[4] / frames, t[5] / frames,
            (double)(shadow_allocs - allocs0) / frames, shim_steps_uploaded - uploads0);
     bh_destroy((bh_engine *)(intptr_t)s.h);
@@ -362,6 +445,10 @@ static int c3_frames(long frames, jint mask) {
 
 int main(int argc, char **argv) {
     env = fake_jvm_env();
+    const char *tv = getenv("BH_SHIM_THREADS");
+    if (tv && atoi(tv) >= 1 && atoi(tv) <= 64) shim_threads = atoi(tv);
+    const char *pm = getenv("BH_SHIM_PAR_MIN");
+    if (pm && atol(pm) >= 1) shim_par_min = atol(pm);
     jint mask = 1; /* GPU 0; BH_DEVICES="0,0,0" in the environment: one handle over a list */
     long timing_frames = 0;
     for (int i = 1; i < argc; ++i) {

@@ -19,15 +19,21 @@ BIN = os.path.join(os.path.dirname(__file__), "c", "bin")
 
 
 @pytest.mark.parametrize("exe,devices", [("abi_harness", None), ("mirror_harness", None),
-                                         ("abi_harness", "0,0,0"), ("mirror_harness", "0,0")])
+                                         ("abi_harness", "0,0,0"), ("mirror_harness", "0,0"),
+                                         ("abi_harness", "chunked")])
 def test_native_harness(exe, devices):
     """devices: the same frames through ONE engine handle over that device list (repeats: the
     members exchange by device-to-device copies) -- the Kotlin drop-in's Native.create with
-    BH_DEVICES set, the C++ mirror's multi-device constructor."""
+    BH_DEVICES set, the C++ mirror's multi-device constructor.  "chunked": one device, the
+    shim's compare/removal/unpack passes split over worker threads even for these short lists
+    (at C3 they always are)."""
     path = os.path.join(BIN, exe)
     assert os.path.exists(path), f"{path} missing: run __graft_entry__.build()"
     env = dict(os.environ)
     args = [path]
+    if devices == "chunked":
+        env["BH_SHIM_PAR_MIN"], env["BH_SHIM_THREADS"] = "256", "7"
+        devices = None
     if devices:
         env["BH_MULTI_MIN_BODIES"] = "0"  # the decomposition even for these small scenes
         if exe == "abi_harness":
