@@ -425,9 +425,12 @@ class Engine:
         self._check(self._lib.bh_get_bodies(self._h, *[_dp(a) for a in out], n, ctypes.byref(got)))
         return tuple(a[: got.value] for a in out)
 
-    def set_mirror(self, on: bool):
-        """bh_set_mirror: every step() call writes the pinned caller-order mirror itself."""
-        self._check(self._lib.bh_set_mirror(self._h, 1 if on else 0))
+    def set_mirror(self, on: bool, buffers: int = 1):
+        """bh_set_mirror: every step() call writes the pinned caller-order mirror itself;
+        buffers=2: two of them, so map_bodies' views stay valid until the next map_bodies."""
+        if buffers not in (1, 2):
+            raise ValueError("buffers is 1 or 2")
+        self._check(self._lib.bh_set_mirror(self._h, buffers if on else 0))
 
     def map_bodies(self):
         """bh_map_bodies: read-only numpy views of the pinned mirror (x, y, vx, vy, m), valid

@@ -280,7 +280,12 @@ struct bh_engine {
     // Pinned caller-order mirror of the bodies (bh_set_mirror / bh_map_bodies): x, y, vx, vy, m
     // at stride mir_cap, filled by the step itself on mir_stream
     bool mirror_on = false;
-    double *mir = nullptr;        // pinned host, 5 * mir_cap
+    double *mir = nullptr;        // pinned host, 5 * mir_cap: the buffer the copies write
+    // bh_set_mirror(e, 2): two buffers; the copies write the one bh_map_bodies did not hand out
+    // last (mir_front), so a caller reads the mapped bodies while the next bh_step runs
+    double *mir_buf[2] = {nullptr, nullptr};
+    int mir_nbuf = 1;
+    int mir_front = -1;
     double *mir_stage = nullptr;  // device, 5 * mir_cap (caller order, compacted)
     uint32_t *mir_keep = nullptr, *mir_pos = nullptr;  // device, caller order
     int64_t mir_cap = 0;
@@ -1784,12 +1789,18 @@ int pipe_alloc(bh_engine *e, bool last) {
 // when the last traversal's kick is -- the device-to-host copies run on the DMA engines while the
 // overlapped next build (and the traversal's tail) still run.
 int mirror_alloc(bh_engine *e) {
-    if (e->mir_cap < e->cap) {
-        if (e->mir) (void)hipHostFree(e->mir);
+    if (e->mir_cap < e->cap || (e->mir_nbuf == 2 && !e->mir_buf[1])) {
+        for (double *&b : e->mir_buf) {
+            if (b) (void)hipHostFree(b);
+            b = nullptr;
+        }
         e->mir = nullptr;
         e->mir_cap = 0;
-        HIPCHK(e, hipHostMalloc((void **)&e->mir, sizeof(double) * 5 * (size_t)e->cap,
-                                hipHostMallocDefault));
+        e->mir_front = -1;
+        for (int i = 0; i < e->mir_nbuf; ++i)
+            HIPCHK(e, hipHostMalloc((void **)&e->mir_buf[i], sizeof(double) * 5 * (size_t)e->cap,
+                                    hipHostMallocDefault));
+        e->mir = e->mir_buf[0];
         TRY(dev_alloc(e, e->mir_stage, 5 * (size_t)e->cap));
         TRY(dev_alloc(e, e->mir_keep, (size_t)e->cap));
         TRY(dev_alloc(e, e->mir_pos, (size_t)e->cap));
@@ -1817,6 +1828,8 @@ int mirror_alloc(bh_engine *e) {
 // stream (before a traversal: queued beside it they wait for its first waves to retire)
 int mirror_pos(bh_engine *e, const BodyState &src, hipStream_t after_pos, bool in_line = false) {
     TRY(mirror_alloc(e));
+    if (e->mir_nbuf == 2 && e->mir_buf[1])  // never the buffer the caller holds
+        e->mir = e->mir_buf[e->mir_front == 0 ? 1 : 0];
     const int64_t n = e->n;
     const int64_t c = e->mir_cap;
     hipStream_t ms = e->mir_stream;
@@ -2648,7 +2661,8 @@ void bh_destroy(bh_engine *e) {
     }
     for (hipEvent_t ev : {e->mir_ev, e->mir_ev2, e->mir_ev3, e->mir_in[0], e->mir_in[1]})
         if (ev) (void)hipEventDestroy(ev);
-    if (e->mir) (void)hipHostFree(e->mir);
+    for (double *b : e->mir_buf)
+        if (b) (void)hipHostFree(b);
     free_state(e->view);
     free_state(e->st);
     free_state(e->alt);
@@ -2753,7 +2767,7 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
                 e->err = "the single-GPU engine for a small body list could not be created";
                 return rc;
             }
-            if (m0->mirror_on) TRY(bh_set_mirror(o, 1));
+            if (m0->mirror_on) TRY(bh_set_mirror(o, m0->mir_nbuf));
             TRY(bh_set_profiling(o, m0->profiling ? 1 : 0));
             e->one = o;
         }
@@ -2934,10 +2948,20 @@ int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, do
 
 int bh_set_mirror(bh_engine *e, int enabled) {
     if (!e) return BH_E_INVALID;
+    if (enabled < 0 || enabled > 2) {
+        e->err = "bh_set_mirror: enabled is 0, 1 or 2";
+        return BH_E_INVALID;
+    }
     // (member 0's replica fills the mirror; the others' bh_set_mirror only reserves its stream)
     MULTI_BOTH(e, r_ == 0 ? bh_set_mirror(m_, enabled) : BH_OK);
     HIPCHK(e, hipSetDevice(e->device));
     e->mirror_on = enabled != 0;
+    if (e->mirror_on && enabled != e->mir_nbuf) {  // another buffer count: made anew
+        if (e->mir_stream) HIPCHK(e, hipStreamSynchronize(e->mir_stream));
+        e->mir_nbuf = enabled;
+        e->mir_cap = 0;
+        e->mir_fresh = false;
+    }
     if (e->mirror_on) TRY(mirror_alloc(e));
     return BH_OK;
 }
@@ -2962,6 +2986,7 @@ int bh_map_bodies(bh_engine *e, const double **x, const double **y, const double
     HIPCHK(e, hipEventSynchronize(e->mir_ev));
     const int64_t c = e->mir_cap;
     const double *b = e->mir;
+    e->mir_front = b == e->mir_buf[1] ? 1 : 0;
     if (x) *x = b;
     if (y) *y = b + c;
     if (vx) *vx = b + 2 * c;

@@ -102,8 +102,9 @@ JNIEXPORT jint JNICALL Java_Native_getInto(JNIEnv *env, jobject self, jlong h, j
  * The engine's pinned caller-order mirror itself (bh_map_bodies), which the step filled: a direct
  * buffer over its five planes (x at 0, y at the stride, then vx, vy, m) and info = [n, stride in
  * doubles].  Nothing is copied -- the shim compares and unpacks straight from pinned host memory
- * -- and the buffer is valid until the next native call that steps, resets or builds the debug
- * tree (the shim maps again after each). */
+ * -- and, with the shim's two mirror buffers (bh_set_mirror(e, 2)), the buffer stays valid and
+ * unchanged until the next map: the shim compares its list against it while the next step runs
+ * on another thread, then maps again. */
 JNIEXPORT jobject JNICALL Java_Native_map(JNIEnv *env, jobject self, jlong h, jlongArray info) {
     (void)self;
     bh_engine *e = (bh_engine *)(intptr_t)h;

@@ -26,7 +26,9 @@ int bh_shim_create(uint32_t device_mask, bh_engine **out) {
     *out = NULL;
     const char *list = getenv("BH_DEVICES");
     int rc = list && *list ? create_from_env(&p, list, out) : bh_create_multi(&p, device_mask, out);
-    if (rc == BH_OK) rc = bh_set_mirror(*out, 1); /* getBodies after every frame (PNL:302) */
+    /* getBodies after every frame (PNL:302); two buffers: the shim compares its list against the
+     * mapped one while the next step runs */
+    if (rc == BH_OK) rc = bh_set_mirror(*out, 2);
     if (rc != BH_OK && *out) {
         bh_destroy(*out);
         *out = NULL;

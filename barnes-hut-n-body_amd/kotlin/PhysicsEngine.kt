@@ -70,8 +70,24 @@ class PhysicsEngine(initialBodies: MutableList<Body>) {
     /** BHA:405-439: one step; Config is read live, as the reference reads it. */
     fun step() {
         params()
-        if (changed()) push()                                // upload only if the caller edited bodies
-        Native.step(handle, 1)
+        if (bodies.size != mirrorN) {                        // the caller added or removed bodies
+            push()
+            Native.step(handle, 1)
+        } else {
+            // The step runs while the caller's list is compared against the mapped mirror (the
+            // engine writes its other buffer, Native.create's bh_set_mirror(e, 2)); if the caller
+            // edited bodies, the upload replaces that step's result and the step runs again
+            val edited = runBlocking {
+                val running = launch(Dispatchers.IO) { Native.step(handle, 1) }
+                val diff = changed()
+                running.join()
+                diff
+            }
+            if (edited) {
+                push()
+                Native.step(handle, 1)
+            }
+        }
         pull(afterStep = true)
     }
 

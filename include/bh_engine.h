@@ -190,7 +190,12 @@ int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, do
  * changed since) and returns pointers to x[N], y[N], vx[N], vy[N], m[N] (any pointer may be
  * NULL).  They stay valid -- and the data unchanged -- until the next call on this engine that
  * changes or moves the bodies (bh_step, bh_reset_bodies, bh_get_quads, bh_compute_accelerations,
- * bh_load_state, bh_set_mirror, bh_destroy). */
+ * bh_load_state, bh_set_mirror, bh_destroy).
+ * bh_set_mirror(e, 2): two pinned buffers -- the calls write the one bh_map_bodies did not hand
+ * out last, so the mapped bodies stay valid and unchanged until the next bh_map_bodies (or
+ * bh_set_mirror, bh_destroy), and a caller may read them on one thread while a bh_step runs
+ * on another (the drop-in compares its list against them during the step).  enabled is 0, 1
+ * or 2 (else BH_E_INVALID). */
 int bh_set_mirror(bh_engine *e, int enabled);
 int bh_map_bodies(bh_engine *e, const double **x, const double **y, const double **vx,
                   const double **vy, const double **m, int64_t *n_out);

@@ -64,6 +64,7 @@ typedef struct {
     Body *spare;         /* the survivors' target list (grown only; swapped with bodies->b) */
     long spare_cap;
     double mergeMaxMass, mergeMinDist; /* BHA:315,321 */
+    double step_ms; /* the last Native.step's own duration (step_thread) */
 } Shim;
 
 static JNIEnv *env;
@@ -293,14 +294,43 @@ static void shim_reset(Shim *s, List *l) {
 }
 
 static long shim_steps_uploaded;
-static void shim_step(Shim *s) {
-    shim_params(s);
-    if (shim_changed(s)) {
+static double now_ms(void);
+/* Native.step on a worker thread (PhysicsEngine.kt: launch(Dispatchers.IO)); its own duration */
+static void *step_thread(void *p) {
+    Shim *s = (Shim *)p;
+    const double t = now_ms();
+    Java_Native_step(env, NULL, s->h, 1);
+    s->step_ms = now_ms() - t;
+    return NULL;
+}
+/* step(): the step runs while the list is compared against the mapped mirror (the engine writes
+ * its other buffer, bh_set_mirror(e, 2)); an edited list is uploaded and stepped again, the
+ * upload replacing the first step's result.  *compare_ms: the compare's own duration. */
+static void shim_step_body(Shim *s, double *compare_ms) {
+    if (s->bodies->n != s->shadow_n) { /* bodies added or removed: upload first */
         shim_push(s);
         ++shim_steps_uploaded;
+        Java_Native_step(env, NULL, s->h, 1);
+        jni_check("step");
+        return;
     }
-    Java_Native_step(env, NULL, s->h, 1);
+    pthread_t t;
+    if (pthread_create(&t, NULL, step_thread, s)) fail("pthread_create", -1);
+    const double c0 = now_ms();
+    const int diff = shim_changed(s);
+    if (compare_ms) *compare_ms += now_ms() - c0;
+    pthread_join(t, NULL);
     jni_check("step");
+    if (diff) {
+        shim_push(s);
+        ++shim_steps_uploaded;
+        Java_Native_step(env, NULL, s->h, 1);
+        jni_check("step");
+    }
+}
+static void shim_step(Shim *s) {
+    shim_params(s);
+    shim_step_body(s, NULL);
     shim_pull(s, 1);
 }
 
@@ -407,37 +437,33 @@ static int c3_frames(long frames, jint mask) {
     shim_create(&s, &list, mask);
     for (int w = 0; w < 5; ++w) shim_step(&s);
     const long allocs0 = shadow_allocs, uploads0 = shim_steps_uploaded;
-    double t[6] = {0, 0, 0, 0, 0, 0}; /* params, changed, step, removals, map, unpack */
+    double t[6] = {0, 0, 0, 0, 0, 0}; /* params, step || compare, removals, map, unpack, compare */
+    double step_own = 0.0;
     const long n0 = s.bodies->n;
     const double t0 = now_ms();
     for (long f = 0; f < frames; ++f) {
         double a = now_ms(), b;
         shim_params(&s);
         b = now_ms(); t[0] += b - a; a = b;
-        if (shim_changed(&s)) {
-            shim_push(&s);
-            ++shim_steps_uploaded;
-        }
+        shim_step_body(&s, &t[5]);
+        step_own += s.step_ms;
         b = now_ms(); t[1] += b - a; a = b;
-        Java_Native_step(env, NULL, s.h, 1);
-        jni_check("step");
-        b = now_ms(); t[2] += b - a; a = b;
         shim_apply_removed(&s);
-        b = now_ms(); t[3] += b - a; a = b;
+        b = now_ms(); t[2] += b - a; a = b;
         const long n = shim_map(&s);
-        b = now_ms(); t[4] += b - a; a = b;
+        b = now_ms(); t[3] += b - a; a = b;
         shim_unpack(&s, n);
-        b = now_ms(); t[5] += b - a;
+        b = now_ms(); t[4] += b - a;
     }
     const double total = now_ms() - t0;
-    const double host = t[0] + t[1] + t[3] + t[4] + t[5];
+    /* host_ms: the frame's time outside the step itself (the compare runs during the step) */
     printf("{\"frames\": %ld, \"bodies\": %ld, \"devices\": %d, \"threads\": %d, \"ms_per_frame\": %.4f, "
-           "\"step_ms\": %.4f, \"host_ms\": %.4f, \"params_ms\": %.4f, \"changed_ms\": %.4f, "
-           "\"removals_ms\": %.4f, \"map_ms\": %.4f, \"unpack_ms\": %.4f, "
+           "\"step_ms\": %.4f, \"host_ms\": %.4f, \"params_ms\": %.4f, \"step_and_compare_ms\": %.4f, "
+           "\"changed_ms\": %.4f, \"removals_ms\": %.4f, \"map_ms\": %.4f, \"unpack_ms\": %.4f, "
            "\"allocations_per_frame\": %.3f, \"uploads\": %ld}\n",
            frames, n0, bh_multi_world((bh_engine *)(intptr_t)s.h), shim_threads, total / frames,
-           t[2] / frames,
-           host / frames, t[0] / frames, t[1] / frames, t[3] / frames, t[4] / frames, t[5] / frames,
+           step_own / frames, (total - step_own) / frames, t[0] / frames, t[1] / frames,
+           t[5] / frames, t[2] / frames, t[3] / frames, t[4] / frames,
            (double)(shadow_allocs - allocs0) / frames, shim_steps_uploaded - uploads0);
     bh_destroy((bh_engine *)(intptr_t)s.h);
     return 0;
@@ -487,6 +513,12 @@ int main(int argc, char **argv) {
             oracle_destroy(o);
             o = oracle_of(&list3, &s);
         }
+        if (frame == 25) { /* the caller edits a body in place (as a drag would): step() uploads */
+            s.bodies->b[7].vx += 1.0;
+            s.bodies->b[s.bodies->n - 1].y -= 3.0;
+            oracle_destroy(o);
+            o = oracle_of(s.bodies, &s); /* the reference steps the edited objects themselves */
+        }
         oracle_params op = oparams(&s);
         oracle_set_params(o, &op);
         long before = s.bodies->n;
@@ -523,6 +555,7 @@ int main(int argc, char **argv) {
     }
     if (removed_total == 0) fail("the scene never merged: identity bookkeeping untested", 40);
     if (removed_max < 3) fail("no frame removed 3+ bodies: the one-pass removal is untested", 40);
+    if (shim_steps_uploaded != 1) fail("the in-place edit of frame 25 was not uploaded exactly once", 40);
     printf("abi_harness: 40 frames through the JNI glue on %d device(s) (%ld native calls) "
            "bit-identical to the oracle; %ld bodies merged away (at most %ld in one frame), %ld "
            "quads checked, %ld uploads after the constructor/resets, %ld shadow allocations after "

@@ -1146,6 +1146,40 @@ def test_one_step_calls_match_the_oracle_frame_by_frame():
     assert eng.num_bodies() < len(arrs[0])  # the heavies merged along the way
 
 
+def test_double_buffered_mirror_views_survive_the_next_step():
+    """bh_set_mirror(e, 2), the drop-in's mode: the views bh_map_bodies handed out stay valid
+    and unchanged while the next step runs on another thread (ctypes releases the GIL) and
+    after it, until the next map -- which holds the oracle's bodies after that step.  A merge
+    and a jitter along the way; the caller's upload (reset) between steps too."""
+    import threading
+    arrs = _frames_scene()
+    p = bh_amd.default_params(theta=0.5)
+    mir = bh_amd.Engine(p)
+    mir.reset_bodies(*arrs)
+    mir.set_mirror(True, buffers=2)
+    ref = oracle.Oracle(*arrs, theta=0.5)
+    held = mir.map_bodies()
+    for f in range(16):
+        kept = [a.copy() for a in held]
+        t = threading.Thread(target=mir.step, args=(1,))
+        t.start()
+        during = [a.copy() for a in held]  # read while the step runs
+        t.join()
+        ref.step(1)
+        _assert_arrays_equal(during, kept, f"frame {f}: the held views during the step")
+        _assert_arrays_equal(held, kept, f"frame {f}: the held views after the step")
+        held = mir.map_bodies()
+        _assert_arrays_equal(held, ref.get_bodies(), f"frame {f} mirror")
+        if f == 7:  # the caller uploads its own list (an edit): the views again from the upload
+            b = [a.copy() for a in held]
+            b[2][3] += 1.0
+            mir.reset_bodies(*b)
+            ref = oracle.Oracle(*b, theta=0.5)
+            held = mir.map_bodies()
+            _assert_arrays_equal(held, ref.get_bodies(), "after the upload")
+    assert mir.num_bodies() < len(arrs[0])  # the heavies merged along the way
+
+
 def test_one_step_calls_then_reconfigure_checkpoint_and_evaluate(tmp_path):
     """What the caller may do between two pipelined calls, each against the oracle: a root-cell
     change (the prebuilt tree and its jitter belong to the old root and are dropped), a
