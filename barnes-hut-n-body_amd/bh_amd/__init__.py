@@ -46,7 +46,7 @@ EXPORTED_SYMBOLS = (
     "bh_save_state", "bh_load_state", "bh_let_stats", "bh_create_solo", "bh_comm_ranks",
     "bh_debug_inject", "bh_set_mirror", "bh_map_bodies", "bh_create_multi",
     "bh_create_multi_list", "bh_multi_world", "bh_multi_member", "bh_collective_log",
-    "bh_collective_log_clear",
+    "bh_collective_log_clear", "bh_step_begin", "bh_step_positions", "bh_step_end",
 )
 
 
@@ -123,6 +123,10 @@ def load_library(path: str | None = None):
     lib.bh_set_mirror.argtypes = [_VP, ctypes.c_int]
     _DPP = ctypes.POINTER(_D)
     lib.bh_map_bodies.argtypes = [_VP, _DPP, _DPP, _DPP, _DPP, _DPP, _I64P]
+    lib.bh_step_begin.argtypes = [_VP, ctypes.c_int32]
+    lib.bh_step_positions.argtypes = [_VP, _DPP, _DPP, _DPP,
+                                      ctypes.POINTER(ctypes.POINTER(ctypes.c_uint32)), _I64P, _I64P]
+    lib.bh_step_end.argtypes = [_VP]
     lib.bh_compute_accelerations.argtypes = [_VP, _D, _D, _I64P]
     lib.bh_get_quads.argtypes = [_VP, _D, _D, _D, ctypes.c_int64, _I64P]
     lib.bh_last_timings.argtypes = [_VP, _D]
@@ -445,6 +449,31 @@ class Engine:
             a.flags.writeable = False
             out.append(a)
         return tuple(out)
+
+    def step_begin(self, k: int = 1):
+        """bh_step_begin: the call runs on the engine's own thread (set_mirror(True, buffers=2))."""
+        self._check(self._lib.bh_step_begin(self._h, int(k)))
+
+    def step_positions(self):
+        """bh_step_positions: (x, y, m, survivors, n_before) of the running call -- read-only
+        views of the mirror buffer it writes (x, y, m final) and survivor j's index in the
+        list before the call."""
+        ptrs = [_D() for _ in range(3)]
+        sv = ctypes.POINTER(ctypes.c_uint32)()
+        n, n0 = ctypes.c_int64(0), ctypes.c_int64(0)
+        self._check(self._lib.bh_step_positions(self._h, *[ctypes.byref(p) for p in ptrs],
+                                                ctypes.byref(sv), ctypes.byref(n), ctypes.byref(n0)))
+        out = [np.ctypeslib.as_array(p, shape=(n.value,)) if n.value else np.empty(0)
+               for p in ptrs]
+        out.append(np.ctypeslib.as_array(sv, shape=(n.value,)) if n.value
+                   else np.empty(0, dtype=np.uint32))
+        for a in out:
+            a.flags.writeable = False
+        return (*out, n0.value)
+
+    def step_end(self):
+        """bh_step_end: joins the call begun by step_begin; raises its error."""
+        self._check(self._lib.bh_step_end(self._h))
 
     def compute_accelerations(self, visits: bool = False):
         n = self.num_bodies()

@@ -570,6 +570,12 @@ void scatter_acc_to_caller(int64_t n, const uint32_t *cidx, const double *a2, do
 // dst_j[pos[c]] = src_j[slot] for the live bodies -- the list after the call's removals.
 hipError_t mirror_index(int64_t n, const uint32_t *cidx, uint32_t *keep, uint32_t *pos, void *tmp,
                         size_t tmp_bytes, hipStream_t s);
+// For bh_step_positions, one array for one copy: out[0..4) = scalars[0..4) (tree flags, removals,
+// mailbox overflow) and zeros up to MIRROR_HDR, then out[MIRROR_HDR + pos[c]] = c for every caller
+// index c < n with keep[c] -- survivor j's index in the list before the call (ascending in j).
+constexpr int MIRROR_HDR = 16;
+void mirror_survivors(int64_t n, const uint32_t *keep, const uint32_t *pos, const uint32_t *scalars,
+                      uint32_t *out, hipStream_t s);
 void mirror_scatter(int64_t n, const uint32_t *cidx, const uint32_t *pos, int k,
                     const double *const *src, double *const *dst, hipStream_t s);
 // *dst = *src by one thread at the chain's wave priority (a 4-byte hipMemcpyAsync beside the

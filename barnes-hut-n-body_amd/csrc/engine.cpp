@@ -23,6 +23,7 @@
 #include <cmath>
 #include <condition_variable>
 #include <mutex>
+#include <thread>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -298,6 +299,27 @@ struct bh_engine {
     hipEvent_t mir_ev = nullptr;   // copy-out complete
     hipEvent_t mir_ev2 = nullptr;  // the mirror's kernels are done reading the state
     hipEvent_t mir_in[2] = {nullptr, nullptr};
+    // bh_step_begin / bh_step_positions / bh_step_end (two mirror buffers only): the call runs
+    // on step_thr of the handle the caller holds; the engine that fills the mirror (this one, or
+    // a multi handle's member 0) hands over positions, masses and the survivors' list indices of
+    // the running call once its last merge rule is done (mid_*), before the last traversal
+    std::thread step_thr;
+    bool async_running = false;
+    int async_rc = 0;
+    int64_t mid_n0 = 0;              // bodies before the running call
+    bool mid_surv_done = false;      // the survivors were derived from the call's removals
+    bh_engine *mid_eng = nullptr;    // the running call's mirror engine
+    std::mutex mid_mu;
+    std::condition_variable mid_cv;
+    bool mid_armed = false, mid_ready = false, mid_done = false, mid_void = false;
+    double *mid_buf = nullptr;       // the mirror buffer of the hand-off
+    int64_t mid_stride = 0;
+    hipEvent_t mid_ev = nullptr;     // the hand-off's copies are done
+    hipEvent_t mid_sv_ev = nullptr;  // ... its survivors' (copied first)
+    // pinned, MIRROR_HDR + mir_cap (mirror_survivors): scalars[0..4) at the hand-off (tree
+    // flags, removals, mailbox overflow), then survivor j's index in the list before the call
+    uint32_t *mir_idx = nullptr;
+    uint32_t *mir_idx_stage = nullptr;  // device, the same
     hipEvent_t mir_ev3 = nullptr;
     // one GPU: the previous evaluation's wave durations and the longest-first run order
     // (slot 0: the one-GPU launch over all lanes; 1 + k: LET round k's piece)
@@ -1751,7 +1773,8 @@ int mirror_streams(bh_engine *e) {
         int lo = 0, hi = 0;
         HIPCHK(e, hipDeviceGetStreamPriorityRange(&lo, &hi));
         HIPCHK(e, hipStreamCreateWithPriority(&e->mir_stream, hipStreamNonBlocking, hi));
-        for (hipEvent_t *ev : {&e->mir_ev, &e->mir_ev2, &e->mir_ev3, &e->mir_in[0], &e->mir_in[1]})
+        for (hipEvent_t *ev : {&e->mir_ev, &e->mir_ev2, &e->mir_ev3, &e->mir_in[0], &e->mir_in[1],
+                               &e->mid_ev, &e->mid_sv_ev})
             HIPCHK(e, hipEventCreateWithFlags(ev, hipEventDisableTiming));
     }
     return BH_OK;
@@ -1801,6 +1824,13 @@ int mirror_alloc(bh_engine *e) {
             HIPCHK(e, hipHostMalloc((void **)&e->mir_buf[i], sizeof(double) * 5 * (size_t)e->cap,
                                     hipHostMallocDefault));
         e->mir = e->mir_buf[0];
+        if (e->mir_idx) (void)hipHostFree(e->mir_idx);
+        e->mir_idx = nullptr;
+        if (e->mir_nbuf == 2) {  // the survivors' list indices for bh_step_positions
+            const size_t w = MIRROR_HDR + (size_t)e->cap;
+            HIPCHK(e, hipHostMalloc((void **)&e->mir_idx, sizeof(uint32_t) * w, hipHostMallocDefault));
+            TRY(dev_alloc(e, e->mir_idx_stage, w));
+        }
         TRY(dev_alloc(e, e->mir_stage, 5 * (size_t)e->cap));
         TRY(dev_alloc(e, e->mir_keep, (size_t)e->cap));
         TRY(dev_alloc(e, e->mir_pos, (size_t)e->cap));
@@ -1847,8 +1877,18 @@ int mirror_pos(bh_engine *e, const BodyState &src, hipStream_t after_pos, bool i
         double *d3[3] = {st, st + c, st + 4 * c};
         mirror_scatter(n, src.cidx, e->mir_pos, 3, s3, d3, ws);
         HIPCHK(e, hipGetLastError());
+        if (e->mir_idx) {  // two buffers: the survivors' indices in the list before the call
+            mirror_survivors(n, e->mir_keep, e->mir_pos, e->scalars, e->mir_idx_stage, ws);
+            HIPCHK(e, hipGetLastError());
+        }
         HIPCHK(e, hipEventRecord(e->mir_ev3, ws));  // the positions' gather is done
         if (in_line) HIPCHK(e, hipStreamWaitEvent(ms, e->mir_ev3, 0));
+        if (e->mir_idx) {  // first: the caller's removal pass needs only them (bh_step_positions)
+            HIPCHK(e, hipMemcpyAsync(e->mir_idx, e->mir_idx_stage,
+                                     sizeof(uint32_t) * (MIRROR_HDR + (size_t)n),
+                                     hipMemcpyDeviceToHost, ms));
+            HIPCHK(e, hipEventRecord(e->mid_sv_ev, ms));
+        }
         for (int j : {0, 1, 4})  // (the survivors are a prefix of each array)
             HIPCHK(e, hipMemcpyAsync(e->mir + j * c, st + j * c, sizeof(double) * n,
                                      hipMemcpyDeviceToHost, ms));
@@ -1927,6 +1967,16 @@ int evaluate_pipelined(bh_engine *e, bool last) {
         HIPCHK(e, hipGetLastError());
         TRY(merge(e, s, merging));  // BHA:438 (the traversal reads its own copies of m, cidx)
         TRY(mirror_pos(e, e->st, s, true));
+        if (e->mid_armed && e->mir_idx && n > 0) {  // bh_step_positions: the hand-off
+            HIPCHK(e, hipEventRecord(e->mid_ev, e->mir_stream));
+            {
+                std::lock_guard<std::mutex> lk(e->mid_mu);
+                e->mid_buf = e->mir;
+                e->mid_stride = e->mir_cap;
+                e->mid_ready = true;
+            }
+            e->mid_cv.notify_all();
+        }
     }
     HIPCHK(e, hipEventRecord(e->pipe_ev[0], s));
     HIPCHK(e, hipStreamWaitEvent(e->pipe_stream, e->pipe_ev[0], 0));
@@ -2628,6 +2678,7 @@ int bh_create_solo(const bh_params *p, int device, int rank, int world, bh_engin
 
 void bh_destroy(bh_engine *e) {
     if (!e) return;
+    if (e->step_thr.joinable()) e->step_thr.join();  // a call begun by bh_step_begin
     if (e->multi) {  // the members, their threads and the exchange; then the handle itself
         bh_destroy(e->one);
         multi_destroy(e->multi);
@@ -2659,10 +2710,12 @@ void bh_destroy(bh_engine *e) {
         (void)hipStreamSynchronize(e->mir_stream);
         (void)hipStreamDestroy(e->mir_stream);
     }
-    for (hipEvent_t ev : {e->mir_ev, e->mir_ev2, e->mir_ev3, e->mir_in[0], e->mir_in[1]})
+    for (hipEvent_t ev : {e->mir_ev, e->mir_ev2, e->mir_ev3, e->mir_in[0], e->mir_in[1], e->mid_ev,
+                          e->mid_sv_ev})
         if (ev) (void)hipEventDestroy(ev);
     for (double *b : e->mir_buf)
         if (b) (void)hipHostFree(b);
+    if (e->mir_idx) (void)hipHostFree(e->mir_idx);
     free_state(e->view);
     free_state(e->st);
     free_state(e->alt);
@@ -2688,7 +2741,7 @@ void bh_destroy(bh_engine *e) {
                     e->leaf_tmp, e->spl, e->bcount, e->bstart, e->nodes_alt, e->wave_cost, e->run_order,
                     e->m_trav, e->cidx_trav, e->lanes_trav, e->T_trav, e->solo_xchg,
                     e->lt_x, e->lt_y, e->a2_alt, e->lt_keys, e->lt_cpl, e->lt_base, e->mir_stage,
-                    e->mir_keep, e->mir_pos, e->mir_tmp, e->lanes_next, e->lr_hkey, e->lr_hkey_s,
+                    e->mir_keep, e->mir_pos, e->mir_tmp, e->mir_idx_stage, e->lanes_next, e->lr_hkey, e->lr_hkey_s,
                     e->lr_slot, e->lr_scratch};
     for (void *q : ptrs)
         if (q) (void)hipFree(q);
@@ -2831,6 +2884,10 @@ int bh_step(bh_engine *e, int32_t k) {
     for (bool first = true;; first = false) {
         e->ev_used = 0;
         e->timings_pending = false;
+        if (!first && e->mid_armed) {  // a replay: an earlier attempt's hand-off is void
+            std::lock_guard<std::mutex> lk(e->mid_mu);
+            e->mid_void = true;
+        }
         // the subset splitters are trusted only within a call (another scene after a reset
         // would put most of a subset into one bucket): the first LET build sorts with rocprim
         e->s_spl_nb = 0;
@@ -2913,6 +2970,116 @@ int bh_step(bh_engine *e, int32_t k) {
     }
     if (e->profiling) TRY(collect_timings(e));
     return BH_OK;
+}
+
+int bh_step_begin(bh_engine *e, int32_t k) {
+    if (!e || k < 0) return BH_E_INVALID;
+    if (e->async_running) {
+        e->err = "bh_step_begin: the previous call was not ended (bh_step_end)";
+        return BH_E_STATE;
+    }
+    bh_engine *t = MULTI_M0(e);  // the engine whose mirror the call fills
+    if (!t->mirror_on || t->mir_nbuf != 2) {
+        e->err = "bh_step_begin: needs the two-buffer mirror (bh_set_mirror(e, 2))";
+        return BH_E_STATE;
+    }
+    if (e->step_thr.joinable()) e->step_thr.join();
+    {
+        std::lock_guard<std::mutex> lk(t->mid_mu);
+        t->mid_armed = k > 0;
+        t->mid_ready = t->mid_done = t->mid_void = false;
+    }
+    e->mid_eng = t;
+    e->mid_n0 = t->n;
+    e->mid_surv_done = false;
+    e->async_rc = BH_OK;
+    e->async_running = true;
+    e->step_thr = std::thread([e, t, k] {
+        const int rc = bh_step(e, k);
+        {
+            std::lock_guard<std::mutex> lk(t->mid_mu);
+            e->async_rc = rc;
+            t->mid_armed = false;
+            t->mid_done = true;
+        }
+        t->mid_cv.notify_all();
+    });
+    return BH_OK;
+}
+
+int bh_step_positions(bh_engine *e, const double **x, const double **y, const double **m,
+                      const uint32_t **survivors, int64_t *n_out, int64_t *n_before) {
+    if (!e) return BH_E_INVALID;
+    if (!e->async_running || !e->mid_eng) {
+        e->err = "bh_step_positions: no call begun (bh_step_begin)";
+        return BH_E_STATE;
+    }
+    bh_engine *t = e->mid_eng;
+    const double *buf = nullptr;
+    int64_t stride = 0, n = 0;
+    std::unique_lock<std::mutex> lk(t->mid_mu);
+    t->mid_cv.wait(lk, [t] { return t->mid_ready || t->mid_done; });
+    if (!t->mid_done && !t->mid_void) {  // the hand-off: usable unless the call will replay
+        buf = t->mid_buf;
+        stride = t->mid_stride;
+        lk.unlock();
+        // x, y, m not asked for: the survivors are enough (their copy runs ahead of the planes')
+        HIPCHK(e, hipEventSynchronize(x || y || m ? t->mid_ev : t->mid_sv_ev));
+        const uint32_t *h = t->mir_idx;  // scalars[1] tree flags, [2] removals, [3] overflow
+        n = e->mid_n0 - (int64_t)h[2];
+        lk.lock();
+        if (h[1] || h[3] || t->mid_void) buf = nullptr;  // an error or a replay follows: the end
+    }
+    if (!buf) {  // no hand-off (a call whose last step is not pipelined, or a replay): the end
+        t->mid_cv.wait(lk, [t] { return t->mid_done; });
+        lk.unlock();
+        if (e->async_rc != BH_OK) return e->async_rc;
+        HIPCHK(e, hipEventSynchronize(t->mir_ev));
+        buf = t->mir;
+        stride = t->mir_cap;
+        n = t->mir_n;
+        if (!e->mid_surv_done) {  // the survivors from the call's removals: a mirror written
+            // after the call's compaction numbers its bodies in the list after the call
+            int64_t nr = 0;
+            int rc = bh_last_removed(e, nullptr, 0, &nr);
+            if (rc != BH_OK && rc != BH_E_CAPACITY) return rc;
+            std::vector<int64_t> rem((size_t)std::max<int64_t>(nr, 1));
+            TRY(bh_last_removed(e, rem.data(), nr, &nr));
+            uint32_t *sv = t->mir_idx + MIRROR_HDR;
+            int64_t j = 0, r = 0;
+            for (int64_t i = 0; i < e->mid_n0; ++i) {
+                if (r < nr && rem[(size_t)r] == i) {
+                    ++r;
+                    continue;
+                }
+                sv[j++] = (uint32_t)i;
+            }
+            if (j != n) {
+                e->err = "bh_step_positions: the removals do not match the mirror";
+                return BH_E_STATE;
+            }
+            e->mid_surv_done = true;
+        }
+    }
+    if (x) *x = buf;
+    if (y) *y = buf + stride;
+    if (m) *m = buf + 4 * stride;
+    if (survivors) *survivors = t->mir_idx + MIRROR_HDR;
+    if (n_out) *n_out = n;
+    if (n_before) *n_before = e->mid_n0;
+    return BH_OK;
+}
+
+int bh_step_end(bh_engine *e) {
+    if (!e) return BH_E_INVALID;
+    if (!e->async_running) {
+        e->err = "bh_step_end: no call begun (bh_step_begin)";
+        return BH_E_STATE;
+    }
+    e->step_thr.join();
+    e->async_running = false;
+    e->mid_eng = nullptr;
+    return e->async_rc;
 }
 
 int64_t bh_num_bodies(const bh_engine *e) { return e ? MULTI_M0(e)->n : -1; }

@@ -140,6 +140,16 @@ __global__ __launch_bounds__(TB) void k_mirror_keep(int64_t n, const uint32_t *_
     keep[c & ~CIDX_DEAD] = (c & CIDX_DEAD) ? 0u : 1u;
 }
 
+__global__ __launch_bounds__(TB) void k_mirror_survivors(int64_t n, const uint32_t *__restrict__ keep,
+                                                         const uint32_t *__restrict__ pos,
+                                                         const uint32_t *__restrict__ hdr_src,
+                                                         uint32_t *__restrict__ out) {
+    chain_prio();
+    const int64_t c = (int64_t)blockIdx.x * TB + threadIdx.x;
+    if (c < MIRROR_HDR) out[c] = c < 4 ? hdr_src[c] : 0u;
+    if (c < n && keep[c]) out[MIRROR_HDR + pos[c]] = (uint32_t)c;
+}
+
 __global__ void k_copy_u32(uint32_t *dst, const uint32_t *src) {
     chain_prio();
     *dst = *src;
@@ -713,6 +723,12 @@ hipError_t mirror_index(int64_t n, const uint32_t *cidx, uint32_t *keep, uint32_
                                             rocprim::plus<uint32_t>(), s);
     if (st != hipSuccess) return st;
     return hipGetLastError();
+}
+
+void mirror_survivors(int64_t n, const uint32_t *keep, const uint32_t *pos, const uint32_t *scalars,
+                      uint32_t *out, hipStream_t s) {
+    k_mirror_survivors<<<grid_for(n > MIRROR_HDR ? n : (int64_t)MIRROR_HDR), TB, 0, s>>>(
+        n, keep, pos, scalars, out);
 }
 
 void copy_u32(uint32_t *dst, const uint32_t *src, hipStream_t s) {

@@ -1,5 +1,5 @@
 /*
- * bh_jni.c -- JNI glue of the Kotlin drop-in PhysicsEngine: the seven
+ * bh_jni.c -- JNI glue of the Kotlin drop-in PhysicsEngine: the
  * `external fun`s of `object Native` (class `Native`, default package).  Every native only moves
  * Java arrays in and out and calls the matching bh_shim_* helper (bh_shim.c), whose logic
  * tests/c/abi_harness.c runs against the oracle; errors become java.lang.RuntimeException with
@@ -69,6 +69,69 @@ JNIEXPORT void JNICALL Java_Native_step(JNIEnv *env, jobject self, jlong h, jint
     (void)self;
     bh_engine *e = (bh_engine *)(intptr_t)h;
     if (bh_shim_step(e, (int32_t)k) != BH_OK) throw_rt(env, e, "step");
+}
+
+/* external fun stepBegin(h: Long, k: Int)  (bh_step_begin: the step runs on the engine's thread) */
+JNIEXPORT void JNICALL Java_Native_stepBegin(JNIEnv *env, jobject self, jlong h, jint k) {
+    (void)self;
+    bh_engine *e = (bh_engine *)(intptr_t)h;
+    if (bh_shim_step_begin(e, (int32_t)k) != BH_OK) throw_rt(env, e, "stepBegin");
+}
+
+/* external fun positions(h: Long, info: LongArray): ByteBuffer
+ * The running call's hand-off (bh_step_positions): a direct buffer over the five planes of the
+ * mirror buffer it writes -- x, y, m final, vx, vy only after stepEnd + map -- with info =
+ * [n after the call, stride in doubles, n before it]. */
+JNIEXPORT jobject JNICALL Java_Native_positions(JNIEnv *env, jobject self, jlong h,
+                                                jlongArray info) {
+    (void)self;
+    bh_engine *e = (bh_engine *)(intptr_t)h;
+    const double *f[5] = {NULL, NULL, NULL, NULL, NULL};
+    const int32_t *sv = NULL;
+    int64_t n = 0, n0 = 0;
+    static double empty[1];
+    if (!info || (*env)->GetArrayLength(env, info) < 3) {
+        throw_rt(env, NULL, "positions: info must hold 3 longs");
+        return NULL;
+    }
+    if (bh_shim_positions(e, f, &n, &n0, &sv) != BH_OK) {
+        throw_rt(env, e, "positions");
+        return NULL;
+    }
+    const int64_t stride = (int64_t)(f[1] - f[0]);
+    if (5 * stride * (int64_t)sizeof(double) > INT32_MAX) {
+        throw_rt(env, NULL, "positions: more bodies than a direct buffer addresses");
+        return NULL;
+    }
+    const jlong out[3] = {(jlong)n, (jlong)stride, (jlong)n0};
+    (*env)->SetLongArrayRegion(env, info, 0, 3, out);
+    return (*env)->NewDirectByteBuffer(env, n > 0 ? (void *)f[0] : (void *)empty,
+                                       (jlong)(5 * stride * (int64_t)sizeof(double)));
+}
+
+/* external fun survivors(h: Long): ByteBuffer
+ * The running call's survivors (bh_step_positions without the planes: as soon as they are
+ * known): int32 list indices before the call, ascending, one per body after it -- the removals
+ * are the indices missing (BHA:519); the buffer's capacity is 4 n. */
+JNIEXPORT jobject JNICALL Java_Native_survivors(JNIEnv *env, jobject self, jlong h) {
+    (void)self;
+    bh_engine *e = (bh_engine *)(intptr_t)h;
+    const int32_t *sv = NULL;
+    int64_t n = 0, n0 = 0;
+    static int32_t empty[1];
+    if (bh_shim_survivors(e, &sv, &n, &n0) != BH_OK) { /* (ahead of the planes' copy) */
+        throw_rt(env, e, "survivors");
+        return NULL;
+    }
+    return (*env)->NewDirectByteBuffer(env, n > 0 ? (void *)sv : (void *)empty,
+                                       (jlong)(n * (int64_t)sizeof(int32_t)));
+}
+
+/* external fun stepEnd(h: Long)  (bh_step_end: joins; the step's error as an exception) */
+JNIEXPORT void JNICALL Java_Native_stepEnd(JNIEnv *env, jobject self, jlong h) {
+    (void)self;
+    bh_engine *e = (bh_engine *)(intptr_t)h;
+    if (bh_shim_step_end(e) != BH_OK) throw_rt(env, e, "stepEnd");
 }
 
 /* external fun getInto(h: Long, soa: DoubleArray): Int  (n, or -n if soa is shorter than 5 n)

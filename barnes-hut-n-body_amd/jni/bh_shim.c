@@ -1,6 +1,7 @@
 /* The Kotlin drop-in's native logic over the C-ABI (see bh_shim.h). */
 #include "bh_shim.h"
 
+#include <stddef.h>
 #include <stdlib.h>
 
 /* BH_DEVICES="0,1,2" (repeats allowed) overrides the mask with an explicit device list */
@@ -57,6 +58,35 @@ int bh_shim_reset(bh_engine *e, int64_t n, const double *soa) {
 }
 
 int bh_shim_step(bh_engine *e, int32_t k) { return bh_step(e, k); }
+
+int bh_shim_step_begin(bh_engine *e, int32_t k) { return bh_step_begin(e, k); }
+
+int bh_shim_positions(bh_engine *e, const double *soa[5], int64_t *n, int64_t *n_before,
+                      const int32_t **survivors) {
+    if (!soa || !n || !n_before || !survivors) return BH_E_INVALID;
+    const double *x = NULL, *y = NULL, *m = NULL;
+    const uint32_t *sv = NULL;
+    const int rc = bh_step_positions(e, &x, &y, &m, &sv, n, n_before);
+    if (rc != BH_OK) return rc;
+    const ptrdiff_t stride = y - x; /* the planes of one buffer: x, y, vx, vy, m */
+    soa[0] = x;
+    soa[1] = y;
+    soa[2] = x + 2 * stride;
+    soa[3] = x + 3 * stride;
+    soa[4] = m;
+    *survivors = (const int32_t *)sv; /* indices < 2^31: the Kotlin IntBuffer */
+    return BH_OK;
+}
+
+int bh_shim_survivors(bh_engine *e, const int32_t **survivors, int64_t *n, int64_t *n_before) {
+    if (!survivors || !n || !n_before) return BH_E_INVALID;
+    const uint32_t *sv = NULL;
+    const int rc = bh_step_positions(e, NULL, NULL, NULL, &sv, n, n_before);
+    if (rc == BH_OK) *survivors = (const int32_t *)sv;
+    return rc;
+}
+
+int bh_shim_step_end(bh_engine *e) { return bh_step_end(e); }
 
 int bh_shim_get(bh_engine *e, double *soa, int64_t cap, int64_t *n) {
     const int64_t cnt = bh_num_bodies(e);

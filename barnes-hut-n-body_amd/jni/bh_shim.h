@@ -1,5 +1,5 @@
 /*
- * bh_shim.h -- the logic of the Kotlin drop-in's seven JNI natives, as plain C
+ * bh_shim.h -- the logic of the Kotlin drop-in's JNI natives, as plain C
  * over the C-ABI (include/bh_engine.h): no JNI types, so tests/c/abi_harness.c drives exactly
  * this code against the oracle, and bh_jni.c only moves Java arrays in and out.
  *
@@ -38,6 +38,18 @@ int bh_shim_reset(bh_engine *e, int64_t n, const double *soa);
 
 /* Native.step(k): k x step() (BHA:405-439). */
 int bh_shim_step(bh_engine *e, int32_t k);
+
+/* Native.stepBegin / positions / stepEnd: step() with the shim's own work beside it
+ * (bh_step_begin / bh_step_positions / bh_step_end).  positions: soa[0..5) point at the planes of
+ * the mirror buffer the running call writes (x, y, m final; vx, vy after stepEnd + map), *n
+ * bodies after the call, *n_before before it, survivors[j] = survivor j's list index before the
+ * call (ascending) -- the merge rule's removals are the indices missing from it (BHA:519). */
+int bh_shim_step_begin(bh_engine *e, int32_t k);
+int bh_shim_positions(bh_engine *e, const double *soa[5], int64_t *n, int64_t *n_before,
+                      const int32_t **survivors);
+/* survivors alone: returns as soon as they are known, ahead of the planes' copy */
+int bh_shim_survivors(bh_engine *e, const int32_t **survivors, int64_t *n, int64_t *n_before);
+int bh_shim_step_end(bh_engine *e);
 
 /* Native.get: getBodies() (BHA:335) into a 5 cap SoA array; *n = body count.  cap < n:
  * BH_E_CAPACITY with *n set (size query with soa = NULL, cap = 0). */

@@ -28,13 +28,26 @@ object Native {
     /** bh_step(k). */
     external fun step(h: Long, k: Int)
 
+    /** bh_step_begin(k): the step runs on the engine's own thread (two-buffer mirror). */
+    external fun stepBegin(h: Long, k: Int)
+
+    /** The running step's hand-off (bh_step_positions): the mirror buffer it writes as a direct
+     *  buffer (x, y, m final; vx, vy after stepEnd + map), info = [n, stride, n before]. */
+    external fun positions(h: Long, info: LongArray): ByteBuffer
+
+    /** The running step's survivors: int32 list indices before it, ascending (BHA:519). */
+    external fun survivors(h: Long): ByteBuffer
+
+    /** bh_step_end: joins the step begun by stepBegin; its error as an exception. */
+    external fun stepEnd(h: Long)
+
     /** The bodies into the caller's SoA array [x[0..n) y[n..2n) vx vy m] from the engine's pinned
      *  mirror (bh_map_bodies), no allocation; returns n, or -n if soa holds fewer than 5 n. */
     external fun getInto(h: Long, soa: DoubleArray): Int
 
     /** The engine's pinned caller-order mirror itself as a direct buffer (five fp64 planes x, y,
-     *  vx, vy, m at multiples of info[1] doubles; info[0] = n): nothing copied.  Valid until the
-     *  next step / reset / quads call. */
+     *  vx, vy, m at multiples of info[1] doubles; info[0] = n): nothing copied.  Valid and
+     *  unchanged until the next map (two mirror buffers: a running step writes the other). */
     external fun map(h: Long, info: LongArray): ByteBuffer
 
     /** bh_get_quads as interleaved (cx, cy, h) triples in visitQuads order. */

@@ -15,6 +15,7 @@
 
 import java.nio.ByteOrder
 import java.nio.DoubleBuffer
+import java.nio.IntBuffer
 import java.util.concurrent.atomic.AtomicBoolean
 import kotlinx.coroutines.Dispatchers
 import kotlinx.coroutines.launch
@@ -41,6 +42,7 @@ class PhysicsEngine(initialBodies: MutableList<Body>) {
     // planes of `stride` doubles), mapped again after every native call that changes it; the
     // upload array is reused (grown only) -- no per-frame allocation that grows with N
     private val info = LongArray(2)
+    private val info3 = LongArray(3)                        // Native.positions' [n, stride, n before]
     private var mirror: DoubleBuffer = DoubleBuffer.allocate(0)
     private var stride = 0
     private var mirrorN = -1
@@ -73,22 +75,73 @@ class PhysicsEngine(initialBodies: MutableList<Body>) {
         if (bodies.size != mirrorN) {                        // the caller added or removed bodies
             push()
             Native.step(handle, 1)
-        } else {
-            // The step runs while the caller's list is compared against the mapped mirror (the
-            // engine writes its other buffer, Native.create's bh_set_mirror(e, 2)); if the caller
-            // edited bodies, the upload replaces that step's result and the step runs again
-            val edited = runBlocking {
-                val running = launch(Dispatchers.IO) { Native.step(handle, 1) }
-                val diff = changed()
-                running.join()
-                diff
+            pull(afterStep = true)
+            return
+        }
+        // The step runs on the engine's own thread (Native.stepBegin) while the caller's list is
+        // compared against the mapped mirror -- the step writes the engine's other buffer
+        // (Native.create's bh_set_mirror(e, 2)); an edited list is uploaded and stepped again,
+        // the upload replacing that step's result
+        Native.stepBegin(handle, 1)
+        val edited = try {
+            changed()
+        } catch (t: Throwable) {
+            runCatching { Native.stepEnd(handle) }
+            throw t
+        }
+        if (edited) {
+            Native.stepEnd(handle)
+            push()
+            Native.step(handle, 1)
+            pull(afterStep = true)
+            return
+        }
+        // The step's hand-off, once its merge rule is done and before its last traversal: the
+        // survivors first, then positions and masses -- the removals (BHA:519) and the x, y, m
+        // unpack run beside the traversal; after it only vx, vy are left
+        var failed: Throwable? = null
+        try {
+            val ids = Native.survivors(handle).order(ByteOrder.nativeOrder()).asIntBuffer()
+            val n = ids.capacity()
+            if (n != bodies.size) keepSurvivors(ids, n)
+            val a = Native.positions(handle, info3).order(ByteOrder.nativeOrder()).asDoubleBuffer()
+            val s = info3[1].toInt()
+            chunks(n) { lo, hi ->
+                for (i in lo until hi) {
+                    val b = bodies[i]
+                    b.x = a.get(i); b.y = a.get(s + i); b.m = a.get(4 * s + i)
+                }
             }
-            if (edited) {
-                push()
-                Native.step(handle, 1)
+        } catch (t: Throwable) {
+            failed = t
+        }
+        try {
+            Native.stepEnd(handle)
+        } catch (t: Throwable) {
+            throw failed ?: t
+        }
+        failed?.let { throw it }
+        val n = map()
+        check(n == bodies.size) { "engine and caller body lists diverged" }
+        val a = mirror
+        val s = stride
+        chunks(n) { lo, hi ->
+            for (i in lo until hi) {
+                val b = bodies[i]
+                b.vx = a.get(2 * s + i); b.vy = a.get(3 * s + i)
             }
         }
-        pull(afterStep = true)
+    }
+
+    /** The step's removals (BHA:519) from its survivors (ids[j] = survivor j's index before the
+     *  step, ascending): the list the reference's removeAt calls leave, gathered in chunks into a
+     *  reused spare array and set back -- the same list object, the same Body objects. */
+    private fun keepSurvivors(ids: IntBuffer, n: Int) {
+        if (spare.size < n) spare = arrayOfNulls(n)
+        val out = spare
+        chunks(n) { lo, hi -> for (j in lo until hi) out[j] = bodies[ids.get(j)] }
+        chunks(n) { lo, hi -> for (j in lo until hi) bodies[j] = out[j]!! }
+        bodies.subList(n, bodies.size).clear()
     }
 
     /** BHA:329-332: the last step's tree, or a fresh one (which may jitter bodies). */

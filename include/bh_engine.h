@@ -174,6 +174,26 @@ int bh_load_state(bh_engine *e, const char *path);
 /* k x PhysicsEngine.step() (BHA:405-439). */
 int bh_step(bh_engine *e, int32_t k);
 
+/* bh_step(e, k) on a thread of the engine's own, for a caller that overlaps its own work with
+ * the call (the drop-in shim: NBodyPanel's tick, PNL:290-306, around step(), BHA:405-439).
+ * Needs the two-buffer mirror (bh_set_mirror(e, 2)), else BH_E_STATE.  Until bh_step_end the
+ * caller may only read the mirror it mapped before (bh_map_bodies: the call writes the other
+ * buffer) and call bh_step_positions; bh_step_end joins and returns bh_step's result (then
+ * bh_last_removed, bh_map_bodies, ... as after bh_step).
+ * bh_step_positions blocks until the call's positions and masses are final -- on one GPU that is
+ * once its last merge rule is done, before its last traversal; else when the call ends -- and
+ * returns the mirror planes x, y, m of the list after the call (n_out bodies; the other buffer
+ * than the one mapped before) and survivors[j], ascending: survivor j's index in the list before
+ * the call (n_before bodies) -- the removals are the indices missing from it (bh_last_removed
+ * after bh_step_end).  vx and vy of the same buffer are final only after bh_step_end +
+ * bh_map_bodies.  With x, y and m all NULL it returns as soon as the survivors are known (their
+ * copy runs ahead of the planes').  If the call fails, bh_step_positions returns its error; if it
+ * fails after the hand-off (an unsupported jitter geometry), bh_step_end does. */
+int bh_step_begin(bh_engine *e, int32_t k);
+int bh_step_positions(bh_engine *e, const double **x, const double **y, const double **m,
+                      const uint32_t **survivors, int64_t *n_out, int64_t *n_before);
+int bh_step_end(bh_engine *e);
+
 /* getBodies().size */
 int64_t bh_num_bodies(const bh_engine *e);
 

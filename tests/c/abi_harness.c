@@ -31,14 +31,16 @@
 static double cfg_G = 80.0, cfg_DT = 0.005, cfg_theta = 0.5, cfg_SOFT2 = 1.0;
 static int cfg_W = 2400, cfg_H = 800;
 
-/* ---- the caller's MutableList<Body> (BHA:21-25); `id` stands for object identity ------- */
+/* ---- the caller's MutableList<Body> (BHA:21-25): an ArrayList of references to Body
+ * objects, as the JVM holds it (the objects allocated together, as a TLAB places them); `id`
+ * names the object for the identity checks ------------------------------------------------- */
 typedef struct {
     double x, y, vx, vy, m;
     long id;
 } Body;
 typedef struct {
-    Body *b;
-    long n;
+    Body **b;
+    long n, cap;
 } List;
 
 static double *start_mass; /* by id */
@@ -61,10 +63,11 @@ typedef struct {
     long shadow_n;       /* bodies in the mapped mirror (-1: none) */
     const jint *rem;     /* lastRemoved, ascending, while a removal pass runs */
     long nrem;
-    Body *spare;         /* the survivors' target list (grown only; swapped with bodies->b) */
+    Body **spare;        /* the survivors' target list (grown only; swapped with bodies->b) */
     long spare_cap;
     double mergeMaxMass, mergeMinDist; /* BHA:315,321 */
-    double step_ms; /* the last Native.step's own duration (step_thread) */
+    jlongArray info3;      /* Native.positions' [n, stride, n before] */
+    const int32_t *surv;   /* Native.survivors: survivor j's list index before the step */
 } Shim;
 
 static JNIEnv *env;
@@ -87,11 +90,11 @@ static void shim_params(Shim *s) {
 static void soa_of(const List *l, double *a) {
     long n = l->n;
     for (long i = 0; i < n; ++i) {
-        a[i] = l->b[i].x;
-        a[n + i] = l->b[i].y;
-        a[2 * n + i] = l->b[i].vx;
-        a[3 * n + i] = l->b[i].vy;
-        a[4 * n + i] = l->b[i].m;
+        a[i] = l->b[i]->x;
+        a[n + i] = l->b[i]->y;
+        a[2 * n + i] = l->b[i]->vx;
+        a[3 * n + i] = l->b[i]->vy;
+        a[4 * n + i] = l->b[i]->m;
     }
 }
 
@@ -164,7 +167,7 @@ static int changed_part(Shim *s, long lo, long hi) {
     const long st = s->mir_stride;
     const double *a = s->mir;
     for (long i = lo; i < hi; ++i) {
-        const Body *b = &s->bodies->b[i];
+        const Body *b = s->bodies->b[i];
         if (memcmp(&b->x, &a[i], 8) || memcmp(&b->y, &a[st + i], 8) ||
             memcmp(&b->vx, &a[2 * st + i], 8) || memcmp(&b->vy, &a[3 * st + i], 8) ||
             memcmp(&b->m, &a[4 * st + i], 8))
@@ -178,6 +181,14 @@ static int shim_changed(Shim *s) {
     return par_any(s, n, changed_part);
 }
 
+static void swap_spare(Shim *s) { /* the spare list becomes the list, and the list the spare */
+    Body **b = s->bodies->b;
+    const long cap = s->bodies->cap;
+    s->bodies->b = s->spare;
+    s->bodies->cap = s->spare_cap;
+    s->spare = b;
+    s->spare_cap = cap;
+}
 static long removed_below(const Shim *s, long i) { /* lower_bound over lastRemoved */
     long lo = 0, hi = s->nrem;
     while (lo < hi) {
@@ -212,7 +223,7 @@ static void shim_apply_removed(Shim *s) {
             for (jsize k = nr; k-- > 0;) { /* removeAt, descending (BHA:519) */
                 long j = (long)r[k];
                 memmove(&s->bodies->b[j], &s->bodies->b[j + 1],
-                        sizeof(Body) * (s->bodies->n - j - 1));
+                        sizeof(Body *) * (s->bodies->n - j - 1));
                 s->bodies->n -= 1;
             }
         } else if (s->bodies->n < shim_par_min || shim_threads <= 1) {
@@ -231,15 +242,13 @@ static void shim_apply_removed(Shim *s) {
             const long n = s->bodies->n;
             if (s->spare_cap < n) {
                 free(s->spare);
-                s->spare = (Body *)malloc(sizeof(Body) * n);
+                s->spare = (Body **)malloc(sizeof(Body *) * n);
                 s->spare_cap = n;
             }
             s->rem = r;
             s->nrem = nr;
             (void)par_any(s, n, compact_part);
-            Body *old = s->bodies->b;
-            s->bodies->b = s->spare;
-            s->spare = old;
+            swap_spare(s);
             s->bodies->n = n - nr;
         }
         fake_jvm_free(rem);
@@ -250,7 +259,7 @@ static int unpack_part(Shim *s, long lo, long hi) {
     const double *a = s->mir;
     const long st = s->mir_stride;
     for (long i = lo; i < hi; ++i) { /* into the SAME Body objects (BHA:414-432) */
-        Body *b = &s->bodies->b[i];
+        Body *b = s->bodies->b[i];
         b->x = a[i];
         b->y = a[st + i];
         b->vx = a[2 * st + i];
@@ -258,6 +267,42 @@ static int unpack_part(Shim *s, long lo, long hi) {
         b->m = a[4 * st + i];
     }
     return 0;
+}
+static int unpack_xym_part(Shim *s, long lo, long hi) { /* the hand-off: x, y, m final */
+    const double *a = s->mir;
+    const long st = s->mir_stride;
+    for (long i = lo; i < hi; ++i) {
+        Body *b = s->bodies->b[i];
+        b->x = a[i];
+        b->y = a[st + i];
+        b->m = a[4 * st + i];
+    }
+    return 0;
+}
+static int unpack_v_part(Shim *s, long lo, long hi) { /* after the step: vx, vy */
+    const double *a = s->mir;
+    const long st = s->mir_stride;
+    for (long i = lo; i < hi; ++i) {
+        Body *b = s->bodies->b[i];
+        b->vx = a[2 * st + i];
+        b->vy = a[3 * st + i];
+    }
+    return 0;
+}
+/* the removals from the survivors' list: survivor j is the body at list index surv[j] */
+static int gather_part(Shim *s, long lo, long hi) {
+    for (long j = lo; j < hi; ++j) s->spare[j] = s->bodies->b[s->surv[j]];
+    return 0;
+}
+static void shim_keep_survivors(Shim *s, long n) {
+    if (s->spare_cap < s->bodies->n) {
+        free(s->spare);
+        s->spare = (Body **)malloc(sizeof(Body *) * s->bodies->n);
+        s->spare_cap = s->bodies->n;
+    }
+    (void)par_any(s, n, gather_part);
+    swap_spare(s);
+    s->bodies->n = n;
 }
 static void shim_unpack(Shim *s, long n) {
     if (n != s->bodies->n) {
@@ -278,6 +323,7 @@ static void shim_create(Shim *s, List *initial, jint device_mask) {
     s->mergeMinDist = 8.0;
     s->shadow_n = -1;
     s->info = fake_jvm_long_array(2);
+    s->info3 = fake_jvm_long_array(3);
     s->h = Java_Native_create(env, NULL, device_mask);
     if (fake_jvm_take_exception() || !s->h) {
         fprintf(stderr, "abi_harness: Native.create failed (no GPU?)\n");
@@ -295,44 +341,72 @@ static void shim_reset(Shim *s, List *l) {
 
 static long shim_steps_uploaded;
 static double now_ms(void);
-/* Native.step on a worker thread (PhysicsEngine.kt: launch(Dispatchers.IO)); its own duration */
-static void *step_thread(void *p) {
-    Shim *s = (Shim *)p;
-    const double t = now_ms();
-    Java_Native_step(env, NULL, s->h, 1);
-    s->step_ms = now_ms() - t;
-    return NULL;
-}
-/* step(): the step runs while the list is compared against the mapped mirror (the engine writes
- * its other buffer, bh_set_mirror(e, 2)); an edited list is uploaded and stepped again, the
- * upload replacing the first step's result.  *compare_ms: the compare's own duration. */
-static void shim_step_body(Shim *s, double *compare_ms) {
+/* step(): Native.stepBegin (the step runs on the engine's thread), the list compared against the
+ * mapped mirror meanwhile (the step writes the other buffer); an edited list is uploaded and
+ * stepped again instead.  Else Native.positions waits for the step's hand-off -- positions and
+ * masses final, its merge rule done -- and the removals (Native.survivors) and the x, y, m unpack
+ * run while its last traversal still does; after Native.stepEnd only vx, vy are unpacked.
+ * t (nullable): params, compare, wait for the survivors, removals, unpack x/y/m, wait for the
+ * end, map + unpack vx/vy, wait for the planes -- ms, accumulated. */
+static void shim_frame(Shim *s, double *t) {
+    double a = now_ms(), b;
+#define LAP(q) do { b = now_ms(); if (t) t[q] += b - a; a = b; } while (0)
+    shim_params(s);
+    LAP(0);
     if (s->bodies->n != s->shadow_n) { /* bodies added or removed: upload first */
         shim_push(s);
         ++shim_steps_uploaded;
         Java_Native_step(env, NULL, s->h, 1);
         jni_check("step");
+        shim_pull(s, 1);
         return;
     }
-    pthread_t t;
-    if (pthread_create(&t, NULL, step_thread, s)) fail("pthread_create", -1);
-    const double c0 = now_ms();
+    Java_Native_stepBegin(env, NULL, s->h, 1);
+    jni_check("stepBegin");
     const int diff = shim_changed(s);
-    if (compare_ms) *compare_ms += now_ms() - c0;
-    pthread_join(t, NULL);
-    jni_check("step");
-    if (diff) {
+    LAP(1);
+    if (diff) { /* the upload replaces that step's result */
+        Java_Native_stepEnd(env, NULL, s->h);
+        jni_check("stepEnd");
         shim_push(s);
         ++shim_steps_uploaded;
         Java_Native_step(env, NULL, s->h, 1);
         jni_check("step");
+        shim_pull(s, 1);
+        return;
     }
+    { /* the survivors first (ahead of the planes' copy): the removals run while it lasts */
+        jobject sb = Java_Native_survivors(env, NULL, s->h);
+        jni_check("survivors");
+        jlong scap = 0;
+        s->surv = (const int32_t *)fake_jvm_direct_address(sb, &scap);
+        fake_jvm_free(sb);
+        const long ns = (long)(scap / (jlong)sizeof(int32_t));
+        LAP(2);
+        if (ns != s->bodies->n) shim_keep_survivors(s, ns);
+        LAP(3);
+    }
+    jobject buf = Java_Native_positions(env, NULL, s->h, s->info3);
+    jni_check("positions");
+    const jlong *in = fake_jvm_longs(s->info3);
+    jlong cap = 0;
+    s->mir = (const double *)fake_jvm_direct_address(buf, &cap);
+    s->mir_stride = (long)in[1];
+    const long n = (long)in[0];
+    if (n != s->bodies->n) fail("positions: the list after the step", -1);
+    fake_jvm_free(buf);
+    LAP(7);
+    (void)par_any(s, n, unpack_xym_part);
+    LAP(4);
+    Java_Native_stepEnd(env, NULL, s->h);
+    jni_check("stepEnd");
+    LAP(5);
+    if (shim_map(s) != n) fail("map after the step: N", -1);
+    (void)par_any(s, n, unpack_v_part);
+    LAP(6);
+#undef LAP
 }
-static void shim_step(Shim *s) {
-    shim_params(s);
-    shim_step_body(s, NULL);
-    shim_pull(s, 1);
-}
+static void shim_step(Shim *s) { shim_frame(s, NULL); }
 
 /* getTreeForDebug(): Native.quads (QuadList: interleaved triples), then pull(false);
  * returned de-interleaved (cx[], cy[], h[]) for the comparison with the oracle */
@@ -356,14 +430,17 @@ static double *shim_tree(Shim *s, int64_t *nq) {
 /* ---- scenes --------------------------------------------------------------------------- */
 static void list_append_soa(List *l, long n, const double *x, const double *y, const double *vx,
                             const double *vy, const double *m) {
-    l->b = realloc(l->b, sizeof(Body) * (l->n + n + 1));
+    l->b = realloc(l->b, sizeof(Body *) * (l->n + n + 1));
+    l->cap = l->n + n + 1;
     start_mass = realloc(start_mass, sizeof(double) * (next_id + n + 1));
+    Body *objs = malloc(sizeof(Body) * (n + 1)); /* (owned by the scene for the whole run) */
     for (long i = 0; i < n; ++i) {
         /* a unique start mass per body (light bodies keep theirs: only heavies absorb) */
         double mi = m[i] <= 4000.0 ? m[i] * (1.0 + (double)(next_id + 1) * 0x1p-40) : m[i];
         Body b = {x[i], y[i], vx[i], vy[i], mi, next_id};
         start_mass[next_id++] = mi;
-        l->b[l->n++] = b;
+        objs[i] = b;
+        l->b[l->n++] = &objs[i];
     }
 }
 
@@ -413,7 +490,7 @@ static void compare(const List *l, oracle_engine *o, long frame) {
     free(a);
     free(b);
     for (long i = 0; i < n; ++i) { /* identity: light bodies keep their unique start mass */
-        const Body *bd = &l->b[i];
+        const Body *bd = l->b[i];
         if (start_mass[bd->id] <= 4000.0 && bd->m != start_mass[bd->id])
             fail("a surviving Body is not the object the reference keeps", frame);
     }
@@ -427,44 +504,28 @@ static double now_ms(void) {
 
 /* --c3-frames K: the shim's per-frame host work at C3 (8e5 + 2e5 galaxy disks, NBodyPanel's
  * two disks scaled), timed beside the GPU step: NBodyPanel's tick() -> step() (PNL:290-293),
- * K frames after 5 warm-up frames.  Prints one JSON line.  (The bodies are C structs here, not
- * JVM objects behind an ArrayList: the loops are a lower bound of the JVM's.) */
+ * K frames after 5 warm-up frames.  Prints one JSON line.  (The list holds references to Body
+ * objects, as an ArrayList does; C loops over them are a lower bound of the JVM's.) */
 static int c3_frames(long frames, jint mask) {
-    List list = {NULL, 0};
+    List list = {NULL, 0, 0};
     add_galaxy(&list, 800000, 1200.0, 400.0, 0.0, 300.0, 50000.0, 5000.0, 1);
     add_galaxy(&list, 200000, 1200.0, 160.0, -50.0, 100.0, 5000.0, 500.0, 2);
     Shim s;
     shim_create(&s, &list, mask);
     for (int w = 0; w < 5; ++w) shim_step(&s);
     const long allocs0 = shadow_allocs, uploads0 = shim_steps_uploaded;
-    double t[6] = {0, 0, 0, 0, 0, 0}; /* params, step || compare, removals, map, unpack, compare */
-    double step_own = 0.0;
+    double t[8] = {0, 0, 0, 0, 0, 0, 0, 0}; /* shim_frame's phases */
     const long n0 = s.bodies->n;
     const double t0 = now_ms();
-    for (long f = 0; f < frames; ++f) {
-        double a = now_ms(), b;
-        shim_params(&s);
-        b = now_ms(); t[0] += b - a; a = b;
-        shim_step_body(&s, &t[5]);
-        step_own += s.step_ms;
-        b = now_ms(); t[1] += b - a; a = b;
-        shim_apply_removed(&s);
-        b = now_ms(); t[2] += b - a; a = b;
-        const long n = shim_map(&s);
-        b = now_ms(); t[3] += b - a; a = b;
-        shim_unpack(&s, n);
-        b = now_ms(); t[4] += b - a;
-    }
+    for (long f = 0; f < frames; ++f) shim_frame(&s, t);
     const double total = now_ms() - t0;
-    /* host_ms: the frame's time outside the step itself (the compare runs during the step) */
     printf("{\"frames\": %ld, \"bodies\": %ld, \"devices\": %d, \"threads\": %d, \"ms_per_frame\": %.4f, "
-           "\"step_ms\": %.4f, \"host_ms\": %.4f, \"params_ms\": %.4f, \"step_and_compare_ms\": %.4f, "
-           "\"changed_ms\": %.4f, \"removals_ms\": %.4f, \"map_ms\": %.4f, \"unpack_ms\": %.4f, "
+           "\"params_ms\": %.4f, \"changed_ms\": %.4f, \"wait_survivors_ms\": %.4f, \"removals_ms\": %.4f, "
+           "\"wait_planes_ms\": %.4f, \"unpack_xym_ms\": %.4f, \"wait_end_ms\": %.4f, \"unpack_v_ms\": %.4f, "
            "\"allocations_per_frame\": %.3f, \"uploads\": %ld}\n",
            frames, n0, bh_multi_world((bh_engine *)(intptr_t)s.h), shim_threads, total / frames,
-           step_own / frames, (total - step_own) / frames, t[0] / frames, t[1] / frames,
-           t[5] / frames, t[2] / frames, t[3] / frames, t[4] / frames,
-           (double)(shadow_allocs - allocs0) / frames, shim_steps_uploaded - uploads0);
+           t[0] / frames, t[1] / frames, t[2] / frames, t[3] / frames, t[7] / frames, t[4] / frames,
+           t[5] / frames, t[6] / frames, (double)(shadow_allocs - allocs0) / frames, shim_steps_uploaded - uploads0);
     bh_destroy((bh_engine *)(intptr_t)s.h);
     return 0;
 }
@@ -482,7 +543,7 @@ int main(int argc, char **argv) {
         else if (!strcmp(argv[i], "--c3-frames") && i + 1 < argc) timing_frames = atol(argv[++i]);
     }
     if (timing_frames > 0) return c3_frames(timing_frames, mask);
-    List list = {NULL, 0};
+    List list = {NULL, 0, 0};
     /* defaultBodies() (PNL:83-100), scaled down */
     add_galaxy(&list, 3000, 1200.0, 400.0, 0.0, 300.0, 50000.0, 5000.0, 1);
     add_galaxy(&list, 800, 1200.0, 160.0, -50.0, 100.0, 5000.0, 500.0, 2);
@@ -490,7 +551,7 @@ int main(int argc, char **argv) {
     shim_create(&s, &list, mask); /* PNL:103 */
     const long allocs0 = shadow_allocs;
     oracle_engine *o = oracle_of(&list, &s);
-    List list2 = {NULL, 0}, list3 = {NULL, 0};
+    List list2 = {NULL, 0, 0}, list3 = {NULL, 0, 0};
     long removed_total = 0, quads_checked = 0, removed_max = 0;
     for (long frame = 0; frame < 40; ++frame) {
         if (frame == 10) cfg_theta = 0.7; /* Z/X keys (PNL:247-248), read live */
@@ -505,7 +566,8 @@ int main(int argc, char **argv) {
         }
         if (frame == 30) { /* mouse release: getBodies() + new disk -> resetBodies (PNL:228-234) */
             for (long i = 0; i < s.bodies->n; ++i) {
-                list3.b = realloc(list3.b, sizeof(Body) * (list3.n + 1));
+                list3.b = realloc(list3.b, sizeof(Body *) * (list3.n + 1));
+                list3.cap = list3.n + 1;
                 list3.b[list3.n++] = s.bodies->b[i]; /* the same objects, re-listed */
             }
             add_galaxy(&list3, 500, 1700.0, 500.0, 0.0, 80.0, 6000.0, 300.0, 9);
@@ -514,8 +576,8 @@ int main(int argc, char **argv) {
             o = oracle_of(&list3, &s);
         }
         if (frame == 25) { /* the caller edits a body in place (as a drag would): step() uploads */
-            s.bodies->b[7].vx += 1.0;
-            s.bodies->b[s.bodies->n - 1].y -= 3.0;
+            s.bodies->b[7]->vx += 1.0;
+            s.bodies->b[s.bodies->n - 1]->y -= 3.0;
             oracle_destroy(o);
             o = oracle_of(s.bodies, &s); /* the reference steps the edited objects themselves */
         }

@@ -30,6 +30,10 @@ void Java_Native_reset(JNIEnv *env, jobject self, jlong h, jint n, jdoubleArray 
 void Java_Native_step(JNIEnv *env, jobject self, jlong h, jint k);
 jint Java_Native_getInto(JNIEnv *env, jobject self, jlong h, jdoubleArray soa);
 jobject Java_Native_map(JNIEnv *env, jobject self, jlong h, jlongArray info);
+void Java_Native_stepBegin(JNIEnv *env, jobject self, jlong h, jint k);
+jobject Java_Native_positions(JNIEnv *env, jobject self, jlong h, jlongArray info);
+jobject Java_Native_survivors(JNIEnv *env, jobject self, jlong h);
+void Java_Native_stepEnd(JNIEnv *env, jobject self, jlong h);
 jdoubleArray Java_Native_quads(JNIEnv *env, jobject self, jlong h);
 jintArray Java_Native_lastRemoved(JNIEnv *env, jobject self, jlong h);
 

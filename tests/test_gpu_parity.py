@@ -1180,6 +1180,73 @@ def test_double_buffered_mirror_views_survive_the_next_step():
     assert mir.num_bodies() < len(arrs[0])  # the heavies merged along the way
 
 
+def _async_call(eng, ref, k, what):
+    """One bh_step_begin / bh_step_positions / bh_step_end call against the oracle's k steps:
+    the mapped views unchanged during the call; positions and masses at the hand-off final;
+    the survivors the complement of bh_last_removed; vx, vy final after the end."""
+    held = eng.map_bodies()
+    kept = [a.copy() for a in held]
+    eng.step_begin(k)
+    during = [a.copy() for a in held]
+    x, y, m, sv, n0 = eng.step_positions()
+    ref.step(k)
+    want = ref.get_bodies()
+    _assert_arrays_equal(during, kept, f"{what}: the held views during the call")
+    assert n0 == len(kept[0]), what
+    for got, w, name in ((x, want[0], "x"), (y, want[1], "y"), (m, want[4], "m")):
+        assert len(got) == len(w) and bits_equal(got, w), f"{what}: {name} at the hand-off"
+    sv = sv.copy()
+    eng.step_end()
+    removed = eng.last_removed()
+    assert np.array_equal(np.setdiff1d(np.arange(n0), removed), sv), f"{what}: survivors"
+    full = eng.map_bodies()
+    _assert_arrays_equal(full, want, f"{what}: after the end")
+    assert full[0].ctypes.data == x.ctypes.data, f"{what}: the hand-off's buffer"
+    return len(removed)
+
+
+def test_async_step_hands_over_positions_before_the_call_ends():
+    """bh_step_begin / bh_step_positions / bh_step_end (the drop-in's frame): positions, masses
+    and the survivors' list indices of the running call, before its last traversal, equal the
+    oracle's after step() (BHA:405-439, 519) -- one-step and three-step calls over merges and
+    jitter, a call replayed for a merge mailbox overflow (the hand-off is void, the end's
+    mirror is handed over), and a call that fails (an injected tree flag) raising from both."""
+    arrs = _frames_scene()
+    p = bh_amd.default_params(theta=0.5)
+    eng = bh_amd.Engine(p)
+    eng.reset_bodies(*arrs)
+    eng.set_mirror(True, buffers=2)
+    ref = oracle.Oracle(*arrs, theta=0.5)
+    merged = 0
+    for f in range(12):
+        merged += _async_call(eng, ref, 3 if f % 4 == 3 else 1, f"frame {f}")
+    assert merged > 0
+    with pytest.raises(bh_amd.BhError):  # no call begun
+        eng.step_positions()
+    # the crowd of heavies: the first step's candidate pairs overflow the mailbox (replay)
+    rng = np.random.default_rng(77)
+    nh = 520
+    hx, hy = 1000.0 + 20.0 * rng.random(nh), 400.0 + 20.0 * rng.random(nh)
+    field = scenes.uniform(3000, 0.5, seed=17)
+    x, y = np.concatenate([hx, field[0]]), np.concatenate([hy, field[1]])
+    mm = np.concatenate([rng.uniform(4001.0, 6000.0, nh), field[4]])
+    crowd = (x, y, np.zeros(len(x)), np.zeros(len(x)), mm)
+    eng.reset_bodies(*crowd)
+    ref = oracle.Oracle(*crowd, theta=0.5)
+    assert _async_call(eng, ref, 1, "overflowing call") > nh // 2
+    _async_call(eng, ref, 1, "after the replay")
+    eng.debug_inject(2)  # this call's own second build reports an unsupported geometry
+    eng.step_begin(1)
+    with pytest.raises(bh_amd.BhError) as err:
+        eng.step_positions()
+    assert err.value.rc == bh_amd.BH_E_STATE
+    with pytest.raises(bh_amd.BhError):
+        eng.step_end()
+    ref.step(1)
+    _assert_arrays_equal(eng.get_bodies(), ref.get_bodies(), "after the failed call")
+    _async_call(eng, ref, 1, "after the failure")
+
+
 def test_one_step_calls_then_reconfigure_checkpoint_and_evaluate(tmp_path):
     """What the caller may do between two pipelined calls, each against the oracle: a root-cell
     change (the prebuilt tree and its jitter belong to the old root and are dropped), a
