@@ -2521,6 +2521,15 @@ bh_engine *multi_active0(const bh_engine *e) { return e->use_one ? e->one : mult
 // the API boundary)
 #define MULTI_M0(e) ((e)->multi ? multi_active0(e) : (e))
 
+// A call begun by bh_step_begin owns the engine until bh_step_end: the other calls that use
+// the engine are refused (BH_E_STATE, without touching the error text the call may be writing)
+// from any thread but the call's own.
+#define ASYNC_GUARD(e)                                                                         \
+    do {                                                                                       \
+        if ((e)->async_running && std::this_thread::get_id() != (e)->step_thr.get_id())      \
+            return BH_E_STATE;                                                                 \
+    } while (0)
+
 // =========================================================================================
 extern "C" {
 
@@ -2756,6 +2765,7 @@ const char *bh_last_error(const bh_engine *e) { return e ? e->err.c_str() : "nul
 
 int bh_set_params(bh_engine *e, const bh_params *p) {
     if (!e || !p) return BH_E_INVALID;
+    ASYNC_GUARD(e);
     Geometry g;
     TRY(make_geometry(*p, g, e->err));
     if (e->multi) {
@@ -2806,6 +2816,7 @@ int bh_get_params(const bh_engine *e, bh_params *p) {
 int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, const double *vx,
                     const double *vy, const double *m) {
     if (!e || n < 0 || (n > 0 && (!x || !y || !vx || !vy || !m))) return BH_E_INVALID;
+    ASYNC_GUARD(e);
     if (n >= (int64_t)NODE_BODY_MASK) {
         e->err = "too many bodies";
         return BH_E_INVALID;
@@ -2863,8 +2874,16 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
     return BH_OK;
 }
 
+static int step_call(bh_engine *e, int32_t k);
+
 int bh_step(bh_engine *e, int32_t k) {
     if (!e || k < 0) return BH_E_INVALID;
+    ASYNC_GUARD(e);
+    return step_call(e, k);
+}
+
+// bh_step's work (bh_step_begin's thread calls it directly)
+static int step_call(bh_engine *e, int32_t k) {
     MULTI_ALL(e, bh_step(m_, k));  // every GPU's share of every step, joined (BHA:374-395, 408)
     ++e->api_calls;
     HIPCHK(e, hipSetDevice(e->device));
@@ -2974,10 +2993,7 @@ int bh_step(bh_engine *e, int32_t k) {
 
 int bh_step_begin(bh_engine *e, int32_t k) {
     if (!e || k < 0) return BH_E_INVALID;
-    if (e->async_running) {
-        e->err = "bh_step_begin: the previous call was not ended (bh_step_end)";
-        return BH_E_STATE;
-    }
+    if (e->async_running) return BH_E_STATE;  // (its call may be writing the error text)
     bh_engine *t = MULTI_M0(e);  // the engine whose mirror the call fills
     if (!t->mirror_on || t->mir_nbuf != 2) {
         e->err = "bh_step_begin: needs the two-buffer mirror (bh_set_mirror(e, 2))";
@@ -2995,7 +3011,7 @@ int bh_step_begin(bh_engine *e, int32_t k) {
     e->async_rc = BH_OK;
     e->async_running = true;
     e->step_thr = std::thread([e, t, k] {
-        const int rc = bh_step(e, k);
+        const int rc = step_call(e, k);
         {
             std::lock_guard<std::mutex> lk(t->mid_mu);
             e->async_rc = rc;
@@ -3087,6 +3103,7 @@ int64_t bh_num_bodies(const bh_engine *e) { return e ? MULTI_M0(e)->n : -1; }
 int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, double *m,
                   int64_t cap, int64_t *n_out) {
     if (!e) return BH_E_INVALID;
+    ASYNC_GUARD(e);
     if (e->multi) {  // every replica is complete at the API boundary: member 0's
         const int rc = bh_get_bodies(MULTI_M0(e), x, y, vx, vy, m, cap, n_out);
         if (rc != BH_OK) e->err = bh_last_error(MULTI_M0(e));
@@ -3115,6 +3132,7 @@ int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, do
 
 int bh_set_mirror(bh_engine *e, int enabled) {
     if (!e) return BH_E_INVALID;
+    ASYNC_GUARD(e);
     if (enabled < 0 || enabled > 2) {
         e->err = "bh_set_mirror: enabled is 0, 1 or 2";
         return BH_E_INVALID;
@@ -3136,6 +3154,7 @@ int bh_set_mirror(bh_engine *e, int enabled) {
 int bh_map_bodies(bh_engine *e, const double **x, const double **y, const double **vx,
                   const double **vy, const double **m, int64_t *n_out) {
     if (!e) return BH_E_INVALID;
+    ASYNC_GUARD(e);
     if (e->multi) {
         const int rc = bh_map_bodies(MULTI_M0(e), x, y, vx, vy, m, n_out);
         if (rc != BH_OK) e->err = bh_last_error(MULTI_M0(e));
@@ -3165,6 +3184,7 @@ int bh_map_bodies(bh_engine *e, const double **x, const double **y, const double
 
 int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visits) {
     if (!e) return BH_E_INVALID;
+    ASYNC_GUARD(e);
     // (every member builds and evaluates -- the build may jitter every replica alike; member 0
     // hands the results out)
     if (e->multi) {  // (the visit-counting walk is not sharded: every member counts)
@@ -3226,6 +3246,7 @@ int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visi
 
 int bh_get_quads(bh_engine *e, double *cx, double *cy, double *h, int64_t cap, int64_t *n_out) {
     if (!e || cap < 0 || (cap > 0 && (!cx || !cy || !h))) return BH_E_INVALID;
+    ASYNC_GUARD(e);
     if (e->multi) {  // every member builds getTreeForDebug's tree (the same jitter in every
                      // replica); member 0 walks it
         const int rc = multi_fan(e, [](bh_engine *m, int) { return quads_prepare(m); }, false);

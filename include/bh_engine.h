@@ -178,7 +178,8 @@ int bh_step(bh_engine *e, int32_t k);
  * the call (the drop-in shim: NBodyPanel's tick, PNL:290-306, around step(), BHA:405-439).
  * Needs the two-buffer mirror (bh_set_mirror(e, 2)), else BH_E_STATE.  Until bh_step_end the
  * caller may only read the mirror it mapped before (bh_map_bodies: the call writes the other
- * buffer) and call bh_step_positions; bh_step_end joins and returns bh_step's result (then
+ * buffer) and call bh_step_positions (bh_step, bh_reset_bodies, bh_set_params, bh_get_bodies,
+ * bh_map_bodies, bh_set_mirror, bh_get_quads and bh_compute_accelerations return BH_E_STATE); bh_step_end joins and returns bh_step's result (then
  * bh_last_removed, bh_map_bodies, ... as after bh_step).
  * bh_step_positions blocks until the call's positions and masses are final -- on one GPU that is
  * once its last merge rule is done, before its last traversal; else when the call ends -- and

@@ -1221,6 +1221,15 @@ def test_async_step_hands_over_positions_before_the_call_ends():
     for f in range(12):
         merged += _async_call(eng, ref, 3 if f % 4 == 3 else 1, f"frame {f}")
     assert merged > 0
+    eng.step_begin(1)  # the running call owns the engine: other calls are refused meanwhile
+    for refused in (lambda: eng.step(1), eng.map_bodies, eng.get_bodies,
+                    lambda: eng.step_begin(1)):
+        with pytest.raises(bh_amd.BhError) as err:
+            refused()
+        assert err.value.rc == bh_amd.BH_E_STATE
+    eng.step_end()
+    ref.step(1)
+    _assert_arrays_equal(eng.map_bodies(), ref.get_bodies(), "after the refused calls")
     with pytest.raises(bh_amd.BhError):  # no call begun
         eng.step_positions()
     # the crowd of heavies: the first step's candidate pairs overflow the mailbox (replay)
