@@ -43,7 +43,7 @@ PhysicsEngine::PhysicsEngine(std::vector<Body> &initialBodies, const std::vector
 }
 
 void PhysicsEngine::init() {
-    check(bh_set_mirror(eng_, 1));  // every step writes the caller-order bodies to pinned memory
+    check(bh_set_mirror(eng_, 2));  // every step writes the caller-order bodies to pinned memory
     pushParams();
     pushBodies();
 }
@@ -72,13 +72,26 @@ void PhysicsEngine::pushBodies() {
         x[i] = b.x; y[i] = b.y; vx[i] = b.vx; vy[i] = b.vy; m[i] = b.m;
     }
     check(bh_reset_bodies(eng_, (int64_t)n, x.data(), y.data(), vx.data(), vy.data(), m.data()));
-    shadow_ = *bodies_;
+    mapMirror();  // (the engine's copy, as uploaded)
 }
 
-// Bitwise: a caller that wrote the same value back (or a NaN) does not force an upload.
+void PhysicsEngine::mapMirror() {
+    check(bh_map_bodies(eng_, &mir_[0], &mir_[1], &mir_[2], &mir_[3], &mir_[4], &mirN_));
+}
+
+// Bitwise against the mapped mirror: a caller that wrote the same value back (or a NaN) does
+// not force an upload.
 bool PhysicsEngine::bodiesChanged() const {
-    return bodies_->size() != shadow_.size() ||
-           std::memcmp(bodies_->data(), shadow_.data(), sizeof(Body) * shadow_.size()) != 0;
+    const size_t n = bodies_->size();
+    if ((int64_t)n != mirN_) return true;
+    for (size_t i = 0; i < n; ++i) {
+        const Body &b = (*bodies_)[i];
+        if (std::memcmp(&b.x, mir_[0] + i, 8) || std::memcmp(&b.y, mir_[1] + i, 8) ||
+            std::memcmp(&b.vx, mir_[2] + i, 8) || std::memcmp(&b.vy, mir_[3] + i, 8) ||
+            std::memcmp(&b.m, mir_[4] + i, 8))
+            return true;
+    }
+    return false;
 }
 
 // Write results back into the SAME Body objects (the reference mutates in place,
@@ -105,19 +118,67 @@ void PhysicsEngine::pullBodies(bool afterStep) {
             bodies_->resize(w);
         }
     }
-    const double *x, *y, *vx, *vy, *m;  // the engine's pinned mirror, filled by the step itself
-    int64_t got = 0;
-    check(bh_map_bodies(eng_, &x, &y, &vx, &vy, &m, &got));
+    mapMirror();  // the engine's pinned mirror, filled by the step itself
+    const int64_t got = mirN_;
     if ((int64_t)bodies_->size() != got) throw std::runtime_error("engine and caller lists diverged");
-    for (int64_t i = 0; i < got; ++i) (*bodies_)[(size_t)i] = Body{x[i], y[i], vx[i], vy[i], m[i]};
-    shadow_ = *bodies_;
+    for (int64_t i = 0; i < got; ++i)
+        (*bodies_)[(size_t)i] = Body{mir_[0][i], mir_[1][i], mir_[2][i], mir_[3][i], mir_[4][i]};
 }
 
 void PhysicsEngine::step() {
     pushParams();
-    if (bodiesChanged()) pushBodies();  // the caller edited bodies between frames
-    check(bh_step(eng_, 1));
-    pullBodies(true);
+    if ((int64_t)bodies_->size() != mirN_) {  // the caller added or removed bodies
+        pushBodies();
+        check(bh_step(eng_, 1));
+        pullBodies(true);
+        return;
+    }
+    // The step runs on the engine's thread while the list is compared against the mapped mirror
+    // (bh_step_begin: the step writes the other buffer); an edited list is uploaded and stepped
+    // again, the upload replacing that step's result.
+    check(bh_step_begin(eng_, 1));
+    bool edited = false;
+    try {
+        edited = bodiesChanged();
+    } catch (...) {
+        (void)bh_step_end(eng_);
+        throw;
+    }
+    if (edited) {
+        check(bh_step_end(eng_));
+        pushBodies();
+        check(bh_step(eng_, 1));
+        pullBodies(true);
+        return;
+    }
+    // The hand-off (bh_step_positions), before the step's last traversal: the survivors first --
+    // the removals (BHA:519) as one in-place pass, survivor j at list index sv[j] >= j --, then
+    // the final positions and masses; after bh_step_end only vx, vy are left.
+    const uint32_t *sv = nullptr;
+    const double *x = nullptr, *y = nullptr, *m = nullptr;
+    int64_t n = 0, n0 = 0;
+    int rc = bh_step_positions(eng_, nullptr, nullptr, nullptr, &sv, &n, &n0);
+    if (rc == BH_OK && n != (int64_t)bodies_->size()) {
+        for (int64_t j = 0; j < n; ++j) (*bodies_)[(size_t)j] = (*bodies_)[sv[j]];
+        bodies_->resize((size_t)n);
+    }
+    if (rc == BH_OK) rc = bh_step_positions(eng_, &x, &y, &m, nullptr, &n, &n0);
+    if (rc == BH_OK)
+        for (int64_t i = 0; i < n; ++i) {
+            Body &b = (*bodies_)[(size_t)i];
+            b.x = x[i];
+            b.y = y[i];
+            b.m = m[i];
+        }
+    const int rc_end = bh_step_end(eng_);
+    check(rc != BH_OK ? rc : rc_end);
+    mapMirror();
+    if (mirN_ != (int64_t)bodies_->size()) throw std::runtime_error("engine and caller lists diverged");
+    for (int64_t i = 0; i < mirN_; ++i) {
+        Body &b = (*bodies_)[(size_t)i];
+        b.vx = mir_[2][i];
+        b.vy = mir_[3][i];
+    }
 }
 
 const std::vector<Body> &PhysicsEngine::getBodies() const { return *bodies_; }

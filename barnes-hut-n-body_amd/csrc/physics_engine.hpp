@@ -82,15 +82,19 @@ private:
     void init();
     void pushParams();
     void pushBodies();
+    void mapMirror();
     bool bodiesChanged() const;
     void pullBodies(bool afterStep);
     void check(int rc) const;
 
     std::vector<Body> *bodies_;
     bh_engine *eng_ = nullptr;
-    // What the engine holds, in the caller's order (as last pushed or pulled): step() re-uploads
-    // only when the caller's list differs, so the engine keeps its Morton-ordered state.
-    std::vector<Body> shadow_;
+    // What the engine holds, in the caller's order: its pinned mirror (two buffers,
+    // bh_set_mirror(e, 2)), mapped after every call that changed it.  step() compares the list
+    // against it in place while the step already runs (the step writes the other buffer) and
+    // re-uploads only when the caller edited a body, so the engine keeps its Morton-ordered state.
+    const double *mir_[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
+    int64_t mirN_ = -1;
 };
 
 }  // namespace bh

@@ -142,6 +142,13 @@ int main(int argc, char **argv) {
             oracle_destroy(o);
             o = oracle_of(list3, engine);
         }
+        if (frame == 25) {  // the caller edits bodies in place (as a drag would): step() uploads
+            auto &live = const_cast<std::vector<bh::Body> &>(engine.getBodies());
+            live[7].vx += 1.0;
+            live.back().y -= 3.0;
+            oracle_destroy(o);
+            o = oracle_of(live, engine);  // the reference steps the edited objects themselves
+        }
         oracle_params op = oparams(engine);
         oracle_set_params(o, &op);
         const size_t before = engine.getBodies().size();
