@@ -163,9 +163,10 @@ class PhysicsEngine(initialBodies: MutableList<Body>) {
 
     private inline fun chunks(n: Int, crossinline body: (Int, Int) -> Unit) {
         if (n < 65_536 || workers == 1) { body(0, n); return }
-        val per = (n + workers - 1) / workers
+        val parts = 4 * workers                             // a worker on a busy core takes fewer
+        val per = (n + parts - 1) / parts
         runBlocking {
-            for (w in 0 until workers) {
+            for (w in 0 until parts) {
                 val lo = w * per
                 val hi = minOf(n, lo + per)
                 if (lo < hi) launch(Dispatchers.Default) { body(lo, hi) }

@@ -17,6 +17,7 @@
  */
 #define _POSIX_C_SOURCE 200809L
 #include <pthread.h>
+#include <stdatomic.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -131,35 +132,74 @@ static void shim_push(Shim *s) {
 }
 
 /* The shim's O(N) passes in chunks over worker threads, as PhysicsEngine.kt runs them on
- * Dispatchers.Default (the reference's own fan-out, BHA:374-395); short lists stay serial. */
+ * Dispatchers.Default (the reference's own fan-out, BHA:374-395): a pool of persistent workers
+ * (started once, as the JVM's shared pool is), 4 chunks per worker taken in turn (a worker that
+ * shares its core with a spinning thread takes fewer); short lists stay serial. */
 static int shim_threads = 8;
 static long shim_par_min = 65536; /* BH_SHIM_PAR_MIN: shorter lists stay serial */
-typedef struct {
+static struct {
+    pthread_mutex_t mu;
+    pthread_cond_t go, done;
+    long gen;
+    int started, pending;
     Shim *s;
-    long lo, hi;
+    long n, chunk;
     int (*fn)(Shim *, long, long);
-    int result;
-} Chunk;
-static void *chunk_run(void *p) {
-    Chunk *c = (Chunk *)p;
-    c->result = c->fn(c->s, c->lo, c->hi);
+    atomic_long next;
+    atomic_int any;
+} pool = {PTHREAD_MUTEX_INITIALIZER, PTHREAD_COND_INITIALIZER, PTHREAD_COND_INITIALIZER, 0, 0, 0,
+        NULL, 0, 0, NULL, 0, 0};
+static void pool_chunks(void) {
+    for (;;) {
+        const long c = atomic_fetch_add(&pool.next, 1);
+        const long lo = c * pool.chunk;
+        if (lo >= pool.n) return;
+        const long hi = lo + pool.chunk < pool.n ? lo + pool.chunk : pool.n;
+        if (pool.fn(pool.s, lo, hi)) atomic_store(&pool.any, 1);
+    }
+}
+static void *pool_worker(void *arg) {
+    (void)arg;
+    long seen = 0;
+    for (;;) {
+        pthread_mutex_lock(&pool.mu);
+        while (pool.gen == seen) pthread_cond_wait(&pool.go, &pool.mu);
+        seen = pool.gen;
+        pthread_mutex_unlock(&pool.mu);
+        pool_chunks();
+        pthread_mutex_lock(&pool.mu);
+        if (--pool.pending == 0) pthread_cond_signal(&pool.done);
+        pthread_mutex_unlock(&pool.mu);
+    }
     return NULL;
 }
 static int par_any(Shim *s, long n, int (*fn)(Shim *, long, long)) { /* OR of fn over chunks */
     const int w = n < shim_par_min ? 1 : shim_threads;
     if (w <= 1) return fn(s, 0, n);
-    Chunk c[64];
-    pthread_t t[64];
-    const long per = (n + w - 1) / w;
-    int any = 0;
-    for (int k = 0; k < w; ++k) {
-        c[k] = (Chunk){s, k * per, (k + 1) * per < n ? (k + 1) * per : n, fn, 0};
-        if (k > 0) pthread_create(&t[k], NULL, chunk_run, &c[k]);
+    if (!pool.started) {
+        for (int k = 1; k < w; ++k) {
+            pthread_t t;
+            if (pthread_create(&t, NULL, pool_worker, NULL)) fail("pthread_create", -1);
+            pthread_detach(t);
+        }
+        pool.started = w;
     }
-    chunk_run(&c[0]);
-    for (int k = 1; k < w; ++k) pthread_join(t[k], NULL);
-    for (int k = 0; k < w; ++k) any |= c[k].result;
-    return any;
+    pthread_mutex_lock(&pool.mu);
+    pool.s = s;
+    pool.n = n;
+    pool.fn = fn;
+    pool.chunk = (n + 4 * (long)w - 1) / (4 * (long)w);
+    atomic_store(&pool.next, 0);
+    atomic_store(&pool.any, 0);
+    pool.pending = pool.started - 1;
+    ++pool.gen;
+    pthread_cond_broadcast(&pool.go);
+    pthread_mutex_unlock(&pool.mu);
+    pool_chunks(); /* the caller's thread takes chunks too */
+    pthread_mutex_lock(&pool.mu);
+    while (pool.pending > 0) pthread_cond_wait(&pool.done, &pool.mu);
+    pthread_mutex_unlock(&pool.mu);
+    return atomic_load(&pool.any);
 }
 
 /* changed(): field by field against the mapped mirror, in place (toRawBits compares) */
