@@ -419,19 +419,15 @@ __global__ __launch_bounds__(TB) void k_key_fixup(int64_t n, int J,
     key_fixup((int64_t)blockIdx.x * TB + threadIdx.x, n, J, keys32_s, keys_s, perm);
 }
 
-__global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *__restrict__ keys_s,
+// k_prep's body for one sorted body a < n: the state gathered into the new order, the splitters,
+// the old -> new slot map, c(a) and the node count (returned)
+__device__ __forceinline__ uint32_t prep_one(int64_t a, int64_t n, int J,
+                                             const uint64_t *__restrict__ keys_s,
                                              const uint32_t *__restrict__ perm, BodyState src,
                                              BodyState dst, int8_t *__restrict__ cpl,
                                              uint32_t *__restrict__ cnt,
                                              uint64_t *__restrict__ spl,
                                              uint32_t *__restrict__ inv) {
-    chain_prio();
-    int64_t a = (int64_t)xcd_block() * TB + threadIdx.x;
-    if (a > n) return;
-    if (a == n) {
-        cnt[n] = 0;
-        return;
-    }
     const uint64_t SENT = sentinel_key(J);
     uint64_t k = keys_s[a];
     uint32_t i = perm[a];  // nearly the identity: the state is kept in the last Morton order
@@ -456,8 +452,98 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
     }
     cpl[a] = (int8_t)c_cur;
     // internal nodes starting at a: depths c_prev+1 .. c_cur; plus a's leaf.
-    cnt[a] = (k == SENT) ? 0u : 1u + (uint32_t)max(0, c_cur - c_prev);
+    const uint32_t c = (k == SENT) ? 0u : 1u + (uint32_t)max(0, c_cur - c_prev);
+    cnt[a] = c;
+    return c;
 }
+
+// The base scan (BH_BASE_SCAN): k_prep also sums its tile's counts into tsum[tile], and
+// k_base_scan turns counts and tile sums into base -- two launches without inter-block waits in
+// place of rocprim's lookback state initialisation and scan.
+#ifndef BH_BASE_SCAN
+#define BH_BASE_SCAN 1
+#endif
+constexpr int BS_TB = 1024, BS_PER = 4, BS_TILES = BS_TB * BS_PER / TB;  // prep tiles per block
+
+__device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+    return v;
+}
+
+__global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *__restrict__ keys_s,
+                                             const uint32_t *__restrict__ perm, BodyState src,
+                                             BodyState dst, int8_t *__restrict__ cpl,
+                                             uint32_t *__restrict__ cnt,
+                                             uint64_t *__restrict__ spl,
+                                             uint32_t *__restrict__ inv,
+                                             uint32_t *__restrict__ tsum) {
+    chain_prio();
+    const uint32_t tile = xcd_block();
+    const int64_t a = (int64_t)tile * TB + threadIdx.x;
+    uint32_t c = 0;
+    if (a < n) c = prep_one(a, n, J, keys_s, perm, src, dst, cpl, cnt, spl, inv);
+    else if (a == n) cnt[n] = 0;
+    if (tsum) {  // the tile's count sum for k_base_scan
+        __shared__ uint32_t s_w[TB / 64];
+        c = wave_sum_u32(c);
+        if ((threadIdx.x & 63) == 0) s_w[threadIdx.x >> 6] = c;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            uint32_t t = 0;
+#pragma unroll
+            for (int w = 0; w < TB / 64; ++w) t += s_w[w];
+            tsum[tile] = t;
+        }
+    }
+}
+
+// base[i] = sum cnt[0..i) for i < n1: block b takes BS_TB * BS_PER consecutive counts, its
+// prefix the sum of the tile sums before them
+__global__ __launch_bounds__(BS_TB) void k_base_scan(int64_t n1, const uint32_t *__restrict__ cnt,
+                                                     const uint32_t *__restrict__ tsum,
+                                                     uint32_t *__restrict__ base) {
+    chain_prio();
+    __shared__ uint32_t s_w[BS_TB / 64];
+    __shared__ uint32_t s_pre;
+    const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    // the prefix: tile sums [0, BS_TILES * blockIdx.x)
+    uint32_t p = 0;
+    for (uint32_t t = threadIdx.x; t < BS_TILES * blockIdx.x; t += BS_TB) p += tsum[t];
+    p = wave_sum_u32(p);
+    if (lane == 0) s_w[w] = p;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t t = 0;
+        for (int k = 0; k < BS_TB / 64; ++k) t += s_w[k];
+        s_pre = t;
+    }
+    __syncthreads();
+    const int64_t i0 = (int64_t)blockIdx.x * (BS_TB * BS_PER) + (int64_t)threadIdx.x * BS_PER;
+    uint32_t v[BS_PER];
+#pragma unroll
+    for (int j = 0; j < BS_PER; ++j) v[j] = i0 + j < n1 ? cnt[i0 + j] : 0u;
+    uint32_t sum = 0;
+#pragma unroll
+    for (int j = 0; j < BS_PER; ++j) sum += v[j];
+    uint32_t inc = sum;  // the wave's inclusive scan of the threads' sums
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(inc, o);
+        if (lane >= (uint32_t)o) inc += u;
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    uint32_t wpre = s_pre;
+    for (uint32_t k = 0; k < w; ++k) wpre += s_w[k];
+    uint32_t run = wpre + inc - sum;
+#pragma unroll
+    for (int j = 0; j < BS_PER; ++j) {
+        if (i0 + j < n1) base[i0 + j] = run;
+        run += v[j];
+    }
+}
+
 
 // First sorted body of every depth-D0 cell (bins 0 .. 4^D0; the sentinel's prefix is 4^D0,
 // so bin 4^D0 starts at the first out-of-root body, i.e. at the in-root count).
@@ -1803,6 +1889,8 @@ size_t tree_scratch_bytes(int64_t n, int J) {
     (void)rocprim::exclusive_scan(nullptr, scan_bytes, (const uint32_t *)nullptr,
                                   (uint32_t *)nullptr, 0u, (size_t)(n + 1),
                                   rocprim::plus<uint32_t>());
+    const size_t tsum_bytes = sizeof(uint32_t) * (size_t)((n + 1 + TB - 1) / TB + 1);  // k_prep
+    scan_bytes = scan_bytes > tsum_bytes ? scan_bytes : tsum_bytes;
     return sort_bytes > scan_bytes ? sort_bytes : scan_bytes;
 }
 
@@ -1846,12 +1934,21 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
             n, g.J, D0, b.keys32_s, b.keys_s, b.perm, b.cell_start, b.super_list, n_super);
     else
         k_key_fixup<<<grid_for(n), TB, 0, s>>>(n, g.J, b.keys32_s, b.keys_s, b.perm);
-    k_prep<<<grid_for(n + 1), TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.src, b.dst, b.cpl, b.cnt,
-                                          b.spl, b.keys32);
-    bytes = b.scratch_bytes;
-    st = rocprim::exclusive_scan(b.scratch, bytes, b.cnt, b.base, 0u, (size_t)(n + 1),
-                                 rocprim::plus<uint32_t>(), s);
-    if (st != hipSuccess) return st;
+    const int64_t prep_blocks = (n + 1 + TB - 1) / TB;
+    const bool own_scan = BH_BASE_SCAN && b.scratch_bytes >= sizeof(uint32_t) * (size_t)prep_blocks;
+    uint32_t *tsum = own_scan ? static_cast<uint32_t *>(b.scratch) : nullptr;
+    k_prep<<<(unsigned)prep_blocks, TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.src, b.dst, b.cpl,
+                                                b.cnt, b.spl, b.keys32, tsum);
+    if (own_scan) {
+        const int64_t per = (int64_t)BS_TB * BS_PER;
+        k_base_scan<<<(unsigned)((n + 1 + per - 1) / per), BS_TB, 0, s>>>(n + 1, b.cnt, tsum,
+                                                                        b.base);
+    } else {
+        bytes = b.scratch_bytes;
+        st = rocprim::exclusive_scan(b.scratch, bytes, b.cnt, b.base, 0u, (size_t)(n + 1),
+                                     rocprim::plus<uint32_t>(), s);
+        if (st != hipSuccess) return st;
+    }
     if (!BH_FIXUP_CELLS)
         k_cells<<<grid_for(nbins1), TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cell_start, b.super_list,
                                                 n_super);
