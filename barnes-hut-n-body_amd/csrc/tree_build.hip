@@ -463,7 +463,7 @@ __device__ __forceinline__ uint32_t prep_one(int64_t a, int64_t n, int J,
 #ifndef BH_BASE_SCAN
 #define BH_BASE_SCAN 1
 #endif
-constexpr int BS_TB = 1024, BS_PER = 4, BS_TILES = BS_TB * BS_PER / TB;  // prep tiles per block
+constexpr int BS_TB = 1024;  // k_base_scan: BS_TB * PER counts per block
 
 __device__ __forceinline__ uint32_t wave_sum_u32(uint32_t v) {
 #pragma unroll
@@ -498,8 +498,9 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
     }
 }
 
-// base[i] = sum cnt[0..i) for i < n1: block b takes BS_TB * BS_PER consecutive counts, its
+// base[i] = sum cnt[0..i) for i < n1: block b takes BS_TB * PER consecutive counts, its
 // prefix the sum of the tile sums before them
+template <int PER>
 __global__ __launch_bounds__(BS_TB) void k_base_scan(int64_t n1, const uint32_t *__restrict__ cnt,
                                                      const uint32_t *__restrict__ tsum,
                                                      uint32_t *__restrict__ base) {
@@ -507,9 +508,10 @@ __global__ __launch_bounds__(BS_TB) void k_base_scan(int64_t n1, const uint32_t 
     __shared__ uint32_t s_w[BS_TB / 64];
     __shared__ uint32_t s_pre;
     const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-    // the prefix: tile sums [0, BS_TILES * blockIdx.x)
+    // the prefix: tile sums [0, TILES * blockIdx.x)
+    constexpr uint32_t TILES = BS_TB * PER / TB;
     uint32_t p = 0;
-    for (uint32_t t = threadIdx.x; t < BS_TILES * blockIdx.x; t += BS_TB) p += tsum[t];
+    for (uint32_t t = threadIdx.x; t < TILES * blockIdx.x; t += BS_TB) p += tsum[t];
     p = wave_sum_u32(p);
     if (lane == 0) s_w[w] = p;
     __syncthreads();
@@ -519,13 +521,13 @@ __global__ __launch_bounds__(BS_TB) void k_base_scan(int64_t n1, const uint32_t 
         s_pre = t;
     }
     __syncthreads();
-    const int64_t i0 = (int64_t)blockIdx.x * (BS_TB * BS_PER) + (int64_t)threadIdx.x * BS_PER;
-    uint32_t v[BS_PER];
+    const int64_t i0 = (int64_t)blockIdx.x * (BS_TB * PER) + (int64_t)threadIdx.x * PER;
+    uint32_t v[PER];
 #pragma unroll
-    for (int j = 0; j < BS_PER; ++j) v[j] = i0 + j < n1 ? cnt[i0 + j] : 0u;
+    for (int j = 0; j < PER; ++j) v[j] = i0 + j < n1 ? cnt[i0 + j] : 0u;
     uint32_t sum = 0;
 #pragma unroll
-    for (int j = 0; j < BS_PER; ++j) sum += v[j];
+    for (int j = 0; j < PER; ++j) sum += v[j];
     uint32_t inc = sum;  // the wave's inclusive scan of the threads' sums
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
@@ -538,7 +540,7 @@ __global__ __launch_bounds__(BS_TB) void k_base_scan(int64_t n1, const uint32_t 
     for (uint32_t k = 0; k < w; ++k) wpre += s_w[k];
     uint32_t run = wpre + inc - sum;
 #pragma unroll
-    for (int j = 0; j < BS_PER; ++j) {
+    for (int j = 0; j < PER; ++j) {
         if (i0 + j < n1) base[i0 + j] = run;
         run += v[j];
     }
@@ -1935,13 +1937,16 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     else
         k_key_fixup<<<grid_for(n), TB, 0, s>>>(n, g.J, b.keys32_s, b.keys_s, b.perm);
     const int64_t prep_blocks = (n + 1 + TB - 1) / TB;
-    const bool own_scan = BH_BASE_SCAN && b.scratch_bytes >= sizeof(uint32_t) * (size_t)prep_blocks;
+    // (above 4 M counts rocprim's single pass is faster: the blocks' prefix reads grow with n^2 /
+    // block size -- C4 16.52-16.54 against 16.57-16.58 ms per step, profiles/r05y4_ab_c4.txt)
+    const bool own_scan = BH_BASE_SCAN && n + 1 <= ((int64_t)1 << 22) &&
+                          b.scratch_bytes >= sizeof(uint32_t) * (size_t)prep_blocks;
     uint32_t *tsum = own_scan ? static_cast<uint32_t *>(b.scratch) : nullptr;
     k_prep<<<(unsigned)prep_blocks, TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.src, b.dst, b.cpl,
                                                 b.cnt, b.spl, b.keys32, tsum);
     if (own_scan) {
-        const int64_t per = (int64_t)BS_TB * BS_PER;
-        k_base_scan<<<(unsigned)((n + 1 + per - 1) / per), BS_TB, 0, s>>>(n + 1, b.cnt, tsum,
+        const int64_t per = (int64_t)BS_TB * 4;
+        k_base_scan<4><<<(unsigned)((n + 1 + per - 1) / per), BS_TB, 0, s>>>(n + 1, b.cnt, tsum,
                                                                         b.base);
     } else {
         bytes = b.scratch_bytes;
