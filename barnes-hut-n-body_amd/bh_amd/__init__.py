@@ -47,6 +47,7 @@ EXPORTED_SYMBOLS = (
     "bh_debug_inject", "bh_set_mirror", "bh_map_bodies", "bh_create_multi",
     "bh_create_multi_list", "bh_multi_world", "bh_multi_member", "bh_collective_log",
     "bh_collective_log_clear", "bh_step_begin", "bh_step_positions", "bh_step_end",
+    "bh_progress",
 )
 
 
@@ -142,6 +143,7 @@ def load_library(path: str | None = None):
     lib.bh_comm_ranks.argtypes = [_VP, ctypes.POINTER(ctypes.c_int32),
                                   ctypes.POINTER(ctypes.c_int32)]
     lib.bh_debug_inject.argtypes = [_VP, ctypes.c_int]
+    lib.bh_progress.argtypes = [_VP, _I64P]
     lib.bh_last_removed.argtypes = [_VP, _I64P, ctypes.c_int64, _I64P]
     lib.bh_shard_range.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    _I64P, _I64P]
@@ -521,8 +523,19 @@ class Engine:
         return c.value, r.value
 
     def debug_inject(self, what: int = 1):
-        """Test hook (bh_debug_inject): 1 = the next LET build of this rank trips its guard."""
+        """Test hook (bh_debug_inject): 1 = the next LET build of this rank trips its guard;
+        2 + k = the k-th next full build raises its jitter flag; 100 + k / 200 + k = this rank
+        fails host-side before its k-th next collective / group barrier."""
         self._check(self._lib.bh_debug_inject(self._h, int(what)))
+
+    def progress(self):
+        """bh_progress (any thread, also while a call runs): dict of api_calls, collectives,
+        last_site, busy, failed, comm_aborted."""
+        out = np.zeros(4, dtype=np.int64)
+        self._check(self._lib.bh_progress(self._h, out.ctypes.data_as(_I64P)))
+        f = int(out[3])
+        return {"api_calls": int(out[0]), "collectives": int(out[1]), "last_site": int(out[2]),
+                "busy": bool(f & 1), "failed": bool(f & 2), "comm_aborted": bool(f & 4)}
 
     def set_profiling(self, on: bool):
         self._check(self._lib.bh_set_profiling(self._h, 1 if on else 0))

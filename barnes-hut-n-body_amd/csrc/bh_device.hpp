@@ -297,6 +297,11 @@ struct TreeBuffers {
     uint32_t spl_nb;
     uint32_t *bcount, *bstart;
     bool keys_ready = false;  // keys, keys32 and the bucket counts were written by the traversal
+    // the merge rule's heavy bodies (live, m > heavy_thr, BHA:474) listed by k_prep in this
+    // build's slot order, any order: heavy[atomicAdd(heavy_count, 1)] = slot (null: not wanted;
+    // *heavy_count is zero before the build -- k_merge_replay clears it after its use)
+    uint32_t *heavy = nullptr, *heavy_count = nullptr;
+    double heavy_thr = 0.0;
 };
 
 int cell_table_depth(int J, int64_t n);
@@ -604,17 +609,20 @@ struct MergeHeader {
 };
 static_assert(sizeof(MergeHeader) == sizeof(MergePair), "mailbox header size");
 // heavy = live m > thr (BHA:474) -> slot list (any order); then the distance test (BHA:493-501)
+// heavy_count: the list was made by the last build (TreeBuffers::heavy): no k_heavy pass
 void merge_candidates(int64_t n, const double *x, const double *y, const double *m,
                       const uint32_t *cidx, double thr, double minD2, uint32_t *heavy,
-                      MergePair *box, uint32_t cap, hipStream_t s, bool header_zeroed = false);
+                      MergePair *box, uint32_t cap, hipStream_t s, bool header_zeroed = false,
+                      const uint32_t *heavy_count = nullptr);
 // Sequential merge rule on the device (one workgroup): removals become tombstones
 // (cidx |= CIDX_DEAD) logged in dlog[scal[2]++]; scal[3] = pair count if the mailbox overflowed.
 // skeys/sidx: scratch of 2 x cap entries (long lists); bits: (n_cap >> 5) + 1 words and
 // slot_of: n_cap entries, n_cap > every caller index (the bitmap replay of long lists); n bounds
 // the caller indices (radix sort width).
+// heavy_count (nullable): the build's heavy-list counter, cleared for the next build
 void merge_replay(const MergePair *box, uint32_t cap, double *m, uint32_t *cidx, uint32_t *scal,
                   uint32_t *dlog, uint64_t *skeys, uint32_t *sidx, uint32_t *bits,
-                  uint32_t *slot_of, int64_t n, hipStream_t s);
+                  uint32_t *slot_of, int64_t n, hipStream_t s, uint32_t *heavy_count = nullptr);
 size_t compact_scratch_bytes(int64_t n);
 // Remove tombstoned slots preserving order; caller indices are renumbered past the removed
 // ones (dead_cidx sorted ascending, n_dead entries).  keep, pos: n-entry scratch.

@@ -20,6 +20,8 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <cmath>
 #include <condition_variable>
 #include <mutex>
@@ -51,6 +53,23 @@ void set_error(bh_engine *e, const std::string &msg);  // for the C-ABI's other 
 // each, that exchange the force pieces through device-to-device copies instead of RCCL -- the
 // same pieces, rounds and in-place layout as the ncclAllGather path, so the multi-rank
 // decomposition runs on one GPU (RCCL refuses several ranks per device).
+//
+// Every wait has a way out (the reference's join always returns, BHA:408, 426): a member whose
+// call fails aborts the group (abort()), which wakes every member waiting in barrier() and makes
+// every later barrier return false, until the members' bh_reset_bodies (reset()); a barrier that
+// waits longer than BH_COMM_TIMEOUT_S aborts the group itself.
+namespace {
+// seconds a multi-rank engine waits for its peers (a barrier, a collective on the device) before
+// it gives up and aborts (BH_COMM_TIMEOUT_S; 0 = forever)
+double comm_timeout_s() {
+    static const double t = [] {
+        const char *v = std::getenv("BH_COMM_TIMEOUT_S");
+        return v ? std::atof(v) : 300.0;
+    }();
+    return t;
+}
+}  // namespace
+
 struct bh_local_group {
     int world = 0;
     std::vector<bh_engine *> members;
@@ -58,16 +77,46 @@ struct bh_local_group {
     std::condition_variable cv;
     int arrived = 0;
     uint64_t generation = 0;
-    void barrier() {
+    std::atomic<bool> aborted{false};
+    bool timed_out = false;  // (under mu) the abort came from a barrier's deadline
+    // false: the group was aborted (before or while this member waited)
+    bool barrier() {
         std::unique_lock<std::mutex> lk(mu);
+        if (aborted.load()) return false;
         const uint64_t gen = generation;
         if (++arrived == world) {
             arrived = 0;
             ++generation;
             cv.notify_all();
-        } else {
-            cv.wait(lk, [&] { return generation != gen; });
+            return true;
         }
+        auto pred = [&] { return generation != gen || aborted.load(); };
+        const double t = comm_timeout_s();
+        if (t > 0.0) {
+            if (!cv.wait_for(lk, std::chrono::duration<double>(t), pred)) {
+                timed_out = true;
+                aborted.store(true);
+                cv.notify_all();
+                return false;
+            }
+        } else {
+            cv.wait(lk, pred);
+        }
+        return generation != gen;
+    }
+    void abort() {
+        std::lock_guard<std::mutex> lk(mu);
+        aborted.store(true);
+        cv.notify_all();
+    }
+    // every member's bh_reset_bodies after an abort (no member waits: their calls have returned)
+    void reset() {
+        std::lock_guard<std::mutex> lk(mu);
+        if (!aborted.load()) return;
+        arrived = 0;
+        ++generation;
+        timed_out = false;
+        aborted.store(false);
     }
 };
 
@@ -138,6 +187,10 @@ struct bh_engine {
     uint32_t *mslot = nullptr;       // caller index -> slot of the victims
     int64_t dlog_cap = 0;
     bool heavy_possible = true;  // false once a step saw no heavy body (heavies never appear)
+    // the last build listed the heavy bodies in its order (heavy, count in scalars[14]): the merge
+    // rule that follows it needs no k_heavy pass (the pipelined step's second build)
+    bool heavy_ready = false;
+    bool heavy_dirty = false;  // scalars[14] may be nonzero (a list no merge rule consumed)
     bool merge_ran = false;      // the running bh_step call launched the merge rule
     std::vector<int64_t> removed;  // removals of the last bh_step call, ascending (BHA:519)
     void *pin = nullptr;  // pinned staging for small read-backs (coherent: kernels write it too)
@@ -304,7 +357,7 @@ struct bh_engine {
     // a multi handle's member 0) hands over positions, masses and the survivors' list indices of
     // the running call once its last merge rule is done (mid_*), before the last traversal
     std::thread step_thr;
-    bool async_running = false;
+    std::atomic<bool> async_running{false};
     int async_rc = 0;
     int64_t mid_n0 = 0;              // bodies before the running call
     bool mid_surv_done = false;      // the survivors were derived from the call's removals
@@ -360,6 +413,21 @@ struct bh_engine {
     std::vector<int64_t> coll_log;  // (api call, site, bytes, stream) per collective
     int64_t api_calls = 0;          // state-changing API calls made on this engine
 
+    // Failure of a multi-rank call (the reference's join always returns, BHA:408, 426): a rank
+    // whose call fails -- or that finds a peer failed, or waits past BH_COMM_TIMEOUT_S -- marks
+    // itself failed, aborts its in-process group / RCCL communicator (ncclCommAbort) so that no
+    // peer waits for it, and every state-changing call returns BH_E_COMM until bh_reset_bodies
+    std::atomic<bool> *abort_flag = nullptr;  // a multi-device handle's members: shared, set by
+                                              // any member that failed (multi.cpp)
+    bool comm_failed = false;
+    bool comm_lost = false;      // the RCCL communicator was aborted (a new one is needed)
+    std::string fail_msg;
+    int inject_coll = -1;        // bh_debug_inject(100 + k): fail before the k-th next collective
+    int inject_barrier = -1;     // bh_debug_inject(200 + k): ... before the k-th next group barrier
+    // progress, readable from any thread while a call runs (bh_progress: heartbeats)
+    std::atomic<int64_t> prog_api{0}, prog_coll{0};
+    std::atomic<int> prog_site{0}, prog_busy{0};
+
     std::string err;
 };
 
@@ -401,11 +469,126 @@ enum CollSite {
     COLL_VMAX = 7,      // every rank's drift speed bound (LET selection), after a drifting round
 };
 enum CollStream { CS_MAIN = 0, CS_COMM = 1 };
-void coll_log(bh_engine *e, int site, int64_t bytes, int stream) {
-    if (e->world <= 1 && !e->comm) return;
-    if (e->coll_log.size() >= ((size_t)1 << 22)) return;  // (bounded: 1 M entries)
+// Called before every collective: logs it, counts it for the heartbeat, and trips an injected
+// host-side failure (bh_debug_inject(100 + k)) -- the rank then returns before the collective its
+// peers have issued, exactly as a rank-local error would.
+int coll_log(bh_engine *e, int site, int64_t bytes, int stream) {
+    if (e->world <= 1 && !e->comm) return BH_OK;
+    if (e->inject_coll >= 0 && e->inject_coll-- == 0) {
+        e->err = "injected host-side failure before a collective (bh_debug_inject)";
+        return BH_E_COMM;
+    }
+    e->prog_coll.fetch_add(1);
+    e->prog_site.store(site);
+    if (e->coll_log.size() >= ((size_t)1 << 22)) return BH_OK;  // (bounded: 1 M entries)
     e->coll_log.insert(e->coll_log.end(), {e->api_calls, (int64_t)site, bytes, (int64_t)stream});
+    return BH_OK;
 }
+
+bool multi_rank(const bh_engine *e) { return (e->comm || e->group || e->comm_lost) && !e->solo; }
+
+bool peers_aborted(const bh_engine *e) {
+    return (e->group && e->group->aborted.load()) || (e->abort_flag && e->abort_flag->load());
+}
+
+// An in-process group's barrier, with its way out: false from an aborted group -> BH_E_COMM.
+int group_barrier(bh_engine *e) {
+    if (e->inject_barrier >= 0 && e->inject_barrier-- == 0) {
+        e->err = "injected host-side failure before a group barrier (bh_debug_inject)";
+        return BH_E_COMM;
+    }
+    if (!e->group->barrier()) {
+        std::lock_guard<std::mutex> lk(e->group->mu);
+        e->err = e->group->timed_out
+                     ? "group barrier: a peer did not arrive within BH_COMM_TIMEOUT_S"
+                     : "group barrier: aborted (a peer rank's call failed)";
+        return BH_E_COMM;
+    }
+    return BH_OK;
+}
+
+// Poll stream s until it is idle, at most `secs` seconds (0: forever).  hipErrorNotReady on expiry.
+hipError_t drain_stream(hipStream_t s, double secs) {
+    if (!s) return hipSuccess;
+    const auto t0 = std::chrono::steady_clock::now();
+    for (int spins = 0;; ++spins) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q != hipErrorNotReady) return q;
+        if (secs > 0.0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > secs)
+            return hipErrorNotReady;
+        if (spins < 2000) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+}
+
+// Abort this rank's RCCL communicator (its kernels waiting for peers exit) and let every stream
+// of the engine drain, bounded.  The engine keeps no communicator afterwards (comm_lost).
+void abort_comm(bh_engine *e) {
+    if (e->comm) {
+        (void)ncclCommAbort(e->comm);
+        e->comm = nullptr;
+        e->comm_lost = true;
+    }
+    for (hipStream_t s : {e->stream, e->stream2, e->comm_stream, e->pipe_stream, e->mir_stream})
+        (void)drain_stream(s, 30.0);
+}
+
+// A multi-rank call failed on this rank (rc != BH_OK): mark the engine failed and make sure no
+// peer waits for it -- abort the in-process group or the multi-device handle's members (the
+// flag every member's waits poll), and this rank's communicator.
+int fail_multi_rank(bh_engine *e, int rc) {
+    if (rc == BH_OK || !multi_rank(e)) return rc;
+    if (!e->comm_failed) e->fail_msg = e->err;
+    e->comm_failed = true;
+    if (e->group) e->group->abort();
+    if (e->abort_flag) e->abort_flag->store(true);
+    abort_comm(e);
+    return rc;
+}
+
+// Wait until stream s is idle.  Multi-rank engines poll: a collective whose peers never arrive
+// would block a plain hipStreamSynchronize forever.  With RCCL the wait ends -- the communicator
+// aborted, BH_E_COMM -- on an asynchronous RCCL error, when another member of the handle failed,
+// or after BH_COMM_TIMEOUT_S; an in-process group's device waits are on recorded events and
+// always end (its barriers carry the abort), so it only gets the deadline.
+int wait_stream(bh_engine *e, hipStream_t s) {
+    if (!multi_rank(e)) {
+        HIPCHK(e, hipStreamSynchronize(s));
+        return BH_OK;
+    }
+    const double limit = comm_timeout_s();
+    const auto t0 = std::chrono::steady_clock::now();
+    const char *why = nullptr;
+    for (int spins = 0;; ++spins) {
+        const hipError_t q = hipStreamQuery(s);
+        if (q == hipSuccess) return BH_OK;
+        if (q != hipErrorNotReady) {
+            e->err = std::string("hipStreamQuery: ") + hipGetErrorString(q);
+            return BH_E_DEVICE;
+        }
+        if (e->comm) {
+            ncclResult_t ar = ncclSuccess;
+            if (ncclCommGetAsyncError(e->comm, &ar) == ncclSuccess && ar != ncclSuccess &&
+                ar != ncclInProgress)
+                why = "RCCL reported an asynchronous error";
+            else if (e->abort_flag && e->abort_flag->load())
+                why = "another member of the handle failed";
+        }
+        if (!why && limit > 0.0 &&
+            std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > limit)
+            why = "timed out (BH_COMM_TIMEOUT_S) waiting for the device: a collective whose peers "
+                  "never arrived?";
+        if (why) break;
+        if (spins < 2000) std::this_thread::yield();
+        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+    }
+    e->err = std::string("wait for the device: ") + why;
+    abort_comm(e);
+    return BH_E_COMM;
+}
+
+#define SYNC(e, s) TRY(wait_stream((e), (s)))
 
 // Root cell (BHA:360-361) and the exact per-depth half-sizes (BHA:74).
 int make_geometry(const bh_params &p, Geometry &g, std::string &err) {
@@ -597,7 +780,7 @@ int mark(bh_engine *e, int phase, int weight = 1) {  // close the interval of `p
 
 int collect_timings(bh_engine *e) {
     if (!e->timings_pending) return BH_OK;
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    SYNC(e, e->stream);
     for (int k = 0; k < kPhases; ++k) e->phase_ms[k] = 0.0;
     e->trav_ms_sum = 0.0;
     e->trav_launches = 0;
@@ -646,9 +829,24 @@ int collect_timings(bh_engine *e) {
 // swap) for a traversal that permutes them as it kicks (KickArgs::perm).
 // carry: a call's last overlapped build, whose tree the next call uses -- its error flags go to
 // scalars[10] instead of the running call's scalars[1] (evaluate / bh_get_quads take them over)
-int build_into(bh_engine *e, hipStream_t s, bool overlap, bool keep_v = false, bool carry = false) {
+#ifndef BH_HEAVY_CARRY
+#define BH_HEAVY_CARRY 1  // the pipelined step's second build lists the heavy bodies (k_prep)
+#endif
+// heavy_list: k_prep lists the merge rule's heavy bodies in this build's order (the rule follows
+// the build before any other build: masses change only in the rule, BHA:518)
+int build_into(bh_engine *e, hipStream_t s, bool overlap, bool keep_v = false, bool carry = false,
+               bool heavy_list = false) {
     const int64_t n = e->n;
     TreeBuffers tb = tree_buffers(e);
+    if (heavy_list && e->heavy_dirty)  // (a list no rule consumed: a call that failed between)
+        HIPCHK(e, hipMemsetAsync(e->scalars + 14, 0, sizeof(uint32_t), s));
+    e->heavy_ready = heavy_list && n > 0;
+    if (e->heavy_ready) {
+        e->heavy_dirty = true;
+        tb.heavy = e->heavy;
+        tb.heavy_count = e->scalars + 14;
+        tb.heavy_thr = e->p.merge_max_mass;
+    }
     if (overlap) {
         tb.src.vx = tb.src.vy = nullptr;
         tb.nodes = e->nodes_alt;
@@ -948,7 +1146,7 @@ int gather_round(bh_engine *e, const GatherLayout &gl, int k, int W, int ev_roun
     const int64_t size = gl.off[k + 1] - gl.off[k];
     double *piece = e->a2 + W * (int64_t)e->world * gl.off[k];  // round k, rank 0
     if (size <= 0) return BH_OK;
-    coll_log(e, site, (int64_t)sizeof(double) * W * size * e->world, CS_COMM);
+    TRY(coll_log(e, site, (int64_t)sizeof(double) * W * size * e->world, CS_COMM));
     if (e->comm) {
         NCCLCHK(e, ncclAllGather(piece + W * e->rank * size, piece, (size_t)(W * size),
                                  ncclDouble, e->comm, e->comm_stream));
@@ -1009,7 +1207,7 @@ int sync_velocities(bh_engine *e) {
     const LetPieces pc{n, sub, e->world, e->rank, R, lanes};
     const GatherLayout gl = shard_layout(n, e->world);
     if (e->group) {  // peers are done reading our previous pieces
-        e->group->barrier();
+        TRY(group_barrier(e));
         for (bh_engine *peer : e->group->members)
             if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->gathered_ev, 0));
     }
@@ -1017,7 +1215,7 @@ int sync_velocities(bh_engine *e) {
     HIPCHK(e, hipGetLastError());
     HIPCHK(e, hipEventRecord(e->round_ev[0], e->stream));
     HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[0], 0));
-    if (e->group) e->group->barrier();
+    if (e->group) TRY(group_barrier(e));
     for (int k = 0; k < R; ++k) TRY(gather_round(e, gl, k, 2, k == 0 ? 0 : -1, COLL_VEL));
     HIPCHK(e, hipEventRecord(e->gathered_ev, e->comm_stream));
     HIPCHK(e, hipStreamWaitEvent(e->stream, e->gathered_ev, 0));
@@ -1039,7 +1237,7 @@ int wave_order_next(bh_engine *e, int slot, int64_t lanes, hipStream_t s);
 // member's.
 int exchange_tables(bh_engine *e, hipStream_t s) {
     const size_t tbytes = sizeof(LetCell) * (size_t)LET_TSTRIDE;
-    coll_log(e, COLL_TABLE, (int64_t)(tbytes * (size_t)e->world), CS_MAIN);
+    TRY(coll_log(e, COLL_TABLE, (int64_t)(tbytes * (size_t)e->world), CS_MAIN));
     if (e->comm) {
         NCCLCHK(e, ncclAllGather(e->L.table, e->L.tables, tbytes, ncclUint8, e->comm, s));
     } else if (e->solo) {  // own values first, the rest from the last full build
@@ -1053,7 +1251,7 @@ int exchange_tables(bh_engine *e, hipStream_t s) {
         e->pub_table = e->L.table;
         e->pub_table_ev = e->table_ev;
         HIPCHK(e, hipEventRecord(e->table_ev, s));
-        e->group->barrier();
+        TRY(group_barrier(e));
         for (int q = 0; q < e->world; ++q) {
             bh_engine *peer = e->group->members[q];
             if (peer != e) HIPCHK(e, hipStreamWaitEvent(s, peer->pub_table_ev, 0));
@@ -1068,7 +1266,7 @@ int exchange_tables(bh_engine *e, hipStream_t s) {
 // L.vmax[1 + rank], on the exchange stream behind the rounds (which it waited for): RCCL, or the
 // peers' words copied (in-process group).  A solo rank has no peers: its own word is the bound.
 int gather_vmax(bh_engine *e) {
-    coll_log(e, COLL_VMAX, (int64_t)sizeof(unsigned long long) * e->world, CS_COMM);
+    TRY(coll_log(e, COLL_VMAX, (int64_t)sizeof(unsigned long long) * e->world, CS_COMM));
     if (e->comm) {
         NCCLCHK(e, ncclAllGather(e->L.vmax, e->L.vmax + 1, 1, ncclUint64, e->comm,
                                  e->comm_stream));
@@ -1096,7 +1294,7 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
     const LetPieces pc{n, sub, e->world, e->rank, R, lanes};
     TRY(mark(e, -1));
     if (e->group) {  // peers are done reading our previous table and pieces
-        e->group->barrier();
+        TRY(group_barrier(e));
         for (bh_engine *peer : e->group->members)
             if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->gathered_ev, 0));
     }
@@ -1166,7 +1364,7 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
             uint32_t *h = static_cast<uint32_t *>(e->pin);
             HIPCHK(e, hipMemcpyAsync(h, e->L.selpos + let_sel_blocks(n), sizeof(uint32_t), hipMemcpyDeviceToHost,
                                      e->stream));
-            HIPCHK(e, hipStreamSynchronize(e->stream));
+            SYNC(e, e->stream);
             e->let_known = std::max<int64_t>(h[0], 1);
             S = std::min<int64_t>(n, let_capacity(e->let_known));  // padded above
         }
@@ -1218,7 +1416,7 @@ int evaluate_let(bh_engine *e, KickMode kick, bool *done) {
         TRY(wave_order_next(e, 1 + k, hi - lo, rs));
         HIPCHK(e, hipEventRecord(e->round_ev[k], rs));
         HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
-        if (e->group) e->group->barrier();
+        if (e->group) TRY(group_barrier(e));
         TRY(gather_round(e, gl, k, W, k, COLL_POS));
     }
     if (bound) TRY(gather_vmax(e));  // behind the last round, on the exchange stream
@@ -1388,7 +1586,7 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
                                                                          BH_SHARD_ROUNDS),
                                  e->stream));
     if (e->group) {  // a collective's implicit ordering: peers' copies of our last pieces done
-        e->group->barrier();
+        TRY(group_barrier(e));
         for (bh_engine *peer : e->group->members)
             if (peer != e) HIPCHK(e, hipStreamWaitEvent(e->stream, peer->gathered_ev, 0));
     }
@@ -1403,7 +1601,7 @@ int evaluate(bh_engine *e, uint32_t *visits, KickMode kick = KICK_NONE, bool *fu
         HIPCHK(e, hipGetLastError());
         HIPCHK(e, hipEventRecord(e->round_ev[k], rs));
         HIPCHK(e, hipStreamWaitEvent(e->comm_stream, e->round_ev[k], 0));
-        if (e->group) e->group->barrier();  // every member recorded round k
+        if (e->group) TRY(group_barrier(e));  // every member recorded round k
         TRY(gather_round(e, gl, k, 2, k, COLL_ACC));
     }
     TRY(mark(e, 1));
@@ -1417,7 +1615,7 @@ int check_tree_flags(bh_engine *e) {
     uint32_t flags = 0;
     HIPCHK(e, hipMemcpyAsync(&flags, e->scalars + 1, sizeof(uint32_t), hipMemcpyDeviceToHost,
                              e->stream));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    SYNC(e, e->stream);
     if (flags) {
         e->err = "jitter replay reached an unsupported geometry (body stayed inside a depth J+1 cell)";
         return BH_E_STATE;
@@ -1476,10 +1674,13 @@ int merge(bh_engine *e, hipStream_t s = nullptr, bool header_zeroed = false) {
     if (marks) TRY(mark(e, -1));
     TRY(merge_bufs(e));
     const double minD2 = e->p.merge_min_dist * e->p.merge_min_dist;  // BHA:468
+    uint32_t *hc = e->heavy_ready ? e->scalars + 14 : nullptr;  // listed by the last build
+    e->heavy_ready = false;
+    if (hc) e->heavy_dirty = false;  // (k_merge_replay clears the count)
     merge_candidates(e->n, e->st.x, e->st.y, e->st.m, e->st.cidx, e->p.merge_max_mass, minD2,
-                     e->heavy, e->box, e->box_cap, s, header_zeroed);
+                     e->heavy, e->box, e->box_cap, s, header_zeroed, hc);
     merge_replay(e->box, e->box_cap, e->st.m, e->st.cidx, e->scalars, e->dlog, e->rkeys, e->ridx,
-                 e->mbits, e->mslot, e->n, s);
+                 e->mbits, e->mslot, e->n, s, hc);
     HIPCHK(e, hipGetLastError());
     e->merge_ran = true;
     if (marks) TRY(mark(e, 3));
@@ -1511,7 +1712,7 @@ int finish_merges(bh_engine *e, uint32_t *overflow, uint32_t *tree_flags = nullp
     pack_readback(e->scalars, e->box, e->dlog, ahead, static_cast<uint32_t *>(e->pin_dev),
                   e->stream);
     HIPCHK(e, hipGetLastError());
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    SYNC(e, e->stream);
     if (tree_flags) *tree_flags = h[1];
     if (have_flags) *have_flags = true;
     const uint32_t nd = h[2];
@@ -1595,7 +1796,7 @@ int finish_merges(bh_engine *e, uint32_t *overflow, uint32_t *tree_flags = nullp
         std::swap(e->lt_x, e->alt.x);
         std::swap(e->lt_y, e->alt.y);
     }
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    SYNC(e, e->stream);
     return BH_OK;
 }
 
@@ -1661,20 +1862,20 @@ int restore(bh_engine *e) {
 int agree_let_flags(bh_engine *e, uint32_t ls[2], uint32_t *own_sub) {
     HIPCHK(e, hipMemcpy(ls, e->scalars + 4, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost));
     *own_sub = ls[1];
-    if (!e->solo) coll_log(e, COLL_FLAGS, 2 * sizeof(uint32_t), CS_MAIN);
+    if (!e->solo) TRY(coll_log(e, COLL_FLAGS, 2 * sizeof(uint32_t), CS_MAIN));
     if (e->comm) {
         NCCLCHK(e, ncclAllReduce(e->scalars + 4, e->scalars + 4, 2, ncclUint32, ncclMax, e->comm,
                                  e->stream));
         HIPCHK(e, hipMemcpyAsync(ls, e->scalars + 4, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost,
                                  e->stream));
-        HIPCHK(e, hipStreamSynchronize(e->stream));
+        SYNC(e, e->stream);
         return BH_OK;
     }
     if (!e->group) return BH_OK;  // solo: no peers
     // a member that cannot read a peer's flags must not decide alone: every member sees its
     // failure after the second barrier and all return an error together (none replays)
     e->agree_failed = false;  // (its previous value was read before this call's LET barriers)
-    e->group->barrier();      // every member's call is complete on the device
+    TRY(group_barrier(e));      // every member's call is complete on the device
     for (bh_engine *peer : e->group->members) {
         if (peer == e) continue;
         uint32_t q[2] = {0, 0};
@@ -1687,7 +1888,7 @@ int agree_let_flags(bh_engine *e, uint32_t ls[2], uint32_t *own_sub) {
         ls[0] = std::max(ls[0], q[0]);
         ls[1] = std::max(ls[1], q[1]);
     }
-    e->group->barrier();  // nobody clears its flags (a replay) before every member has read them
+    TRY(group_barrier(e));  // nobody clears its flags (a replay) before every member has read them
     bool failed = false;
     for (bh_engine *peer : e->group->members) failed = failed || peer->agree_failed;
     if (failed) {
@@ -1949,7 +2150,8 @@ int evaluate_pipelined(bh_engine *e, bool last) {
         e->lanes_age = 0;
     }
     e->lane_hold = true;
-    const int rc_b2 = build_into(e, s, false, true);  // velocities: permuted by the kick below
+    // velocities: permuted by the kick below; the heavy list for the merge rule that follows
+    const int rc_b2 = build_into(e, s, false, true, false, merging && BH_HEAVY_CARRY);
     e->lane_hold = false;
     TRY(rc_b2);
     TRY(mark(e, 0));
@@ -2330,7 +2532,7 @@ static int agree_settings(bh_engine *e) {
     // happened locally, so a local failure cannot leave the peers waiting in a collective
     double *d = static_cast<double *>(e->scratch);
     double lo[K], hi[K];
-    coll_log(e, COLL_SETTINGS, (int64_t)sizeof(double) * 2 * K, CS_MAIN);
+    TRY(coll_log(e, COLL_SETTINGS, (int64_t)sizeof(double) * 2 * K, CS_MAIN));
     ncclResult_t nr = ncclSuccess;
     if (!d || e->scratch_bytes < sizeof(double) * 3 * K) {
         e->err = "agree_settings: no device scratch";
@@ -2344,7 +2546,7 @@ static int agree_settings(bh_engine *e) {
     nr = n1 != ncclSuccess ? n1 : n2;
     hipError_t h2 = hipMemcpyAsync(lo, d + K, sizeof(lo), hipMemcpyDeviceToHost, e->stream);
     if (h2 == hipSuccess) h2 = hipMemcpyAsync(hi, d + 2 * K, sizeof(hi), hipMemcpyDeviceToHost, e->stream);
-    if (h2 == hipSuccess) h2 = hipStreamSynchronize(e->stream);
+    if (h2 == hipSuccess && wait_stream(e, e->stream) != BH_OK) return BH_E_COMM;  // (bounded)
     if (hr == hipSuccess) hr = h2;
     if (nr != ncclSuccess) {
         e->err = std::string("agree_settings: ") + ncclGetErrorString(nr);
@@ -2391,6 +2593,22 @@ int bh::member_agree(bh_engine *e) {
     if (!e->comm) return BH_OK;
     HIPCHK(e, hipSetDevice(e->device));  // (a pool thread: RCCL calls on the member's device)
     return agree_settings(e);
+}
+
+void bh::member_set_abort(bh_engine *e, std::atomic<bool> *flag) { e->abort_flag = flag; }
+
+void bh::member_drop_comm(bh_engine *e) {
+    if (e->comm) {
+        (void)hipSetDevice(e->device);
+        (void)ncclCommAbort(e->comm);
+        e->comm = nullptr;
+        e->comm_lost = true;
+    }
+}
+
+void bh::member_set_comm(bh_engine *e, void *comm) {
+    e->comm = static_cast<ncclComm_t>(comm);
+    e->comm_lost = false;
 }
 
 // (comm: an RCCL communicator made in this process; on failure it stays the caller's)
@@ -2530,8 +2748,24 @@ bh_engine *multi_active0(const bh_engine *e) { return e->use_one ? e->one : mult
             return BH_E_STATE;                                                                 \
     } while (0)
 
+// A rank of a decomposition whose last call failed -- here or on a peer (the group / handle was
+// aborted) -- refuses the calls that use the replica or issue collectives until bh_reset_bodies:
+// every rank refuses alike, so none waits in a collective the others never issue.
+namespace {
+int comm_refused(bh_engine *e) {
+    if (!multi_rank(e) || (!e->comm_failed && !peers_aborted(e))) return BH_OK;
+    e->err = "a previous call of this multi-rank engine failed (" +
+             (e->comm_failed ? e->fail_msg : std::string("on a peer rank")) +
+             "); bh_reset_bodies before the next call";
+    return BH_E_COMM;
+}
+}  // namespace
+#define COMM_GUARD(e) TRY(comm_refused(e))
+
 // =========================================================================================
 extern "C" {
+
+static int last_removed(const bh_engine *e, int64_t *idx, int64_t cap, int64_t *n_out);
 
 void bh_default_params(bh_params *p) {
     if (p) set_defaults(p);
@@ -2695,8 +2929,13 @@ void bh_destroy(bh_engine *e) {
         return;
     }
     (void)hipSetDevice(e->device);
-    if (e->stream) (void)hipStreamSynchronize(e->stream);
-    if (e->comm_stream) (void)hipStreamSynchronize(e->comm_stream);
+    // (a rank of a decomposition waits for its streams at most BH_COMM_TIMEOUT_S: a collective
+    // whose peers are gone never completes; after a failed call its communicator is aborted --
+    // ncclCommDestroy would wait for the peers)
+    const double drain_s = multi_rank(e) ? std::max(comm_timeout_s(), 1.0) : 0.0;
+    if (e->comm && (e->comm_failed || peers_aborted(e))) abort_comm(e);
+    (void)drain_stream(e->stream, drain_s);
+    if (e->comm && drain_stream(e->comm_stream, drain_s) != hipSuccess) abort_comm(e);
     if (e->comm) (void)ncclCommDestroy(e->comm);
     if (e->group && e->rank < (int)e->group->members.size() && e->group->members[e->rank] == e)
         e->group->members[e->rank] = nullptr;
@@ -2799,7 +3038,7 @@ int bh_set_params(bh_engine *e, const bh_params *p) {
         e->lanes_valid = e->lr_pending = e->lr_ready = false;
         e->inv_valid = false;
         if (g.J != e->J_alloc) {  // tree workspace sized for another depth; the state stays
-            HIPCHK(e, hipStreamSynchronize(e->stream));
+            SYNC(e, e->stream);
             TRY(ensure_capacity(e, e->n));
         }
     }
@@ -2837,10 +3076,27 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
         }
         e->use_one = one;
     }
+    if (e->multi) TRY(multi_repair(e->multi, e));  // after a failed call: fresh communicators
     MULTI_ALL(e, bh_reset_bodies(m_, n, x, y, vx, vy, m));
-    ++e->api_calls;
+    e->prog_api.store(++e->api_calls);
     HIPCHK(e, hipSetDevice(e->device));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    if (multi_rank(e) && (e->comm_failed || e->comm_lost || peers_aborted(e))) {
+        // the way back from a failed call: every stream idle, the group's barriers usable again
+        if (e->comm_lost) {
+            e->err = "bh_reset_bodies: the RCCL communicator was aborted after a failed call; "
+                     "create the engine anew";
+            return BH_E_COMM;
+        }
+        for (hipStream_t s : {e->stream, e->stream2, e->comm_stream, e->pipe_stream, e->mir_stream})
+            if (drain_stream(s, 30.0) != hipSuccess) {
+                e->err = "bh_reset_bodies: a stream did not drain after the failed call";
+                return BH_E_DEVICE;
+            }
+        e->comm_failed = false;
+        e->fail_msg.clear();
+        if (e->group) e->group->reset();
+    }
+    SYNC(e, e->stream);
     TRY(drop_carried_flags(e));
     e->vel_perm = nullptr;  // (the state is replaced)
     TRY(ensure_capacity(e, n));
@@ -2853,7 +3109,7 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
         iota_u32(e->st.cidx, n, e->stream);
         HIPCHK(e, hipGetLastError());
     }
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    SYNC(e, e->stream);
     e->n = n;
     e->heavy_possible = true;
     e->removed.clear();
@@ -2875,6 +3131,7 @@ int bh_reset_bodies(bh_engine *e, int64_t n, const double *x, const double *y, c
 }
 
 static int step_call(bh_engine *e, int32_t k);
+static int step_call_rank(bh_engine *e, int32_t k);
 
 int bh_step(bh_engine *e, int32_t k) {
     if (!e || k < 0) return BH_E_INVALID;
@@ -2882,10 +3139,20 @@ int bh_step(bh_engine *e, int32_t k) {
     return step_call(e, k);
 }
 
-// bh_step's work (bh_step_begin's thread calls it directly)
+// bh_step's work (bh_step_begin's thread calls it directly): a multi-device handle's members, or
+// this engine's steps -- a rank of a decomposition refuses them after a failed call, and a call
+// that fails on it aborts its peers' waits (fail_multi_rank)
 static int step_call(bh_engine *e, int32_t k) {
     MULTI_ALL(e, bh_step(m_, k));  // every GPU's share of every step, joined (BHA:374-395, 408)
-    ++e->api_calls;
+    COMM_GUARD(e);
+    e->prog_busy.store(1);
+    const int rc = fail_multi_rank(e, step_call_rank(e, k));
+    e->prog_busy.store(0);
+    return rc;
+}
+
+static int step_call_rank(bh_engine *e, int32_t k) {
+    e->prog_api.store(++e->api_calls);
     HIPCHK(e, hipSetDevice(e->device));
     const bool may_merge = k > 0 && e->n > 1 && e->p.merge_min_dist > 0.0 && e->heavy_possible;
     // a multi-rank call with LET builds may have to be replayed with a larger subset capacity
@@ -2922,7 +3189,7 @@ static int step_call(bh_engine *e, int32_t k) {
         if (e->mir_launched) HIPCHK(e, hipStreamWaitEvent(e->stream, e->mir_ev2, 0));
         // (one GPU: no wait here -- the merge bookkeeping's read-back below, or the tree flags'
         // when nothing merged, is queued behind the steps and waited for once)
-        if (may_let) HIPCHK(e, hipStreamSynchronize(e->stream));
+        if (may_let) SYNC(e, e->stream);
         if (may_let) {  // LET subset sizes of this call: [4] some rank overflowed, [5] largest
             uint32_t ls[2] = {0, 0};
             // [4] can be set after the cell tables were exchanged (k_let_guard, k_let_w): on one
@@ -3057,10 +3324,10 @@ int bh_step_positions(bh_engine *e, const double **x, const double **y, const do
         if (!e->mid_surv_done) {  // the survivors from the call's removals: a mirror written
             // after the call's compaction numbers its bodies in the list after the call
             int64_t nr = 0;
-            int rc = bh_last_removed(e, nullptr, 0, &nr);
+            int rc = last_removed(e, nullptr, 0, &nr);
             if (rc != BH_OK && rc != BH_E_CAPACITY) return rc;
             std::vector<int64_t> rem((size_t)std::max<int64_t>(nr, 1));
-            TRY(bh_last_removed(e, rem.data(), nr, &nr));
+            TRY(last_removed(e, rem.data(), nr, &nr));
             uint32_t *sv = t->mir_idx + MIRROR_HDR;
             int64_t j = 0, r = 0;
             for (int64_t i = 0; i < e->mid_n0; ++i) {
@@ -3098,7 +3365,12 @@ int bh_step_end(bh_engine *e) {
     return e->async_rc;
 }
 
-int64_t bh_num_bodies(const bh_engine *e) { return e ? MULTI_M0(e)->n : -1; }
+int64_t bh_num_bodies(const bh_engine *e) {
+    if (!e) return -1;
+    if (e->async_running && std::this_thread::get_id() != e->step_thr.get_id())
+        return -1;  // (a call begun by bh_step_begin writes n: ask after bh_step_end)
+    return MULTI_M0(e)->n;
+}
 
 int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, double *m,
                   int64_t cap, int64_t *n_out) {
@@ -3109,6 +3381,7 @@ int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, do
         if (rc != BH_OK) e->err = bh_last_error(MULTI_M0(e));
         return rc;
     }
+    COMM_GUARD(e);  // (a failed call's replica is not the reference's state)
     if (n_out) *n_out = e->n;
     if (cap < e->n) return BH_E_CAPACITY;
     HIPCHK(e, hipSetDevice(e->device));
@@ -3126,7 +3399,7 @@ int bh_get_bodies(bh_engine *e, double *x, double *y, double *vx, double *vy, do
                 HIPCHK(e, hipMemcpyAsync(dst[k], stage[k], sizeof(double) * n,
                                          hipMemcpyDeviceToHost, e->stream));
     }
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    SYNC(e, e->stream);
     return BH_OK;
 }
 
@@ -3142,7 +3415,7 @@ int bh_set_mirror(bh_engine *e, int enabled) {
     HIPCHK(e, hipSetDevice(e->device));
     e->mirror_on = enabled != 0;
     if (e->mirror_on && enabled != e->mir_nbuf) {  // another buffer count: made anew
-        if (e->mir_stream) HIPCHK(e, hipStreamSynchronize(e->mir_stream));
+        if (e->mir_stream) SYNC(e, e->mir_stream);
         e->mir_nbuf = enabled;
         e->mir_cap = 0;
         e->mir_fresh = false;
@@ -3160,6 +3433,7 @@ int bh_map_bodies(bh_engine *e, const double **x, const double **y, const double
         if (rc != BH_OK) e->err = bh_last_error(MULTI_M0(e));
         return rc;
     }
+    COMM_GUARD(e);
     HIPCHK(e, hipSetDevice(e->device));
     if (!e->mir_fresh || e->mir_cap < e->n) {  // not written by the last call: copy out now
         TRY(materialize_positions(e));
@@ -3182,6 +3456,8 @@ int bh_map_bodies(bh_engine *e, const double **x, const double **y, const double
     return BH_OK;
 }
 
+static int compute_accelerations_rank(bh_engine *e, double *ax, double *ay, int64_t *visits);
+
 int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visits) {
     if (!e) return BH_E_INVALID;
     ASYNC_GUARD(e);
@@ -3196,7 +3472,12 @@ int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visi
                                               !visits ? nullptr
                                                       : r_ == 0 ? visits : vis[(size_t)r_].data()));
     }
-    ++e->api_calls;
+    COMM_GUARD(e);
+    return fail_multi_rank(e, compute_accelerations_rank(e, ax, ay, visits));
+}
+
+static int compute_accelerations_rank(bh_engine *e, double *ax, double *ay, int64_t *visits) {
+    e->prog_api.store(++e->api_calls);
     HIPCHK(e, hipSetDevice(e->device));
     const int64_t n = e->n;
     e->ev_used = 0;
@@ -3208,7 +3489,7 @@ int bh_compute_accelerations(bh_engine *e, double *ax, double *ay, int64_t *visi
         scatter_acc_to_caller(n, e->st.cidx, e->a2, e->ax, e->ay, e->stream, e->a2_lanes,
                               e->a2_layout);
         HIPCHK(e, hipGetLastError());
-        HIPCHK(e, hipStreamSynchronize(e->stream));
+        SYNC(e, e->stream);
         TRY(check_tree_flags(e));
         if (ax) HIPCHK(e, hipMemcpy(ax, e->ax, sizeof(double) * n, hipMemcpyDeviceToHost));
         if (ay) HIPCHK(e, hipMemcpy(ay, e->ay, sizeof(double) * n, hipMemcpyDeviceToHost));
@@ -3249,18 +3530,22 @@ int bh_get_quads(bh_engine *e, double *cx, double *cy, double *h, int64_t cap, i
     ASYNC_GUARD(e);
     if (e->multi) {  // every member builds getTreeForDebug's tree (the same jitter in every
                      // replica); member 0 walks it
-        const int rc = multi_fan(e, [](bh_engine *m, int) { return quads_prepare(m); }, false);
+        const int rc = multi_fan(e, [](bh_engine *m, int) {
+            TRY(comm_refused(m));
+            return fail_multi_rank(m, quads_prepare(m));
+        }, false);
         if (rc != BH_OK) return rc;
         const int rc0 = bh_get_quads(MULTI_M0(e), cx, cy, h, cap, n_out);
         if (rc0 != BH_OK) e->err = bh_last_error(MULTI_M0(e));
         return rc0;
     }
-    TRY(quads_prepare(e));
+    COMM_GUARD(e);
+    TRY(fail_multi_rank(e, quads_prepare(e)));
     const int64_t n = e->n;
     std::vector<uint64_t> keys((size_t)n);
     std::vector<int8_t> cpl((size_t)n);
     std::vector<uint32_t> base((size_t)n + 1);
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    SYNC(e, e->stream);
     // lastTree kept aside by a pipelined last step, or the tree in the build buffers
     const bool aside = e->tree_valid && e->lt_aside;
     if (n > 0) {
@@ -3282,6 +3567,12 @@ int bh_get_quads(bh_engine *e, double *cx, double *cy, double *h, int64_t cap, i
 
 int bh_last_removed(const bh_engine *e, int64_t *idx, int64_t cap, int64_t *n_out) {
     if (!e || cap < 0 || (cap > 0 && !idx)) return BH_E_INVALID;
+    // (a call begun by bh_step_begin writes the log: read it after bh_step_end)
+    if (e->async_running && std::this_thread::get_id() != e->step_thr.get_id()) return BH_E_STATE;
+    return last_removed(e, idx, cap, n_out);
+}
+
+static int last_removed(const bh_engine *e, int64_t *idx, int64_t cap, int64_t *n_out) {
     e = MULTI_M0(e);
     // caller indices are not renumbered inside a call, so the log is already relative to the
     // list before the call
@@ -3364,6 +3655,7 @@ int bh_let_stats(const bh_engine *e, int64_t *out4) {
 
 int bh_set_profiling(bh_engine *e, int enabled) {
     if (!e) return BH_E_INVALID;
+    ASYNC_GUARD(e);
     MULTI_BOTH(e, bh_set_profiling(m_, enabled));
     e->profiling = enabled != 0;
     return BH_OK;
@@ -3401,9 +3693,10 @@ int bh_selftest_fast_math(int device, int64_t n, uint64_t seed, int64_t *mismatc
 
 int bh_synchronize(bh_engine *e) {
     if (!e) return BH_E_INVALID;
+    ASYNC_GUARD(e);
     MULTI_ALL(e, bh_synchronize(m_));
     HIPCHK(e, hipSetDevice(e->device));
-    HIPCHK(e, hipStreamSynchronize(e->stream));
+    SYNC(e, e->stream);
     return BH_OK;
 }
 
@@ -3423,13 +3716,35 @@ int bh_comm_ranks(const bh_engine *e, int32_t *nranks, int32_t *rank) {
 
 int bh_debug_inject(bh_engine *e, int what) {
     if (!e) return BH_E_INVALID;
+    ASYNC_GUARD(e);
     MULTI_ALL(e, bh_debug_inject(m_, what));  // (one member alone: bh_multi_member)
-    if (what < 1) {
+    if (what < 1 || what >= 300) {
         e->err = "bh_debug_inject: unknown fault";
         return BH_E_INVALID;
     }
+    if (what == 99) {  // the carried tree (the next call's first) raises its error flag now
+        if (!e->carried_flags || !e->prebuilt) {
+            e->err = "bh_debug_inject(99): no tree carried to the next call";
+            return BH_E_STATE;
+        }
+        HIPCHK(e, hipMemsetAsync(e->scalars + 10, 1, sizeof(uint32_t), e->stream));
+        return BH_OK;
+    }
     if (what == 1) e->inject_guard = true;
+    else if (what >= 200) e->inject_barrier = what - 200;
+    else if (what >= 100) e->inject_coll = what - 100;
     else e->inject_build = what - 2;
+    return BH_OK;
+}
+
+int bh_progress(const bh_engine *e, int64_t *out4) {
+    if (!e || !out4) return BH_E_INVALID;
+    e = MULTI_M0(e);  // (a member's own: bh_multi_member)
+    out4[0] = e->prog_api.load();
+    out4[1] = e->prog_coll.load();
+    out4[2] = e->prog_site.load();
+    const bool failed = e->comm_failed || (multi_rank(e) && peers_aborted(e));  // (will refuse)
+    out4[3] = (e->prog_busy.load() ? 1 : 0) | (failed ? 2 : 0) | (e->comm_lost ? 4 : 0);
     return BH_OK;
 }
 
@@ -3457,6 +3772,7 @@ int bh_collective_log(const bh_engine *e, int64_t *out4, int64_t cap, int64_t *n
 
 int bh_collective_log_clear(bh_engine *e) {
     if (!e) return BH_E_INVALID;
+    ASYNC_GUARD(e);
     MULTI_BOTH(e, bh_collective_log_clear(m_));
     e->coll_log.clear();
     return BH_OK;

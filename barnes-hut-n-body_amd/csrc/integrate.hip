@@ -195,17 +195,22 @@ __global__ __launch_bounds__(TB) void k_heavy(int64_t n, const double *__restric
 
 // BHA:493-501: for every heavy body h and every live body j != h: dx*dx + dy*dy < minD2 with
 // dx = bj.x - bi.x.  Pairs are appended in any order; the replay sorts them.
+// heavy_count (nullable): the heavy list was made by the build (k_prep); its count is copied to
+// the header, which the host reads (finish_merges: no heavy body left -> the rule is skipped)
 __global__ __launch_bounds__(TB) void k_candidates(int64_t n, const double *__restrict__ x,
                                                    const double *__restrict__ y,
                                                    const double *__restrict__ m,
                                                    const uint32_t *__restrict__ cidx,
                                                    const uint32_t *__restrict__ heavy,
-                                                   double minD2, MergePair *box, uint32_t cap) {
+                                                   double minD2, MergePair *box, uint32_t cap,
+                                                   const uint32_t *__restrict__ heavy_count) {
     chain_prio();
     int64_t j = (int64_t)blockIdx.x * TB + threadIdx.x;
     MergeHeader *hdr = reinterpret_cast<MergeHeader *>(box);
     const uint32_t H = __builtin_amdgcn_readfirstlane(
-        __hip_atomic_load(&hdr->heavies, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        heavy_count ? *heavy_count
+                    : __hip_atomic_load(&hdr->heavies, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+    if (heavy_count && j == 0) hdr->heavies = H;
     if (j >= n || H == 0) return;
     const uint32_t cj = cidx[j];
     if (cj & CIDX_DEAD) return;
@@ -409,8 +414,11 @@ __global__ __launch_bounds__(REPLAY_TB) void k_merge_replay(const MergePair *__r
                                                             uint32_t *cidx, uint32_t *scal,
                                                             uint32_t *dlog, uint64_t *skeys,
                                                             uint32_t *sidx, uint32_t *bits,
-                                                            uint32_t *slot_of, int key_bits) {
+                                                            uint32_t *slot_of, int key_bits,
+                                                            uint32_t *heavy_count) {
     chain_prio();
+    // (k_candidates, before this kernel on the stream, has read the build's heavy-list count)
+    if (heavy_count && threadIdx.x == 0) *heavy_count = 0u;
     __shared__ uint64_t lk[REPLAY_LDS];
     __shared__ uint32_t li[REPLAY_LDS];
     __shared__ uint32_t hkey[REPLAY_HASH], hcidx[REPLAY_HASH];
@@ -783,21 +791,23 @@ void scatter_acc_to_caller(int64_t n, const uint32_t *cidx, const double *a2, do
 
 void merge_candidates(int64_t n, const double *x, const double *y, const double *m,
                       const uint32_t *cidx, double thr, double minD2, uint32_t *heavy,
-                      MergePair *box, uint32_t cap, hipStream_t s, bool header_zeroed) {
+                      MergePair *box, uint32_t cap, hipStream_t s, bool header_zeroed,
+                      const uint32_t *heavy_count) {
     if (!header_zeroed) (void)hipMemsetAsync(box, 0, sizeof(MergeHeader), s);
     if (n <= 0) return;
     MergeHeader *hdr = reinterpret_cast<MergeHeader *>(box);
-    k_heavy<<<grid_for(n), TB, 0, s>>>(n, m, cidx, thr, heavy, hdr);
-    k_candidates<<<grid_for(n), TB, 0, s>>>(n, x, y, m, cidx, heavy, minD2, box, cap);
+    if (!heavy_count) k_heavy<<<grid_for(n), TB, 0, s>>>(n, m, cidx, thr, heavy, hdr);
+    k_candidates<<<grid_for(n), TB, 0, s>>>(n, x, y, m, cidx, heavy, minD2, box, cap,
+                                            heavy_count);
 }
 
 void merge_replay(const MergePair *box, uint32_t cap, double *m, uint32_t *cidx, uint32_t *scal,
                   uint32_t *dlog, uint64_t *skeys, uint32_t *sidx, uint32_t *bits,
-                  uint32_t *slot_of, int64_t n, hipStream_t s) {
+                  uint32_t *slot_of, int64_t n, hipStream_t s, uint32_t *heavy_count) {
     int key_bits = 1;  // caller indices are < n
     while (key_bits < 32 && (int64_t(1) << key_bits) < n) ++key_bits;
     k_merge_replay<<<1, REPLAY_TB, 0, s>>>(box, cap, m, cidx, scal, dlog, skeys, sidx, bits,
-                                           slot_of, key_bits);
+                                           slot_of, key_bits, heavy_count);
 }
 
 size_t compact_scratch_bytes(int64_t n) {

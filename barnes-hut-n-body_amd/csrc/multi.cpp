@@ -10,6 +10,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
 #include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
@@ -31,8 +32,14 @@ namespace bh {
 struct Multi {
     int world = 0;
     std::vector<bh_engine *> members;
+    std::vector<int> devices;
     bh_local_group *group = nullptr;  // copy exchange (repeated devices / BH_MULTI_EXCHANGE=copy)
     bool rccl = false;
+    // set by a member whose call failed: every member's waits poll it (engine.cpp wait_stream)
+    // and every member refuses further calls until the handle's bh_reset_bodies (multi_repair)
+    std::atomic<bool> abort{false};
+    std::atomic<bool> busy{false};  // run() is not reentrant: a second caller gets kBusy
+    static constexpr int kBusy = 1;
     // the worker pool: member r > 0 runs on threads[r - 1]; member 0 on the caller's thread
     std::vector<std::thread> threads;
     std::mutex mu;
@@ -62,6 +69,8 @@ struct Multi {
     }
 
     int run(const std::function<int(bh_engine *, int)> &fn) {
+        bool idle = false;
+        if (!busy.compare_exchange_strong(idle, true)) return kBusy;
         {
             std::lock_guard<std::mutex> lk(mu);
             task = &fn;
@@ -75,6 +84,7 @@ struct Multi {
         done.wait(lk, [&] { return pending == 0; });
         rc[0] = r0;
         task = nullptr;
+        busy.store(false);
         for (int v : rc)
             if (v != BH_OK) return v;
         return BH_OK;
@@ -83,6 +93,10 @@ struct Multi {
 
 int multi_all(Multi *mu, bh_engine *facade, const std::function<int(bh_engine *, int)> &fn) {
     const int rc = mu->run(fn);
+    if (rc == Multi::kBusy) {
+        set_error(facade, "another call of this handle is running on another thread");
+        return BH_E_STATE;
+    }
     if (rc != BH_OK) {
         for (int r = 0; r < mu->world; ++r)
             if (mu->rc[(size_t)r] != BH_OK) {
@@ -100,6 +114,30 @@ bh_engine *multi_member(const Multi *mu, int rank) {
 }
 
 int multi_world(const Multi *mu) { return mu ? mu->world : 1; }
+
+// bh_reset_bodies of the handle after a failed call: the members' RCCL communicators -- one of
+// them aborted, the others in an unknown state -- are all aborted and made anew (the members'
+// streams are drained by their own resets), and the abort flag is cleared; the in-process group
+// is reset by the members' own resets.
+int multi_repair(Multi *mu, bh_engine *facade) {
+    if (!mu || !mu->abort.load()) return BH_OK;
+    if (mu->rccl) {
+        for (bh_engine *m : mu->members) member_drop_comm(m);
+        std::vector<ncclComm_t> comms((size_t)mu->world, nullptr);
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        const ncclResult_t nr = ncclCommInitAll(comms.data(), mu->world, mu->devices.data());
+        (void)hipSetDevice(cur);
+        if (nr != ncclSuccess) {
+            set_error(facade, std::string("bh_reset_bodies: ncclCommInitAll: ") +
+                                  ncclGetErrorString(nr));
+            return BH_E_COMM;
+        }
+        for (int r = 0; r < mu->world; ++r) member_set_comm(mu->members[(size_t)r], comms[(size_t)r]);
+    }
+    mu->abort.store(false);
+    return BH_OK;
+}
 
 void multi_destroy(Multi *mu) {
     if (!mu) return;
@@ -147,6 +185,13 @@ int make_multi(const bh_params *p, const std::vector<int> &dev, bh_engine **out)
         return rc;
     };
     std::vector<ncclComm_t> comms;
+    int cur_dev = 0;
+    (void)hipGetDevice(&cur_dev);  // (the peer loop sets devices: the caller's is restored)
+    struct Restore {
+        int d;
+        ~Restore() { (void)hipSetDevice(d); }
+    } restore{cur_dev};
+    mu->devices = dev;
     if (copy) {
         int rc = bh_local_group_create(world, &mu->group);
         if (rc != BH_OK) return fail(rc, "bh_local_group_create failed");
@@ -184,6 +229,7 @@ int make_multi(const bh_params *p, const std::vector<int> &dev, bh_engine **out)
                                 std::to_string(dev[(size_t)r]) + " could not be created");
         }
         mu->members[(size_t)r] = m;
+        member_set_abort(m, &mu->abort);
     }
     for (int r = 1; r < world; ++r) mu->threads.emplace_back([mu, r] { mu->worker(r); });
     bh_engine *f = nullptr;

@@ -10,6 +10,7 @@
 // replica is complete at the API boundary).
 #pragma once
 
+#include <atomic>
 #include <functional>
 
 #include "bh_engine.h"
@@ -24,6 +25,8 @@ int multi_all(Multi *mu, bh_engine *facade, const std::function<int(bh_engine *,
 bh_engine *multi_member(const Multi *mu, int rank);
 int multi_world(const Multi *mu);
 void multi_destroy(Multi *mu);  // destroys the members, joins the threads
+// bh_reset_bodies after a failed call: fresh RCCL communicators for every member, abort cleared
+int multi_repair(Multi *mu, bh_engine *facade);
 
 // engine.cpp: the pieces a multi-device handle is made of
 int facade_create(const bh_params *p, Multi *mu, bh_engine **out);
@@ -33,6 +36,11 @@ int member_create(const bh_params *p, int device, int rank, int world, void *com
                   bh_local_group *group, bh_engine **out);
 // the per-process settings check of bh_create_dist (a collective: every member at once)
 int member_agree(bh_engine *e);
+// the handle's abort flag, which the member's waits poll (a failed peer ends them)
+void member_set_abort(bh_engine *e, std::atomic<bool> *flag);
+// after a failed call: the member's communicator aborted (if still alive), then a new one
+void member_drop_comm(bh_engine *e);
+void member_set_comm(bh_engine *e, void *comm);
 // getTreeForDebug's tree on a member (the first half of bh_get_quads: every rank builds it, so
 // every replica takes the same jitter); the walk is member 0's
 int quads_prepare(bh_engine *e);

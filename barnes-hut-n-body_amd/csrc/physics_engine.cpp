@@ -145,7 +145,9 @@ void PhysicsEngine::step() {
         throw;
     }
     if (edited) {
-        check(bh_step_end(eng_));
+        // (that step ran on the state before the edit: its result -- and an error it met, e.g. on
+        // the tree the previous call left, whose flags it took over -- is replaced by the upload)
+        (void)bh_step_end(eng_);
         pushBodies();
         check(bh_step(eng_, 1));
         pullBodies(true);

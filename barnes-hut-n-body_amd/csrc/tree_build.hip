@@ -419,15 +419,20 @@ __global__ __launch_bounds__(TB) void k_key_fixup(int64_t n, int J,
     key_fixup((int64_t)blockIdx.x * TB + threadIdx.x, n, J, keys32_s, keys_s, perm);
 }
 
+struct HeavyList {  // TreeBuffers::heavy (null list: not wanted)
+    uint32_t *list, *count;
+    double thr;
+};
+
 // k_prep's body for one sorted body a < n: the state gathered into the new order, the splitters,
-// the old -> new slot map, c(a) and the node count (returned)
+// the old -> new slot map, c(a) and the node count (returned); the heavy list
 __device__ __forceinline__ uint32_t prep_one(int64_t a, int64_t n, int J,
                                              const uint64_t *__restrict__ keys_s,
                                              const uint32_t *__restrict__ perm, BodyState src,
                                              BodyState dst, int8_t *__restrict__ cpl,
                                              uint32_t *__restrict__ cnt,
                                              uint64_t *__restrict__ spl,
-                                             uint32_t *__restrict__ inv) {
+                                             uint32_t *__restrict__ inv, const HeavyList &hl) {
     const uint64_t SENT = sentinel_key(J);
     uint64_t k = keys_s[a];
     uint32_t i = perm[a];  // nearly the identity: the state is kept in the last Morton order
@@ -440,8 +445,13 @@ __device__ __forceinline__ uint32_t prep_one(int64_t a, int64_t n, int J,
     // only the replicated slot in vx (LET)
     if (src.vx) dst.vx[a] = src.vx[i];
     if (src.vy) dst.vy[a] = src.vy[i];
-    dst.m[a] = src.m[i];
-    dst.cidx[a] = src.cidx[i];
+    const double mi = src.m[i];
+    const uint32_t ci = src.cidx[i];
+    dst.m[a] = mi;
+    dst.cidx[a] = ci;
+    // the merge rule's heavy bodies in this order (k_heavy's test, BHA:474): masses change only in
+    // the merge rule, so the list stays right until the rule that follows this build has run
+    if (hl.list && mi > hl.thr && !(ci & CIDX_DEAD)) hl.list[atomicAdd(hl.count, 1u)] = (uint32_t)a;
     int c_cur = -1, c_prev = -1;
     if (k != SENT) {
         if (a + 1 < n) {
@@ -477,12 +487,12 @@ __global__ __launch_bounds__(TB) void k_prep(int64_t n, int J, const uint64_t *_
                                              uint32_t *__restrict__ cnt,
                                              uint64_t *__restrict__ spl,
                                              uint32_t *__restrict__ inv,
-                                             uint32_t *__restrict__ tsum) {
+                                             uint32_t *__restrict__ tsum, HeavyList hl) {
     chain_prio();
     const uint32_t tile = xcd_block();
     const int64_t a = (int64_t)tile * TB + threadIdx.x;
     uint32_t c = 0;
-    if (a < n) c = prep_one(a, n, J, keys_s, perm, src, dst, cpl, cnt, spl, inv);
+    if (a < n) c = prep_one(a, n, J, keys_s, perm, src, dst, cpl, cnt, spl, inv, hl);
     else if (a == n) cnt[n] = 0;
     if (tsum) {  // the tile's count sum for k_base_scan
         __shared__ uint32_t s_w[TB / 64];
@@ -1943,7 +1953,8 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
                           b.scratch_bytes >= sizeof(uint32_t) * (size_t)prep_blocks;
     uint32_t *tsum = own_scan ? static_cast<uint32_t *>(b.scratch) : nullptr;
     k_prep<<<(unsigned)prep_blocks, TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.src, b.dst, b.cpl,
-                                                b.cnt, b.spl, b.keys32, tsum);
+                                                b.cnt, b.spl, b.keys32, tsum,
+                                                HeavyList{b.heavy, b.heavy_count, b.heavy_thr});
     if (own_scan) {
         const int64_t per = (int64_t)BS_TB * 4;
         k_base_scan<4><<<(unsigned)((n + 1 + per - 1) / per), BS_TB, 0, s>>>(n + 1, b.cnt, tsum,

@@ -20,8 +20,8 @@ static void throw_rt(JNIEnv *env, const bh_engine *e, const char *what) {
     if (rt) (*env)->ThrowNew(env, rt, e ? bh_last_error(e) : what);
 }
 
-/* external fun create(deviceMask: Int): Long  (bit d = HIP device d; 0 = every visible GPU) */
-JNIEXPORT jlong JNICALL Java_Native_create(JNIEnv *env, jobject self, jint deviceMask) {
+/* external fun createMask(deviceMask: Int): Long  (bit d = HIP device d; 0 = every visible GPU) */
+JNIEXPORT jlong JNICALL Java_Native_createMask(JNIEnv *env, jobject self, jint deviceMask) {
     (void)self;
     bh_engine *e = NULL;
     if (bh_shim_create((uint32_t)deviceMask, &e) != BH_OK) {
@@ -29,6 +29,15 @@ JNIEXPORT jlong JNICALL Java_Native_create(JNIEnv *env, jobject self, jint devic
         return 0;
     }
     return (jlong)(intptr_t)e;
+}
+
+/* external fun create(device: Int): Long  (one GPU: HIP device `device`) */
+JNIEXPORT jlong JNICALL Java_Native_create(JNIEnv *env, jobject self, jint device) {
+    if (device < 0 || device > 31) {
+        throw_rt(env, NULL, "create: device index out of range (0..31)");
+        return 0;
+    }
+    return Java_Native_createMask(env, self, (jint)(1u << device));
 }
 
 /* external fun setParams(h: Long, G: Double, dt: Double, theta: Double, soft2: Double,

@@ -12,9 +12,13 @@ object Native {
         System.loadLibrary("bh_jni")
     }
 
+    /** One GPU, HIP device `device` (the default); the engine fills its pinned body mirror every
+     *  step. */
+    external fun create(device: Int): Long
+
     /** bh_create_multi over the HIP devices of `deviceMask` (bit d = device d, 0 = every visible
-     *  GPU); the engine fills its pinned body mirror every step. */
-    external fun create(deviceMask: Int): Long
+     *  GPU): opt-in -- the distinct-device RCCL path has not run on more than one GPU yet. */
+    external fun createMask(deviceMask: Int): Long
 
     /** bh_set_params: Config.G/DT/theta/SOFT2/WIDTH_PX/HEIGHT_PX (CFG:5-23) + merge knobs. */
     external fun setParams(

@@ -35,9 +35,11 @@ class QuadList(private val q: DoubleArray) {
 
 class PhysicsEngine(initialBodies: MutableList<Body>) {
     private var bodies: MutableList<Body> = initialBodies
-    // bh_create_multi over the GPUs of -Dbh.deviceMask (bit d = HIP device d; default 0 = every
-    // visible GPU): one handle, every step fanned out over the GPUs and joined (BHA:374-395)
-    private val handle: Long = Native.create(Integer.decode(System.getProperty("bh.deviceMask", "0")))
+    // One GPU (-Dbh.device, default 0); opt-in: -Dbh.deviceMask (bit d = HIP device d, 0 = every
+    // visible GPU) -- bh_create_multi, one handle, every step fanned out over the GPUs and joined
+    // (BHA:374-395).  (BH_DEVICES in the environment overrides either with a device list.)
+    private val handle: Long = System.getProperty("bh.deviceMask")?.let { Native.createMask(Integer.decode(it)) }
+        ?: Native.create(Integer.decode(System.getProperty("bh.device", "0")))
     // What the engine holds, read in place: its pinned caller-order mirror (Native.map, five
     // planes of `stride` doubles), mapped again after every native call that changes it; the
     // upload array is reused (grown only) -- no per-frame allocation that grows with N
@@ -90,7 +92,9 @@ class PhysicsEngine(initialBodies: MutableList<Body>) {
             throw t
         }
         if (edited) {
-            Native.stepEnd(handle)
+            // that step ran on the state before the edit: its result -- and an error it met, e.g.
+            // on the tree the previous call left (whose flags it took over) -- is replaced
+            runCatching { Native.stepEnd(handle) }
             push()
             Native.step(handle, 1)
             pull(afterStep = true)

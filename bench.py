@@ -29,9 +29,13 @@ import argparse
 import hashlib
 import json
 import os
+import shutil
+import signal
 import socket
 import subprocess
 import sys
+import tempfile
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -89,6 +93,10 @@ def parse():
                     help="--single-process rehearsal on fewer GPUs: the handle's device list, "
                          "e.g. 0,0 (a repeated device exchanges by device-to-device copies, "
                          "not RCCL)")
+    ap.add_argument("--deadline", type=float, default=600.0,
+                    help="N > 1: seconds the parent waits for the measuring child (torchrun, or "
+                         "the --single-process child) before it kills it and prints one JSON "
+                         "line with \"error\": \"timeout\" and every rank's last heartbeat")
     return ap.parse_args()
 
 
@@ -98,20 +106,160 @@ def _free_port() -> int:
         return sk.getsockname()[1]
 
 
+# ---- the parent's watchdog (N > 1) ------------------------------------------------------
+# The reference's join always returns (BHA:408, 426); a multi-GPU run can hang instead -- a rank
+# that returned early leaves its peers in a collective.  The engine bounds its own waits
+# (BH_COMM_TIMEOUT_S, set below the deadline for the child) and aborts its communicators; the
+# parent, which never touches the GPU, bounds the whole run: past the deadline it ends the child
+# and every rank it knows of, and prints one JSON line with each rank's last heartbeat.
+HEARTBEAT_ENV = "BH_BENCH_HEARTBEAT"
+_phase = {"name": "start"}
+
+
+def set_phase(name):
+    _phase["name"] = name
+
+
+def start_heartbeat(rank, engine_fn, period=1.0):
+    """Rank side: every `period` s write <$BH_BENCH_HEARTBEAT>/rank<R>.json -- pid, phase, and
+    the engine's progress (bh_progress of every member: API calls, collectives, last site,
+    busy / failed flags), read from a daemon thread while the main thread is inside a call."""
+    d = os.environ.get(HEARTBEAT_ENV)
+    if not d:
+        return
+    path = os.path.join(d, f"rank{rank}.json")
+    t0 = time.monotonic()
+
+    def beat():
+        while True:
+            rec = {"rank": rank, "pid": os.getpid(), "phase": _phase["name"],
+                   "elapsed_s": round(time.monotonic() - t0, 1)}
+            try:
+                eng = engine_fn()
+                if eng is not None:
+                    rec["progress"] = [eng.member(r).progress()
+                                       for r in range(max(1, eng.multi_world()))]
+            except Exception as exc:  # noqa: BLE001 - diagnostics only
+                rec["progress_error"] = repr(exc)[:200]
+            try:
+                with open(path + ".tmp", "w") as fh:
+                    json.dump(rec, fh)
+                os.replace(path + ".tmp", path)
+            except OSError:
+                return
+            time.sleep(period)
+    threading.Thread(target=beat, daemon=True).start()
+
+
+def read_heartbeats(d):
+    out = []
+    for name in sorted(os.listdir(d)) if d and os.path.isdir(d) else []:
+        if name.startswith("rank") and name.endswith(".json"):
+            try:
+                with open(os.path.join(d, name)) as fh:
+                    out.append(json.load(fh))
+            except (OSError, ValueError):
+                pass
+    return out
+
+
+def _kill_group(pid, sig):
+    try:
+        os.killpg(pid, sig)
+    except (ProcessLookupError, PermissionError):
+        pass
+
+
+def run_child(cmd, env, deadline, what, n_gpus=None):
+    """Run `cmd` (its own session) relaying its stdout; past `deadline` seconds end it -- SIGTERM
+    to its group (torchrun then stops its workers), SIGKILL 15 s later to that group and to every
+    rank that wrote a heartbeat (torchrun starts each worker in a session of its own) -- and print
+    one JSON line {"error": "timeout", "heartbeats": [...]}; returns the child's status (5 on a
+    timeout).  A child that fails without printing a bench line gets an error line too."""
+    hb_dir = tempfile.mkdtemp(prefix="bh_bench_hb_")
+    env = dict(env)
+    env[HEARTBEAT_ENV] = hb_dir
+    # the ranks give up on a collective before the parent gives up on them
+    env.setdefault("BH_COMM_TIMEOUT_S", str(max(10, int(deadline / 3))))
+    t0 = time.monotonic()
+    proc = subprocess.Popen(cmd, env=env, start_new_session=True, stdout=subprocess.PIPE,
+                            text=True, bufsize=1)
+    saw_line = threading.Event()
+
+    def relay():
+        for line in proc.stdout:
+            sys.stdout.write(line)
+            sys.stdout.flush()
+            if line.startswith("{") and '"metric"' in line:
+                saw_line.set()
+    rt = threading.Thread(target=relay, daemon=True)
+    rt.start()
+    try:
+        rc = proc.wait(timeout=deadline)
+    except subprocess.TimeoutExpired:
+        beats = read_heartbeats(hb_dir)
+        _kill_group(proc.pid, signal.SIGTERM)
+        try:
+            proc.wait(timeout=15)
+        except subprocess.TimeoutExpired:
+            pass
+        _kill_group(proc.pid, signal.SIGKILL)
+        for b in beats:  # the workers torchrun started in sessions of their own
+            if isinstance(b.get("pid"), int) and b["pid"] != os.getpid():
+                _kill_group(b["pid"], signal.SIGKILL)
+                try:
+                    os.kill(b["pid"], signal.SIGKILL)
+                except (ProcessLookupError, PermissionError):
+                    pass
+        try:
+            proc.wait(timeout=10)
+        except subprocess.TimeoutExpired:
+            pass
+        rt.join(timeout=5)
+        print(json.dumps({"metric": None, "value": None, "error": "timeout", "launch": what,
+                          "n_gpus": n_gpus, "deadline_s": deadline,
+                          "elapsed_s": round(time.monotonic() - t0, 1),
+                          "heartbeats": beats}), flush=True)
+        shutil.rmtree(hb_dir, ignore_errors=True)
+        return 5
+    rt.join(timeout=30)
+    if rc != 0 and not saw_line.is_set():
+        print(json.dumps({"metric": None, "value": None, "error": f"child exited with {rc}",
+                          "launch": what, "n_gpus": n_gpus,
+                          "heartbeats": read_heartbeats(hb_dir)}), flush=True)
+    shutil.rmtree(hb_dir, ignore_errors=True)
+    return rc
+
+
+def _child_env():
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver
+    return env
+
+
 def spawn_torchrun(args) -> int:
     """`--gpus N` (N > 1) without torchrun: run the same command under torch.distributed.run as
     a child process -- nothing in this process has touched the GPU, and no exec replaces it --
-    relaying the child's output (rank 0 prints the JSON line) and returning its exit status."""
+    relaying the child's output (rank 0 prints the JSON line) and returning its exit status,
+    under the watchdog (run_child)."""
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
            f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
            "--master-port", str(_free_port()), os.path.abspath(__file__)]
     cmd += [a for a in sys.argv[1:] if a != "--dry-run"]
     if args.dry_run:
-        print(json.dumps({"launch": "torchrun child", "cmd": cmd}), flush=True)
+        print(json.dumps({"launch": "torchrun child", "cmd": cmd, "deadline_s": args.deadline}),
+              flush=True)
         return 0
-    env = dict(os.environ)
-    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this driver
-    return subprocess.run(cmd, env=env).returncode
+    return run_child(cmd, _child_env(), args.deadline, "torchrun", args.gpus)
+
+
+def spawn_single_process(args) -> int:
+    """`--gpus N --single-process`: the one-handle run in a child process under the watchdog."""
+    cmd = [sys.executable, os.path.abspath(__file__)] + [a for a in sys.argv[1:]
+                                                         if a != "--dry-run"]
+    env = _child_env()
+    env["BH_BENCH_CHILD"] = "1"
+    return run_child(cmd, env, args.deadline, "single process", args.gpus)
 
 
 def committed_traffic(config, kernel):
@@ -446,6 +594,8 @@ def main():
         sys.exit(2)
     if env_world is None and args.gpus is not None and args.gpus > 1 and not single_proc:
         sys.exit(spawn_torchrun(args))  # before anything touches the GPU
+    if single_proc and not os.environ.get("BH_BENCH_CHILD") and not args.dry_run:
+        sys.exit(spawn_single_process(args))  # (the watchdog's child)
     world = int(env_world) if env_world is not None else 1
     if args.gpus is None:
         args.gpus = world
@@ -479,6 +629,9 @@ def main():
 
     if world > 1:
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    holder = {"eng": None}
+    start_heartbeat(rank, lambda: holder["eng"])
+    set_phase("engine")
     torch.cuda.set_device(local_rank)
 
     params = bh_amd.default_params(theta=args.theta)
@@ -525,9 +678,11 @@ def main():
         eng.set_mirror(True)
         eng.set_mirror(False)
 
+    holder["eng"] = eng
     arrs, scene_name, scaling = scene_for(args.config, n_gpus)
     n0 = len(arrs[0])
 
+    set_phase("warmup")
     eng.reset_bodies(*arrs)
     if args.warmup > 0:
         eng.step(args.warmup)
@@ -539,6 +694,7 @@ def main():
         cnt_start = traversal_counters(bh_amd, params, local_rank, eng.get_bodies())
 
     clocks = ClockSampler(local_rank) if rank == 0 else None
+    set_phase("timed")
     eng.set_profiling(not args.no_events)
     if world > 1:
         dist.barrier()
@@ -656,6 +812,7 @@ def main():
     roofline.update(extra)
 
     # rank 0's extra legs; the other ranks wait at the next collective
+    set_phase("extra legs")
     drop_in = None
     if n_gpus == 1 and not args.no_drop_in:
         drop_in = drop_in_leg(eng, args.drop_in_calls)
@@ -671,6 +828,7 @@ def main():
     if world > 1:
         dist.barrier()  # rank 0's extra legs are done: the verify leg's collectives start together
     if args.verify:
+        set_phase("verify")
         from bh_amd import scenes
         case = "c4_k10" if n_gpus > 1 else "c3_k10"
         golden_scene = "c4" if n_gpus > 1 else "c3"
@@ -724,6 +882,8 @@ def main():
         if per_rank is not None:
             line["per_rank_phase_ms_per_step"] = per_rank
         print(json.dumps(line), flush=True)
+    set_phase("done")
+    holder["eng"] = None
     eng.close()
     if world > 1:
         dist.barrier()

@@ -68,7 +68,14 @@ int bh_create(const bh_params *p, int device, bh_engine **out);
  * (member 0 by the caller's).  Every call of this header takes the handle: calls that change the
  * state run on every member, calls that read it read member 0's replica (complete at every API
  * boundary), bh_set_mirror / bh_map_bodies use member 0's mirror.  One set bit = bh_create (the
- * pipelined one-GPU engine).  Results are bit-identical to bh_create's for any mask. */
+ * pipelined one-GPU engine).  Results are bit-identical to bh_create's on the paths tested: one
+ * GPU, members that share a device (device-to-device copies) and a one-rank RCCL communicator;
+ * the distinct-device RCCL path (more than one rank) has not run on hardware yet, so callers
+ * should keep one GPU (mask 1, or bh_create) unless they opt in (the Kotlin drop-in's default).
+ * A call that fails on one member -- or whose waits for the others exceed BH_COMM_TIMEOUT_S
+ * seconds (default 300; 0 = forever) -- aborts the others' waits (RCCL: ncclCommAbort) and returns
+ * an error from every member; the handle then returns BH_E_COMM for every call that uses the
+ * bodies until bh_reset_bodies, which makes new communicators. */
 int bh_create_multi(const bh_params *p, uint32_t device_mask, bh_engine **out);
 
 /* The same over an explicit device list, repeats allowed: a device listed twice hosts two members
@@ -125,11 +132,23 @@ int bh_comm_ranks(const bh_engine *e, int32_t *nranks, int32_t *rank);
 
 /* Test hooks.  what == 1: the next locally essential tree build of this rank trips the node
  * array guard (let.hip k_let_guard), as a broken invariant on one rank would; the call must then
- * be replayed by every rank of the group alike.  what == 2 + k: the k-th next full tree build
- * (k = 0: the next one) raises the jitter replay's error flag, as the unsupported-geometry guard
- * would; the bh_step call whose step uses that tree returns BH_E_STATE -- for a call's last
- * pipelined build (the next call's first tree) that is the next call. */
+ * be replayed by every rank of the group alike.  what == 2 + k (k < 98): the k-th next full tree
+ * build (k = 0: the next one) raises the jitter replay's error flag, as the unsupported-geometry
+ * guard would; the bh_step call whose step uses that tree returns BH_E_STATE -- for a call's last
+ * pipelined build (the next call's first tree) that is the next call; what == 99: that carried tree
+ * (one GPU, after a call) raises its flag now (BH_E_STATE if there is none).  what == 100 + k: this rank
+ * fails host-side (BH_E_COMM) right before its k-th next collective; what == 200 + k: before its
+ * k-th next in-process group barrier -- a rank-local error between collectives: every rank of the
+ * decomposition must then return an error within a bounded time, refuse further calls with
+ * BH_E_COMM, and step bit-exactly again after bh_reset_bodies. */
 int bh_debug_inject(bh_engine *e, int what);
+
+/* Progress of an engine, safe to read from any thread while a call runs (a watchdog's
+ * heartbeat): out4[0] state-changing API calls begun, [1] collectives issued, [2] the site of
+ * the last one (as bh_collective_log), [3] bit 0 a call is running, bit 1 the last multi-rank
+ * call failed (BH_E_COMM until bh_reset_bodies), bit 2 its RCCL communicator was aborted.  A
+ * multi-device handle reports member 0's (bh_multi_member for the others). */
+int bh_progress(const bh_engine *e, int64_t *out4);
 
 /* In-process rank group (testing the multi-GPU decomposition on one device, where RCCL refuses
  * several ranks): `world` engines of one process, each driven by its own host thread with

@@ -82,6 +82,12 @@ static void jni_check(const char *call) { /* a RuntimeException thrown by the gl
     }
 }
 
+static long step_end_errors_replaced; /* stepEnd errors of speculative steps an upload replaced */
+static void jni_clear(void) { /* a call whose exception the shim discards (PhysicsEngine.kt) */
+    ++jni_calls;
+    if (fake_jvm_take_exception()) ++step_end_errors_replaced;
+}
+
 static void shim_params(Shim *s) {
     Java_Native_setParams(env, NULL, s->h, cfg_G, cfg_DT, cfg_theta, cfg_SOFT2, cfg_W, cfg_H,
                           s->mergeMaxMass, s->mergeMinDist);
@@ -364,7 +370,7 @@ static void shim_create(Shim *s, List *initial, jint device_mask) {
     s->shadow_n = -1;
     s->info = fake_jvm_long_array(2);
     s->info3 = fake_jvm_long_array(3);
-    s->h = Java_Native_create(env, NULL, device_mask);
+    s->h = Java_Native_createMask(env, NULL, device_mask); /* (-Dbh.deviceMask) */
     if (fake_jvm_take_exception() || !s->h) {
         fprintf(stderr, "abi_harness: Native.create failed (no GPU?)\n");
         exit(1);
@@ -405,9 +411,9 @@ static void shim_frame(Shim *s, double *t) {
     jni_check("stepBegin");
     const int diff = shim_changed(s);
     LAP(1);
-    if (diff) { /* the upload replaces that step's result */
+    if (diff) { /* the upload replaces that step's result -- and an error it met (PhysicsEngine.kt) */
         Java_Native_stepEnd(env, NULL, s->h);
-        jni_check("stepEnd");
+        jni_clear();
         shim_push(s);
         ++shim_steps_uploaded;
         Java_Native_step(env, NULL, s->h, 1);
@@ -621,6 +627,11 @@ int main(int argc, char **argv) {
             oracle_destroy(o);
             o = oracle_of(s.bodies, &s); /* the reference steps the edited objects themselves */
         }
+        if (frame == 25 && bh_multi_world((bh_engine *)(intptr_t)s.h) == 1)
+            /* the tree the last frame left for this one -- which the edited frame's speculative
+             * step takes over -- raises its error flag: the upload must replace that step's error
+             * too (the edited list never uses that tree) */
+            if (bh_debug_inject((bh_engine *)(intptr_t)s.h, 99) != 0) fail("bh_debug_inject", frame);
         oracle_params op = oparams(&s);
         oracle_set_params(o, &op);
         long before = s.bodies->n;
@@ -658,6 +669,8 @@ int main(int argc, char **argv) {
     if (removed_total == 0) fail("the scene never merged: identity bookkeeping untested", 40);
     if (removed_max < 3) fail("no frame removed 3+ bodies: the one-pass removal is untested", 40);
     if (shim_steps_uploaded != 1) fail("the in-place edit of frame 25 was not uploaded exactly once", 40);
+    if (bh_multi_world((bh_engine *)(intptr_t)s.h) == 1 && step_end_errors_replaced != 1)
+        fail("the edited frame's speculative step did not meet the injected carried-tree error", 40);
     printf("abi_harness: 40 frames through the JNI glue on %d device(s) (%ld native calls) "
            "bit-identical to the oracle; %ld bodies merged away (at most %ld in one frame), %ld "
            "quads checked, %ld uploads after the constructor/resets, %ld shadow allocations after "

@@ -23,7 +23,8 @@ void *fake_jvm_direct_address(jobject buf, jlong *capacity);
 void fake_jvm_free(jarray a);
 
 /* the glue's natives (bh_jni.c), declared for the harness */
-jlong Java_Native_create(JNIEnv *env, jobject self, jint deviceMask);
+jlong Java_Native_create(JNIEnv *env, jobject self, jint device);
+jlong Java_Native_createMask(JNIEnv *env, jobject self, jint deviceMask);
 void Java_Native_setParams(JNIEnv *env, jobject self, jlong h, jdouble G, jdouble dt,
                            jdouble theta, jdouble soft2, jint w, jint hgt, jdouble mm, jdouble md);
 void Java_Native_reset(JNIEnv *env, jobject self, jlong h, jint n, jdoubleArray soa);

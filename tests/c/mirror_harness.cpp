@@ -149,6 +149,11 @@ int main(int argc, char **argv) {
             oracle_destroy(o);
             o = oracle_of(live, engine);  // the reference steps the edited objects themselves
         }
+        if (frame == 25 && bh_multi_world(engine.handle()) == 1 &&
+            bh_debug_inject(engine.handle(), 99) != 0)
+            // the tree the last frame left for this one (the edited frame's speculative first
+            // tree) raises its error flag: the upload replaces that step's error with its result
+            fail("bh_debug_inject", frame);
         oracle_params op = oparams(engine);
         oracle_set_params(o, &op);
         const size_t before = engine.getBodies().size();

@@ -5,6 +5,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
@@ -47,7 +48,7 @@ def test_single_gpu_runs_in_process_with_verification():
 
 def test_single_process_multi_gpu_stays_in_process():
     """--single-process: one process, one engine handle over the N GPUs (bh_create_multi), no
-    torchrun child; refused under torchrun."""
+    torchrun (the measuring process is a child of the watchdog parent); refused under torchrun."""
     r = _run(["--gpus", "8", "--single-process", "--dry-run"])
     assert r.returncode == 0, r.stderr
     plan = json.loads(r.stdout.strip().splitlines()[-1])
@@ -56,3 +57,63 @@ def test_single_process_multi_gpu_stays_in_process():
     r = _run(["--gpus", "4", "--single-process", "--dry-run"],
              {"WORLD_SIZE": "4", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode == 2 and "torchrun" in r.stderr
+
+
+_DUMMY_WORKER = """
+import sys, time
+sys.path.insert(0, sys.argv[1])
+import bench
+bench.set_phase("collective")
+bench.start_heartbeat(1, lambda: None, period=0.2)
+time.sleep(120)
+"""
+
+_DUMMY_LAUNCHER = """
+import subprocess, sys, time
+sys.path.insert(0, sys.argv[1])
+import bench
+# a worker in a session of its own, as torchrun starts its ranks
+subprocess.Popen([sys.executable, "-c", sys.argv[2], sys.argv[1]], start_new_session=True)
+bench.set_phase("timed")
+bench.start_heartbeat(0, lambda: None, period=0.2)
+time.sleep(120)
+"""
+
+
+def _alive(pid):
+    try:
+        with open(f"/proc/{pid}/status") as fh:
+            return fh.read().split("State:")[1].split()[0] != "Z"
+    except OSError:
+        return False
+
+
+def test_watchdog_ends_a_hung_child_and_reports_heartbeats(capsys):
+    """bench.py's parent watchdog (run_child) against a child that never finishes -- a launcher
+    that starts a 'rank' in a session of its own (as torchrun does) and both sleep: past the
+    deadline the parent kills the launcher's group and every rank that wrote a heartbeat, and
+    prints one JSON line with "error": "timeout" and each rank's last phase; status 5."""
+    sys.path.insert(0, ROOT)
+    import bench
+    t0 = time.monotonic()
+    rc = bench.run_child([sys.executable, "-c", _DUMMY_LAUNCHER, ROOT, _DUMMY_WORKER],
+                         dict(os.environ), 3.0, "dummy", 2)
+    elapsed = time.monotonic() - t0
+    assert rc == 5 and elapsed < 40, (rc, elapsed)
+    line = json.loads([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][-1])
+    assert line["error"] == "timeout" and line["deadline_s"] == 3.0 and line["value"] is None
+    beats = {b["rank"]: b for b in line["heartbeats"]}
+    assert beats[0]["phase"] == "timed" and beats[1]["phase"] == "collective", beats
+    time.sleep(0.5)
+    for b in beats.values():
+        assert not _alive(b["pid"]), f"rank {b['rank']} (pid {b['pid']}) survived the watchdog"
+
+
+def test_watchdog_reports_a_child_that_fails_without_a_line(capsys):
+    sys.path.insert(0, ROOT)
+    import bench
+    rc = bench.run_child([sys.executable, "-c", "import sys; sys.exit(7)"], dict(os.environ),
+                         30.0, "dummy", 2)
+    assert rc == 7
+    line = json.loads([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][-1])
+    assert line["error"] == "child exited with 7"

@@ -46,7 +46,7 @@ def test_native_externals_match_the_jni_exports():
     assert set(kt) == set(c), f"Kotlin {sorted(kt)} vs C {sorted(c)}"
     for name in kt:
         assert kt[name] == c[name], f"{name}: Kotlin {kt[name]} vs C {c[name]}"
-    assert len(kt) == 12
+    assert len(kt) == 13
 
 
 def test_physics_engine_offers_the_reference_surface():

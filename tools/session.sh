@@ -22,6 +22,7 @@
 #                  build (SOLO_LIBS="A default" to change), 2 rounds          -> ${TAG}_soloab.jsonl
 #   ab             A/B of in-tree library builds (tools/ab.sh; LIBS="A B", AB_ARGS=...)
 #   kstats         C3 bench under rocprofv3 --kernel-trace --stats per library (KSTATS_LIBS)
+#   rehearse       bench.py --gpus 2 --single-process --devices 0,0 (the watchdog parent + child)
 # Every GPU step runs under its own time limit; a failing step (any rc but 0) ends the session, so
 # nothing else touches the GPU after a fault, an abort or a timeout.
 # (Older one-off session scripts are kept in tools/archive/: committed profiles cite them; see tools/README.md.)
@@ -107,6 +108,10 @@ for step in "$@"; do
           echo "{\"lib\": \"$L\", \"line\": $(grep '^{' ${O}_soloab_$L$rr.log | tail -1)}" >> ${O}_soloab.jsonl
         done
       done ;;
+    rehearse)  # the N > 1 launch path on one GPU: bench.py's watchdog parent, the
+               # --single-process child over a repeated device (device-to-device copies)
+      bench_line --gpus 2 --single-process --devices 0,0 --config c2 --steps 3 --warmup 1 \
+        --no-cpu-baseline --no-single-gpu --no-verify ;;
     ab) run 1800 ${O}_ab.log bash tools/ab.sh ;;
     kstats)  # kernel-trace stats of C3 per library (KSTATS_LIBS="default X ..."; lib/lib<X>.so)
       export TMPDIR=/tmp
