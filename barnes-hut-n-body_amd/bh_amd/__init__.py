@@ -424,7 +424,7 @@ class Engine:
     def get_bodies(self, out=None):
         """bh_get_bodies: (x, y, vx, vy, m) in caller order; `out` = five float64 arrays of at
         least N entries to fill (a caller that reuses its buffers), else new arrays."""
-        n = self.num_bodies()
+        n = max(self.num_bodies(), 0)  # (-1 while a call begun by step_begin runs: refused below)
         if out is None or any(len(a) < n or a.dtype != np.float64 for a in out):
             out = [np.empty(n, dtype=np.float64) for _ in range(5)]
         got = ctypes.c_int64(0)
