@@ -1914,13 +1914,22 @@ int agree_let_flags(bh_engine *e, uint32_t ls[2], uint32_t *own_sub) {
 #ifndef BH_PIPE_PRIORITY
 #define BH_PIPE_PRIORITY 1  // the overlapped work's stream at the highest priority
 #endif
-#ifndef BH_DEEP_PIPE
-// 1: the next step's a(t) evaluated beside this step's second traversal (kick + drift + keys as
-// their own pass).  Measured slower (C3 1.925 against 1.884 ms per step, round 4):
-// the next tree is ready only after the traversal's last waves are placed, so the two
-// evaluations barely overlap and share the caches when they do.
-#define BH_DEEP_PIPE 0
+// The deep pipeline: the next step's a(t) evaluated beside this step's second traversal (kick +
+// drift + keys as their own pass) -- for body lists up to BH_DEEP_PIPE_MAX_N.  Measured slower at
+// C3 (1.925 against 1.884 ms per step, round 4): the next tree is ready only after the
+// traversal's last waves are placed, so the two evaluations barely overlap and share the caches
+// when they do.  A small list leaves most of the GPU idle in each traversal (a few hundred waves
+// on 1 024 SIMDs), so there the two evaluations run side by side (round 6).
+#ifndef BH_DEEP_PIPE_MAX_N
+#define BH_DEEP_PIPE_MAX_N 0
 #endif
+int64_t deep_pipe_max_n() {
+    static const int64_t v = [] {
+        const char *t = std::getenv("BH_DEEP_PIPE_MAX_N");
+        return t ? (int64_t)std::atoll(t) : (int64_t)BH_DEEP_PIPE_MAX_N;
+    }();
+    return v;
+}
 #ifndef BH_PIPE_LAST
 #define BH_PIPE_LAST 1  // pipeline a call's last step too (the next call starts on its tree)
 #endif
@@ -2194,7 +2203,8 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     traverse(e->nodes, e->node_cap, e->T_trav, e->st.x, e->st.y, e->m_trav, e->cidx_trav, 0, n,
              e->geo, fp, e->a2, nullptr, s, &ka, lanes ? e->lanes_trav : nullptr, &wo);
     HIPCHK(e, hipGetLastError());
-    if (!BH_DEEP_PIPE) TRY(mark(e, 1));
+    const bool deep = deep_pipe_max_n() > 0 && e->n <= deep_pipe_max_n();
+    if (!deep) TRY(mark(e, 1));
     TRY(wave_order_next(e, 0, n, s));
     if (last) {
         hipStream_t ps = e->pipe_stream;
@@ -2215,7 +2225,7 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     const int rc_b1 = build_into(e, e->pipe_stream, true, false, last);  // step s+1's first tree (BHA:359)
     e->lane_defer = false;
     TRY(rc_b1);
-    if (BH_DEEP_PIPE) {
+    if (deep) {
         // ... and a(t) of step s+1 on it (BHA:407-408): a force evaluation reads positions and
         // masses only, so it runs beside this traversal, whose tail it fills; the next step's
         // kick and drift need this traversal's velocities and run after both (kick_drift_keys)
@@ -2226,8 +2236,8 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     }
     HIPCHK(e, hipEventRecord(e->pipe_ev[1], e->pipe_stream));
     HIPCHK(e, hipStreamWaitEvent(s, e->pipe_ev[1], 0));
-    if (BH_DEEP_PIPE) TRY(mark(e, 1, 2));  // this traversal, the overlapped chain, the next a(t)
-    if (!last && !BH_DEEP_PIPE && BH_FOLD_VEL_PERM) {
+    if (deep) TRY(mark(e, 1, 2));  // this traversal, the overlapped chain, the next a(t)
+    if (!last && !deep && BH_FOLD_VEL_PERM) {
         e->vel_perm = e->perm2;  // the next step's first kick reads them through the permutation
     } else {
         permute_velocities(n, e->perm2, e->st.vx, e->st.vy, e->alt.vx, e->alt.vy, s);
@@ -2239,7 +2249,7 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     std::swap(e->node_cap, e->nodes_alt_cap);
     e->prebuilt = true;
     e->carried_flags = last;
-    e->forces_ready = BH_DEEP_PIPE != 0;
+    e->forces_ready = deep;
     e->fp_ready = fp;
     if (last) {  // the previous order's state (kicked, merged, not yet jittered) is what the caller sees
         std::swap(e->view, e->alt);

@@ -15,6 +15,8 @@
 // The kernel is bound by fp64 VALU issue (the IEEE sqrt and two IEEE divisions per
 // interaction), not by HBM: the node stream is shared by 64 lanes and served from the
 // scalar cache / L2.  See DESIGN.md for the roofline accounting.
+#include <cstdlib>
+
 #include "bh_device.hpp"
 #include "fastmath.hpp"
 
@@ -188,9 +190,10 @@ __device__ __forceinline__ void own_kick(int64_t q, double bx, double by, double
 // KICK (KickMode): the integration step that follows the evaluation is applied by the lane
 // itself after its walk -- the body's x, y are only ever read by its own lane (other lanes see
 // it through the leaf records), so the update in place is race-free and a2 is not written.
-// One wave's 64 lanes [lo + 64 v, lo + 64 v + 64): walk, then the epilogue.
+// Wave v evaluates the bpw lanes [lo + bpw v, lo + bpw v + bpw) (64 = one body per lane; fewer
+// for small launches, the wave's other lanes idle -- see traverse()): walk, then the epilogue.
 template <bool COUNT, bool OFF32, int KICK>
-__device__ __forceinline__ void trav_wave(uint32_t v, uint64_t t_start,
+__device__ __forceinline__ void trav_wave(uint32_t v, uint32_t bpw, uint64_t t_start,
                                           const Node *__restrict__ nodes,
                                           const uint32_t *__restrict__ d_T, double *x, double *y,
                                           const double *__restrict__ m,
@@ -200,9 +203,10 @@ __device__ __forceinline__ void trav_wave(uint32_t v, uint64_t t_start,
                                           const KickArgs &kick,
                                           const uint32_t *__restrict__ lanes,
                                           const WaveOrder &wo) {
-    const int64_t q = lo + (int64_t)v * TB + threadIdx.x;  // lane
-    const uint32_t lp = lanes && q < hi ? lanes[q] : (uint32_t)q;
-    const bool valid = q < hi && (!lanes || lp != LANE_IDLE);
+    const bool in_wave = threadIdx.x < bpw;
+    const int64_t q = lo + (int64_t)v * bpw + threadIdx.x;  // lane
+    const uint32_t lp = lanes && in_wave && q < hi ? lanes[q] : (uint32_t)q;
+    const bool valid = in_wave && q < hi && (!lanes || lp != LANE_IDLE);
     const int64_t p = lanes ? (int64_t)lp : q;  // its body's slot
     // A body merged away earlier in this bh_step call (a tombstone until the call's compaction)
     // needs no force: it does not walk.  Tombstones sort to the tail with the out-of-root
@@ -231,15 +235,15 @@ __device__ __forceinline__ void trav_wave(uint32_t v, uint64_t t_start,
         walk<false, COUNT, OFF32>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx,
                                   fy, nvis, niters, ncontrib, nblocks);
     if (wo.cost && threadIdx.x == 0 && q < hi)
-        wo.cost[(q - lo) >> 6] = (uint32_t)(wall_clock64() - t_start < 0xFFFFFFull
-                                                  ? wall_clock64() - t_start : 0xFFFFFFull);
+        wo.cost[v] = (uint32_t)(wall_clock64() - t_start < 0xFFFFFFull
+                                    ? wall_clock64() - t_start : 0xFFFFFFull);
     if (COUNT && (threadIdx.x & 63) == 0) {
-        cnt.wave_iters[(q - lo) >> 6] = niters;
-        cnt.wave_blocks[(q - lo) >> 6] = nblocks;
+        cnt.wave_iters[v] = niters;
+        cnt.wave_blocks[v] = nblocks;
     }
 #ifdef BH_TRAV_TIMING
-    if (threadIdx.x == 0 && ((q - lo) >> 6) < TRAV_TIMING_MAX) {
-        uint64_t *t = g_trav_times + 4 * ((q - lo) >> 6);
+    if (threadIdx.x == 0 && v < TRAV_TIMING_MAX) {
+        uint64_t *t = g_trav_times + 4 * v;
         t[0] = t_start;
         t[1] = wall_clock64();
         t[2] = __builtin_amdgcn_s_getreg((31 << 11) | 4);    // HW_ID: wave, SIMD, CU, SE
@@ -313,7 +317,7 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
                                                  Geometry g, double *__restrict__ a2,
                                                  TraverseCounters cnt, KickArgs kick,
                                                  const uint32_t *__restrict__ lanes,
-                                                 WaveOrder wo) {
+                                                 WaveOrder wo, uint32_t bpw) {
 #if defined(BH_TRAV_TIMING)
     const uint64_t t_start = wall_clock64();
 #else
@@ -322,8 +326,8 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
     uint32_t v = xcd_block<BH_TRAV_XCD_RUN>();
     if (wo.order)  // the v-th run to start is the order[v]-th run of waves (wave_order)
         v = wo.order[v / BH_TRAV_XCD_RUN] * BH_TRAV_XCD_RUN + v % BH_TRAV_XCD_RUN;
-    trav_wave<COUNT, OFF32, KICK>(v, t_start, nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, cnt,
-                                  kick, lanes, wo);
+    trav_wave<COUNT, OFF32, KICK>(v, bpw, t_start, nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2,
+                                  cnt, kick, lanes, wo);
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
@@ -434,13 +438,44 @@ hipError_t selftest_fast_math(int64_t n, uint64_t seed, unsigned long long *d_ba
     return hipGetLastError();
 }
 
+// Bodies per wave of a small launch.  A wave walks the union of its bodies' interaction lists,
+// one dependent fp64 chain per stop, and a launch of a few thousand waves leaves most of the 1 024
+// SIMDs with one wave or none: the kernel then lasts as long as its slowest wave's walk (C1's
+// 12 500 bodies = 196 waves, C2's 1e5 = 1 563).  Fewer bodies per wave -- the wave's other lanes
+// idle -- make more, shorter walks (the union of fewer lists) that fill the SIMDs: halved until
+// the launch has BH_TRAV_MIN_WAVES waves or BH_TRAV_MIN_BPW bodies per wave.  Each body's sum is
+// untouched (its own criterion and order), so the results are bit-identical for any grouping.
+#ifndef BH_TRAV_MIN_WAVES
+#define BH_TRAV_MIN_WAVES 1024
+#endif
+#ifndef BH_TRAV_MIN_BPW
+#define BH_TRAV_MIN_BPW 1
+#endif
+uint32_t bodies_per_wave(int64_t lanes) {
+    // (environment overrides for A/B sweeps; BH_TRAV_MIN_WAVES=0: always 64)
+    static const int64_t min_waves = [] {
+        const char *v = std::getenv("BH_TRAV_MIN_WAVES");
+        return v ? (int64_t)std::atoll(v) : (int64_t)BH_TRAV_MIN_WAVES;
+    }();
+    static const uint32_t min_bpw = [] {
+        const char *v = std::getenv("BH_TRAV_MIN_BPW");
+        const long b = v ? std::atol(v) : (long)BH_TRAV_MIN_BPW;
+        return (uint32_t)(b < 1 ? 1 : b > TB ? TB : b);
+    }();
+    uint32_t bpw = TB;
+    while (bpw > min_bpw && (lanes + bpw - 1) / bpw < min_waves) bpw >>= 1;
+    return bpw;
+}
+
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
               const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, const TraverseCounters *cnt,
               hipStream_t s, const KickArgs *kick, const uint32_t *lanes, const WaveOrder *wo) {
     if (hi <= lo) return;
-    unsigned grid = (unsigned)((hi - lo + TB - 1) / TB);
-    const WaveOrder w = wo && wave_order_runs(hi - lo) ? *wo : WaveOrder{};
+    // (the counting walk keeps 64 bodies per wave: its per-wave counters define lane efficiency)
+    const uint32_t bpw = cnt ? (uint32_t)TB : bodies_per_wave(hi - lo);
+    unsigned grid = (unsigned)((hi - lo + bpw - 1) / bpw);
+    const WaveOrder w = wo && bpw == TB && wave_order_runs(hi - lo) ? *wo : WaveOrder{};
     if (w.order)  // whole runs: every run index the order maps to exists in the grid
         grid = (unsigned)(wave_order_runs(hi - lo) * BH_TRAV_XCD_RUN);
     // node records addressed by a 32-bit byte offset while the array stays below 4 GiB
@@ -449,7 +484,7 @@ void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x
     const TraverseCounters tc = cnt ? *cnt : TraverseCounters{nullptr, nullptr, nullptr, nullptr};
 #define BH_TRAV(C, O, K) \
     k_traverse<C, O, K><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, tc, ka, \
-                                            lanes, w)
+                                            lanes, w, bpw)
     if (cnt) {  // diagnostic counting walk: accelerations out, never fused
         if (off32) BH_TRAV(true, true, KICK_NONE);
         else BH_TRAV(true, false, KICK_NONE);

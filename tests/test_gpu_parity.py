@@ -1048,7 +1048,9 @@ def test_profiling_timings_do_not_change_results():
     samples = a.traverse_kernel_samples()
     avg, launches = a.traverse_kernel_ms()
     assert t["build"] > 0 and t["traverse"] > 0
-    assert launches == 8 and len(samples) == 8 and np.all(samples > 0)
+    # 8 evaluations; the deep pipeline of small lists (BH_DEEP_PIPE_MAX_N) also evaluates the
+    # next call's a(t) beside the last step's second traversal: one more
+    assert launches in (8, 9) and len(samples) == launches and np.all(samples > 0)
     assert abs(avg - samples.mean()) < 1e-9
     b = bh_amd.Engine(bh_amd.default_params(theta=0.5))
     b.reset_bodies(*arrs)

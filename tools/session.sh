@@ -23,6 +23,7 @@
 #   ab             A/B of in-tree library builds (tools/ab.sh; LIBS="A B", AB_ARGS=...)
 #   kstats         C3 bench under rocprofv3 --kernel-trace --stats per library (KSTATS_LIBS)
 #   rehearse       bench.py --gpus 2 --single-process --devices 0,0 (the watchdog parent + child)
+#   envab          A/B of environment settings (ENVS="X=0 X=1", AB_ARGS, ROUNDS) -> ${TAG}_envab.jsonl
 # Every GPU step runs under its own time limit; a failing step (any rc but 0) ends the session, so
 # nothing else touches the GPU after a fault, an abort or a timeout.
 # (Older one-off session scripts are kept in tools/archive/: committed profiles cite them; see tools/README.md.)
@@ -75,9 +76,16 @@ for step in "$@"; do
         ${O}_timed_fetch ${O}_timed_write 8
       cp "$(find ${O}_timed_trace -name '*kernel_stats.csv' | head -1)" ${O}_c3_timed_kernel_stats.csv
       rm -rf ${O}_timed_trace ${O}_timed_fetch ${O}_timed_write ;;  # (raw traces: see sq)
-    timeline)
-      run 600 ${O}_timeline.log rocprofv3 --kernel-trace -d ${O}_tl -o run --output-format csv \
-        -- python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --no-counters --no-drop-in ;;
+    timeline)  # CONFIG=c2 etc. for another workload -> ${TAG}_${CONFIG}_timeline.txt
+      export TMPDIR=/tmp
+      C=${CONFIG:-c3}
+      run 600 ${O}_timeline.log rocprofv3 --kernel-trace -d ${O}_tl_$C -o run --output-format csv \
+        -- python3 bench.py --config $C --steps 10 --warmup 2 --no-cpu-baseline --no-counters --no-drop-in --no-verify
+      grep '^{' ${O}_timeline.log | tail -1 >> ${O}_bench_lines.jsonl
+      kt=$(find ${O}_tl_$C -name '*kernel_trace.csv' | head -1)
+      python3 tools/timeline.py "$kt" 2 ${O}_${C}_timeline.txt > /dev/null
+      tail -3 ${O}_${C}_timeline.txt
+      rm -rf ${O}_tl_$C ;;
     dropin)
       export TMPDIR=/tmp
       run 600 ${O}_dropin.log rocprofv3 --kernel-trace --memory-copy-trace -d ${O}_dropin_trace \
@@ -113,6 +121,18 @@ for step in "$@"; do
       bench_line --gpus 2 --single-process --devices 0,0 --config c2 --steps 3 --warmup 1 \
         --no-cpu-baseline --no-single-gpu --no-verify ;;
     ab) run 1800 ${O}_ab.log bash tools/ab.sh ;;
+    envab)  # A/B of environment settings with the in-tree library: ENVS="A=1 A=2" (one
+            # assignment per label, or 'none'), AB_ARGS, ROUNDS -> ${TAG}_envab.jsonl
+      for rr in $(seq 1 ${ROUNDS:-2}); do
+        for E in ${ENVS:-none}; do
+          if [ "$E" = none ]; then
+            run 600 ${O}_envab.log python -u bench.py ${AB_ARGS:---steps 10 --warmup 2 --no-cpu-baseline}
+          else
+            run 600 ${O}_envab.log env "$E" python -u bench.py ${AB_ARGS:---steps 10 --warmup 2 --no-cpu-baseline}
+          fi
+          echo "{\"env\": \"$E\", \"line\": $(grep '^{' ${O}_envab.log | tail -1)}" >> ${O}_envab.jsonl
+        done
+      done ;;
     kstats)  # kernel-trace stats of C3 per library (KSTATS_LIBS="default X ..."; lib/lib<X>.so)
       export TMPDIR=/tmp
       for L in ${KSTATS_LIBS:-default}; do
