@@ -518,7 +518,7 @@ hipError_t drain_stream(hipStream_t s, double secs) {
             std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > secs)
             return hipErrorNotReady;
         if (spins < 2000) std::this_thread::yield();
-        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
 }
 
@@ -581,7 +581,7 @@ int wait_stream(bh_engine *e, hipStream_t s) {
                   "never arrived?";
         if (why) break;
         if (spins < 2000) std::this_thread::yield();
-        else std::this_thread::sleep_for(std::chrono::microseconds(50));
+        else std::this_thread::sleep_for(std::chrono::microseconds(20));
     }
     e->err = std::string("wait for the device: ") + why;
     abort_comm(e);
