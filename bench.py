@@ -171,20 +171,31 @@ def _kill_group(pid, sig):
         pass
 
 
+def _die_with_parent():
+    """(preexec_fn) the child gets SIGTERM when this process dies -- killed by whoever runs the
+    bench -- so torchrun stops its workers instead of leaving them on the GPUs."""
+    try:
+        import ctypes
+        ctypes.CDLL(None, use_errno=True).prctl(1, signal.SIGTERM)  # PR_SET_PDEATHSIG
+    except Exception:  # noqa: BLE001 - best effort
+        pass
+
+
 def run_child(cmd, env, deadline, what, n_gpus=None):
-    """Run `cmd` (its own session) relaying its stdout; past `deadline` seconds end it -- SIGTERM
-    to its group (torchrun then stops its workers), SIGKILL 15 s later to that group and to every
-    rank that wrote a heartbeat (torchrun starts each worker in a session of its own) -- and print
+    """Run `cmd` relaying its stdout; past `deadline` seconds end it -- SIGTERM (torchrun then
+    stops its workers), SIGKILL 15 s later to it and to every rank that wrote a heartbeat, with
+    that rank's process group (torchrun starts each worker in a session of its own) -- and print
     one JSON line {"error": "timeout", "heartbeats": [...]}; returns the child's status (5 on a
-    timeout).  A child that fails without printing a bench line gets an error line too."""
+    timeout).  A child that fails without printing a bench line gets an error line too.  The
+    child stays in this process's group and dies with it (PR_SET_PDEATHSIG)."""
     hb_dir = tempfile.mkdtemp(prefix="bh_bench_hb_")
     env = dict(env)
     env[HEARTBEAT_ENV] = hb_dir
     # the ranks give up on a collective before the parent gives up on them
     env.setdefault("BH_COMM_TIMEOUT_S", str(max(10, int(deadline / 3))))
     t0 = time.monotonic()
-    proc = subprocess.Popen(cmd, env=env, start_new_session=True, stdout=subprocess.PIPE,
-                            text=True, bufsize=1)
+    proc = subprocess.Popen(cmd, env=env, stdout=subprocess.PIPE, text=True, bufsize=1,
+                            preexec_fn=_die_with_parent)
     saw_line = threading.Event()
 
     def relay():
@@ -199,12 +210,11 @@ def run_child(cmd, env, deadline, what, n_gpus=None):
         rc = proc.wait(timeout=deadline)
     except subprocess.TimeoutExpired:
         beats = read_heartbeats(hb_dir)
-        _kill_group(proc.pid, signal.SIGTERM)
+        proc.terminate()
         try:
             proc.wait(timeout=15)
         except subprocess.TimeoutExpired:
-            pass
-        _kill_group(proc.pid, signal.SIGKILL)
+            proc.kill()
         for b in beats:  # the workers torchrun started in sessions of their own
             if isinstance(b.get("pid"), int) and b["pid"] != os.getpid():
                 _kill_group(b["pid"], signal.SIGKILL)

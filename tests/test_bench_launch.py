@@ -117,3 +117,34 @@ def test_watchdog_reports_a_child_that_fails_without_a_line(capsys):
     assert rc == 7
     line = json.loads([ln for ln in capsys.readouterr().out.splitlines() if ln.startswith("{")][-1])
     assert line["error"] == "child exited with 7"
+
+
+_PARENT = """
+import os, sys
+sys.path.insert(0, sys.argv[1])
+import bench
+bench.run_child([sys.executable, "-c",
+                 "import os, sys, time; open(sys.argv[1], 'w').write(str(os.getpid())); time.sleep(120)",
+                 sys.argv[2]], dict(os.environ), 120.0, "dummy", 2)
+"""
+
+
+def test_watchdog_child_dies_with_the_parent(tmp_path):
+    """Whoever runs the bench may kill its parent outright (SIGKILL): the measuring child must
+    not outlive it on the GPUs -- it gets SIGTERM from the kernel (PR_SET_PDEATHSIG)."""
+    import signal
+    pidfile = tmp_path / "child.pid"
+    parent = subprocess.Popen([sys.executable, "-c", _PARENT, ROOT, str(pidfile)])
+    for _ in range(200):
+        if pidfile.exists() and pidfile.read_text():
+            break
+        time.sleep(0.05)
+    child = int(pidfile.read_text())
+    assert _alive(child)
+    parent.send_signal(signal.SIGKILL)
+    parent.wait(timeout=10)
+    for _ in range(100):
+        if not _alive(child):
+            break
+        time.sleep(0.05)
+    assert not _alive(child), "the child outlived the killed watchdog parent"
