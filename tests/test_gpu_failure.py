@@ -199,3 +199,59 @@ def test_calls_during_an_async_step_are_refused():
     want = _oracle_after(arrs, 0.5, 4)
     _assert_arrays_equal(eng.get_bodies(), want, "after the async call")
     eng.close()
+
+
+@pytest.mark.parametrize("exchange", ["copy", "rccl"])
+def test_injection_sweep_never_hangs(exchange, monkeypatch):
+    """Every injection point of a 2-step call: a member fails before each of its collectives
+    (100 + k) and, in-process, before each of its group barriers (200 + k) in turn -- the call
+    always raises within seconds, every member refuses the next call, and after the reset two
+    steps equal the single-GPU engine's.  (3 members on device 0 for 'copy'; the one-rank RCCL
+    handle for 'rccl'.)"""
+    if exchange == "rccl":
+        monkeypatch.setenv("BH_MULTI_EXCHANGE", "rccl")
+        monkeypatch.setenv("BH_LET", "1")
+        devices = [0]
+    else:
+        devices = [0, 0, 0]
+    arrs = scenes.two_disks(8000, 2000)
+    p = bh_amd.default_params(theta=0.5)
+    single = bh_amd.Engine(p, device=0)
+    single.reset_bodies(*arrs)
+    single.step(2)
+    want = single.get_bodies()
+    single.close()
+    eng = bh_amd.Engine(p, devices=devices)
+    eng.reset_bodies(*arrs)
+    eng.collective_log_clear()
+    eng.step(2)  # how many collectives a 2-step call issues from a reset
+    n_coll = len(eng.member(0).collective_log())
+    assert n_coll > 0
+    points = [100 + k for k in range(0, n_coll)]
+    if exchange == "copy":
+        points += [200 + k for k in range(0, 2 * n_coll, 2)]
+    victim = len(devices) - 1
+    failed = 0
+    for what in points:
+        eng.reset_bodies(*arrs)
+        eng.member(victim).debug_inject(what)
+        t0 = time.monotonic()
+        try:
+            eng.step(2)
+            tripped = False
+        except bh_amd.BhError as err:
+            tripped = True
+            assert err.rc in (bh_amd.BH_E_COMM, bh_amd.BH_E_DEVICE), (what, err)
+        assert time.monotonic() - t0 < 60.0, what
+        if not tripped:  # (fewer barriers than that in the call: the fault stays armed)
+            continue
+        failed += 1
+        for r in range(eng.multi_world()):
+            assert eng.member(r).progress()["failed"], (what, r)
+        with pytest.raises(bh_amd.BhError):
+            eng.step(1)
+        eng.reset_bodies(*arrs)
+        eng.step(2)
+        _assert_arrays_equal(eng.get_bodies(), want, f"after the fault {what}")
+    assert failed >= n_coll, (failed, n_coll)
+    eng.close()
