@@ -49,6 +49,27 @@ __device__ __forceinline__ double as_f64(uint32_t lo, uint32_t hi) {
     return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
 }
 
+// Which lanes are active at a stop (cur >= the lane's resume point).  BH_TRAV_STACK 0: a per-lane
+// compare at every stop and a per-lane `resume = next` in every point-force block.  1 (round 6):
+// the active set is a wave-uniform mask that changes only at "mixed" internal nodes -- some
+// active lanes accept the node, others open it: the accepting lanes park until the cursor reaches
+// the node's `next`.  Parked subtrees nest (a node pushed later lies inside the earlier ones), so
+// their `next` values form a stack: its top in an SGPR, the entries below in one VGPR, entry i in
+// lane i (v_writelane / v_readlane), the parked lanes' `next` in a per-lane VGPR written only at
+// mixed nodes.  When the cursor reaches the top, every lane whose `next` equals it is active
+// again (one compare per pop).  The mask is the per-lane compare's at every stop, exactly: a lane
+// active again keeps a stale `next` below every entry pushed after it.  At C3: ~645 stops and
+// ~548 blocks per wave against ~106 mixed nodes.  Measured (profiles/r06p_*):
+// bit-exact, VALU per wave 21572 -> 20758 (-3.8 %), but SALU 10416 -> 15537 (the pop test at
+// every stop, the park test at every internal node) and k_traverse 0.768 -> 0.797 ms (+3.7 %):
+// the wave is issue-bound over both units, so the trade loses.  Off by default.
+#ifndef BH_TRAV_STACK
+#define BH_TRAV_STACK 0
+#endif
+// (the stack holds one entry per tree level above the cursor: depth < MAX_DEPTH_TAB <= 64 lanes)
+static_assert(MAX_DEPTH_TAB <= 64, "the parked-subtree stack holds one level per lane");
+// v_writelane_b32 (the lane select goes through M0; no clang builtin on this toolchain)
+extern "C" __device__ int bh_writelane(int value, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
 template <bool FAST, bool COUNT, bool OFF32>
 __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T, double bx,
                                      double by, double Gm, double soft2, double theta2,
@@ -56,6 +77,11 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
                                      double &fy, uint32_t &nvis, uint32_t &niters,
                                      uint32_t &ncontrib, uint32_t &nblocks) {
     uint32_t cur = 0;
+#if BH_TRAV_STACK
+    uint64_t active = __builtin_amdgcn_ballot_w64(resume == 0u);  // (idle lanes never are)
+    uint32_t top = 0xFFFFFFFFu, sp = 0u;  // the stack's top and its entries below, wave-uniform
+    uint32_t below = 0u;                  // entry i of those in lane i
+#endif
     // one iteration on record `rec`; the next record is requested into `nrec`.  The loop body
     // is unrolled twice with the two records swapping roles (no SGPR copies per iteration).
     // Loading node T (past the last one) is harmless: the node array has slack beyond T.
@@ -77,7 +103,20 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
             return;
         }
         // lane masks in SGPRs straight from the compares; per-lane booleans via inverse ballot
+#if BH_TRAV_STACK
+        while (cur >= top) {  // the cursor left a parked subtree: its lanes walk again
+            active |= __builtin_amdgcn_ballot_w64(resume == top);
+            if (sp == 0u) {
+                top = 0xFFFFFFFFu;
+            } else {
+                --sp;
+                top = (uint32_t)__builtin_amdgcn_readlane((int)below, (int)sp);
+            }
+        }
+        const uint64_t act_m = active;
+#else
         const uint64_t act_m = __builtin_amdgcn_ballot_w64(cur >= resume);
+#endif
         if (COUNT) {
             nvis += __builtin_amdgcn_inverse_ballot_w64(act_m) ? 1u : 0u;
             niters += 1;
@@ -111,6 +150,17 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
             }
             contrib_m = act_m & acc_m;
             open_m = act_m & ~acc_m;
+#if BH_TRAV_STACK
+            if (open_m != 0ull && contrib_m != 0ull) {  // mixed: the accepting lanes park
+                if (top != 0xFFFFFFFFu) {
+                    below = (uint32_t)bh_writelane((int)top, (int)sp, (int)below);
+                    ++sp;
+                }
+                top = next;  // (<= the entry below: this node lies inside that subtree)
+                active &= ~contrib_m;
+                if (__builtin_amdgcn_inverse_ballot_w64(contrib_m)) resume = next;
+            }
+#endif
         }
         const uint32_t ncur = open_m != 0ull ? cur + 1 : next;  // descend iff some lane opened
         nrec = OFF32 ? nload_off(nodes, ncur) : nload(nodes + ncur);
@@ -133,7 +183,9 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
             const double f = Gm * mass * invR2;
             fx += f * dx * invR;
             fy += f * dy * invR;
+#if !BH_TRAV_STACK
             resume = next;
+#endif
         }
         nwait(nrec);
         cur = ncur;
