@@ -23,7 +23,18 @@
 namespace bh {
 namespace {
 
+// Workgroups in runs of BH_TRAV_XCD_RUN consecutive waves per XCD (bh_device.hpp): neighbouring
+// waves walk nearly the same nodes, so a run shares its XCD's L2 (C3 -1.5 % at runs of 32..512
+// against the round-robin default).
+#ifndef BH_TRAV_XCD_RUN
+#define BH_TRAV_XCD_RUN 64
+#endif
 constexpr int TB = 64;  // one wave per workgroup: finest dispatch granularity (C4 -1.5 %, C3 -0.5 %)
+// Waves per workgroup of k_traverse: up to MAX_WPB, chosen per launch (waves_per_group below).
+// A workgroup's waves share one CU and its scalar data cache, and neighbouring waves walk nearly
+// the same node records.
+constexpr int MAX_WPB = 8;
+static_assert(BH_TRAV_XCD_RUN % MAX_WPB == 0, "an XCD run holds whole workgroups");
 
 typedef double double4_t __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x8 __attribute__((ext_vector_type(8)));
@@ -203,12 +214,6 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
     }
 }
 
-// Workgroups in runs of BH_TRAV_XCD_RUN consecutive waves per XCD (bh_device.hpp): neighbouring
-// waves walk nearly the same nodes, so a run shares its XCD's L2 (C3 -1.5 % at runs of 32..512
-// against the round-robin default).
-#ifndef BH_TRAV_XCD_RUN
-#define BH_TRAV_XCD_RUN 64
-#endif
 
 #ifdef BH_TRAV_TIMING  // diagnostic build only: per-wave wall-clock start / end, hardware ids
 constexpr int TRAV_TIMING_MAX = 1 << 18;
@@ -255,8 +260,9 @@ __device__ __forceinline__ void trav_wave(uint32_t v, uint32_t bpw, uint64_t t_s
                                           const KickArgs &kick,
                                           const uint32_t *__restrict__ lanes,
                                           const WaveOrder &wo) {
-    const bool in_wave = threadIdx.x < bpw;
-    const int64_t q = lo + (int64_t)v * bpw + threadIdx.x;  // lane
+    const uint32_t lane = threadIdx.x & 63u;
+    const bool in_wave = lane < bpw;
+    const int64_t q = lo + (int64_t)v * bpw + lane;  // lane
     const uint32_t lp = lanes && in_wave && q < hi ? lanes[q] : (uint32_t)q;
     const bool valid = in_wave && q < hi && (!lanes || lp != LANE_IDLE);
     const int64_t p = lanes ? (int64_t)lp : q;  // its body's slot
@@ -286,15 +292,15 @@ __device__ __forceinline__ void trav_wave(uint32_t v, uint32_t bpw, uint64_t t_s
     else
         walk<false, COUNT, OFF32>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx,
                                   fy, nvis, niters, ncontrib, nblocks);
-    if (wo.cost && threadIdx.x == 0 && q < hi)
+    if (wo.cost && lane == 0 && q < hi)
         wo.cost[v] = (uint32_t)(wall_clock64() - t_start < 0xFFFFFFull
                                     ? wall_clock64() - t_start : 0xFFFFFFull);
-    if (COUNT && (threadIdx.x & 63) == 0) {
+    if (COUNT && lane == 0 && lo + (int64_t)v * bpw < hi) {  // (a workgroup's last waves may be empty)
         cnt.wave_iters[v] = niters;
         cnt.wave_blocks[v] = nblocks;
     }
 #ifdef BH_TRAV_TIMING
-    if (threadIdx.x == 0 && v < TRAV_TIMING_MAX) {
+    if (lane == 0 && v < TRAV_TIMING_MAX) {
         uint64_t *t = g_trav_times + 4 * v;
         t[0] = t_start;
         t[1] = wall_clock64();
@@ -361,7 +367,7 @@ __device__ __forceinline__ void trav_wave(uint32_t v, uint32_t bpw, uint64_t t_s
 }
 
 template <bool COUNT, bool OFF32, int KICK>
-__global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
+__global__ __launch_bounds__(TB * MAX_WPB) void k_traverse(const Node *__restrict__ nodes,
                                                  const uint32_t *__restrict__ d_T, double *x,
                                                  double *y, const double *__restrict__ m,
                                                  const uint32_t *__restrict__ cidx,
@@ -369,13 +375,19 @@ __global__ __launch_bounds__(TB) void k_traverse(const Node *__restrict__ nodes,
                                                  Geometry g, double *__restrict__ a2,
                                                  TraverseCounters cnt, KickArgs kick,
                                                  const uint32_t *__restrict__ lanes,
-                                                 WaveOrder wo, uint32_t bpw) {
+                                                 WaveOrder wo, uint32_t bpw, uint32_t wpb) {
 #if defined(BH_TRAV_TIMING)
     const uint64_t t_start = wall_clock64();
 #else
     const uint64_t t_start = wo.cost ? wall_clock64() : 0;
 #endif
-    uint32_t v = xcd_block<BH_TRAV_XCD_RUN>();
+    // xcd_block() with runs of BH_TRAV_XCD_RUN / wpb workgroups (= BH_TRAV_XCD_RUN waves)
+    uint32_t b = blockIdx.x;
+    {
+        const uint32_t C = BH_TRAV_XCD_RUN / wpb, G = 8 * C, full = gridDim.x / G;
+        if (b < full * G) b = (b / 8 / C) * G + (b % 8) * C + (b / 8) % C;
+    }
+    uint32_t v = b * wpb + (threadIdx.x >> 6);
     if (wo.order)  // the v-th run to start is the order[v]-th run of waves (wave_order)
         v = wo.order[v / BH_TRAV_XCD_RUN] * BH_TRAV_XCD_RUN + v % BH_TRAV_XCD_RUN;
     trav_wave<COUNT, OFF32, KICK>(v, bpw, t_start, nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2,
@@ -519,6 +531,27 @@ uint32_t bodies_per_wave(int64_t lanes) {
     return bpw;
 }
 
+// Waves per workgroup for a launch of `waves` waves (profiles/r06s_*, r06t_wpb_sweep.jsonl, two
+// interleaved rounds; ms per step for 1 / 2 / 4 / 8 waves per group):
+//   C2 (1 563 waves)   0.507 / 0.489 / 0.500 / 0.478  -- 8 neighbouring waves on one CU share its
+//                      scalar cache (196 groups: a quarter of the CUs idle, still the fastest)
+//   C3 (15.6 K waves)  1.770 / 1.782 / 1.757 / 1.801
+//   C4 (156 K waves)   16.45 / 16.51 / 16.38 / 16.40;  the solo C4 / 8 rank step within noise
+//   C1 (1 563 waves of 8 bodies)  +1.5 % with 2: short walks keep one wave per group.
+// BH_TRAV_WPB (1, 2, 4, 8) overrides.
+#ifndef BH_TRAV_WPB_FULL_WAVES
+#define BH_TRAV_WPB_FULL_WAVES 8192
+#endif
+static uint32_t waves_per_group(uint32_t waves, uint32_t bpw) {
+    static const long over = [] {
+        const char *v = std::getenv("BH_TRAV_WPB");
+        return v ? std::atol(v) : 0L;
+    }();
+    if (over == 1 || over == 2 || over == 4 || over == 8) return (uint32_t)over;
+    if (bpw < TB) return 1u;  // (short walks of a few bodies: C1 +1.5 % with 2)
+    return waves >= BH_TRAV_WPB_FULL_WAVES ? 4u : waves >= 1024 ? 8u : 1u;
+}
+
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
               const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, const TraverseCounters *cnt,
@@ -526,17 +559,19 @@ void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x
     if (hi <= lo) return;
     // (the counting walk keeps 64 bodies per wave: its per-wave counters define lane efficiency)
     const uint32_t bpw = cnt ? (uint32_t)TB : bodies_per_wave(hi - lo);
-    unsigned grid = (unsigned)((hi - lo + bpw - 1) / bpw);
+    unsigned grid = (unsigned)((hi - lo + bpw - 1) / bpw);  // waves
     const WaveOrder w = wo && bpw == TB && wave_order_runs(hi - lo) ? *wo : WaveOrder{};
     if (w.order)  // whole runs: every run index the order maps to exists in the grid
         grid = (unsigned)(wave_order_runs(hi - lo) * BH_TRAV_XCD_RUN);
+    const uint32_t wpb = waves_per_group(grid, bpw);
+    grid = (grid + wpb - 1) / wpb;  // workgroups
     // node records addressed by a 32-bit byte offset while the array stays below 4 GiB
     const bool off32 = node_cap * sizeof(Node) < (size_t(1) << 32);
     const KickArgs ka = kick ? *kick : KickArgs{KICK_NONE, nullptr, nullptr, 0.0, 0.0, nullptr};
     const TraverseCounters tc = cnt ? *cnt : TraverseCounters{nullptr, nullptr, nullptr, nullptr};
 #define BH_TRAV(C, O, K) \
-    k_traverse<C, O, K><<<grid, TB, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, tc, ka, \
-                                            lanes, w, bpw)
+    k_traverse<C, O, K><<<grid, TB * wpb, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, tc, \
+                                                  ka, lanes, w, bpw, wpb)
     if (cnt) {  // diagnostic counting walk: accelerations out, never fused
         if (off32) BH_TRAV(true, true, KICK_NONE);
         else BH_TRAV(true, false, KICK_NONE);

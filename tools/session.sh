@@ -10,7 +10,8 @@
 #   configs        one bench line per BASELINE configuration (c1_baseline, c1_code, c2, c4, c5)
 #   profile        rocprofv3 kernel trace + stats and FETCH_SIZE / WRITE_SIZE passes of C3
 #                  (tools/profile.sh; CONFIG=c5 etc. for another workload) -> prof_<CONFIG>/
-#   sq             SQ counters of the traversal (tools/profile_sq.sh)
+#   sq             SQ counters of the traversal (tools/profile_sq.sh; CONFIG=c2 etc., SQ_CACHE=1 adds
+#                  scalar-cache and L2 hit counters)
 #   timed          the C3 bench's timed call alone: kernel trace, FETCH / WRITE passes, summarised
 #                  over that call only (tools/timed_window.py)               -> ${TAG}_c3_timed*
 #   timeline       one C3 bench under a kernel trace, summarised per step (tools/timeline.py)
@@ -58,7 +59,7 @@ for step in "$@"; do
     profile) run 1800 ${O}_profile.log bash tools/profile.sh ;;
     sq)
       run 900 ${O}_sq.log bash tools/profile_sq.sh
-      run 120 ${O}_sq_sum.log python3 tools/summarize_sq.py gpurun_out/prof_sq ${O}_c3
+      run 120 ${O}_sq_sum.log python3 tools/summarize_sq.py gpurun_out/prof_sq ${O}_${CONFIG:-c3}
       rm -rf gpurun_out/prof_sq/p* ;;  # (raw counter files: gpurun_out travels back only under 64 MiB)
     timed)  # the driver's C3 call alone under rocprofv3 (no drop-in / counter / verify legs):
             # kernel trace + stats, FETCH_SIZE and WRITE_SIZE passes, summarised over the timed

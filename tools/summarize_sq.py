@@ -33,7 +33,8 @@ def main():
             acc[c].append(v)
     avg = {c: sum(v) / len(v) for c, v in acc.items()}
     waves = avg.get("SQ_WAVES", 0.0)
-    out = [f"## {KERNEL.strip(', ')}...> SQ counters (C3, average per dispatch; rocprofv3 --pmc, "
+    config = os.environ.get("CONFIG", "c3")
+    out = [f"## {KERNEL.strip(', ')}...> SQ counters ({config.upper()}, average per dispatch; rocprofv3 --pmc, "
            f"{len([d for d in glob.glob(os.path.join(src, 'p*')) if os.path.isdir(d)])} passes)", "",
            "| counter | per dispatch | per wave |", "|---|---|---|"]
     for c in sorted(avg):
@@ -54,6 +55,13 @@ def main():
         out.append(f"- wave time split: active {100 * avg.get('SQ_ACTIVE_INST_ANY', 0) / wc:.0f} %, "
                    f"waiting on memory (WAIT_ANY) {100 * avg.get('SQ_WAIT_ANY', 0) / wc:.0f} %, "
                    f"waiting for issue (WAIT_INST_ANY) {100 * avg.get('SQ_WAIT_INST_ANY', 0) / wc:.0f} %")
+    if avg.get("SQC_DCACHE_REQ"):
+        out.append(f"- scalar data cache: {100 * avg.get('SQC_DCACHE_HITS', 0) / avg['SQC_DCACHE_REQ']:.1f} % "
+                   f"hits, {avg.get('SQC_TC_DATA_READ_REQ', 0) / waves if waves else 0:.0f} L2 read "
+                   f"requests per wave (SQC_TC_DATA_READ_REQ)")
+    if avg.get("TCC_HIT", 0) + avg.get("TCC_MISS", 0):
+        out.append(f"- L2 (all requests of the kernel): "
+                   f"{100 * avg['TCC_HIT'] / (avg['TCC_HIT'] + avg.get('TCC_MISS', 0)):.1f} % hits")
     open(prefix + "_sq_summary.md", "w").write("\n".join(out) + "\n")
     if KERNEL.startswith("k_traverse") and "GRBM_GUI_ACTIVE" in avg and "SQ_ACTIVE_INST_VALU" in avg:
         path = os.path.join(os.path.dirname(prefix) or ".", "valu_busy.json")
@@ -61,7 +69,7 @@ def main():
             doc = json.load(open(path))
         except (OSError, ValueError):
             doc = {}
-        doc.setdefault("c3", {})["k_traverse"] = {
+        doc.setdefault(config, {})["k_traverse"] = {
             "valu_busy": round(busy / klen, 4),
             "valu_insts_per_wave": round(avg.get("SQ_INSTS_VALU", 0) / waves) if waves else None,
             "method": "SQ_ACTIVE_INST_VALU x 4 / 1024 SIMDs over GRBM_GUI_ACTIVE / 8 XCDs",
