@@ -215,6 +215,173 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
 }
 
 
+// ---- one body per wave, breadth first (small launches) -----------------------------------
+// A walk is a chain of dependent stops -- the next node is known only after the criterion at
+// this one -- so a launch of a few thousand waves (C1's 12 500 bodies) lasts as long as one
+// wave's ~250-350 stops at ~0.3 us each, whatever the GPU's width.  Here the whole wave serves
+// ONE body and examines the tree level by level: every lane takes one opened node of the current
+// level and examines its children (chasing `next` from node + 1), so the chain is the tree's depth
+// (~15 levels), not the body's visit count.  Accepted nodes are marked in an LDS bitmap over node
+// indices; since the flattened tree is in pre-order, the reference's DFS order of the terms
+// (BHA:215-239) IS ascending node index, so the set bits read in ascending order give the terms
+// in the order walk() adds them.  The terms are then evaluated 64 at a time, one per lane, and
+// added into the sums in that order by one lane each (fx: lane 0, fy: lane 1).  Each term is the
+// same expression as walk<true>'s, and the sum is the same sequence of additions from +0.0:
+// bit-identical.  A body whose levels or accepted set exceed the LDS buffers, or whose tree
+// exceeds the bitmap, is walked by walk() instead (the caller), so every body gets its exact sum.
+constexpr uint32_t BFS_E_CAP = 128;  // opened nodes per level (two buffers of (node, next))
+constexpr uint32_t BFS_A_CAP = 4 * BFS_E_CAP;  // accepted nodes per body (in the same space)
+// LDS bytes of one wave: the bitmap, the level buffers / accepted list, two counters, the terms
+__host__ __device__ constexpr size_t bfs_lds_bytes(uint32_t bm_words) {
+    return sizeof(uint32_t) * ((size_t)bm_words + 4 * BFS_E_CAP + 4) + sizeof(double) * 2 * 64;
+}
+
+__device__ __forceinline__ double rfl_f64(double v) {  // lane 0's value in every lane
+    const long long b = __double_as_longlong(v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)b);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(b >> 32));
+    return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+
+__device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, uint32_t &total) {
+    uint32_t x = v;
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint32_t y = (uint32_t)__shfl_up((int)x, d, 64);
+        if (lane >= (uint32_t)d) x += y;
+    }
+    total = (uint32_t)__shfl((int)x, 63, 64);
+    return x - v;
+}
+
+// false: a buffer overflowed (the caller walks the body with walk()).  fx, fy: wave-uniform.
+__device__ bool bfs_walk(const Node *__restrict__ nodes, uint32_t T, double bx, double by,
+                         double Gm, double soft2, double theta2, double s2root, uint32_t *lds,
+                         uint32_t bm_words, double &fx, double &fy) {
+    const uint32_t lane = threadIdx.x & 63u;
+    fx = 0.0;
+    fy = 0.0;
+    if (T == 0) return true;  // an empty tree
+    const uint32_t nbw = (T + 31u) / 32u;
+    if (nbw > bm_words) return false;
+    uint32_t *bits = lds;
+    uint2 *E0 = reinterpret_cast<uint2 *>(lds + bm_words);
+    uint2 *E1 = E0 + BFS_E_CAP;
+    uint32_t *ctr = lds + bm_words + 4 * BFS_E_CAP;  // [0]: next level's count, [1]: overflow
+    double *terms = reinterpret_cast<double *>(ctr + 4);
+    for (uint32_t w = lane; w < nbw; w += 64) bits[w] = 0u;
+    // the criterion at node c (BHA:216-228 in walk<true>'s fast form): 0 accept, 1 open
+    auto opens = [&](const Node &r) __attribute__((always_inline)) -> bool {
+        if (r.meta & NODE_LEAF) return false;  // (massless cells carry the leaf flag too)
+        const double dx = r.comX - bx, dy = r.comY - by;
+        const double d2 = dx * dx + dy * dy + soft2;
+        const uint64_t s2b = (uint64_t)__double_as_longlong(s2root) -
+                             ((uint64_t)(r.meta & NODE_DEPTH2_MASK) << 52);
+        return !(__longlong_as_double((long long)s2b) < theta2 * d2);
+    };
+    uint32_t nE = 0;
+    {
+        const Node r = nodes[0];  // (every lane: the same address)
+        if (opens(r)) {
+            if (lane == 0) E0[0] = make_uint2(0u, r.next > 0u ? r.next : 1u);
+            nE = 1;
+        } else if (lane == 0) {
+            bits[0] = 1u;
+        }
+    }
+    if (lane == 0) {
+        ctr[0] = 0u;
+        ctr[1] = 0u;
+    }
+    __syncthreads();
+    while (nE > 0) {
+        for (uint32_t i = lane; i < nE; i += 64) {  // lane: one opened node, all its children
+            const uint2 e = E0[i];
+            uint32_t c = e.x + 1u;  // first child (pre-order)
+            if (c >= e.y) continue;
+            Node r = nodes[c];
+            while (true) {
+                const uint32_t nx = r.next > c ? r.next : c + 1u;
+                const bool more = nx < e.y;
+                Node rn;
+                if (more) rn = nodes[nx];  // the next sibling's record, before this criterion
+                if (opens(r)) {
+                    const uint32_t at = atomicAdd(&ctr[0], 1u);
+                    if (at < BFS_E_CAP) E1[at] = make_uint2(c, nx);
+                    else ctr[1] = 1u;
+                } else {
+                    atomicOr(&bits[c >> 5], 1u << (c & 31u));
+                }
+                if (!more) break;
+                r = rn;
+                c = nx;
+            }
+        }
+        __syncthreads();
+        nE = __builtin_amdgcn_readfirstlane(ctr[0]);
+        const uint32_t over = __builtin_amdgcn_readfirstlane(ctr[1]);
+        __syncthreads();
+        if (over) return false;
+        if (lane == 0) ctr[0] = 0u;
+        uint2 *t = E0;
+        E0 = E1;
+        E1 = t;
+        __syncthreads();
+    }
+    // the accepted nodes in ascending order: each lane a contiguous run of bitmap words
+    uint32_t *A = reinterpret_cast<uint32_t *>(lds + bm_words);  // (the level buffers' space)
+    const uint32_t per = (nbw + 63u) / 64u, w0 = min(lane * per, nbw), w1 = min(w0 + per, nbw);
+    uint32_t cnt = 0;
+    for (uint32_t w = w0; w < w1; ++w) cnt += (uint32_t)__popc(bits[w]);
+    uint32_t nA = 0;
+    uint32_t at = wave_excl_scan(cnt, lane, nA);
+    if (nA > BFS_A_CAP) return false;
+    for (uint32_t w = w0; w < w1; ++w) {
+        uint32_t b = bits[w];
+        while (b) {
+            const uint32_t k = (uint32_t)__ffs((int)b) - 1u;
+            A[at++] = w * 32u + k;
+            b &= b - 1u;
+        }
+    }
+    __syncthreads();
+    // the terms, 64 at a time; lane 0 adds the x terms and lane 1 the y terms, in order
+    double acc = 0.0;
+    for (uint32_t base = 0; base < nA; base += 64) {
+        const uint32_t i = base + lane;
+        if (i < nA) {
+            const Node r = nodes[A[i]];
+            const double dx = r.comX - bx;  // BHA:251-253
+            const double dy = r.comY - by;
+            const double d2 = dx * dx + dy * dy + soft2;
+            double h;
+            const double sr = sqrt_rn_inrange_h(d2, h);
+            const double invR = rcp_rn_seeded(sr, h + h);
+            const double invR2 = rcp_rn_seeded(d2, invR * invR);
+            const double f = Gm * r.mass * invR2;  // BHA:256
+            terms[lane] = f * dx * invR;           // BHA:257-258
+            terms[64 + lane] = f * dy * invR;
+        }
+        __syncthreads();
+        if (lane < 2) {  // (reads issued 16 ahead of the dependent additions)
+            const uint32_t m = min(64u, nA - base);
+            const double *tl = terms + 64 * lane;
+            uint32_t j = 0;
+            for (; j + 16 <= m; j += 16) {
+                double t[16];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) t[u] = tl[j + u];
+#pragma unroll
+                for (int u = 0; u < 16; ++u) acc += t[u];
+            }
+            for (; j < m; ++j) acc += tl[j];
+        }
+        __syncthreads();
+    }
+    fx = __shfl(acc, 0, 64);
+    fy = __shfl(acc, 1, 64);
+    return true;
+}
+
 #ifdef BH_TRAV_TIMING  // diagnostic build only: per-wave wall-clock start / end, hardware ids
 constexpr int TRAV_TIMING_MAX = 1 << 18;
 __device__ uint64_t g_trav_times[4 * TRAV_TIMING_MAX];
@@ -249,7 +416,7 @@ __device__ __forceinline__ void own_kick(int64_t q, double bx, double by, double
 // it through the leaf records), so the update in place is race-free and a2 is not written.
 // Wave v evaluates the bpw lanes [lo + bpw v, lo + bpw v + bpw) (64 = one body per lane; fewer
 // for small launches, the wave's other lanes idle -- see traverse()): walk, then the epilogue.
-template <bool COUNT, bool OFF32, int KICK>
+template <bool COUNT, bool OFF32, int KICK, bool BFS>
 __device__ __forceinline__ void trav_wave(uint32_t v, uint32_t bpw, uint64_t t_start,
                                           const Node *__restrict__ nodes,
                                           const uint32_t *__restrict__ d_T, double *x, double *y,
@@ -259,7 +426,8 @@ __device__ __forceinline__ void trav_wave(uint32_t v, uint32_t bpw, uint64_t t_s
                                           double *__restrict__ a2, const TraverseCounters &cnt,
                                           const KickArgs &kick,
                                           const uint32_t *__restrict__ lanes,
-                                          const WaveOrder &wo) {
+                                          const WaveOrder &wo, uint32_t *lds,
+                                          uint32_t bm_words) {
     const uint32_t lane = threadIdx.x & 63u;
     const bool in_wave = lane < bpw;
     const int64_t q = lo + (int64_t)v * bpw + lane;  // lane
@@ -286,7 +454,18 @@ __device__ __forceinline__ void trav_wave(uint32_t v, uint32_t bpw, uint64_t t_s
     const uint32_t T = __builtin_amdgcn_readfirstlane(*d_T);
     const bool fast = fast_s2_ok(s2root) &&
         __ballot(walks && !(lane_fast_ok(bx, by, soft2) && lane_self_ok(Gm, bm))) == 0ull;
-    if (fast)
+    bool walked = false;
+    if (BFS && fast && (__ballot(walks) & 1ull)) {  // one body per wave: lane 0's (bpw == 1)
+        double ux, uy;
+        walked = bfs_walk(nodes, T, rfl_f64(bx), rfl_f64(by), rfl_f64(Gm), soft2, theta2, s2root,
+                          lds, bm_words, ux, uy);
+        if (walked) {
+            fx = ux;
+            fy = uy;
+        }
+    }
+    if (walked) {
+    } else if (fast)
         walk<true, COUNT, OFF32>(nodes, T, bx, by, Gm, soft2, theta2, s2root, self, resume, fx,
                                  fy, nvis, niters, ncontrib, nblocks);
     else
@@ -366,7 +545,7 @@ __device__ __forceinline__ void trav_wave(uint32_t v, uint32_t bpw, uint64_t t_s
     }
 }
 
-template <bool COUNT, bool OFF32, int KICK>
+template <bool COUNT, bool OFF32, int KICK, bool BFS>
 __global__ __launch_bounds__(TB * MAX_WPB) void k_traverse(const Node *__restrict__ nodes,
                                                  const uint32_t *__restrict__ d_T, double *x,
                                                  double *y, const double *__restrict__ m,
@@ -375,7 +554,9 @@ __global__ __launch_bounds__(TB * MAX_WPB) void k_traverse(const Node *__restric
                                                  Geometry g, double *__restrict__ a2,
                                                  TraverseCounters cnt, KickArgs kick,
                                                  const uint32_t *__restrict__ lanes,
-                                                 WaveOrder wo, uint32_t bpw, uint32_t wpb) {
+                                                 WaveOrder wo, uint32_t bpw, uint32_t wpb,
+                                                 uint32_t bm_words) {
+    extern __shared__ uint32_t trav_lds[];  // (bfs_walk only: bfs_lds_bytes(bm_words))
 #if defined(BH_TRAV_TIMING)
     const uint64_t t_start = wall_clock64();
 #else
@@ -390,8 +571,8 @@ __global__ __launch_bounds__(TB * MAX_WPB) void k_traverse(const Node *__restric
     uint32_t v = b * wpb + (threadIdx.x >> 6);
     if (wo.order)  // the v-th run to start is the order[v]-th run of waves (wave_order)
         v = wo.order[v / BH_TRAV_XCD_RUN] * BH_TRAV_XCD_RUN + v % BH_TRAV_XCD_RUN;
-    trav_wave<COUNT, OFF32, KICK>(v, bpw, t_start, nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2,
-                                  cnt, kick, lanes, wo);
+    trav_wave<COUNT, OFF32, KICK, BFS>(v, bpw, t_start, nodes, d_T, x, y, m, cidx, lo, hi, fp, g,
+                                       a2, cnt, kick, lanes, wo, trav_lds, bm_words);
 }
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {  // splitmix64 finaliser
@@ -552,41 +733,75 @@ static uint32_t waves_per_group(uint32_t waves, uint32_t bpw) {
     return waves >= BH_TRAV_WPB_FULL_WAVES ? 4u : waves >= 1024 ? 8u : 1u;
 }
 
+// Breadth-first walks (bfs_walk, one body per wave) for launches of up to BH_TRAV_BFS_MAX bodies
+// (environment override; 0: never).  Measured (profiles/r06z2_*): C1 'R' (2 000 bodies) traversal
+// 67.5 -> 39.8 us; C1 code default (12 500) 102 -> 135 us -- 12 500 one-body waves are ~3
+// generations of ~40 us walks, against 1 563 eight-body union walks of ~100 us.  The bitmap covers min(node capacity, 2.25 x bodies + 256, 64 K)
+// node indices -- a tree beyond it is walked by walk() body by body.
+#ifndef BH_TRAV_BFS_MAX
+#define BH_TRAV_BFS_MAX 4096
+#endif
+constexpr uint32_t BFS_MAX_BM_WORDS = 2048;
+static int64_t bfs_max_bodies() {
+    static const int64_t v = [] {
+        const char *e = std::getenv("BH_TRAV_BFS_MAX");
+        return e ? (int64_t)std::atoll(e) : (int64_t)BH_TRAV_BFS_MAX;
+    }();
+    return v;
+}
+
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
               const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,
               const ForceParams &fp, double *a2, const TraverseCounters *cnt,
               hipStream_t s, const KickArgs *kick, const uint32_t *lanes, const WaveOrder *wo) {
     if (hi <= lo) return;
+    // node records addressed by a 32-bit byte offset while the array stays below 4 GiB
+    const bool off32 = node_cap * sizeof(Node) < (size_t(1) << 32);
+    // (one-GPU evaluations of the whole list only: a rank's lane range walks a tree of every
+    // rank's bodies, which the bitmap's size estimate does not cover)
+    const bool bfs = !cnt && off32 && lo == 0 && hi <= bfs_max_bodies() &&
+                     !(kick && (kick->mode == KICK_OWN_DRIFT || kick->mode == KICK_OWN_ONLY));
+    uint32_t bm_words = 0;
+    if (bfs) {
+        // (a one-GPU tree has ~1.7 nodes per body: C1 21 565 for 12 500, 3 511 for 2 000)
+        const size_t bits = std::min<size_t>(node_cap, (size_t)(9 * (hi - lo) / 4 + 256));
+        bm_words = (uint32_t)std::min<size_t>((bits + 31) / 32, BFS_MAX_BM_WORDS);
+    }
     // (the counting walk keeps 64 bodies per wave: its per-wave counters define lane efficiency)
-    const uint32_t bpw = cnt ? (uint32_t)TB : bodies_per_wave(hi - lo);
+    const uint32_t bpw = cnt ? (uint32_t)TB : bfs ? 1u : bodies_per_wave(hi - lo);
     unsigned grid = (unsigned)((hi - lo + bpw - 1) / bpw);  // waves
     const WaveOrder w = wo && bpw == TB && wave_order_runs(hi - lo) ? *wo : WaveOrder{};
     if (w.order)  // whole runs: every run index the order maps to exists in the grid
         grid = (unsigned)(wave_order_runs(hi - lo) * BH_TRAV_XCD_RUN);
     const uint32_t wpb = waves_per_group(grid, bpw);
     grid = (grid + wpb - 1) / wpb;  // workgroups
-    // node records addressed by a 32-bit byte offset while the array stays below 4 GiB
-    const bool off32 = node_cap * sizeof(Node) < (size_t(1) << 32);
+    const size_t lds = bfs ? bfs_lds_bytes(bm_words) : 0;
     const KickArgs ka = kick ? *kick : KickArgs{KICK_NONE, nullptr, nullptr, 0.0, 0.0, nullptr};
     const TraverseCounters tc = cnt ? *cnt : TraverseCounters{nullptr, nullptr, nullptr, nullptr};
-#define BH_TRAV(C, O, K) \
-    k_traverse<C, O, K><<<grid, TB * wpb, 0, s>>>(nodes, d_T, x, y, m, cidx, lo, hi, fp, g, a2, tc, \
-                                                  ka, lanes, w, bpw, wpb)
+#define BH_TRAV(C, O, K, B)                                                                  \
+    k_traverse<C, O, K, B><<<grid, TB * wpb, lds, s>>>(nodes, d_T, x, y, m, cidx, lo, hi, fp, g, \
+                                                       a2, tc, ka, lanes, w, bpw, wpb, bm_words)
     if (cnt) {  // diagnostic counting walk: accelerations out, never fused
-        if (off32) BH_TRAV(true, true, KICK_NONE);
-        else BH_TRAV(true, false, KICK_NONE);
+        if (off32) BH_TRAV(true, true, KICK_NONE, false);
+        else BH_TRAV(true, false, KICK_NONE, false);
+    } else if (bfs) {
+        if (ka.mode == KICK_DRIFT) BH_TRAV(false, true, KICK_DRIFT, true);
+        else if (ka.mode == KICK_ONLY) BH_TRAV(false, true, KICK_ONLY, true);
+        else if (ka.mode == KICK_OWN_DRIFT) BH_TRAV(false, true, KICK_OWN_DRIFT, true);
+        else if (ka.mode == KICK_OWN_ONLY) BH_TRAV(false, true, KICK_OWN_ONLY, true);
+        else BH_TRAV(false, true, KICK_NONE, true);
     } else if (off32) {
-        if (ka.mode == KICK_DRIFT) BH_TRAV(false, true, KICK_DRIFT);
-        else if (ka.mode == KICK_ONLY) BH_TRAV(false, true, KICK_ONLY);
-        else if (ka.mode == KICK_OWN_DRIFT) BH_TRAV(false, true, KICK_OWN_DRIFT);
-        else if (ka.mode == KICK_OWN_ONLY) BH_TRAV(false, true, KICK_OWN_ONLY);
-        else BH_TRAV(false, true, KICK_NONE);
+        if (ka.mode == KICK_DRIFT) BH_TRAV(false, true, KICK_DRIFT, false);
+        else if (ka.mode == KICK_ONLY) BH_TRAV(false, true, KICK_ONLY, false);
+        else if (ka.mode == KICK_OWN_DRIFT) BH_TRAV(false, true, KICK_OWN_DRIFT, false);
+        else if (ka.mode == KICK_OWN_ONLY) BH_TRAV(false, true, KICK_OWN_ONLY, false);
+        else BH_TRAV(false, true, KICK_NONE, false);
     } else {
-        if (ka.mode == KICK_DRIFT) BH_TRAV(false, false, KICK_DRIFT);
-        else if (ka.mode == KICK_ONLY) BH_TRAV(false, false, KICK_ONLY);
-        else if (ka.mode == KICK_OWN_DRIFT) BH_TRAV(false, false, KICK_OWN_DRIFT);
-        else if (ka.mode == KICK_OWN_ONLY) BH_TRAV(false, false, KICK_OWN_ONLY);
-        else BH_TRAV(false, false, KICK_NONE);
+        if (ka.mode == KICK_DRIFT) BH_TRAV(false, false, KICK_DRIFT, false);
+        else if (ka.mode == KICK_ONLY) BH_TRAV(false, false, KICK_ONLY, false);
+        else if (ka.mode == KICK_OWN_DRIFT) BH_TRAV(false, false, KICK_OWN_DRIFT, false);
+        else if (ka.mode == KICK_OWN_ONLY) BH_TRAV(false, false, KICK_OWN_ONLY, false);
+        else BH_TRAV(false, false, KICK_NONE, false);
     }
 #undef BH_TRAV
 }
