@@ -217,23 +217,35 @@ __device__ __forceinline__ void walk(const Node *__restrict__ nodes, uint32_t T,
 
 // ---- one body per wave, breadth first (small launches) -----------------------------------
 // A walk is a chain of dependent stops -- the next node is known only after the criterion at
-// this one -- so a launch of a few thousand waves (C1's 12 500 bodies) lasts as long as one
-// wave's ~250-350 stops at ~0.3 us each, whatever the GPU's width.  Here the whole wave serves
-// ONE body and examines the tree level by level: every lane takes one opened node of the current
-// level and examines its children (chasing `next` from node + 1), so the chain is the tree's depth
-// (~15 levels), not the body's visit count.  Accepted nodes are marked in an LDS bitmap over node
-// indices; since the flattened tree is in pre-order, the reference's DFS order of the terms
-// (BHA:215-239) IS ascending node index, so the set bits read in ascending order give the terms
-// in the order walk() adds them.  The terms are then evaluated 64 at a time, one per lane, and
-// added into the sums in that order by one lane each (fx: lane 0, fy: lane 1).  Each term is the
-// same expression as walk<true>'s, and the sum is the same sequence of additions from +0.0:
-// bit-identical.  A body whose levels or accepted set exceed the LDS buffers, or whose tree
-// exceeds the bitmap, is walked by walk() instead (the caller), so every body gets its exact sum.
+// this one -- so a launch of a few thousand waves (C1's 2 000 or 12 500 bodies) lasts as long as
+// one wave's ~250-350 stops of ~0.3 us, however wide the GPU.  Here the whole wave serves ONE
+// body and examines the tree level by level: every lane takes one child of an opened node of the
+// current level, so the chain is the tree's depth (~15 levels), not the body's visit count.
+// The lane that takes an opened node examines its children, from node + 1 along `next` (each
+// sibling's record requested before the criterion at the previous one).  Accepted nodes are marked in an LDS bitmap over node indices;
+// the flattened tree is in pre-order, so the reference's DFS order of the terms (BHA:215-239)
+// IS ascending node index and the set bits, read in ascending order, give the terms in the order
+// walk() adds them.  The terms are evaluated 64 at a time, one per lane, and added into the sums
+// in that order by one lane each (fx: lane 0, fy: lane 1).  Each term is the expression of
+// walk<true>, and each sum the same additions from +0.0: bit-identical.  A body whose levels or
+// accepted set overflow the LDS buffers, or whose tree exceeds the bitmap, is walked by walk()
+// instead (the caller), so every body gets its exact sum.
+// LDS of one wave (~5 KB at C1's 12 500 bodies: 31 waves per CU): the bitmap -- after the scan,
+// the terms of one round of 64 --, the level buffers or the accepted list, two counters.
 constexpr uint32_t BFS_E_CAP = 128;  // opened nodes per level (two buffers of (node, next))
-constexpr uint32_t BFS_A_CAP = 4 * BFS_E_CAP;  // accepted nodes per body (in the same space)
-// LDS bytes of one wave: the bitmap, the level buffers / accepted list, two counters, the terms
+constexpr uint32_t BFS_A_CAP = 384;  // accepted nodes per body (in the level buffers' space)
+// (children blocks -- each internal node's child records side by side, built by a kernel before
+// the walk, one gather per child -- measured the same as the chase: C1 'R' 40.5 against 40.0 us
+// per evaluation, profiles/r06z5_bfs_child_blocks_ab.txt)
+constexpr uint32_t BFS_E_WORDS = 2u;  // words per level entry
+constexpr uint32_t BFS_R_WORDS = BFS_A_CAP > 2 * BFS_E_CAP * BFS_E_WORDS
+                                     ? BFS_A_CAP : 2 * BFS_E_CAP * BFS_E_WORDS;
+constexpr uint32_t BFS_TERM_WORDS = 2 * 64 * 2;  // 64 x (tx, ty) doubles
+__host__ __device__ constexpr uint32_t bfs_bm_space(uint32_t bm_words) {
+    return bm_words > BFS_TERM_WORDS ? bm_words : BFS_TERM_WORDS;
+}
 __host__ __device__ constexpr size_t bfs_lds_bytes(uint32_t bm_words) {
-    return sizeof(uint32_t) * ((size_t)bm_words + 4 * BFS_E_CAP + 4) + sizeof(double) * 2 * 64;
+    return sizeof(uint32_t) * ((size_t)bfs_bm_space(bm_words) + BFS_R_WORDS + 4);
 }
 
 __device__ __forceinline__ double rfl_f64(double v) {  // lane 0's value in every lane
@@ -253,10 +265,28 @@ __device__ __forceinline__ uint32_t wave_excl_scan(uint32_t v, uint32_t lane, ui
     return x - v;
 }
 
+#ifdef BH_BFS_TIMING  // diagnostic build only: per-wave phase stamps of bfs_walk
+constexpr int BFS_T_W = 16384, BFS_T_REC = 24;
+__device__ uint64_t g_bfs_times[BFS_T_W * BFS_T_REC];
+#define BFS_STAMP(slot)                                                                     \
+    do {                                                                                    \
+        const uint32_t wv_ = blockIdx.x;                                                    \
+        if (lane == 0 && wv_ < (uint32_t)BFS_T_W) g_bfs_times[wv_ * BFS_T_REC + (slot)] = wall_clock64(); \
+    } while (0)
+#define BFS_NOTE(slot, v)                                                                    \
+    do {                                                                                     \
+        const uint32_t wv_ = blockIdx.x;                                                     \
+        if (lane == 0 && wv_ < (uint32_t)BFS_T_W) g_bfs_times[wv_ * BFS_T_REC + (slot)] = (v); \
+    } while (0)
+#else
+#define BFS_STAMP(slot) (void)0
+#define BFS_NOTE(slot, v) (void)0
+#endif
+
 // false: a buffer overflowed (the caller walks the body with walk()).  fx, fy: wave-uniform.
-__device__ bool bfs_walk(const Node *__restrict__ nodes, uint32_t T, double bx, double by,
-                         double Gm, double soft2, double theta2, double s2root, uint32_t *lds,
-                         uint32_t bm_words, double &fx, double &fy) {
+__device__ bool bfs_walk(const Node *__restrict__ nodes, uint32_t T,
+                         double bx, double by, double Gm, double soft2, double theta2,
+                         double s2root, uint32_t *lds, uint32_t bm_words, double &fx, double &fy) {
     const uint32_t lane = threadIdx.x & 63u;
     fx = 0.0;
     fy = 0.0;
@@ -264,12 +294,13 @@ __device__ bool bfs_walk(const Node *__restrict__ nodes, uint32_t T, double bx, 
     const uint32_t nbw = (T + 31u) / 32u;
     if (nbw > bm_words) return false;
     uint32_t *bits = lds;
-    uint2 *E0 = reinterpret_cast<uint2 *>(lds + bm_words);
-    uint2 *E1 = E0 + BFS_E_CAP;
-    uint32_t *ctr = lds + bm_words + 4 * BFS_E_CAP;  // [0]: next level's count, [1]: overflow
-    double *terms = reinterpret_cast<double *>(ctr + 4);
+    uint32_t *E0 = lds + bfs_bm_space(bm_words);
+    uint32_t *E1 = E0 + BFS_E_CAP * BFS_E_WORDS;
+    uint32_t *ctr = E0 + BFS_R_WORDS;  // [0]: next level's count, [1]: overflow
+    double *terms = reinterpret_cast<double *>(lds);  // (the bitmap's space, after the scan)
+    BFS_STAMP(0);
     for (uint32_t w = lane; w < nbw; w += 64) bits[w] = 0u;
-    // the criterion at node c (BHA:216-228 in walk<true>'s fast form): 0 accept, 1 open
+    // the criterion (BHA:216-228 in walk<true>'s fast form): does the body open this node?
     auto opens = [&](const Node &r) __attribute__((always_inline)) -> bool {
         if (r.meta & NODE_LEAF) return false;  // (massless cells carry the leaf flag too)
         const double dx = r.comX - bx, dy = r.comY - by;
@@ -282,7 +313,10 @@ __device__ bool bfs_walk(const Node *__restrict__ nodes, uint32_t T, double bx, 
     {
         const Node r = nodes[0];  // (every lane: the same address)
         if (opens(r)) {
-            if (lane == 0) E0[0] = make_uint2(0u, r.next > 0u ? r.next : 1u);
+            if (lane == 0) {
+                E0[0] = 0u;
+                E0[1] = r.next > 0u ? r.next : 1u;
+            }
             nE = 1;
         } else if (lane == 0) {
             bits[0] = 1u;
@@ -293,21 +327,27 @@ __device__ bool bfs_walk(const Node *__restrict__ nodes, uint32_t T, double bx, 
         ctr[1] = 0u;
     }
     __syncthreads();
+    BFS_STAMP(1);
+    uint32_t level = 0;
     while (nE > 0) {
-        for (uint32_t i = lane; i < nE; i += 64) {  // lane: one opened node, all its children
-            const uint2 e = E0[i];
-            uint32_t c = e.x + 1u;  // first child (pre-order)
-            if (c >= e.y) continue;
+        for (uint32_t j = lane; j < nE; j += 64) {  // lane: every child of opened node j
+            const uint32_t k = E0[2 * j], end = E0[2 * j + 1];
+            uint32_t c = k + 1u;  // first child (pre-order)
+            if (c >= end) continue;
             Node r = nodes[c];
             while (true) {
                 const uint32_t nx = r.next > c ? r.next : c + 1u;
-                const bool more = nx < e.y;
+                const bool more = nx < end;
                 Node rn;
                 if (more) rn = nodes[nx];  // the next sibling's record, before this criterion
                 if (opens(r)) {
                     const uint32_t at = atomicAdd(&ctr[0], 1u);
-                    if (at < BFS_E_CAP) E1[at] = make_uint2(c, nx);
-                    else ctr[1] = 1u;
+                    if (at < BFS_E_CAP) {
+                        E1[2 * at] = c;
+                        E1[2 * at + 1] = nx;
+                    } else {
+                        ctr[1] = 1u;
+                    }
                 } else {
                     atomicOr(&bits[c >> 5], 1u << (c & 31u));
                 }
@@ -322,34 +362,56 @@ __device__ bool bfs_walk(const Node *__restrict__ nodes, uint32_t T, double bx, 
         __syncthreads();
         if (over) return false;
         if (lane == 0) ctr[0] = 0u;
-        uint2 *t = E0;
+        uint32_t *t = E0;
         E0 = E1;
         E1 = t;
         __syncthreads();
+        ++level;
+        BFS_STAMP(2 + min(level, 15u));
     }
-    // the accepted nodes in ascending order: each lane a contiguous run of bitmap words
-    uint32_t *A = reinterpret_cast<uint32_t *>(lds + bm_words);  // (the level buffers' space)
+    BFS_NOTE(20, level);
+    (void)level;
+    // the accepted nodes in ascending order: each lane a contiguous run of bitmap words, read
+    // 16 at a time (at most 32 per lane: BFS_MAX_BM_WORDS)
+    uint32_t *A = lds + bfs_bm_space(bm_words);  // (the level buffers' space)
     const uint32_t per = (nbw + 63u) / 64u, w0 = min(lane * per, nbw), w1 = min(w0 + per, nbw);
     uint32_t cnt = 0;
-    for (uint32_t w = w0; w < w1; ++w) cnt += (uint32_t)__popc(bits[w]);
+    for (uint32_t b0 = w0; b0 < w1; b0 += 16) {
+        uint32_t wv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) wv[u] = b0 + u < w1 ? bits[b0 + u] : 0u;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) cnt += (uint32_t)__popc(wv[u]);
+    }
     uint32_t nA = 0;
     uint32_t at = wave_excl_scan(cnt, lane, nA);
     if (nA > BFS_A_CAP) return false;
-    for (uint32_t w = w0; w < w1; ++w) {
-        uint32_t b = bits[w];
-        while (b) {
-            const uint32_t k = (uint32_t)__ffs((int)b) - 1u;
-            A[at++] = w * 32u + k;
-            b &= b - 1u;
+    for (uint32_t b0 = w0; b0 < w1; b0 += 16) {
+        uint32_t wv[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) wv[u] = b0 + u < w1 ? bits[b0 + u] : 0u;
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            uint32_t b = wv[u];
+            while (b) {
+                A[at++] = (b0 + u) * 32u + (uint32_t)__ffs((int)b) - 1u;
+                b &= b - 1u;
+            }
         }
     }
     __syncthreads();
-    // the terms, 64 at a time; lane 0 adds the x terms and lane 1 the y terms, in order
+    BFS_STAMP(18);
+    BFS_NOTE(21, nA);
+    // the terms, 64 at a time (the next round's records requested before this round's terms);
+    // lane 0 adds the x terms and lane 1 the y terms, in order
     double acc = 0.0;
+    Node rn;
+    if (lane < nA) rn = nodes[A[lane]];
     for (uint32_t base = 0; base < nA; base += 64) {
         const uint32_t i = base + lane;
+        const Node r = rn;
+        if (i + 64 < nA) rn = nodes[A[i + 64]];
         if (i < nA) {
-            const Node r = nodes[A[i]];
             const double dx = r.comX - bx;  // BHA:251-253
             const double dy = r.comY - by;
             const double d2 = dx * dx + dy * dy + soft2;
@@ -379,6 +441,7 @@ __device__ bool bfs_walk(const Node *__restrict__ nodes, uint32_t T, double bx, 
     }
     fx = __shfl(acc, 0, 64);
     fy = __shfl(acc, 1, 64);
+    BFS_STAMP(19);
     return true;
 }
 
@@ -805,6 +868,14 @@ void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x
     }
 #undef BH_TRAV
 }
+
+#ifdef BH_BFS_TIMING
+extern "C" int bh_debug_bfs_times(uint64_t *out, int waves) {
+    if (waves > BFS_T_W) waves = BFS_T_W;
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bfs_times),
+                                    sizeof(uint64_t) * BFS_T_REC * (size_t)waves);
+}
+#endif
 
 #ifdef BH_TRAV_TIMING
 extern "C" int bh_debug_trav_times(uint64_t *out, int waves) {

@@ -3,7 +3,7 @@
 warm-up, then CALLS x (bh_step(1) + bh_map_bodies) with the pinned mirror on (or, with
 --get-bodies, bh_get_bodies into resident buffers).  Run under
 `rocprofv3 --kernel-trace --memory-copy-trace -- python3 tools/dropin_calls.py` and summarise with
-tools/timeline.py (anchor k_traverse<false, true, 1>: one per call)."""
+tools/timeline.py (anchor k_traverse<false, true, 1, *>: one per call)."""
 import argparse
 import os
 import sys

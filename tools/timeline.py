@@ -3,7 +3,7 @@
 
 Usage: python tools/timeline.py <run_kernel_trace.csv> [step_from_end=2] [out.txt] [anchor]
 
-A one-GPU C3 step launches two fused traversals (`k_traverse<false, true, 1>` = kick + drift,
+A one-GPU C3 step launches two fused traversals (`k_traverse<false, true, 1, *>` = kick + drift,
 `<..., 2>` = kick only).  The window is from the start of the n-th last kick+drift traversal to
 the start of the next one (another anchor kernel: 4th argument, e.g. k_let_flags for one LET
 evaluation); every kernel in it is printed with its start / end offsets in us,
@@ -23,7 +23,7 @@ def main():
         ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"],
                    r.get("Queue_Id", "?"), r.get("Stream_Id", "?")))
     ks.sort()
-    anchor = sys.argv[4] if len(sys.argv) > 4 else "k_traverse<false, true, 1>"
+    anchor = sys.argv[4] if len(sys.argv) > 4 else "k_traverse<false, true, 1,"
     starts = [k[0] for k in ks if anchor in k[2]]
     if len(starts) < back + 1:
         sys.exit("not enough steps in the trace")
