@@ -187,6 +187,11 @@ constexpr uint32_t RADIX_MAXBIN = 48;
 #define BH_SORT_BLOCK_RADIX 1
 #endif
 using BucketRadix = rocprim::block_radix_sort<unsigned long long, SORT_TB, SORT_CAP / SORT_TB>;
+// Buckets of up to BH_SORT_BITONIC_MAX elements that the bin radix cannot take go to the bitonic
+// network instead of the block radix sort.
+#ifndef BH_SORT_BITONIC_MAX
+#define BH_SORT_BITONIC_MAX 0
+#endif
 
 #ifdef BH_SORT_STATS  // diagnostic build: which path each bucket took (radix / bitonic / global)
 __device__ unsigned long long g_sort_stats[8];
@@ -332,7 +337,7 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
         SORT_STAT(2, 1);
         SORT_STAT(3, s);
         SORT_LOGV(1, 1);
-        if (BH_SORT_BLOCK_RADIX) {
+        if (BH_SORT_BLOCK_RADIX && s > (uint32_t)BH_SORT_BITONIC_MAX) {
             constexpr int IPT = SORT_CAP / SORT_TB;
             const uint32_t kmn = s_min, smn = s_smin;
             const uint32_t kspan = s_max - kmn, sspan = s_smax - smn;
