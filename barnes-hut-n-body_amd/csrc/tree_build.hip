@@ -79,8 +79,8 @@ __global__ __launch_bounds__(TB) void k_morton(int64_t n, const double *__restri
 // composites.  Sorting by the composite (key32, slot) IS the stable sort of key32 (ties in
 // slot order), so buckets [spl[t], spl[t+1]) partition it exactly whatever the bucket sizes
 // are, and each bucket is sorted on its own:
-//   k_bucket_count    bucket of every element (galloping from its old position's bucket),
-//                     wave-aggregated atomic count -> offset inside the bucket
+//   k_morton_count    key and bucket of every element (galloping from its old position's
+//                     bucket), wave-aggregated atomic count -> offset inside the bucket
 //   exclusive scan    bucket starts
 //   k_bucket_scatter  composites to their bucket's range (any order inside it)
 //   k_bucket_sort     one workgroup per bucket: bitonic sort in LDS (global memory for a
@@ -94,8 +94,14 @@ constexpr int SORT_TB = 256;
 #endif
 constexpr int SORT_CAP = BH_SORT_CAP;  // LDS bucket capacity (16 KB of composites; 4 x SORT_B)
 
-__global__ __launch_bounds__(SORT_TB) void k_bucket_count(int64_t n,
-                                                          const uint32_t *__restrict__ keys32,
+// k_morton and k_bucket_count in one launch (a build whose keys the drifting traversal did not
+// compute: the overlapped next tree, a build after a reset with splitters): the same index space
+// (TB == SORT_TB), the key kept in a register between the two.
+__global__ __launch_bounds__(SORT_TB) void k_morton_count(int64_t n, const double *__restrict__ x,
+                                                          const double *__restrict__ y,
+                                                          const uint32_t *__restrict__ cidx,
+                                                          Geometry g, uint64_t *__restrict__ keys,
+                                                          uint32_t *__restrict__ keys32,
                                                           const uint64_t *__restrict__ spl,
                                                           uint32_t nb, uint32_t *__restrict__ bkt,
                                                           uint32_t *__restrict__ off,
@@ -103,19 +109,23 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_count(int64_t n,
     chain_prio();
     const int64_t i = (int64_t)blockIdx.x * SORT_TB + threadIdx.x;
     const bool valid = i < n;
+    uint32_t k32 = 0;
+    if (valid) {
+        const uint64_t key = morton_key(g, x[i], y[i], (cidx[i] & CIDX_DEAD) != 0u);
+        k32 = (uint32_t)(key >> key32_shift(g.J));
+        keys[i] = key;
+        keys32[i] = k32;
+    }
     uint32_t b = 0;
-    // the wave's old bucket t (its first lane's) and its bounds through scalar loads: most
-    // elements are still inside it; the others gallop
     const int64_t i0 = (int64_t)blockIdx.x * SORT_TB + (threadIdx.x & ~63u);
     const uint32_t t = __builtin_amdgcn_readfirstlane(min((uint32_t)(i0 / SORT_B), nb - 1));
     const uint64_t lo_s = t == 0 ? 0ull : spl[t];
     const uint64_t hi_s = t + 1 < nb ? spl[t + 1] : ~0ull;
     if (valid) {
-        const uint64_t v = ((uint64_t)keys32[i] << 32) | (uint64_t)i;
+        const uint64_t v = ((uint64_t)k32 << 32) | (uint64_t)i;
         if (lo_s <= v && (v < hi_s || t + 1 == nb)) b = t;
         else b = find_bucket(spl, nb, v, (uint32_t)(i / SORT_B));
     }
-    // one atomic per distinct bucket of the wave (usually one): offsets in lane order
     if (!valid) return;
     const uint32_t myoff = bucket_offset(b, counts);
     bkt[i] = b;
@@ -1917,14 +1927,16 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     const int D0 = cell_table_depth(g.J, n);
     const bool bucket = b.spl_nb > 0;
     const bool ready = bucket && b.keys_ready;  // the drifting traversal did both passes
-    if (!ready)
+    static_assert(TB == SORT_TB, "k_morton_count: one index space");
+    if (!ready && !bucket)
         k_morton<<<grid_for(n), TB, 0, s>>>(n, b.src.x, b.src.y, b.src.cidx, g, b.keys, b.keys32,
-                                            bucket ? nullptr : b.idx);
+                                            b.idx);
     size_t bytes = b.scratch_bytes;
     if (bucket) {  // bucket ids / offsets live in cnt / base until k_prep needs them
         const unsigned sg = (unsigned)((n + SORT_TB - 1) / SORT_TB);
         if (!ready)
-            k_bucket_count<<<sg, SORT_TB, 0, s>>>(n, b.keys32, b.spl, b.spl_nb, b.cnt, b.base,
+            k_morton_count<<<sg, SORT_TB, 0, s>>>(n, b.src.x, b.src.y, b.src.cidx, g, b.keys,
+                                                  b.keys32, b.spl, b.spl_nb, b.cnt, b.base,
                                                   b.bcount);
         st = rocprim::exclusive_scan(b.scratch, bytes, b.bcount, b.bstart, 0u,
                                      (size_t)b.spl_nb + 1, rocprim::plus<uint32_t>(), s);
