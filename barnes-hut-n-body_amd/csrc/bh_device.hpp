@@ -386,6 +386,8 @@ struct WaveOrder {
     uint32_t *cost = nullptr;
 };
 size_t wave_order_runs(int64_t n);  // runs of a launch over n lanes (0: too many to order)
+// Whether traverse() walks [lo, hi) breadth first, one body per wave (traverse.hip bfs_walk)
+bool traverse_is_bfs(size_t node_cap, int64_t lo, int64_t hi, int kick_mode, bool counting);
 hipError_t wave_order(const uint32_t *cost, int64_t n, uint32_t *order, hipStream_t s);
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
               const double *m, const uint32_t *cidx, int64_t lo, int64_t hi, const Geometry &g,

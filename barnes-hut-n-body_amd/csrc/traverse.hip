@@ -804,13 +804,31 @@ static uint32_t waves_per_group(uint32_t waves, uint32_t bpw) {
 #ifndef BH_TRAV_BFS_MAX
 #define BH_TRAV_BFS_MAX 4096
 #endif
+// The kick-only walk -- the pipelined step's second, which shares the GPU with the overlapped merge
+// rule and next build -- keeps the cursor walk up to BH_TRAV_BFS_MAX_KICK bodies (0: always): the
+// breadth-first walk's LDS would keep those kernels off the CUs until it ends.  C1 'R', 3
+// interleaved rounds (profiles/r06e_bfs_first_walk_only_ab.txt): breadth first for both walks
+// 0.277 ms per step, for the first only 0.272 (0.295 with neither).
+#ifndef BH_TRAV_BFS_MAX_KICK
+#define BH_TRAV_BFS_MAX_KICK 0
+#endif
 constexpr uint32_t BFS_MAX_BM_WORDS = 2048;
-static int64_t bfs_max_bodies() {
-    static const int64_t v = [] {
-        const char *e = std::getenv("BH_TRAV_BFS_MAX");
-        return e ? (int64_t)std::atoll(e) : (int64_t)BH_TRAV_BFS_MAX;
-    }();
-    return v;
+static int64_t env_or(const char *name, int64_t dflt) {
+    const char *e = std::getenv(name);
+    return e ? (int64_t)std::atoll(e) : dflt;
+}
+static int64_t bfs_max_bodies(int kick_mode) {
+    static const int64_t v = env_or("BH_TRAV_BFS_MAX", BH_TRAV_BFS_MAX);
+    static const int64_t vk = env_or("BH_TRAV_BFS_MAX_KICK", BH_TRAV_BFS_MAX_KICK);
+    return kick_mode == KICK_ONLY ? vk : v;
+}
+
+// (one-GPU evaluations of the whole list only: a rank's lane range walks a tree of every rank's
+// bodies, which the bitmap's size estimate does not cover)
+bool traverse_is_bfs(size_t node_cap, int64_t lo, int64_t hi, int kick_mode, bool counting) {
+    const bool off32 = node_cap * sizeof(Node) < (size_t(1) << 32);
+    return !counting && off32 && lo == 0 && hi > 0 && hi <= bfs_max_bodies(kick_mode) &&
+           kick_mode != KICK_OWN_DRIFT && kick_mode != KICK_OWN_ONLY;
 }
 
 void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x, double *y,
@@ -820,10 +838,7 @@ void traverse(const Node *nodes, size_t node_cap, const uint32_t *d_T, double *x
     if (hi <= lo) return;
     // node records addressed by a 32-bit byte offset while the array stays below 4 GiB
     const bool off32 = node_cap * sizeof(Node) < (size_t(1) << 32);
-    // (one-GPU evaluations of the whole list only: a rank's lane range walks a tree of every
-    // rank's bodies, which the bitmap's size estimate does not cover)
-    const bool bfs = !cnt && off32 && lo == 0 && hi <= bfs_max_bodies() &&
-                     !(kick && (kick->mode == KICK_OWN_DRIFT || kick->mode == KICK_OWN_ONLY));
+    const bool bfs = traverse_is_bfs(node_cap, lo, hi, kick ? kick->mode : KICK_NONE, cnt);
     uint32_t bm_words = 0;
     if (bfs) {
         // (a one-GPU tree has ~1.7 nodes per body: C1 21 565 for 12 500, 3 511 for 2 000)
