@@ -3,6 +3,8 @@
 //
 //   chain   K launches back to back on one stream, per launch: 1 wave; 1024 x 256 threads each
 //           writing one word; the same chain captured in a hipGraph and replayed
+//   events  K launches of 1024 x 256 threads with timing: an event recorded between launches
+//           (a marker in the queue) vs events attached to the launches (hipExtLaunchKernelGGL)
 //   barrier one launch of B workgroups that meet R times at a grid barrier (one atomic counter and
 //           a generation word, agent scope), per barrier: B spread over the XCDs, or B on one XCD
 //           (8 B workgroups launched, those with blockIdx % 8 != 0 leave at once)
@@ -10,6 +12,7 @@
 // A barrier poll gives up after ~2^24 tries and counts an error, so a non-resident workgroup
 // cannot hang the run.
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cstdio>
 #include <cstdlib>
@@ -100,6 +103,41 @@ static float time_chain(hipStream_t s, int K, dim3 grid, dim3 block, bool touch,
     return best * 1000.0f / K;  // us per launch
 }
 
+// mode 0: no events, 1: hipEventRecord before and after every launch, 2: events attached to the
+// launch (hipExtLaunchKernelGGL start / stop)
+static float time_events(hipStream_t s, int K, int mode, uint32_t *buf) {
+    hipEvent_t a, b;
+    CHK(hipEventCreate(&a));
+    CHK(hipEventCreate(&b));
+    hipEvent_t ev[2 * 64];
+    for (int i = 0; i < 2 * 64; ++i) CHK(hipEventCreate(&ev[i]));
+    float best = 1e30f;
+    for (int rep = 0; rep < 5; ++rep) {
+        CHK(hipEventRecord(a, s));
+        for (int i = 0; i < K; ++i) {
+            hipEvent_t e0 = ev[(2 * i) % 128], e1 = ev[(2 * i + 1) % 128];
+            if (mode == 1) CHK(hipEventRecord(e0, s));
+            if (mode == 2)
+                hipExtLaunchKernelGGL(k_touch, dim3(1024), dim3(256), 0, s, e0, e1, 0, buf);
+            else
+                k_touch<<<1024, 256, 0, s>>>(buf);
+            if (mode == 1) CHK(hipEventRecord(e1, s));
+        }
+        CHK(hipEventRecord(b, s));
+        CHK(hipEventSynchronize(b));
+        float ms = 0;
+        CHK(hipEventElapsedTime(&ms, a, b));
+        if (ms < best) best = ms;
+    }
+    if (mode > 0) {  // the last launch's own interval
+        float ms = 0;
+        CHK(hipEventElapsedTime(&ms, ev[(2 * (K - 1)) % 128], ev[(2 * (K - 1) + 1) % 128]));
+        std::printf("{\"probe\": \"event_interval\", \"mode\": %d, \"last_launch_us\": %.2f}\n", mode,
+                    ms * 1000.0f);
+    }
+    return best * 1000.0f / K;
+}
+
 static float time_barriers(hipStream_t s, uint32_t nb, uint32_t stride, int rounds, uint32_t *sync,
                            uint32_t *data, uint32_t *err_out) {
     hipEvent_t a, b;
@@ -138,6 +176,10 @@ int main() {
         std::printf("{\"probe\": \"chain\", \"graph\": %s, \"shape\": \"1024x256 one store\", \"us_per_launch\": %.2f}\n",
                     graph ? "true" : "false", time_chain(s, K, dim3(1024), dim3(256), true, buf, graph));
     }
+    for (int mode = 0; mode < 3; ++mode)
+        std::printf("{\"probe\": \"events\", \"mode\": \"%s\", \"us_per_launch\": %.2f}\n",
+                    mode == 0 ? "none" : mode == 1 ? "hipEventRecord around" : "attached (hipExtLaunchKernelGGL)",
+                    time_events(s, K, mode, buf));
     const uint32_t nbs[] = {8, 32, 64, 256};
     for (uint32_t nb : nbs) {
         for (uint32_t stride : {1u, 8u}) {
