@@ -15,6 +15,8 @@
 // The kernel is bound by fp64 VALU issue (the IEEE sqrt and two IEEE divisions per
 // interaction), not by HBM: the node stream is shared by 64 lanes and served from the
 // scalar cache / L2.  See DESIGN.md for the roofline accounting.
+// Small lists (bfs_walk below): the first walk of a step over <= 4 096 bodies serves one body
+// per wave and examines the tree level by level, the terms added in pre-order -- the same sum.
 #include <cstdlib>
 
 #include "bh_device.hpp"
