@@ -22,6 +22,9 @@
 //                records, replay of BHA:125-156 inside each jitter cell, centre of mass
 //                bottom-up (children 0..3 in order, BHA:184-200) of the chunk-local nodes
 //   k_span_*     the chunk-spanning nodes, levels J..0
+#include <atomic>
+#include <cstdlib>
+
 #include <rocprim/device/device_scan.hpp>
 #include <rocprim/device/device_radix_sort.hpp>
 #include <rocprim/block/block_radix_sort.hpp>
@@ -142,6 +145,89 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_scatter(int64_t n,
     const int64_t i = (int64_t)blockIdx.x * SORT_TB + threadIdx.x;
     if (i >= n) return;
     comp[starts[bkt[i]] + off[i]] = ((uint64_t)keys32[i] << 32) | (uint64_t)i;
+}
+
+// ---- one-workgroup sort for small lists -------------------------------------------------
+// Up to BH_SMALL_SORT_MAX bodies the bucket sort's three launches (bucket starts, scatter, the
+// buckets' sorts: ~30 us at C1, each a latency chain after a launch boundary) are one workgroup's
+// bitonic network over all composites (key32 << 32 | slot) in LDS -- the same total order, so the
+// same permutation (the composites are distinct).  It also clears the bucket counts the drifting
+// traversal may have made, as k_bucket_sort does for the next build.  The network moves
+// P log2(P)^2 / 2 elements through one CU's LDS: at C1 'R' (P = 2 048) a few us, at 12 500 bodies
+// (P = 16 384) ~110 us -- C1 code 0.339 -> 0.572 ms per step (profiles/r06s_small_sort_ab.txt) --
+// hence 4 096.
+constexpr int SS_TB = 1024;
+#ifndef BH_SMALL_SORT_MAX
+#define BH_SMALL_SORT_MAX 4096
+#endif
+__global__ __launch_bounds__(SS_TB) void k_small_sort(int64_t n, uint32_t P,
+                                                      const uint32_t *__restrict__ keys32,
+                                                      const uint64_t *__restrict__ keys,
+                                                      uint32_t *__restrict__ keys32_s,
+                                                      uint32_t *__restrict__ perm,
+                                                      uint64_t *__restrict__ keys_s,
+                                                      uint32_t *__restrict__ counts, uint32_t nb) {
+    chain_prio();
+    extern __shared__ uint64_t ss_L[];  // P = the power of two >= n, padded with ~0
+    const uint32_t t = threadIdx.x;
+    for (uint32_t i = t; i < P; i += SS_TB)
+        ss_L[i] = (int64_t)i < n ? ((uint64_t)keys32[i] << 32) | (uint64_t)i : ~0ull;
+    for (uint32_t i = t; i <= nb; i += SS_TB) counts[i] = 0u;
+    __syncthreads();
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t q = t; q < P / 2; q += SS_TB) {  // pair (lo, lo + j), bit j of lo clear
+                const uint32_t lo = ((q & ~(j - 1)) << 1) | (q & (j - 1));
+                const uint32_t hi = lo | j;
+                const uint64_t a = ss_L[lo], c = ss_L[hi];
+                if ((a > c) == ((lo & k) == 0)) {
+                    ss_L[lo] = c;
+                    ss_L[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t j = t; (int64_t)j < n; j += SS_TB) {
+        const uint64_t v = ss_L[j];
+        const uint32_t src = (uint32_t)v;
+        keys32_s[j] = (uint32_t)(v >> 32);
+        perm[j] = src;
+        keys_s[j] = keys[src];
+    }
+}
+
+static bool small_sort_ok(int64_t n, uint32_t &P) {
+    static const int64_t lim = [] {
+        const char *v = std::getenv("BH_SMALL_SORT_MAX");
+        return v ? (int64_t)std::atoll(v) : (int64_t)BH_SMALL_SORT_MAX;
+    }();
+    if (n <= 0 || n > lim) return false;
+    P = 1;
+    while ((int64_t)P < n) P <<= 1;
+    const size_t bytes = sizeof(uint64_t) * (size_t)P;
+    if (bytes > 160 * 1024) return false;
+    if (bytes > 64 * 1024) {  // (dynamic LDS above 64 KB is allowed once per kernel and device)
+        static std::atomic<uint64_t> allowed{0}, refused{0};
+        int dev = 0;
+        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
+            (void)hipGetLastError();
+            return false;
+        }
+        const uint64_t bit = 1ull << dev;
+        if (refused.load() & bit) return false;
+        if (!(allowed.load() & bit)) {
+            if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_small_sort),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize,
+                                    160 * 1024) != hipSuccess) {
+                (void)hipGetLastError();
+                refused.fetch_or(bit);
+                return false;
+            }
+            allowed.fetch_or(bit);
+        }
+    }
+    return true;
 }
 
 // Bitonic network in its all-ascending form (the first step of every merge compares mirrored
@@ -1928,11 +2014,16 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     const bool bucket = b.spl_nb > 0;
     const bool ready = bucket && b.keys_ready;  // the drifting traversal did both passes
     static_assert(TB == SORT_TB, "k_morton_count: one index space");
-    if (!ready && !bucket)
+    uint32_t P = 0;
+    const bool small = bucket && small_sort_ok(n, P);
+    if (!ready && (!bucket || small))
         k_morton<<<grid_for(n), TB, 0, s>>>(n, b.src.x, b.src.y, b.src.cidx, g, b.keys, b.keys32,
-                                            b.idx);
+                                            bucket ? nullptr : b.idx);
     size_t bytes = b.scratch_bytes;
-    if (bucket) {  // bucket ids / offsets live in cnt / base until k_prep needs them
+    if (small) {
+        k_small_sort<<<1, SS_TB, sizeof(uint64_t) * P, s>>>(n, P, b.keys32, b.keys, b.keys32_s,
+                                                             b.perm, b.keys_s, b.bcount, b.spl_nb);
+    } else if (bucket) {  // bucket ids / offsets live in cnt / base until k_prep needs them
         const unsigned sg = (unsigned)((n + SORT_TB - 1) / SORT_TB);
         if (!ready)
             k_morton_count<<<sg, SORT_TB, 0, s>>>(n, b.src.x, b.src.y, b.src.cidx, g, b.keys,
