@@ -22,7 +22,6 @@
 //                records, replay of BHA:125-156 inside each jitter cell, centre of mass
 //                bottom-up (children 0..3 in order, BHA:184-200) of the chunk-local nodes
 //   k_span_*     the chunk-spanning nodes, levels J..0
-#include <atomic>
 #include <cstdlib>
 
 #include <rocprim/device/device_scan.hpp>
@@ -145,89 +144,6 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_scatter(int64_t n,
     const int64_t i = (int64_t)blockIdx.x * SORT_TB + threadIdx.x;
     if (i >= n) return;
     comp[starts[bkt[i]] + off[i]] = ((uint64_t)keys32[i] << 32) | (uint64_t)i;
-}
-
-// ---- one-workgroup sort for small lists -------------------------------------------------
-// Up to BH_SMALL_SORT_MAX bodies the bucket sort's three launches (bucket starts, scatter, the
-// buckets' sorts: ~30 us at C1, each a latency chain after a launch boundary) are one workgroup's
-// bitonic network over all composites (key32 << 32 | slot) in LDS -- the same total order, so the
-// same permutation (the composites are distinct).  It also clears the bucket counts the drifting
-// traversal may have made, as k_bucket_sort does for the next build.  The network moves
-// P log2(P)^2 / 2 elements through one CU's LDS: at C1 'R' (P = 2 048) a few us, at 12 500 bodies
-// (P = 16 384) ~110 us -- C1 code 0.339 -> 0.572 ms per step (profiles/r06s_small_sort_ab.txt) --
-// hence 4 096.
-constexpr int SS_TB = 1024;
-#ifndef BH_SMALL_SORT_MAX
-#define BH_SMALL_SORT_MAX 4096
-#endif
-__global__ __launch_bounds__(SS_TB) void k_small_sort(int64_t n, uint32_t P,
-                                                      const uint32_t *__restrict__ keys32,
-                                                      const uint64_t *__restrict__ keys,
-                                                      uint32_t *__restrict__ keys32_s,
-                                                      uint32_t *__restrict__ perm,
-                                                      uint64_t *__restrict__ keys_s,
-                                                      uint32_t *__restrict__ counts, uint32_t nb) {
-    chain_prio();
-    extern __shared__ uint64_t ss_L[];  // P = the power of two >= n, padded with ~0
-    const uint32_t t = threadIdx.x;
-    for (uint32_t i = t; i < P; i += SS_TB)
-        ss_L[i] = (int64_t)i < n ? ((uint64_t)keys32[i] << 32) | (uint64_t)i : ~0ull;
-    for (uint32_t i = t; i <= nb; i += SS_TB) counts[i] = 0u;
-    __syncthreads();
-    for (uint32_t k = 2; k <= P; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t q = t; q < P / 2; q += SS_TB) {  // pair (lo, lo + j), bit j of lo clear
-                const uint32_t lo = ((q & ~(j - 1)) << 1) | (q & (j - 1));
-                const uint32_t hi = lo | j;
-                const uint64_t a = ss_L[lo], c = ss_L[hi];
-                if ((a > c) == ((lo & k) == 0)) {
-                    ss_L[lo] = c;
-                    ss_L[hi] = a;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    for (uint32_t j = t; (int64_t)j < n; j += SS_TB) {
-        const uint64_t v = ss_L[j];
-        const uint32_t src = (uint32_t)v;
-        keys32_s[j] = (uint32_t)(v >> 32);
-        perm[j] = src;
-        keys_s[j] = keys[src];
-    }
-}
-
-static bool small_sort_ok(int64_t n, uint32_t &P) {
-    static const int64_t lim = [] {
-        const char *v = std::getenv("BH_SMALL_SORT_MAX");
-        return v ? (int64_t)std::atoll(v) : (int64_t)BH_SMALL_SORT_MAX;
-    }();
-    if (n <= 0 || n > lim) return false;
-    P = 1;
-    while ((int64_t)P < n) P <<= 1;
-    const size_t bytes = sizeof(uint64_t) * (size_t)P;
-    if (bytes > 160 * 1024) return false;
-    if (bytes > 64 * 1024) {  // (dynamic LDS above 64 KB is allowed once per kernel and device)
-        static std::atomic<uint64_t> allowed{0}, refused{0};
-        int dev = 0;
-        if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) {
-            (void)hipGetLastError();
-            return false;
-        }
-        const uint64_t bit = 1ull << dev;
-        if (refused.load() & bit) return false;
-        if (!(allowed.load() & bit)) {
-            if (hipFuncSetAttribute(reinterpret_cast<const void *>(&k_small_sort),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize,
-                                    160 * 1024) != hipSuccess) {
-                (void)hipGetLastError();
-                refused.fetch_or(bit);
-                return false;
-            }
-            allowed.fetch_or(bit);
-        }
-    }
-    return true;
 }
 
 // Bitonic network in its all-ascending form (the first step of every merge compares mirrored
@@ -704,6 +620,129 @@ __global__ __launch_bounds__(TB) void k_fixup_cells(int64_t n, int J, int D0,
     const int64_t t = (int64_t)blockIdx.x * TB + threadIdx.x;
     cells(t, (int64_t)gridDim.x * TB, n, J, D0, keys_s, cell_start, super_list, n_super);
     key_fixup(t, n, J, keys32_s, keys_s, perm);
+}
+
+// ---- the front of a small list's build in one workgroup ----------------------------------
+// Up to BH_SMALL_FRONT_MAX (4 096) bodies, the build's first five launches -- the Morton keys,
+// the bucket sort's three (bucket starts, scatter, the buckets' sorts), k_fixup_cells, k_prep and
+// k_base_scan: ~45 us at C1 'R', each a latency chain after a launch boundary -- run as the phases
+// of one 1 024-thread workgroup: the keys; a bitonic network over all composites
+// (key32 << 32 | slot) in LDS, the same total order as the bucket sort's (the composites are
+// distinct), so the same permutation; then key_fixup, cells and prep_one -- the very functions the
+// separate kernels run -- per body, and the exclusive scan of the node counts into base.  It also
+// clears the bucket counts the drifting traversal may have made, as k_bucket_sort does for the
+// next build.  (The network alone over 16 384 composites -- C1 code -- is bound by one CU's LDS
+// bandwidth: ~110 us, C1 code 0.339 -> 0.572 ms per step, profiles/r06s_small_sort_ab.txt.)
+constexpr int SF_TB = 1024;
+constexpr int64_t SMALL_FRONT_CAP = 4096;  // (P * 8 bytes of LDS: 32 KB)
+#ifndef BH_SMALL_FRONT_MAX
+#define BH_SMALL_FRONT_MAX SMALL_FRONT_CAP
+#endif
+__global__ __launch_bounds__(SF_TB) void k_small_front(
+    int64_t n, uint32_t P, bool need_keys, Geometry g, int D0, BodyState src, BodyState dst,
+    uint64_t *__restrict__ keys, uint32_t *__restrict__ keys32, uint32_t *__restrict__ keys32_s,
+    uint32_t *__restrict__ perm, uint64_t *__restrict__ keys_s, uint32_t *__restrict__ counts,
+    uint32_t nb, uint32_t *__restrict__ cell_start, uint32_t *__restrict__ super_list,
+    int64_t n_super, int8_t *__restrict__ cpl, uint32_t *__restrict__ cnt,
+    uint64_t *__restrict__ spl, HeavyList hl, uint32_t *__restrict__ base) {
+    chain_prio();
+    extern __shared__ uint64_t sf_L[];  // P = the power of two >= n, padded with ~0
+    __shared__ uint32_t s_w[SF_TB / 64];
+    const int J = g.J;
+    const uint32_t t = threadIdx.x;
+    // (k_morton) the keys, or the drifting traversal's
+    for (uint32_t i = t; i < P; i += SF_TB) {
+        uint64_t v = ~0ull;
+        if ((int64_t)i < n) {
+            uint32_t k32;
+            if (need_keys) {
+                const uint64_t key = morton_key(g, src.x[i], src.y[i], (src.cidx[i] & CIDX_DEAD) != 0u);
+                k32 = (uint32_t)(key >> key32_shift(J));
+                keys[i] = key;
+            } else {
+                k32 = keys32[i];
+            }
+            v = ((uint64_t)k32 << 32) | (uint64_t)i;
+        }
+        sf_L[i] = v;
+    }
+    for (uint32_t i = t; i <= nb; i += SF_TB) counts[i] = 0u;
+    __syncthreads();
+    // (the bucket sort) all composites, ascending
+    for (uint32_t k = 2; k <= P; k <<= 1) {
+        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
+            for (uint32_t q = t; q < P / 2; q += SF_TB) {  // pair (lo, lo + j), bit j of lo clear
+                const uint32_t lo = ((q & ~(j - 1)) << 1) | (q & (j - 1));
+                const uint32_t hi = lo | j;
+                const uint64_t a = sf_L[lo], c = sf_L[hi];
+                if ((a > c) == ((lo & k) == 0)) {
+                    sf_L[lo] = c;
+                    sf_L[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (uint32_t a = t; (int64_t)a < n; a += SF_TB) {
+        const uint64_t v = sf_L[a];
+        const uint32_t i = (uint32_t)v;
+        keys32_s[a] = (uint32_t)(v >> 32);
+        perm[a] = i;
+        keys_s[a] = keys[i];
+    }
+    __syncthreads();
+    // (k_fixup_cells) runs of equal prefixes by (full key, index); the depth-D0 cell starts
+    for (uint32_t a = t; (int64_t)a < n; a += SF_TB) key_fixup(a, n, J, keys32_s, keys_s, perm);
+    __syncthreads();
+    const int64_t nbins1 = ((int64_t)1 << (2 * D0)) + 1;
+    const int64_t cells_hi = nbins1 > n_super ? nbins1 : n_super;
+    for (int64_t bin = t; bin < cells_hi; bin += SF_TB)
+        cells(bin, SF_TB, n, J, D0, keys_s, cell_start, super_list, n_super);
+    __syncthreads();
+    // (k_prep) the state in the new order, c(a), node counts -- kept in LDS for the scan
+    uint32_t *c_l = reinterpret_cast<uint32_t *>(sf_L);  // (n + 1 <= 2 P counts)
+    for (uint32_t a = t; (int64_t)a <= n; a += SF_TB) {
+        uint32_t c = 0;
+        if ((int64_t)a < n) c = prep_one(a, n, J, keys_s, perm, src, dst, cpl, cnt, spl, keys32, hl);
+        else cnt[n] = 0;
+        c_l[a] = c;
+    }
+    __syncthreads();
+    // (k_base_scan) base[i] = sum cnt[0..i), i <= n: each thread a run of E counts
+    const uint32_t n1 = (uint32_t)n + 1u, E = (n1 + SF_TB - 1) / SF_TB;
+    const uint32_t i0 = t * E;
+    uint32_t sum = 0;
+    for (uint32_t e = 0; e < E; ++e)
+        if (i0 + e < n1) sum += c_l[i0 + e];
+    const uint32_t lane = t & 63u, w = t >> 6;
+    uint32_t inc = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t u = __shfl_up(inc, o);
+        if (lane >= (uint32_t)o) inc += u;
+    }
+    if (lane == 63) s_w[w] = inc;
+    __syncthreads();
+    uint32_t run = inc - sum;
+    for (uint32_t k = 0; k < w; ++k) run += s_w[k];
+    for (uint32_t e = 0; e < E; ++e) {
+        if (i0 + e < n1) {
+            base[i0 + e] = run;
+            run += c_l[i0 + e];
+        }
+    }
+}
+
+static bool small_front(int64_t n, uint32_t &P) {
+    static const int64_t lim = [] {
+        const char *v = std::getenv("BH_SMALL_FRONT_MAX");
+        const int64_t x = v ? (int64_t)std::atoll(v) : (int64_t)BH_SMALL_FRONT_MAX;
+        return x < SMALL_FRONT_CAP ? x : SMALL_FRONT_CAP;
+    }();
+    if (n <= 0 || n > lim) return false;
+    P = 1;
+    while ((int64_t)P < n) P <<= 1;
+    return true;
 }
 
 // Largest e in [from, limit] with (keys_s[e] >> shift) == pref (keys_s[from] matches).
@@ -2015,14 +2054,19 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     const bool ready = bucket && b.keys_ready;  // the drifting traversal did both passes
     static_assert(TB == SORT_TB, "k_morton_count: one index space");
     uint32_t P = 0;
-    const bool small = bucket && small_sort_ok(n, P);
-    if (!ready && (!bucket || small))
+    const bool small = bucket && small_front(n, P);
+    const uint32_t n_groups = span_groups(b.span_stride);
+    const int64_t n_super = n_groups > 1 ? (int64_t)(g.J + 1) * n_groups : 0;
+    const int64_t nbins1 = ((int64_t)1 << (2 * D0)) + 1;
+    if (!ready && !bucket)
         k_morton<<<grid_for(n), TB, 0, s>>>(n, b.src.x, b.src.y, b.src.cidx, g, b.keys, b.keys32,
-                                            bucket ? nullptr : b.idx);
+                                            b.idx);
     size_t bytes = b.scratch_bytes;
     if (small) {
-        k_small_sort<<<1, SS_TB, sizeof(uint64_t) * P, s>>>(n, P, b.keys32, b.keys, b.keys32_s,
-                                                             b.perm, b.keys_s, b.bcount, b.spl_nb);
+        k_small_front<<<1, SF_TB, sizeof(uint64_t) * P, s>>>(
+            n, P, !ready, g, D0, b.src, b.dst, b.keys, b.keys32, b.keys32_s, b.perm, b.keys_s,
+            b.bcount, b.spl_nb, b.cell_start, b.super_list, n_super, b.cpl, b.cnt, b.spl,
+            HeavyList{b.heavy, b.heavy_count, b.heavy_thr}, b.base);
     } else if (bucket) {  // bucket ids / offsets live in cnt / base until k_prep needs them
         const unsigned sg = (unsigned)((n + SORT_TB - 1) / SORT_TB);
         if (!ready)
@@ -2046,10 +2090,8 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
         if (st != hipSuccess) return st;
         k_key_gather<<<grid_for(n), TB, 0, s>>>(n, b.keys, b.perm, b.keys_s);
     }
-    const uint32_t n_groups = span_groups(b.span_stride);
-    const int64_t n_super = n_groups > 1 ? (int64_t)(g.J + 1) * n_groups : 0;
-    const int64_t nbins1 = ((int64_t)1 << (2 * D0)) + 1;
-    if (BH_FIXUP_CELLS)
+    if (small) {
+    } else if (BH_FIXUP_CELLS)
         k_fixup_cells<<<grid_for(std::max<int64_t>(n, nbins1)), TB, 0, s>>>(
             n, g.J, D0, b.keys32_s, b.keys_s, b.perm, b.cell_start, b.super_list, n_super);
     else
@@ -2060,10 +2102,12 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     const bool own_scan = BH_BASE_SCAN && n + 1 <= ((int64_t)1 << 22) &&
                           b.scratch_bytes >= sizeof(uint32_t) * (size_t)prep_blocks;
     uint32_t *tsum = own_scan ? static_cast<uint32_t *>(b.scratch) : nullptr;
-    k_prep<<<(unsigned)prep_blocks, TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.src, b.dst, b.cpl,
-                                                b.cnt, b.spl, b.keys32, tsum,
-                                                HeavyList{b.heavy, b.heavy_count, b.heavy_thr});
-    if (own_scan) {
+    if (!small)
+        k_prep<<<(unsigned)prep_blocks, TB, 0, s>>>(n, g.J, b.keys_s, b.perm, b.src, b.dst, b.cpl,
+                                                    b.cnt, b.spl, b.keys32, tsum,
+                                                    HeavyList{b.heavy, b.heavy_count, b.heavy_thr});
+    if (small) {
+    } else if (own_scan) {
         const int64_t per = (int64_t)BS_TB * 4;
         k_base_scan<4><<<(unsigned)((n + 1 + per - 1) / per), BS_TB, 0, s>>>(n + 1, b.cnt, tsum,
                                                                         b.base);
@@ -2073,7 +2117,7 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
                                      rocprim::plus<uint32_t>(), s);
         if (st != hipSuccess) return st;
     }
-    if (!BH_FIXUP_CELLS)
+    if (!BH_FIXUP_CELLS && !small)
         k_cells<<<grid_for(nbins1), TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cell_start, b.super_list,
                                                 n_super);
     k_emit_com<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), EC_TB, 0, s>>>(
