@@ -635,6 +635,17 @@ __global__ __launch_bounds__(TB) void k_fixup_cells(int64_t n, int J, int D0,
 // bandwidth: ~110 us, C1 code 0.339 -> 0.572 ms per step, profiles/r06s_small_sort_ab.txt.)
 constexpr int SF_TB = 1024;
 constexpr int64_t SMALL_FRONT_CAP = 4096;  // (P * 8 bytes of LDS: 32 KB)
+#ifdef BH_SF_TIMING  // diagnostic build: phase stamps of the last k_small_front launches (ring)
+constexpr int SF_T_REC = 64, SF_T_W = 8;
+__device__ uint64_t g_sf_times[SF_T_REC * SF_T_W];
+__device__ uint32_t g_sf_launch;
+#define SF_STAMP(q)                                                                      \
+    do {                                                                                 \
+        if (threadIdx.x == 0) sf_t[(q)] = wall_clock64();                                 \
+    } while (0)
+#else
+#define SF_STAMP(q) (void)0
+#endif
 #ifndef BH_SMALL_FRONT_MAX
 #define BH_SMALL_FRONT_MAX SMALL_FRONT_CAP
 #endif
@@ -648,8 +659,12 @@ __global__ __launch_bounds__(SF_TB) void k_small_front(
     chain_prio();
     extern __shared__ uint64_t sf_L[];  // P = the power of two >= n, padded with ~0
     __shared__ uint32_t s_w[SF_TB / 64];
+#ifdef BH_SF_TIMING
+    __shared__ uint64_t sf_t[SF_T_W];
+#endif
     const int J = g.J;
     const uint32_t t = threadIdx.x;
+    SF_STAMP(0);
     // (k_morton) the keys, or the drifting traversal's
     for (uint32_t i = t; i < P; i += SF_TB) {
         uint64_t v = ~0ull;
@@ -668,7 +683,12 @@ __global__ __launch_bounds__(SF_TB) void k_small_front(
     }
     for (uint32_t i = t; i <= nb; i += SF_TB) counts[i] = 0u;
     __syncthreads();
-    // (the bucket sort) all composites, ascending
+    SF_STAMP(1);
+    // (the bucket sort) all composites, ascending.  A stage is bound by the LDS (~0.27 us for
+    // 2 048 elements with 16 waves; 17.8 us of the front's ~33 at C1 'R', tools/sf_timing.py):
+    // skipping the barrier of stages whose pairs stay inside a wave, and keeping the closest
+    // stages in registers (fewer threads on the LDS stages), both measured no faster
+    // (profiles/r06sk_small_front_sort_variants.txt).
     for (uint32_t k = 2; k <= P; k <<= 1) {
         for (uint32_t j = k >> 1; j > 0; j >>= 1) {
             for (uint32_t q = t; q < P / 2; q += SF_TB) {  // pair (lo, lo + j), bit j of lo clear
@@ -683,6 +703,7 @@ __global__ __launch_bounds__(SF_TB) void k_small_front(
             __syncthreads();
         }
     }
+    SF_STAMP(2);
     for (uint32_t a = t; (int64_t)a < n; a += SF_TB) {
         const uint64_t v = sf_L[a];
         const uint32_t i = (uint32_t)v;
@@ -691,14 +712,38 @@ __global__ __launch_bounds__(SF_TB) void k_small_front(
         keys_s[a] = keys[i];
     }
     __syncthreads();
-    // (k_fixup_cells) runs of equal prefixes by (full key, index); the depth-D0 cell starts
-    for (uint32_t a = t; (int64_t)a < n; a += SF_TB) key_fixup(a, n, J, keys32_s, keys_s, perm);
-    __syncthreads();
-    const int64_t nbins1 = ((int64_t)1 << (2 * D0)) + 1;
-    const int64_t cells_hi = nbins1 > n_super ? nbins1 : n_super;
-    for (int64_t bin = t; bin < cells_hi; bin += SF_TB)
-        cells(bin, SF_TB, n, J, D0, keys_s, cell_start, super_list, n_super);
-    __syncthreads();
+    SF_STAMP(3);
+    // (k_fixup_cells) runs of equal prefixes by (full key, index) -- a run start is found in LDS,
+    // only the (rare) starts read the global arrays --; the depth-D0 cell starts, searched in LDS:
+    // the depth-D0 prefix is in the 32-bit one (2 (J - D0) >= key32_shift(J)) and the fixup
+    // reorders inside runs of one 32-bit prefix only
+    for (uint32_t a = t; (int64_t)a + 1 < n; a += SF_TB) {
+        const uint32_t k = (uint32_t)(sf_L[a] >> 32);
+        if ((uint32_t)(sf_L[a + 1] >> 32) == k && (a == 0 || (uint32_t)(sf_L[a - 1] >> 32) != k))
+            key_fixup(a, n, J, keys32_s, keys_s, perm);
+    }
+    const int sh32 = 2 * (J - D0) - key32_shift(J);
+    const int64_t nbins = (int64_t)1 << (2 * D0);
+    const int64_t cells_hi = nbins + 1 > n_super ? nbins + 1 : n_super;
+    if (sh32 >= 0) {
+        for (int64_t k = t; k < n_super; k += SF_TB) super_list[k] = 0xFFFFFFFFu;
+        for (int64_t bin = t; bin <= nbins; bin += SF_TB) {
+            int64_t lo = 0, hi = n;  // first index with its depth-D0 prefix >= bin (cells())
+            while (lo < hi) {
+                const int64_t mid = (lo + hi) >> 1;
+                if ((int64_t)((uint32_t)(sf_L[mid] >> 32) >> sh32) < bin) lo = mid + 1;
+                else hi = mid;
+            }
+            cell_start[bin] = (uint32_t)lo;
+        }
+        __syncthreads();
+    } else {
+        __syncthreads();
+        for (int64_t bin = t; bin < cells_hi; bin += SF_TB)
+            cells(bin, SF_TB, n, J, D0, keys_s, cell_start, super_list, n_super);
+        __syncthreads();
+    }
+    SF_STAMP(4);
     // (k_prep) the state in the new order, c(a), node counts -- kept in LDS for the scan
     uint32_t *c_l = reinterpret_cast<uint32_t *>(sf_L);  // (n + 1 <= 2 P counts)
     for (uint32_t a = t; (int64_t)a <= n; a += SF_TB) {
@@ -708,6 +753,7 @@ __global__ __launch_bounds__(SF_TB) void k_small_front(
         c_l[a] = c;
     }
     __syncthreads();
+    SF_STAMP(5);
     // (k_base_scan) base[i] = sum cnt[0..i), i <= n: each thread a run of E counts
     const uint32_t n1 = (uint32_t)n + 1u, E = (n1 + SF_TB - 1) / SF_TB;
     const uint32_t i0 = t * E;
@@ -731,7 +777,21 @@ __global__ __launch_bounds__(SF_TB) void k_small_front(
             run += c_l[i0 + e];
         }
     }
+#ifdef BH_SF_TIMING
+    __syncthreads();
+    SF_STAMP(6);
+    if (t == 0) {
+        const uint32_t r = atomicAdd(&g_sf_launch, 1u) % SF_T_REC;
+        for (int q = 0; q < 7; ++q) g_sf_times[r * SF_T_W + q] = sf_t[q];
+    }
+#endif
 }
+
+#ifdef BH_SF_TIMING
+extern "C" int bh_debug_sf_times(uint64_t *out) {
+    return (int)hipMemcpyFromSymbol(out, HIP_SYMBOL(g_sf_times), sizeof(uint64_t) * SF_T_REC * SF_T_W);
+}
+#endif
 
 static bool small_front(int64_t n, uint32_t &P) {
     static const int64_t lim = [] {
