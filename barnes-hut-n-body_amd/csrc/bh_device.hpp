@@ -273,6 +273,18 @@ __device__ __forceinline__ uint32_t bucket_offset(uint32_t b, uint32_t *__restri
 #endif
 
 // ---- launchers (tree_build.hip) --------------------------------------------------
+// The pipelined step's traversal copies of what the overlapped merge rule and build overwrite
+// while the second traversal reads it (k_trav_inputs' job, integrate.hip), written by k_emit_com
+// when m is set: masses and flags in the new order, the carried lane map, the node count; the
+// merge rule's mailbox header cleared.
+struct TravCopy {
+    double *m = nullptr;
+    uint32_t *cidx = nullptr;
+    uint32_t *lanes = nullptr;  // (with lanes_remap only)
+    uint32_t *T = nullptr;
+    uint32_t *box_header = nullptr;
+};
+
 struct TreeBuffers {
     BodyState src;  // state before the build (previous slot order)
     BodyState dst;  // receives the state in the new Morton order (positions may be jittered)
@@ -302,6 +314,7 @@ struct TreeBuffers {
     // *heavy_count is zero before the build -- k_merge_replay clears it after its use)
     uint32_t *heavy = nullptr, *heavy_count = nullptr;
     double heavy_thr = 0.0;
+    TravCopy tc{};  // (m null: none)
 };
 
 int cell_table_depth(int J, int64_t n);

@@ -298,6 +298,8 @@ struct bh_engine {
     size_t nodes_alt_cap = 0;
     double *m_trav = nullptr;
     uint32_t *cidx_trav = nullptr, *lanes_trav = nullptr, *T_trav = nullptr;
+    bool tc_want = false, tc_done = false;  // build_into: the copies above made by k_emit_com
+    uint32_t *tc_box = nullptr;             // (and the merge rule's mailbox header cleared)
     int64_t trav_cap = 0;
     bool prebuilt = false;  // the current step's first build was made by the previous step
     // ... by the previous call's last step: that build's error flags are in scalars[10] (they
@@ -864,6 +866,16 @@ int build_into(bh_engine *e, hipStream_t s, bool overlap, bool keep_v = false, b
     const bool defer = due && BH_LANE_DEFER && ((overlap && e->lane_defer) || e->lane_hold);
     const bool refresh = use_lanes && (!e->lanes_valid || (due && !defer));
     tb.lanes_remap = use_lanes && !refresh ? e->lanes : nullptr;
+    // the second traversal's copies made by the build (k_emit_com) instead of k_trav_inputs --
+    // not when the map is re-sorted after the build (lane_order rewrites it)
+    e->tc_done = e->tc_want && n > 0 && !refresh;
+    if (e->tc_done) {
+        tb.tc.m = e->m_trav;
+        tb.tc.cidx = e->cidx_trav;
+        tb.tc.lanes = tb.lanes_remap ? e->lanes_trav : nullptr;
+        tb.tc.T = e->T_trav;
+        tb.tc.box_header = e->tc_box;
+    }
     tb.keys_ready = e->keys_ready && !overlap;
     e->keys_ready = false;
     if (!overlap) e->mir_fresh = false;  // the jitter may move bodies
@@ -2147,6 +2159,11 @@ int mirror_launch(bh_engine *e, const BodyState &src, hipStream_t after_pos, hip
 // copied aside before the overlapped build reuses them, and the state before that build's jitter
 // (the previous slot order) becomes the caller-visible `view`.
 
+// The second traversal's input copies (masses, flags, lane map, node count) written by the
+// second build's k_emit_com instead of a k_trav_inputs launch between the build and the traversal.
+#ifndef BH_TRAV_COPY_IN_BUILD
+#define BH_TRAV_COPY_IN_BUILD 1
+#endif
 int evaluate_pipelined(bh_engine *e, bool last) {
     const int64_t n = e->n;
     hipStream_t s = e->stream;
@@ -2163,15 +2180,22 @@ int evaluate_pipelined(bh_engine *e, bool last) {
         e->lanes_age = 0;
     }
     e->lane_hold = true;
+    e->tc_want = BH_TRAV_COPY_IN_BUILD != 0;
+    e->tc_box = merging ? reinterpret_cast<uint32_t *>(e->box) : nullptr;
     // velocities: permuted by the kick below; the heavy list for the merge rule that follows
     const int rc_b2 = build_into(e, s, false, true, false, merging && BH_HEAVY_CARRY);
     e->lane_hold = false;
+    e->tc_want = false;
     TRY(rc_b2);
     TRY(mark(e, 0));
     const bool lanes = e->lanes_valid;
-    copy_trav_inputs(n, e->st.m, e->m_trav, e->st.cidx, e->cidx_trav, lanes ? e->lanes : nullptr,
-                     e->lanes_trav, e->base + n, e->T_trav, s, merging ? e->box : nullptr);
-    HIPCHK(e, hipGetLastError());
+    if (!e->tc_done) {  // (the build made them otherwise)
+        copy_trav_inputs(n, e->st.m, e->m_trav, e->st.cidx, e->cidx_trav,
+                         lanes ? e->lanes : nullptr, e->lanes_trav, e->base + n, e->T_trav, s,
+                         merging ? e->box : nullptr);
+        HIPCHK(e, hipGetLastError());
+    }
+    e->tc_done = false;
     // With the mirror on, a call's last step runs the merge rule and the mirror's caller-order
     // gather of positions and masses before the traversal (~0.15 ms in line): the mirror's 40 MB
     // cross PCIe from then on instead of from when the overlapped merge rule and gather find wave

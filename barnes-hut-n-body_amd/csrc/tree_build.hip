@@ -1115,7 +1115,8 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
                                                      uint32_t *scratch, Node *nodes,
                                                      uint32_t *err,
                                                      const uint32_t *__restrict__ inv,
-                                                     uint32_t *__restrict__ lanes, SpanOut so) {
+                                                     uint32_t *__restrict__ lanes, SpanOut so,
+                                                     TravCopy tc) {
     chain_prio();
     __shared__ double s_m[COM_CAP + 1], s_x[COM_CAP + 1], s_y[COM_CAP + 1];  // [COM_CAP]: pad
     __shared__ uint32_t s_next[COM_CAP];
@@ -1162,6 +1163,23 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
         ccs[i] = a < n ? cc : -1;
         bases[i] = a < n ? ba : 0u;
         lmax = max(lmax, ccs[i]);
+    }
+    if (tc.m) {  // the second traversal's copies (k_trav_inputs): masses, flags, node count
+        uint32_t cs[EC_PER];
+#pragma unroll
+        for (int i = 0; i < EC_PER; ++i) cs[i] = cidx[min(a0 + i, n - 1)];
+#pragma unroll
+        for (int i = 0; i < EC_PER; ++i) {
+            if (a0 + i < n) {
+                tc.m[a0 + i] = ms[i];
+                tc.cidx[a0 + i] = cs[i];
+            }
+        }
+        if (blockIdx.x == 0) {
+            if (threadIdx.x == 0) *tc.T = base[n];
+            if (tc.box_header && threadIdx.x < sizeof(MergeHeader) / sizeof(uint32_t))
+                tc.box_header[threadIdx.x] = 0u;
+        }
     }
     {
         // one 8-byte word of c(j) + 1 per thread (EC_WIN / 8 threads): the word minimum in
@@ -1223,6 +1241,11 @@ __global__ __launch_bounds__(EC_TB) void k_emit_com(int64_t n, Geometry g, int D
 #pragma unroll
         for (int i = 0; i < EC_PER; ++i)
             if (a0 + i < n) lanes[a0 + i] = nl[i];
+        if (tc.lanes) {
+#pragma unroll
+            for (int i = 0; i < EC_PER; ++i)
+                if (a0 + i < n) tc.lanes[a0 + i] = nl[i];
+        }
     }
     const uint32_t S0 = base[c0], S1 = base[c1];
     const uint32_t cnt = S1 - S0;
@@ -2183,7 +2206,7 @@ hipError_t tree_build(const TreeBuffers &b, int64_t n, const Geometry &g, hipStr
     k_emit_com<<<(unsigned)((n + (1 << COM_CHUNK_SHIFT) - 1) >> COM_CHUNK_SHIFT), EC_TB, 0, s>>>(
         n, g, D0, b.keys_s, b.cpl, b.base, b.cell_start, b.dst.x, b.dst.y, b.dst.m, b.dst.cidx,
         b.idx, b.nodes, b.scalars + 1, b.keys32, b.lanes_remap,
-        SpanOut{b.span_list, b.span_stride, b.super_list, n_groups});
+        SpanOut{b.span_list, b.span_stride, b.super_list, n_groups}, b.tc);
     const dim3 span_grid((b.span_stride + TB - 1) / TB, g.J + 1);
     if (!BH_EMIT_SPANS)
         k_span_find<<<span_grid, TB, 0, s>>>(n, g.J, D0, b.keys_s, b.cpl, b.base, b.cell_start,
