@@ -2164,6 +2164,9 @@ int mirror_launch(bh_engine *e, const BodyState &src, hipStream_t after_pos, hip
 #ifndef BH_TRAV_COPY_IN_BUILD
 #define BH_TRAV_COPY_IN_BUILD 1
 #endif
+#ifndef BH_PIPE_REUSE_MARK
+#define BH_PIPE_REUSE_MARK 1
+#endif
 int evaluate_pipelined(bh_engine *e, bool last) {
     const int64_t n = e->n;
     hipStream_t s = e->stream;
@@ -2188,6 +2191,12 @@ int evaluate_pipelined(bh_engine *e, bool last) {
     e->tc_want = false;
     TRY(rc_b2);
     TRY(mark(e, 0));
+    // with profiling on, the overlapped chain waits for the timing event just recorded after the
+    // build (when nothing else follows the build on this stream): each event recorded on the
+    // stream holds the next kernel back by a few microseconds
+    const hipEvent_t built_mark = e->profiling && e->ev_used > 0 && e->tc_done && BH_PIPE_REUSE_MARK
+                                      ? e->ev[e->ev_used - 1]
+                                      : nullptr;
     const bool lanes = e->lanes_valid;
     if (!e->tc_done) {  // (the build made them otherwise)
         copy_trav_inputs(n, e->st.m, e->m_trav, e->st.cidx, e->cidx_trav,
@@ -2217,8 +2226,12 @@ int evaluate_pipelined(bh_engine *e, bool last) {
             e->mid_cv.notify_all();
         }
     }
-    HIPCHK(e, hipEventRecord(e->pipe_ev[0], s));
-    HIPCHK(e, hipStreamWaitEvent(e->pipe_stream, e->pipe_ev[0], 0));
+    if (built_mark && !early) {
+        HIPCHK(e, hipStreamWaitEvent(e->pipe_stream, built_mark, 0));
+    } else {
+        HIPCHK(e, hipEventRecord(e->pipe_ev[0], s));
+        HIPCHK(e, hipStreamWaitEvent(e->pipe_stream, e->pipe_ev[0], 0));
+    }
     const ForceParams fp{e->p.G, e->p.soft2, e->p.theta * e->p.theta};  // BHA:378
     KickArgs ka{KICK_ONLY, e->st.vx, e->st.vy, e->p.dt * 0.5, e->p.dt};
     if (n > 0) {  // (the build swapped: the previous order's velocities are in alt)
