@@ -204,6 +204,13 @@ using BucketRadix = rocprim::block_radix_sort<unsigned long long, SORT_TB, SORT_
 #ifndef BH_SORT_BITONIC_MAX
 #define BH_SORT_BITONIC_MAX 0
 #endif
+// Buckets of up to BH_SORT_RANK_MAX elements (a multiple of SORT_TB) that the bin radix cannot
+// take -- a few per build, whose key span holds an outlier: all but one element in one bin -- are
+// sorted by counting each element's rank in LDS instead of the block radix sort (0: off).
+#ifndef BH_SORT_RANK_MAX
+#define BH_SORT_RANK_MAX 1024
+#endif
+static_assert(BH_SORT_RANK_MAX % SORT_TB == 0 && BH_SORT_RANK_MAX <= SORT_CAP, "rank sort size");
 
 #ifdef BH_SORT_STATS  // diagnostic build: which path each bucket took (radix / bitonic / global)
 __device__ unsigned long long g_sort_stats[8];
@@ -349,6 +356,29 @@ __global__ __launch_bounds__(SORT_TB) void k_bucket_sort(const uint32_t *__restr
         SORT_STAT(2, 1);
         SORT_STAT(3, s);
         SORT_LOGV(1, 1);
+        if (s <= (uint32_t)BH_SORT_RANK_MAX) {
+            // every element's rank = the number of smaller composites (distinct: the slot is in
+            // them), counted against the whole bucket in LDS -- broadcast reads, no barriers
+            constexpr int RPT = BH_SORT_RANK_MAX > 0 ? BH_SORT_RANK_MAX / SORT_TB : 1;
+            uint64_t v[RPT];
+            uint32_t r[RPT];
+#pragma unroll
+            for (int q = 0; q < RPT; ++q) {
+                const uint32_t j = threadIdx.x + q * SORT_TB;
+                v[q] = j < s ? L[j] : 0ull;
+                r[q] = 0;
+            }
+#pragma unroll 4
+            for (uint32_t j = 0; j < s; ++j) {
+                const uint64_t u = L[j];
+#pragma unroll
+                for (int q = 0; q < RPT; ++q) r[q] += u < v[q] ? 1u : 0u;
+            }
+#pragma unroll
+            for (int q = 0; q < RPT; ++q)
+                if (threadIdx.x + q * SORT_TB < s) emit(r[q], v[q]);
+            return;
+        }
         if (BH_SORT_BLOCK_RADIX && s > (uint32_t)BH_SORT_BITONIC_MAX) {
             constexpr int IPT = SORT_CAP / SORT_TB;
             const uint32_t kmn = s_min, smn = s_smin;
